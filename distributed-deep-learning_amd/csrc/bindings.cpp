@@ -1,0 +1,229 @@
+// Python bindings of the native extension ``_C`` (kernels launch on torch's current HIP
+// stream so they compose with RCCL collectives and hipGraph capture).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kernels/api.h"
+#include "runtime/mailbox.h"
+
+namespace py = pybind11;
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_f32_cuda(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void adam_flat(at::Tensor w, at::Tensor g, at::Tensor m, at::Tensor v, double lr_t, double b1,
+               double b2, double eps, double scale) {
+  check_f32_cuda(w, "w");
+  check_f32_cuda(g, "g");
+  check_f32_cuda(m, "m");
+  check_f32_cuda(v, "v");
+  const int64_t n = w.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adam_flat: size mismatch");
+  ddl::launch_adam(w.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
+                   v.data_ptr<float>(), n, (float)lr_t, (float)b1, (float)b2, (float)eps,
+                   (float)scale, cur_stream());
+}
+
+void momentum_flat(at::Tensor w, at::Tensor g, at::Tensor m, double lr, double mu, double scale) {
+  check_f32_cuda(w, "w");
+  check_f32_cuda(g, "g");
+  check_f32_cuda(m, "m");
+  const int64_t n = w.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n, "momentum_flat: size mismatch");
+  ddl::launch_momentum(w.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), n,
+                       (float)lr, (float)mu, (float)scale, cur_stream());
+}
+
+// Python-facing wrapper of ddl::Engine: owns the workspace tensor.
+class PyEngine {
+ public:
+  PyEngine(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, int64_t max_batch,
+           int64_t train_batch, double keep_prob)
+      : params_(params), grads_(grads) {
+    TORCH_CHECK(params.size() == 14 && grads.size() == 14, "need 14 parameter/gradient tensors");
+    for (int i = 0; i < 14; ++i) {
+      check_f32_cuda(params[i], "param");
+      check_f32_cuda(grads[i], "grad");
+      e_.P[i] = params[i].data_ptr<float>();
+      e_.G[i] = grads[i].data_ptr<float>();
+    }
+    device_ = params[0].device();
+    e_.max_batch = (int)std::max(max_batch, train_batch);
+    e_.train_batch = (int)train_batch;
+    set_keep_prob(keep_prob);
+    {
+      c10::hip::HIPGuard guard(device_.index());
+      e_.init_streams();
+    }
+    realloc();
+  }
+
+  void set_cfg(std::vector<int64_t> c) {
+    TORCH_CHECK((int)c.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " tile configs");
+    for (int i = 0; i < ddl::OP_COUNT; ++i) {
+      TORCH_CHECK(c[i] >= 0 && c[i] < ddl::NUM_TILE_CFGS, "tile config out of range");
+      e_.cfg[i] = (int)c[i];
+    }
+    realloc();
+  }
+  std::vector<int64_t> get_cfg() const {
+    return std::vector<int64_t>(e_.cfg, e_.cfg + ddl::OP_COUNT);
+  }
+  void set_concurrent(bool on) { e_.concurrent = on; }
+  void set_wide_thr(int64_t t) { e_.wide_thr = (int)std::max<int64_t>(1, t); }
+
+  void set_keep_prob(double keep) {
+    const double rate = 1.0 - keep;
+    e_.thr24 = (uint32_t)std::llround(rate * 16777216.0);
+    e_.inv_keep = keep > 0.0 ? (float)(1.0 / keep) : 0.f;
+  }
+
+  void set_splits(std::vector<int64_t> s) {
+    TORCH_CHECK((int)s.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " split factors");
+    for (int i = 0; i < ddl::OP_COUNT; ++i) e_.splits[i] = (int)std::max<int64_t>(1, s[i]);
+    realloc();
+  }
+  std::vector<int64_t> get_splits() const {
+    return std::vector<int64_t>(e_.splits, e_.splits + ddl::OP_COUNT);
+  }
+
+  void forward(at::Tensor x, at::Tensor seed, bool train) {
+    check_x(x);
+    e_.forward(x.data_ptr<float>(), (int)x.size(0), seed_ptr(seed), train, cur_stream());
+  }
+  void backward_segment(int64_t s, at::Tensor x, at::Tensor labels, at::Tensor seed) {
+    check_x(x);
+    TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_cuda(), "labels must be int64 GPU");
+    e_.backward_segment((int)s, x.data_ptr<float>(), labels.data_ptr<int64_t>(), (int)x.size(0),
+                        seed_ptr(seed), cur_stream());
+  }
+  void run_op(int64_t op, at::Tensor x, at::Tensor seed, bool train) {
+    check_x(x);
+    e_.run_op((int)op, x.data_ptr<float>(), (int)x.size(0), seed_ptr(seed), train, cur_stream());
+  }
+  void zero_correct() {
+    TORCH_CHECK(hipMemsetAsync(e_.correct, 0, sizeof(int), cur_stream()) == hipSuccess);
+  }
+  void eval_count(at::Tensor x, at::Tensor labels) {
+    check_x(x);
+    e_.eval_count(x.data_ptr<float>(), labels.data_ptr<int64_t>(), (int)x.size(0), cur_stream());
+  }
+  void head_fwd(at::Tensor labels, int64_t B) {
+    ddl::launch_head_fwd(e_.h2, e_.P[12], e_.P[13], labels.data_ptr<int64_t>(), (int)B, e_.dlog,
+                         e_.loss, nullptr, cur_stream());
+  }
+
+  // Views of internal buffers (testing / debugging).  Shapes are for batch B.
+  at::Tensor buffer(const std::string& name, int64_t B) {
+    auto f = at::TensorOptions().dtype(at::kFloat).device(device_);
+    auto u8 = at::TensorOptions().dtype(at::kByte).device(device_);
+    auto i32 = at::TensorOptions().dtype(at::kInt).device(device_);
+    if (name == "p1") return torch::from_blob(e_.p1, {B, 14, 14, 32}, f);
+    if (name == "p2") return torch::from_blob(e_.p2, {B, 7, 7, 64}, f);
+    if (name == "p3") return torch::from_blob(e_.p3, {B, 4, 4, 128}, f);
+    if (name == "p4") return torch::from_blob(e_.p4, {B, 1024}, f);
+    if (name == "h1") return torch::from_blob(e_.h1, {B, 1024}, f);
+    if (name == "h2") return torch::from_blob(e_.h2, {B, 512}, f);
+    if (name == "dlog") return torch::from_blob(e_.dlog, {B, 10}, f);
+    if (name == "loss") return torch::from_blob(e_.loss, {B}, f);
+    if (name == "dpre2fc") return torch::from_blob(e_.dpre2fc, {B, 512}, f);
+    if (name == "dpre1fc") return torch::from_blob(e_.dpre1fc, {B, 1024}, f);
+    if (name == "d4") return torch::from_blob(e_.d4, {B, 4, 4, 256}, f);
+    if (name == "d3") return torch::from_blob(e_.d3, {B, 7, 7, 128}, f);
+    if (name == "d2") return torch::from_blob(e_.d2, {B, 14, 14, 64}, f);
+    if (name == "d1") return torch::from_blob(e_.d1, {B, 28, 28, 32}, f);
+    if (name == "c1") return torch::from_blob(e_.c1, {B, 14, 14, 32}, u8);
+    if (name == "c2") return torch::from_blob(e_.c2, {B, 7, 7, 64}, u8);
+    if (name == "c3") return torch::from_blob(e_.c3, {B, 4, 4, 128}, u8);
+    if (name == "c4") return torch::from_blob(e_.c4, {B, 1024}, u8);
+    if (name == "correct") return torch::from_blob(e_.correct, {1}, i32);
+    TORCH_CHECK(false, "unknown buffer ", name);
+  }
+
+  int64_t max_batch() const { return e_.max_batch; }
+  int64_t workspace_bytes() const { return (int64_t)e_.workspace_bytes(); }
+  static std::vector<int64_t> op_shape(int64_t op, int64_t B) {
+    int M, N, K;
+    ddl::Engine::op_shape((int)op, (int)B, &M, &N, &K);
+    return {M, N, K};
+  }
+
+ private:
+  void realloc() {
+    e_.slab_floats = e_.slab_floats_needed(e_.train_batch);
+    const size_t bytes = e_.workspace_bytes();
+    // zeroed once: the split-K arrival tickets must start at 0 (reducers re-arm them)
+    ws_ = at::zeros({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).device(device_));
+    e_.bind_workspace(ws_.data_ptr());
+  }
+  void check_x(const at::Tensor& x) {
+    check_f32_cuda(x, "x");
+    TORCH_CHECK(x.dim() == 2 && x.size(1) == 784, "x must be [B,784]");
+    TORCH_CHECK(x.size(0) <= e_.max_batch, "batch ", x.size(0), " exceeds engine max_batch ",
+                e_.max_batch);
+  }
+  static const uint32_t* seed_ptr(const at::Tensor& s) {
+    if (!s.defined() || s.numel() == 0) return nullptr;
+    TORCH_CHECK(s.is_cuda() && s.scalar_type() == at::kInt, "seed must be an int32 GPU tensor");
+    return reinterpret_cast<const uint32_t*>(s.data_ptr<int32_t>());
+  }
+
+  ddl::Engine e_;
+  std::vector<at::Tensor> params_, grads_;
+  at::Tensor ws_;
+  at::Device device_{at::kCPU};
+};
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "ddl_amd native extension: gfx950 HIP kernels + C++ runtime";
+  m.def("adam_flat", &adam_flat, "Fused TF1 Adam on a flat shard",
+        py::arg("w"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr_t"), py::arg("b1"),
+        py::arg("b2"), py::arg("eps"), py::arg("scale") = 1.0);
+  m.def("momentum_flat", &momentum_flat, "Fused momentum SGD on a flat shard");
+  m.attr("OP_COUNT") = (int)ddl::OP_COUNT;
+
+  py::class_<PyEngine>(m, "Engine")
+      .def(py::init<std::vector<at::Tensor>, std::vector<at::Tensor>, int64_t, int64_t, double>(),
+           py::arg("params"), py::arg("grads"), py::arg("max_batch"), py::arg("train_batch"),
+           py::arg("keep_prob"))
+      .def("set_keep_prob", &PyEngine::set_keep_prob)
+      .def("set_splits", &PyEngine::set_splits)
+      .def("get_splits", &PyEngine::get_splits)
+      .def("set_cfg", &PyEngine::set_cfg)
+      .def("get_cfg", &PyEngine::get_cfg)
+      .def("set_concurrent", &PyEngine::set_concurrent)
+      .def("set_wide_thr", &PyEngine::set_wide_thr)
+      .def("forward", &PyEngine::forward)
+      .def("backward_segment", &PyEngine::backward_segment)
+      .def("run_op", &PyEngine::run_op)
+      .def("zero_correct", &PyEngine::zero_correct)
+      .def("eval_count", &PyEngine::eval_count)
+      .def("head_fwd", &PyEngine::head_fwd)
+      .def("buffer", &PyEngine::buffer)
+      .def("max_batch", &PyEngine::max_batch)
+      .def("workspace_bytes", &PyEngine::workspace_bytes)
+      .def_static("op_shape", &PyEngine::op_shape);
+
+  py::class_<ddl::ShmMailbox>(m, "ShmMailbox")
+      .def(py::init<const std::string&, int64_t, bool>(), py::arg("name"), py::arg("capacity"),
+           py::arg("create"))
+      .def("push", &ddl::ShmMailbox::push, py::call_guard<py::gil_scoped_release>())
+      .def("pop", &ddl::ShmMailbox::pop, py::call_guard<py::gil_scoped_release>())
+      .def("size", &ddl::ShmMailbox::size)
+      .def("capacity", &ddl::ShmMailbox::capacity)
+      .def("unlink", &ddl::ShmMailbox::unlink);
+}

@@ -1,0 +1,276 @@
+// The CNN step engine: every forward / backward kernel launch of one worker step.
+//
+// Reference step: sess.run(grads) on the TF runtime, 14 host round trips
+// to push, 14 to pull.  Here a step is ~20 GEMM-engine launches + 2 head kernels, all
+// buffers preallocated (graph-capturable: no malloc, no sync).  The backward is split
+// into 4 segments so the host can push a segment's gradients on a side stream while the
+// next segment computes (SURVEY.md §5.8 bucket plan); inside a segment the weight-gradient
+// GEMM runs on a second stream concurrently with the data-gradient GEMM that feeds the
+// next segment (fork/join events, captured as parallel graph branches).
+#include <string.h>
+
+#include "api.h"
+#include "layers.h"
+
+namespace ddl {
+
+Engine::Engine() {
+  // {tile config, split-K} per op — defaults from the op_bench sweep (scripts/op_bench.py)
+  static const int defc[OP_COUNT] = {3, 3, 3, 2, 3, 3, 3, 3, 3, 3, 2, 3, 3, 3, 3, 3, 3};
+  static const int defs[OP_COUNT] = {8, 4, 3, 16, 8, 16, 4, 1, 4, 1, 32, 4, 3, 32, 4, 64, 256};
+  memcpy(cfg, defc, sizeof(defc));
+  memcpy(splits, defs, sizeof(defs));
+}
+
+Engine::~Engine() {
+  if (ev_fork) (void)hipEventDestroy(ev_fork);
+  if (ev_join) (void)hipEventDestroy(ev_join);
+  if (side) (void)hipStreamDestroy(side);
+}
+
+void Engine::init_streams() {
+  if (side) return;
+  (void)hipStreamCreateWithFlags(&side, hipStreamNonBlocking);
+  (void)hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming);
+  (void)hipEventCreateWithFlags(&ev_join, hipEventDisableTiming);
+}
+
+void Engine::op_shape(int op, int B, int* M, int* N, int* K) {
+  int m = 0, n = 0, k = 0;
+  switch (op) {
+    case OP_CONV1_FWD: m = B * 14 * 14 * 4; n = 32; k = 25; break;
+    case OP_CONV2_FWD: m = B * 7 * 7 * 4; n = 64; k = 800; break;
+    case OP_CONV3_FWD: m = B * 4 * 4 * 4; n = 128; k = 1600; break;
+    case OP_CONV4_FWD: m = B * 2 * 2 * 4; n = 256; k = 3200; break;
+    case OP_FC1_FWD: m = B; n = 1024; k = 1024; break;
+    case OP_FC2_FWD: m = B; n = 512; k = 1024; break;
+    case OP_FC2_DGRAD: m = B; n = 1024; k = 512; break;
+    case OP_FC2_WGRAD: m = 1025; n = 512; k = B; break;
+    case OP_FC1_DGRAD: m = B; n = 1024; k = 1024; break;
+    case OP_FC1_WGRAD: m = 1025; n = 1024; k = B; break;
+    case OP_CONV4_DGRAD: m = B * 16; n = 128; k = 6400; break;
+    case OP_CONV4_WGRAD: m = 3201; n = 256; k = B * 16; break;
+    case OP_CONV3_DGRAD: m = B * 49; n = 64; k = 3200; break;
+    case OP_CONV3_WGRAD: m = 1601; n = 128; k = B * 49; break;
+    case OP_CONV2_DGRAD: m = B * 196; n = 32; k = 1600; break;
+    case OP_CONV2_WGRAD: m = 801; n = 64; k = B * 196; break;
+    case OP_CONV1_WGRAD: m = 26; n = 32; k = B * 784; break;
+    default: break;
+  }
+  *M = m; *N = n; *K = k;
+}
+
+#define TILE_0 64, 64, 32, 1, 1
+#define TILE_1 128, 64, 32, 2, 1
+#define TILE_2 64, 32, 32, 1, 1
+#define TILE_3 32, 32, 32, 1, 1
+
+static size_t slab_need(int c, int M, int N, int K, int s) {
+  switch (c) {
+    case 0: return splitk_slab_f4<TILE_0>(M, N, K, s);
+    case 1: return splitk_slab_f4<TILE_1>(M, N, K, s);
+    case 2: return splitk_slab_f4<TILE_2>(M, N, K, s);
+    default: return splitk_slab_f4<TILE_3>(M, N, K, s);
+  }
+}
+
+template <class P>
+static void launch_cfg(int c, const P& p, int s, int wide_thr, const SplitScratch& sc,
+                       hipStream_t st) {
+  switch (c) {
+    case 0: launch_gemm<TILE_0>(p, s, wide_thr, sc, st); break;
+    case 1: launch_gemm<TILE_1>(p, s, wide_thr, sc, st); break;
+    case 2: launch_gemm<TILE_2>(p, s, wide_thr, sc, st); break;
+    default: launch_gemm<TILE_3>(p, s, wide_thr, sc, st); break;
+  }
+}
+
+size_t Engine::slab_floats_needed(int B) const {
+  size_t mx = 0;
+  for (int op = 0; op < OP_COUNT; ++op) {
+    int M, N, K;
+    op_shape(op, B, &M, &N, &K);
+    const size_t f = 4 * slab_need(cfg[op], M, N, K, splits[op]);
+    if (f > mx) mx = f;
+  }
+  return mx;
+}
+
+static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+static const size_t kActPer[] = {6272, 3136, 2048, 1024, 1024, 512, 16, 1,
+                                 512, 1024, 4096, 6272, 12544, 25088};
+static const size_t kCodePer[] = {6272, 3136, 2048, 1024};
+
+size_t Engine::workspace_bytes() const {
+  const size_t B = (size_t)max_batch;
+  size_t f = 0;
+  for (size_t p : kActPer) f += al256(4 * B * p);
+  f += 2 * al256(4 * slab_floats);
+  for (size_t c : kCodePer) f += al256(B * c);
+  f += 256;                          // correct counter
+  f += 2 * al256(4 * kMaxTickets);   // split-K arrival tickets (two streams)
+  return f;
+}
+
+void Engine::bind_workspace(void* base) {
+  const size_t B = (size_t)max_batch;
+  char* p = (char*)base;
+  auto take = [&](size_t bytes) { char* r = p; p += al256(bytes); return r; };
+  float** acts[] = {&p1, &p2, &p3, &p4, &h1, &h2, &dlog, &loss,
+                    &dpre2fc, &dpre1fc, &d4, &d3, &d2, &d1};
+  for (int i = 0; i < 14; ++i) *acts[i] = (float*)take(4 * B * kActPer[i]);
+  for (int s = 0; s < 2; ++s) {
+    scratch[s].slab = take(4 * slab_floats);
+    scratch[s].slab_f4 = slab_floats / 4;
+  }
+  uint8_t** codes[] = {&c1, &c2, &c3, &c4};
+  for (int i = 0; i < 4; ++i) *codes[i] = (uint8_t*)take(B * kCodePer[i]);
+  correct = (int*)take(256);
+  for (int s = 0; s < 2; ++s) {
+    scratch[s].tickets = (int*)take(4 * kMaxTickets);
+    scratch[s].max_tiles = kMaxTickets;
+  }
+}
+
+void Engine::run_op(int op, const float* x, int B, const uint32_t* seed, bool train,
+                    hipStream_t st, int si) {
+  int M, N, K;
+  op_shape(op, B, &M, &N, &K);
+  const int s = train ? splits[op] : 1;
+  const int c = cfg[op];
+  const uint32_t thr = train ? thr24 : 0u;
+  const SplitScratch& sc = scratch[si];
+  switch (op) {
+    case OP_CONV1_FWD: {
+      ConvFwd<28, 1, 32> p{M, N, K, x, P[0], P[1], p1, c1};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_CONV2_FWD: {
+      ConvFwd<14, 32, 64> p{M, N, K, p1, P[2], P[3], p2, c2};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_CONV3_FWD: {
+      ConvFwd<7, 64, 128> p{M, N, K, p2, P[4], P[5], p3, c3};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_CONV4_FWD: {
+      ConvFwd<4, 128, 256> p{M, N, K, p3, P[6], P[7], p4, c4};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_FC1_FWD: {
+      FcFwd<true> p{M, N, K, p4, P[8], P[9], h1, seed, 1u, thr, inv_keep};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_FC2_FWD: {
+      FcFwd<false> p{M, N, K, h1, P[10], P[11], h2, seed, 2u, thr, inv_keep};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_FC2_DGRAD: {
+      FcDgradAct p{{M, N, K, dpre2fc, P[10]}, h1, inv_keep, dpre1fc};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_FC2_WGRAD: {
+      FcWgrad p{M, N, K, 1024, h1, dpre2fc, G[10], G[11]};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_FC1_DGRAD: {
+      FcDgradPool<2, 256> p{{M, N, K, dpre1fc, P[8]}, c4, d4};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_FC1_WGRAD: {
+      FcWgrad p{M, N, K, 1024, p4, dpre1fc, G[8], G[9]};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_CONV4_DGRAD: {
+      ConvDgrad<4, 128, 256, 7> p{M, N, K, d4, P[6], c3, d3};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_CONV4_WGRAD: {
+      ConvWgrad<4, 128, 256> p{M, N, K, p3, d4, G[6], G[7]};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_CONV3_DGRAD: {
+      ConvDgrad<7, 64, 128, 14> p{M, N, K, d3, P[4], c2, d2};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_CONV3_WGRAD: {
+      ConvWgrad<7, 64, 128> p{M, N, K, p2, d3, G[4], G[5]};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_CONV2_DGRAD: {
+      ConvDgrad<14, 32, 64, 28> p{M, N, K, d2, P[2], c1, d1};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_CONV2_WGRAD: {
+      ConvWgrad<14, 32, 64> p{M, N, K, p1, d2, G[2], G[3]};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    case OP_CONV1_WGRAD: {
+      ConvWgrad<28, 1, 32> p{M, N, K, x, d1, G[0], G[1]};
+      launch_cfg(c, p, s, wide_thr, sc, st);
+    } break;
+    default: break;
+  }
+}
+
+void Engine::forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st) {
+  for (int op = OP_CONV1_FWD; op <= OP_FC2_FWD; ++op) run_op(op, x, B, seed, train, st, 0);
+}
+
+// The side stream waits for everything enqueued on `st` so far.
+void Engine::fork(hipStream_t st) {
+  (void)hipEventRecord(ev_fork, st);
+  (void)hipStreamWaitEvent(side, ev_fork, 0);
+}
+
+// `st` waits for everything enqueued on the side stream so far.
+void Engine::join(hipStream_t st) {
+  (void)hipEventRecord(ev_join, side);
+  (void)hipStreamWaitEvent(st, ev_join, 0);
+}
+
+void Engine::wgrad(int op, const float* x, int B, const uint32_t* seed, hipStream_t st) {
+  if (concurrent && side) {
+    fork(st);
+    run_op(op, x, B, seed, true, side, 1);
+  } else {
+    run_op(op, x, B, seed, true, st, 0);
+  }
+}
+
+void Engine::backward_segment(int s, const float* x, const int64_t* labels, int B,
+                              const uint32_t* seed, hipStream_t st) {
+  switch (s) {
+    case 0:
+      launch_head_fwd(h2, P[12], P[13], labels, B, dlog, loss, nullptr, st);
+      launch_head_bwd(h2, P[12], dlog, B, seed, thr24, inv_keep, G[12], G[13], dpre2fc, st);
+      wgrad(OP_FC2_WGRAD, x, B, seed, st);
+      run_op(OP_FC2_DGRAD, x, B, seed, true, st, 0);
+      wgrad(OP_FC1_WGRAD, x, B, seed, st);
+      run_op(OP_FC1_DGRAD, x, B, seed, true, st, 0);
+      break;
+    case 1:
+      wgrad(OP_CONV4_WGRAD, x, B, seed, st);
+      run_op(OP_CONV4_DGRAD, x, B, seed, true, st, 0);
+      break;
+    case 2:
+      wgrad(OP_CONV3_WGRAD, x, B, seed, st);
+      run_op(OP_CONV3_DGRAD, x, B, seed, true, st, 0);
+      break;
+    case 3:
+      wgrad(OP_CONV2_WGRAD, x, B, seed, st);
+      run_op(OP_CONV2_DGRAD, x, B, seed, true, st, 0);
+      wgrad(OP_CONV1_WGRAD, x, B, seed, st);
+      break;
+    default: break;
+  }
+  if (concurrent && side) join(st);
+}
+
+void Engine::eval_count(const float* x, const int64_t* labels, int B, hipStream_t st) {
+  forward(x, B, nullptr, false, st);
+  launch_head_fwd(h2, P[12], P[13], labels, B, nullptr, nullptr, correct, st);
+}
+
+}  // namespace ddl

@@ -47,8 +47,9 @@ def adam_torch_(w: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tens
     lr_t = adam_coeffs(h, t)
     if grad_scale != 1.0:
         g = g * grad_scale
-    m.mul_(h.beta1).add_(g, alpha=1.0 - h.beta1)
-    v.mul_(h.beta2).addcmul_(g, g, value=1.0 - h.beta2)
+    # TF ApplyAdam form: m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2)
+    m.add_((g - m) * (1.0 - h.beta1))
+    v.add_((g * g - v) * (1.0 - h.beta2))
     w.sub_(lr_t * m / (v.sqrt() + h.eps))
 
 

@@ -86,8 +86,9 @@ class ParameterServer:
                                        grad_scale)
             else:
                 gg = g * grad_scale if grad_scale != 1.0 else g
-                m.mul_(self.h.beta1).add_(gg, alpha=1.0 - self.h.beta1)
-                v.mul_(self.h.beta2).addcmul_(gg, gg, value=1.0 - self.h.beta2)
+                # TF ApplyAdam update form (same as the HIP kernel)
+                m.add_((gg - m) * (1.0 - self.h.beta1))
+                v.add_((gg * gg - v) * (1.0 - self.h.beta2))
                 w.sub_(lr_t * m / (v.sqrt() + self.h.eps))
         elif self.optimizer == "momentum":
             if w.is_cuda:

@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Per-op timing of the HIP engine's GEMM ops and split-K sweep (run on the GPU box).
+
+usage: python scripts/op_bench.py [--batch 100] [--iters 50] [--splits 1,2,4,8,16]
+Prints one line per (op, split): mean us per launch (device events), plus the step total.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+OPS = ["conv1_fwd", "conv2_fwd", "conv3_fwd", "conv4_fwd", "fc1_fwd", "fc2_fwd",
+       "fc2_dgrad", "fc2_wgrad", "fc1_dgrad", "fc1_wgrad", "conv4_dgrad", "conv4_wgrad",
+       "conv3_dgrad", "conv3_wgrad", "conv2_dgrad", "conv2_wgrad", "conv1_wgrad"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=100)
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--splits", default="1,2,4,8,16,32")
+    ap.add_argument("--cfgs", default="0,1,2,3")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    from ddl_amd.models.layout import CANON_OFFSETS, TOTAL_NUMEL
+    from ddl_amd.models.mnist_cnn import init_params_
+    from ddl_amd.models.hip_engine import HipEngine
+    dev = torch.device("cuda")
+    params = torch.zeros(TOTAL_NUMEL, device=dev)
+    init_params_(params, CANON_OFFSETS, 0)
+    grads = torch.zeros_like(params)
+    B = a.batch
+    eng = HipEngine(params, grads, CANON_OFFSETS, batch=B, graph=False, eval_chunk=B)
+    x = torch.rand(B, 784, device=dev)
+    y = torch.randint(0, 10, (B,), device=dev)
+    seed = torch.tensor([7], dtype=torch.int32, device=dev)
+    base = eng.get_splits()
+    eng.forward_backward(x, y, 0.5, 7)
+    torch.cuda.synchronize()
+
+    def time_op(op, iters):
+        for _ in range(3):
+            eng.eng.run_op(op, x, seed, True)
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        for _ in range(iters):
+            eng.eng.run_op(op, x, seed, True)
+        en.record()
+        torch.cuda.synchronize()
+        return 1e3 * st.elapsed_time(en) / iters
+
+    res = {}
+    sweep = [int(s) for s in a.splits.split(",")]
+    cfgs = [int(c) for c in a.cfgs.split(",")]
+    base_cfg = eng.get_cfg()
+    best_cfg, best_split = list(base_cfg), list(base)
+    for op, name in enumerate(OPS):
+        M, N, K = eng.eng.op_shape(op, B)
+        flop = 2.0 * M * N * K
+        row = {}
+        for c in cfgs:
+            for s in sweep:
+                cf = list(base_cfg)
+                cf[op] = c
+                sp = list(base)
+                sp[op] = s
+                eng.set_splits(sp)
+                eng.set_cfg(cf)
+                row[(c, s)] = time_op(op, a.iters)
+        eng.set_splits(base)
+        eng.set_cfg(base_cfg)
+        best = min(row, key=row.get)
+        best_cfg[op], best_split[op] = best
+        res[name] = {"M": M, "N": N, "K": K, "us": {f"c{c}s{s}": v for (c, s), v in row.items()},
+                     "best": f"c{best[0]}s{best[1]}", "best_us": row[best],
+                     "default_us": row.get((base_cfg[op], base[op])),
+                     "best_tflops": flop / row[best] / 1e6}
+        print(f"{name:12s} M={M:6d} N={N:5d} K={K:6d} default c{base_cfg[op]}s{base[op]}="
+              f"{row.get((base_cfg[op], base[op]), float('nan')):7.1f}  best c{best[0]}s{best[1]}="
+              f"{row[best]:7.1f} us {flop / row[best] / 1e6:6.1f} TF", flush=True)
+        for c in cfgs:
+            print("      c%d " % c + " ".join(f"s{s}:{row[(c, s)]:7.1f}" for s in sweep), flush=True)
+    print("BEST_CFG", ",".join(map(str, best_cfg)))
+    print("BEST_SPLITS", ",".join(map(str, best_split)))
+    eng.set_cfg(best_cfg)
+    eng.set_splits(best_split)
+    # whole step eager vs graph
+    for g in (False, True):
+        e2 = HipEngine(params, grads, CANON_OFFSETS, batch=B, graph=g, eval_chunk=B)
+        e2.set_cfg(best_cfg)
+        e2.set_splits(best_split)
+        for _ in range(5):
+            e2.forward_backward(x, y, 0.5, 7)
+        torch.cuda.synchronize()
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        for _ in range(a.iters):
+            e2.forward_backward(x, y, 0.5, 7)
+        en.record()
+        torch.cuda.synchronize()
+        print(f"fwd+bwd step graph={g}: {1e3 * st.elapsed_time(en) / a.iters:.1f} us", flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
