@@ -24,7 +24,7 @@ import time
 METRIC = "images/sec (whole node) + time-to-target-acc, MNIST CNN sync-sharding at 1/2/4/8 MI355X"
 # Faithful reference-semantics baseline measured on MI355X with stock PyTorch-ROCm ops
 # (``bench.py --engine torch``), per GPU; see BASELINE.md.  None until measured.
-BASELINE_IMG_PER_S_PER_GPU = None
+BASELINE_IMG_PER_S_PER_GPU = 51308.5  # measured round 1, BASELINE.md
 
 
 def main(argv=None):

@@ -28,8 +28,10 @@ from ..ops.adam import AdamHyper, adam_coeffs
 class ParameterServer:
     def __init__(self, plan: ShardPlan, ps_id: int, device, hyper: Optional[AdamHyper] = None,
                  optimizer: str = "adam", momentum: float = 0.9,
-                 own_params: Optional[torch.Tensor] = None):
+                 own_params: Optional[torch.Tensor] = None, native_optim: bool = True):
         self.plan, self.id, self.device = plan, ps_id, torch.device(device)
+        # False only for the stock-PyTorch baseline engine (bench.py --engine torch)
+        self.native_optim = native_optim
         self.h = hyper or AdamHyper()
         self.optimizer, self.momentum = optimizer, momentum
         self.segments: List[Tuple[int, int]] = plan.ps_segments(ps_id)
@@ -81,7 +83,7 @@ class ParameterServer:
         if self.optimizer == "adam":
             v = self.v[state_off:state_off + n]
             lr_t = adam_coeffs(self.h, self.t)
-            if w.is_cuda:
+            if w.is_cuda and self.native_optim:
                 native.ops().adam_flat(w, g, m, v, lr_t, self.h.beta1, self.h.beta2, self.h.eps,
                                        grad_scale)
             else:
@@ -91,7 +93,7 @@ class ParameterServer:
                 v.add_((gg * gg - v) * (1.0 - self.h.beta2))
                 w.sub_(lr_t * m / (v.sqrt() + self.h.eps))
         elif self.optimizer == "momentum":
-            if w.is_cuda:
+            if w.is_cuda and self.native_optim:
                 native.ops().momentum_flat(w, g, m, self.h.lr, self.momentum, grad_scale)
             else:
                 m.mul_(self.momentum).add_(g, alpha=grad_scale)

@@ -79,7 +79,8 @@ class Trainer:
                     init_params_(tmp, self.plan.tensor_offsets, cfg.seed + 10007 + p)
                     own = tmp
             self.servers[p] = ParameterServer(self.plan, p, dev, hyper, cfg.optimizer,
-                                              cfg.momentum, own_params=own)
+                                              cfg.momentum, own_params=own,
+                                              native_optim=self.engine.name != "torch")
         self.data = dataset if dataset is not None else get_dataset(cfg.data, seed=1234)
         self.data = self.data.to(dev)
         self.steps = cfg.steps or (self.data.total_batch // cfg.batch_size)
