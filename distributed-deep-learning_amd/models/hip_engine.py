@@ -99,7 +99,8 @@ class HipEngine:
         with torch.cuda.stream(side):
             for s in range(len(self.segments)):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=side):
+                # thread_local: RCCL's watchdog thread keeps polling events while we capture
+                with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
                     if s == 0:
                         self.eng.forward(self.x_static, self.seed_static, True)
                     self.eng.backward_segment(s, self.x_static, self.y_static, self.seed_static)

@@ -170,8 +170,7 @@ class SyncExchange:
                     continue
                 runs: List[Tuple[int, int]] = []
                 for i in sorted(ids, key=lambda i: plan.tensor_offsets[i]):
-                    lo = plan.tensor_offsets[i]
-                    hi = lo + [t for t in tensor_of_elem if t[2] == i][0][1] - lo
+                    lo, hi = plan.tensor_extent(i)  # includes alignment padding
                     if runs and runs[-1][1] == lo:
                         runs[-1] = (runs[-1][0], hi)
                     else:

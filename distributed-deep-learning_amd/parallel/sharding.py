@@ -30,6 +30,7 @@ from ..models.layout import TENSORS, NUM_TENSORS
 
 POLICIES = ("none", "contiguous", "greedy", "lpt", "flat")
 FLAT_ALIGN = 64  # elements (256 B): keeps every shard 16-B aligned for dwordx4 access
+TENSOR_ALIGN = 64  # elements: every tensor's offset in a plan buffer
 
 
 def greedy_order(numels: Sequence[int]) -> List[int]:
@@ -105,7 +106,18 @@ class ShardPlan:
         return sum(hi - lo for lo, hi in self.ps_segments(p))
 
     def shard_bytes(self) -> List[int]:
+        """Payload bytes per PS (alignment padding excluded for tensor-granular plans)."""
+        if self.owner is not None:
+            out = [0] * self.num_ps
+            for t in TENSORS:
+                out[self.owner[t.index]] += t.nbytes
+            return out
         return [4 * self.shard_numel(p) for p in range(self.num_ps)]
+
+    def tensor_extent(self, i: int) -> Tuple[int, int]:
+        """[lo, hi) of tensor i in the plan buffer including its alignment padding."""
+        o = self.tensor_offsets[i]
+        return o, o + padded(TENSORS[i].numel)
 
     def imbalance(self) -> float:
         """max/mean shard bytes (1.0 = perfectly balanced), SURVEY.md §2.8."""
@@ -132,6 +144,13 @@ class ShardPlan:
                 ",".join(f"{m:.2f}" for m in mib) + f" max/mean={self.imbalance():.2f}")
 
 
+def padded(numel: int) -> int:
+    """Tensor extent in the plan buffer: every tensor starts TENSOR_ALIGN-aligned (256 B), so
+    the GEMM operand loads and the Adam kernel's 16-B vector path see aligned views, and the
+    extents of consecutive tensors stay adjacent (one collective per run of tensors)."""
+    return -(-numel // TENSOR_ALIGN) * TENSOR_ALIGN
+
+
 def _tensor_granular(policy: str, order: List[int], owner: List[int], num_ps: int) -> ShardPlan:
     # owner must be non-decreasing along `order` so each PS's tensors are contiguous.
     numel = [t.numel for t in TENSORS]
@@ -144,7 +163,7 @@ def _tensor_granular(policy: str, order: List[int], owner: List[int], num_ps: in
         for i in order:
             if owner[i] == p:
                 offsets[i] = pos
-                pos += numel[i]
+                pos += padded(numel[i])
                 seq.append(i)
         ranges.append((lo, pos))
     return ShardPlan(policy, num_ps, seq, offsets, ranges, pos, owner=list(owner))
@@ -201,7 +220,7 @@ def make_plan(policy: str, num_ps: int,
         lo = pos
         for i in sorted(b):
             offsets[i] = pos
-            pos += numel[i]
+            pos += padded(numel[i])
         pos = lo + -(-(pos - lo) // unit) * unit
         branges.append((lo, pos))
     plan = ShardPlan("flat", num_ps, list(range(NUM_TENSORS)), offsets, [], pos,

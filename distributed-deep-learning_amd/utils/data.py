@@ -54,7 +54,10 @@ class Dataset:
 
 
 def synthetic_mnist(n_train: int = TRAIN_SIZE, n_test: int = TEST_SIZE,
-                    seed: int = 1234, noise: float = 0.35) -> Dataset:
+                    seed: int = 1234, noise: float = 0.45, mix: float = 0.25) -> Dataset:
+    """Difficulty tuned so the reference recipe (Adam 1e-4, batch 100) learns it on an
+    MNIST-like curve: ~0.5 accuracy after 50 steps, ~0.97 after 200 (gaussian pixel
+    noise ``noise``, distractor-class blend ``mix``, +-3 px shifts)."""
     g = torch.Generator().manual_seed(seed)
     # Smooth prototypes: low-res random field upsampled, thresholded into strokes.
     low = torch.rand(NUM_CLASSES, 1, 7, 7, generator=g)
@@ -62,19 +65,23 @@ def synthetic_mnist(n_train: int = TRAIN_SIZE, n_test: int = TEST_SIZE,
     proto = (proto - proto.mean(dim=(2, 3), keepdim=True)) * 3.0
     proto = proto.clamp(0.0, 1.0)  # [10,1,28,28]
 
+    shift = 3
+
     def make(n: int) -> Tuple[torch.Tensor, torch.Tensor]:
         y = torch.randint(0, NUM_CLASSES, (n,), generator=g)
-        img = proto[y]  # [n,1,28,28]
-        # random translation by up to +-2 px via roll (cheap, deterministic)
-        sx = torch.randint(-2, 3, (n,), generator=g)
-        sy = torch.randint(-2, 3, (n,), generator=g)
+        other = torch.randint(0, NUM_CLASSES, (n,), generator=g)
+        # own class prototype blended with a random distractor class
+        img = proto[y, 0] * (1.0 - mix) + proto[other, 0] * mix  # [n,28,28]
+        # random translation by up to +-3 px via roll (cheap, deterministic)
+        sx = torch.randint(-shift, shift + 1, (n,), generator=g)
+        sy = torch.randint(-shift, shift + 1, (n,), generator=g)
         out = torch.empty(n, IMAGE, IMAGE)
-        for dx in range(-2, 3):
-            for dy in range(-2, 3):
+        for dx in range(-shift, shift + 1):
+            for dy in range(-shift, shift + 1):
                 sel = (sx == dx) & (sy == dy)
                 if sel.any():
-                    out[sel] = torch.roll(img[sel, 0], shifts=(dy, dx), dims=(1, 2))
-        out = out + noise * torch.rand(n, IMAGE, IMAGE, generator=g)
+                    out[sel] = torch.roll(img[sel], shifts=(dy, dx), dims=(1, 2))
+        out = out + noise * torch.randn(n, IMAGE, IMAGE, generator=g)
         return out.clamp(0.0, 1.0).reshape(n, INPUT_DIM).contiguous(), y
 
     xtr, ytr = make(n_train)

@@ -45,7 +45,9 @@ def test_sync_matches_single_process_simulation(tmp_path, world, kw):
     ref = simulate_sync(cfg, world)
     for r, rec in enumerate(recs):
         got = _canon(rec)
-        assert torch.allclose(got, ref, atol=2e-6, rtol=0), (r, float((got - ref).abs().max()))
+        # fp32 sums of W gradients in a different order; Adam can move a ~0 gradient by
+        # up to lr per step, so allow 2e-5 (lr * steps = 3e-4)
+        assert torch.allclose(got, ref, atol=2e-5, rtol=0), (r, float((got - ref).abs().max()))
     # every worker ends with identical parameters
     for rec in recs[1:]:
         assert torch.equal(_canon(rec), _canon(recs[0]))
