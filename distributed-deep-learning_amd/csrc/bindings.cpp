@@ -194,6 +194,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("w"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr_t"), py::arg("b1"),
         py::arg("b2"), py::arg("eps"), py::arg("scale") = 1.0);
   m.def("momentum_flat", &momentum_flat, "Fused momentum SGD on a flat shard");
+  m.def("mfma_peak", [](at::Tensor out, int64_t blocks, int64_t iters) {
+    check_f32_cuda(out, "out");
+    TORCH_CHECK(out.numel() >= blocks * 64, "out too small");
+    ddl::launch_mfma_peak(out.data_ptr<float>(), (int)blocks, (int)iters, cur_stream());
+  }, "diagnostic: 2 chains of v_mfma_f32_32x32x2_f32 per wave (2*iters MFMAs)");
+  m.def("gemm_nomem", [](at::Tensor out, at::Tensor slab, int64_t M, int64_t N, int64_t K,
+                         int64_t splits) {
+    ddl::launch_gemm_nomem(out.data_ptr<float>(), (int)M, (int)N, (int)K, (int)splits,
+                           slab.data_ptr(), nullptr, cur_stream());
+  }, "diagnostic: engine GEMM structure with register-only operand loads");
   m.attr("OP_COUNT") = (int)ddl::OP_COUNT;
 
   py::class_<PyEngine>(m, "Engine")

@@ -21,6 +21,11 @@ void launch_head_bwd(const float* h2, const float* w, const float* dlog, int B,
                      const uint32_t* seed, uint32_t thr24, float inv_keep, float* gw, float* gb,
                      float* dpre2, hipStream_t st);
 
+// ---- diagnostics (diag.hip) -------------------------------------------------------------------
+void launch_mfma_peak(float* out, int blocks, int iters, hipStream_t st);
+void launch_gemm_nomem(float* out, int M, int N, int K, int splits, void* slab, int* tickets,
+                       hipStream_t st);
+
 // ---- the CNN step engine (engine.hip) --------------------------------------------------------
 // GEMM-shaped ops, in SURVEY.md §2.6 order.  Index into Engine::splits / Engine::cfg.
 enum Op {
@@ -33,8 +38,8 @@ enum Op {
 
 // Block-tile configurations selectable per op at run time (gemm.h template args
 // <BM, BN, BK=32, WM, WN>): 0 = 64x64 (1 wave 64x64), 1 = 128x64 (2 waves 64x64),
-// 2 = 64x32 (1 wave), 3 = 32x32 (1 wave).
-constexpr int NUM_TILE_CFGS = 4;
+// 2 = 64x32 (1 wave), 3 = 32x32 (1 wave), 4 = 32x64 (1 wave).
+constexpr int NUM_TILE_CFGS = 5;
 
 struct Engine {
   const float* P[14] = {};   // parameter tensors v0..v13 (any flat layout)

@@ -64,13 +64,15 @@ void Engine::op_shape(int op, int B, int* M, int* N, int* K) {
 #define TILE_1 128, 64, 32, 2, 1
 #define TILE_2 64, 32, 32, 1, 1
 #define TILE_3 32, 32, 32, 1, 1
+#define TILE_4 32, 64, 32, 1, 1
 
 static size_t slab_need(int c, int M, int N, int K, int s) {
   switch (c) {
     case 0: return splitk_slab_f4<TILE_0>(M, N, K, s);
     case 1: return splitk_slab_f4<TILE_1>(M, N, K, s);
     case 2: return splitk_slab_f4<TILE_2>(M, N, K, s);
-    default: return splitk_slab_f4<TILE_3>(M, N, K, s);
+    case 3: return splitk_slab_f4<TILE_3>(M, N, K, s);
+    default: return splitk_slab_f4<TILE_4>(M, N, K, s);
   }
 }
 
@@ -81,7 +83,8 @@ static void launch_cfg(int c, const P& p, int s, int wide_thr, const SplitScratc
     case 0: launch_gemm<TILE_0>(p, s, wide_thr, sc, st); break;
     case 1: launch_gemm<TILE_1>(p, s, wide_thr, sc, st); break;
     case 2: launch_gemm<TILE_2>(p, s, wide_thr, sc, st); break;
-    default: launch_gemm<TILE_3>(p, s, wide_thr, sc, st); break;
+    case 3: launch_gemm<TILE_3>(p, s, wide_thr, sc, st); break;
+    default: launch_gemm<TILE_4>(p, s, wide_thr, sc, st); break;
   }
 }
 
