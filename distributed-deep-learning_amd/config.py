@@ -34,7 +34,7 @@ class TrainConfig:
     ref_quirks: bool = False        # reproduce SURVEY.md §2.10 Q1/Q2/Q4
     seed: int = 0
     engine: str = "auto"            # auto | hip | torch
-    graph: bool = True              # capture the compute step in a HIP graph
+    graph: bool = False             # replay the compute step as HIP graphs (eager is faster)
     overlap: bool = True            # bucketed grad push overlapped with backward
     log_jsonl: Optional[str] = None
     checkpoint_dir: Optional[str] = None
@@ -72,7 +72,8 @@ def add_args(p: argparse.ArgumentParser, mode_default: str = "sync") -> argparse
     p.add_argument("--ref-quirks", action="store_true")
     p.add_argument("--seed", type=int, default=d.seed)
     p.add_argument("--engine", default=d.engine, choices=["auto", "hip", "torch"])
-    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--graph", action="store_true", help="replay the engine step as HIP graphs")
+    p.add_argument("--no-graph", action="store_true", help="(default)")
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--log-jsonl", default=None)
     p.add_argument("--checkpoint-dir", default=None)
@@ -93,6 +94,6 @@ def from_args(a: argparse.Namespace) -> TrainConfig:
         steps=a.steps, lr=a.lr, optimizer=a.optimizer, keep_prob=a.keep_prob,
         eval_every=a.eval_every, data=a.data, data_sharding=a.data_sharding,
         grad_reduce=a.grad_reduce, ref_quirks=a.ref_quirks, seed=a.seed, engine=a.engine,
-        graph=not a.no_graph, overlap=not a.no_overlap, log_jsonl=a.log_jsonl,
+        graph=a.graph and not a.no_graph, overlap=not a.no_overlap, log_jsonl=a.log_jsonl,
         checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
         resume=a.resume, target_acc=a.target_acc, quiet=a.quiet, watchdog_s=a.watchdog_s)

@@ -98,6 +98,18 @@ class PyEngine {
   std::vector<int64_t> get_splits() const {
     return std::vector<int64_t>(e_.splits, e_.splits + ddl::OP_COUNT);
   }
+  // stream-K worker counts per op (0 = split-K by `splits`)
+  void set_workers(std::vector<int64_t> w) {
+    TORCH_CHECK((int)w.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " worker counts");
+    for (int i = 0; i < ddl::OP_COUNT; ++i) {
+      TORCH_CHECK(w[i] >= 0 && w[i] <= (1 << 20), "worker count out of range");
+      e_.workers[i] = (int)w[i];
+    }
+    realloc();
+  }
+  std::vector<int64_t> get_workers() const {
+    return std::vector<int64_t>(e_.workers, e_.workers + ddl::OP_COUNT);
+  }
 
   void forward(at::Tensor x, at::Tensor seed, bool train) {
     check_x(x);
@@ -213,6 +225,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_keep_prob", &PyEngine::set_keep_prob)
       .def("set_splits", &PyEngine::set_splits)
       .def("get_splits", &PyEngine::get_splits)
+      .def("set_workers", &PyEngine::set_workers)
+      .def("get_workers", &PyEngine::get_workers)
       .def("set_cfg", &PyEngine::set_cfg)
       .def("get_cfg", &PyEngine::get_cfg)
       .def("set_concurrent", &PyEngine::set_concurrent)

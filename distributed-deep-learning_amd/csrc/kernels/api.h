@@ -48,6 +48,7 @@ struct Engine {
   int train_batch = 0;       // slab sized for this batch with the current splits/cfgs
   int splits[OP_COUNT];
   int cfg[OP_COUNT];
+  int workers[OP_COUNT];     // > 0: stream-K with this many workers (overrides splits)
   int wide_thr = 1;          // split count above which the separate wide reduce is used
   uint32_t thr24 = 0;        // dropout threshold (train)
   float inv_keep = 1.f;

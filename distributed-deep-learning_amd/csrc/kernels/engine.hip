@@ -15,11 +15,14 @@
 namespace ddl {
 
 Engine::Engine() {
-  // {tile config, split-K} per op — defaults from the op_bench sweep (scripts/op_bench.py)
-  static const int defc[OP_COUNT] = {3, 3, 3, 2, 3, 3, 3, 3, 3, 3, 2, 3, 3, 3, 3, 3, 3};
-  static const int defs[OP_COUNT] = {8, 4, 3, 16, 8, 16, 4, 1, 4, 1, 32, 4, 3, 32, 4, 64, 256};
+  // {tile config, split-K, stream-K workers} per op: whole-step coordinate-descent tune
+  // (scripts/step_tune.py over the scripts/op_bench.py per-op sweep) on one MI355X, batch 100
+  static const int defc[OP_COUNT] = {3, 3, 3, 3, 3, 2, 3, 3, 3, 3, 3, 2, 3, 3, 3, 4, 3};
+  static const int defs[OP_COUNT] = {8, 1, 3, 1, 8, 16, 4, 1, 4, 1, 16, 1, 1, 32, 4, 64, 1024};
+  static const int defw[OP_COUNT] = {0, 3072, 0, 3072, 0, 0, 0, 0, 0, 0, 0, 2048, 2048, 0, 0, 0, 0};
   memcpy(cfg, defc, sizeof(defc));
   memcpy(splits, defs, sizeof(defs));
+  memcpy(workers, defw, sizeof(defw));
 }
 
 Engine::~Engine() {
@@ -66,25 +69,25 @@ void Engine::op_shape(int op, int B, int* M, int* N, int* K) {
 #define TILE_3 32, 32, 32, 1, 1
 #define TILE_4 32, 64, 32, 1, 1
 
-static size_t slab_need(int c, int M, int N, int K, int s) {
+static size_t slab_need(int c, int M, int N, int K, int s, int w) {
   switch (c) {
-    case 0: return splitk_slab_f4<TILE_0>(M, N, K, s);
-    case 1: return splitk_slab_f4<TILE_1>(M, N, K, s);
-    case 2: return splitk_slab_f4<TILE_2>(M, N, K, s);
-    case 3: return splitk_slab_f4<TILE_3>(M, N, K, s);
-    default: return splitk_slab_f4<TILE_4>(M, N, K, s);
+    case 0: return gemm_slab_f4<TILE_0>(M, N, K, s, w);
+    case 1: return gemm_slab_f4<TILE_1>(M, N, K, s, w);
+    case 2: return gemm_slab_f4<TILE_2>(M, N, K, s, w);
+    case 3: return gemm_slab_f4<TILE_3>(M, N, K, s, w);
+    default: return gemm_slab_f4<TILE_4>(M, N, K, s, w);
   }
 }
 
 template <class P>
-static void launch_cfg(int c, const P& p, int s, int wide_thr, const SplitScratch& sc,
+static void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const SplitScratch& sc,
                        hipStream_t st) {
   switch (c) {
-    case 0: launch_gemm<TILE_0>(p, s, wide_thr, sc, st); break;
-    case 1: launch_gemm<TILE_1>(p, s, wide_thr, sc, st); break;
-    case 2: launch_gemm<TILE_2>(p, s, wide_thr, sc, st); break;
-    case 3: launch_gemm<TILE_3>(p, s, wide_thr, sc, st); break;
-    default: launch_gemm<TILE_4>(p, s, wide_thr, sc, st); break;
+    case 0: launch_gemm<TILE_0>(p, s, wide_thr, sc, st, w); break;
+    case 1: launch_gemm<TILE_1>(p, s, wide_thr, sc, st, w); break;
+    case 2: launch_gemm<TILE_2>(p, s, wide_thr, sc, st, w); break;
+    case 3: launch_gemm<TILE_3>(p, s, wide_thr, sc, st, w); break;
+    default: launch_gemm<TILE_4>(p, s, wide_thr, sc, st, w); break;
   }
 }
 
@@ -93,7 +96,7 @@ size_t Engine::slab_floats_needed(int B) const {
   for (int op = 0; op < OP_COUNT; ++op) {
     int M, N, K;
     op_shape(op, B, &M, &N, &K);
-    const size_t f = 4 * slab_need(cfg[op], M, N, K, splits[op]);
+    const size_t f = 4 * slab_need(cfg[op], M, N, K, splits[op], workers[op]);
     if (f > mx) mx = f;
   }
   return mx;
@@ -141,77 +144,78 @@ void Engine::run_op(int op, const float* x, int B, const uint32_t* seed, bool tr
   int M, N, K;
   op_shape(op, B, &M, &N, &K);
   const int s = train ? splits[op] : 1;
+  const int w = train ? workers[op] : 0;
   const int c = cfg[op];
   const uint32_t thr = train ? thr24 : 0u;
   const SplitScratch& sc = scratch[si];
   switch (op) {
     case OP_CONV1_FWD: {
       ConvFwd<28, 1, 32> p{M, N, K, x, P[0], P[1], p1, c1};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_CONV2_FWD: {
       ConvFwd<14, 32, 64> p{M, N, K, p1, P[2], P[3], p2, c2};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_CONV3_FWD: {
       ConvFwd<7, 64, 128> p{M, N, K, p2, P[4], P[5], p3, c3};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_CONV4_FWD: {
       ConvFwd<4, 128, 256> p{M, N, K, p3, P[6], P[7], p4, c4};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_FC1_FWD: {
       FcFwd<true> p{M, N, K, p4, P[8], P[9], h1, seed, 1u, thr, inv_keep};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_FC2_FWD: {
       FcFwd<false> p{M, N, K, h1, P[10], P[11], h2, seed, 2u, thr, inv_keep};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_FC2_DGRAD: {
       FcDgradAct p{{M, N, K, dpre2fc, P[10]}, h1, inv_keep, dpre1fc};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_FC2_WGRAD: {
       FcWgrad p{M, N, K, 1024, h1, dpre2fc, G[10], G[11]};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_FC1_DGRAD: {
       FcDgradPool<2, 256> p{{M, N, K, dpre1fc, P[8]}, c4, d4};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_FC1_WGRAD: {
       FcWgrad p{M, N, K, 1024, p4, dpre1fc, G[8], G[9]};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_CONV4_DGRAD: {
       ConvDgrad<4, 128, 256, 7> p{M, N, K, d4, P[6], c3, d3};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_CONV4_WGRAD: {
       ConvWgrad<4, 128, 256> p{M, N, K, p3, d4, G[6], G[7]};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_CONV3_DGRAD: {
       ConvDgrad<7, 64, 128, 14> p{M, N, K, d3, P[4], c2, d2};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_CONV3_WGRAD: {
       ConvWgrad<7, 64, 128> p{M, N, K, p2, d3, G[4], G[5]};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_CONV2_DGRAD: {
       ConvDgrad<14, 32, 64, 28> p{M, N, K, d2, P[2], c1, d1};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_CONV2_WGRAD: {
       ConvWgrad<14, 32, 64> p{M, N, K, p1, d2, G[2], G[3]};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     case OP_CONV1_WGRAD: {
       ConvWgrad<28, 1, 32> p{M, N, K, x, d1, G[0], G[1]};
-      launch_cfg(c, p, s, wide_thr, sc, st);
+      launch_cfg(c, p, s, w, wide_thr, sc, st);
     } break;
     default: break;
   }

@@ -12,12 +12,12 @@
 //     layout gives each lane 4 groups of 4 consecutive rows of one column; with M
 //     enumerated pool-window-major each group is exactly one 2x2 pool window.
 //
-// Math: v_mfma_f32_32x32x2_f32 (exact fp32; gfx950 has no xf32; 64-cycle issue and
-// dependent latency, so one accumulator chain per fragment runs at the full rate).
+// Math: v_mfma_f32_32x32x2_f32 (exact fp32; gfx950 has no xf32), 64-cycle issue; a wave
+// with a single fragment alternates two accumulator chains.
 // Tiling: BM x BN block tile, BK-deep K step, WM x WN waves (wave64), wave tile
-// (BM/WM) x (BN/WN) of 32x32 fragments.  LDS double buffer + register prefetch of the next
-// K tile (one barrier per K step); the LDS fragment reads of K sub-step r+1 are issued
-// before the MFMAs of sub-step r.  LDS operand images follow global contiguity so the
+// (BM/WM) x (BN/WN) of 32x32 fragments.  One-wave blocks use a single LDS buffer (no
+// barriers), multi-wave blocks a double buffer; global loads run two K tiles ahead in
+// registers; a whole K tile's fragments are read from LDS in one burst before its MFMAs.  LDS operand images follow global contiguity so the
 // global->LDS copy is a straight float4 store:
 //   K-contiguous operand -> [mn][BK+4]   one ds_read_b128 per 4 MFMAs: lane half
 //                                        h = l>>5 owns k = 8r+4h .. 8r+4h+3 of every
@@ -27,11 +27,14 @@
 //   MN-contiguous operand -> [BK][mn+4]  ds_read_b32; the two 32-lane halves read rows
 //                                        4 apart (separate conflict groups)
 //
+// Two drivers share the per-tile main loop / epilogue (GemmTile):
+// Stream-K (gemm_streamk_kernel): W one-block workers split the (tile, K-tile) iteration
+//   space evenly; partial boundary tiles are reduced in-launch by their last contributor.
 // Split-K (gridDim.z = S > 1), deterministic, no float atomics:
-//   mode 1: every split stores its fp32 partial fragments (float4 per lane, coalesced)
-//     and takes an arrival ticket; the last arriver of a tile sums the S partials in z
-//     order and runs the fused epilogue (MI355X guide §5, in-launch split-K reduction:
-//     agent-scope release before the ticket, acquire in the reducer).
+//   mode 1: every split stores its fp32 partial fragments (float4 per lane, coalesced,
+//     write-through sc1) and takes an arrival ticket; the last arriver of a tile sums the S
+//     partials in z order with sc1 loads and runs the fused epilogue (MI355X guide §5 /
+//     §6 G16 in-launch reduction, sc1 form: no release or acquire fence).
 //   mode 2: partials only; splitk_wide_reduce sums them with RL lanes per output element
 //     and runs the epilogue.
 #pragma once
@@ -56,166 +59,204 @@ struct TileGeo {
   static constexpr int PART4 = NW * FRAGS * 4 * 64;
 };
 
+// ---- per-tile building blocks shared by the split-K and stream-K drivers ---------------------
 template <int BM, int BN, int BK, int WM, int WN, class P>
-__global__ void __launch_bounds__(WM * WN * 64)
-gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets) {
+struct GemmTile {
   using G = TileGeo<BM, BN, WM, WN>;
-  constexpr int NT = WM * WN * 64;
-  constexpr bool AK = P::A_KCONTIG;
-  constexpr bool BKC = P::B_KCONTIG;
-  constexpr int SA = AK ? (BK + 4) : (BM + 4);
-  constexpr int A_ELEMS = AK ? BM * SA : BK * SA;
-  constexpr int SB = BKC ? (BK + 4) : (BN + 4);
-  constexpr int B_ELEMS = BKC ? BN * SB : BK * SB;
-  constexpr int WTM = G::WTM, WTN = G::WTN, TM = G::TM, TN = G::TN;
-  constexpr int FA = (BM * BK / 4) / NT;
-  constexpr int FB = (BN * BK / 4) / NT;
-  constexpr int R = BK / 8;
+  static constexpr int NT = WM * WN * 64;
+  static constexpr bool AK = P::A_KCONTIG;
+  static constexpr bool BKC = P::B_KCONTIG;
+  static constexpr int SA = AK ? (BK + 4) : (BM + 4);
+  static constexpr int A_ELEMS = AK ? BM * SA : BK * SA;
+  static constexpr int SB = BKC ? (BK + 4) : (BN + 4);
+  static constexpr int B_ELEMS = BKC ? BN * SB : BK * SB;
+  static constexpr int WTM = G::WTM, WTN = G::WTN, TM = G::TM, TN = G::TN;
+  static constexpr int FA = (BM * BK / 4) / NT;
+  static constexpr int FB = (BN * BK / 4) / NT;
+  static constexpr int R = BK / 8;
   static_assert(FA >= 1 && FA * NT == BM * BK / 4, "A tile must split evenly over threads");
   static_assert(FB >= 1 && FB * NT == BN * BK / 4, "B tile must split evenly over threads");
   static_assert(TM * 32 == WTM && TN * 32 == WTN, "wave tile must be 32-multiples");
   static_assert(BK % 8 == 0, "BK must be a multiple of 8");
-
   // One-wave blocks need neither a second LDS buffer nor barriers: a wave's LDS ops execute
   // in order, so the next tile's ds_writes cannot overtake this tile's ds_reads.  Halving
   // the LDS footprint doubles the resident waves per CU (LDS was the occupancy limit).
-  constexpr bool SOLO = (NT == 64);
-  constexpr int NBUF = SOLO ? 1 : 2;
-  __shared__ float4 lds4[(NBUF * (A_ELEMS + B_ELEMS)) / 4];
-  float* const As0 = reinterpret_cast<float*>(lds4);
-  float* const Bs0 = As0 + NBUF * A_ELEMS;
+  static constexpr bool SOLO = (NT == 64);
+  static constexpr int NBUF = SOLO ? 1 : 2;
+  static constexpr int LDS_F4 = (NBUF * (A_ELEMS + B_ELEMS)) / 4;
+  // A wave with a single 32x32 fragment alternates two accumulator chains (summed at the
+  // end) so consecutive MFMAs are independent.
+  static constexpr int NCH = (TM * TN == 1) ? 2 : 1;
+  static constexpr int WPART = TM * TN * 4 * 64;  // float4 of one wave's partial fragments
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int m_blk = blockIdx.x * BM;
-  const int n_blk = blockIdx.y * BN;
-  const int kb = blockIdx.z * kchunk;
-  const int ke = min(p.K, kb + kchunk);
-  const int nk = (ke - kb + BK - 1) / BK;
+  // acc = sum over k in [kb, ke) of the (m_blk, n_blk) block tile; kb is a multiple of BK.
+  static DDL_DEV void mainloop(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
+                               f32x16 (&acc)[TM][TN]) {
+    float* const As0 = lds;
+    float* const Bs0 = lds + NBUF * A_ELEMS;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int nk = (ke - kb + BK - 1) / BK;
 
-  // ---- per-thread hoisted gather state ------------------------------------------------------
-  // Loader protocol: prepX(mn, kk) fixes a thread's row/column (group) and its k offset
-  // inside every K tile; loadX(info, k0) gathers at tile base k0 (wave-uniform, a multiple
-  // of BK = 32), so per-tile index math that depends only on k0 runs on the scalar unit.
-  typename P::AInfo ai[FA];
-  typename P::BInfo bi[FB];
-  int a_off[FA], b_off[FB];
+    // Loader protocol: prepX(mn, kk) fixes a thread's row/column (group) and its k offset
+    // inside every K tile; loadX(info, k0) gathers at tile base k0 (wave-uniform, a multiple
+    // of BK = 32), so per-tile index math that depends only on k0 runs on the scalar unit.
+    typename P::AInfo ai[FA];
+    typename P::BInfo bi[FB];
+    int a_off[FA], b_off[FB];
 #pragma unroll
-  for (int it = 0; it < FA; ++it) {
-    const int idx = tid + it * NT;
-    if constexpr (AK) {
-      const int kq = idx % (BK / 4), row = idx / (BK / 4);
-      ai[it] = p.prepA(m_blk + row, kq * 4);
-      a_off[it] = row * SA + kq * 4;
-    } else {
-      const int mq = idx % (BM / 4), kk = idx / (BM / 4);
-      ai[it] = p.prepA(m_blk + mq * 4, kk);
-      a_off[it] = kk * SA + mq * 4;
+    for (int it = 0; it < FA; ++it) {
+      const int idx = tid + it * NT;
+      if constexpr (AK) {
+        const int kq = idx % (BK / 4), row = idx / (BK / 4);
+        ai[it] = p.prepA(m_blk + row, kq * 4);
+        a_off[it] = row * SA + kq * 4;
+      } else {
+        const int mq = idx % (BM / 4), kk = idx / (BM / 4);
+        ai[it] = p.prepA(m_blk + mq * 4, kk);
+        a_off[it] = kk * SA + mq * 4;
+      }
     }
-  }
 #pragma unroll
-  for (int it = 0; it < FB; ++it) {
-    const int idx = tid + it * NT;
-    if constexpr (BKC) {
-      const int kq = idx % (BK / 4), row = idx / (BK / 4);
-      bi[it] = p.prepB(n_blk + row, kq * 4);
-      b_off[it] = row * SB + kq * 4;
-    } else {
-      const int nq = idx % (BN / 4), kk = idx / (BN / 4);
-      bi[it] = p.prepB(n_blk + nq * 4, kk);
-      b_off[it] = kk * SB + nq * 4;
+    for (int it = 0; it < FB; ++it) {
+      const int idx = tid + it * NT;
+      if constexpr (BKC) {
+        const int kq = idx % (BK / 4), row = idx / (BK / 4);
+        bi[it] = p.prepB(n_blk + row, kq * 4);
+        b_off[it] = row * SB + kq * 4;
+      } else {
+        const int nq = idx % (BN / 4), kk = idx / (BN / 4);
+        bi[it] = p.prepB(n_blk + nq * 4, kk);
+        b_off[it] = kk * SB + nq * 4;
+      }
     }
+
+    // Two register-prefetch stages of the global operands: K tile t+1 is stored to LDS
+    // while tile t's fragments are already in VGPRs, and tile t+2 loads during t's MFMAs.
+    float4 ra[FA], rb[FB];
+    auto gload = [&](int k0) {
+#pragma unroll
+      for (int it = 0; it < FA; ++it) ra[it] = p.loadA(ai[it], k0);
+#pragma unroll
+      for (int it = 0; it < FB; ++it) rb[it] = p.loadB(bi[it], k0);
+    };
+    auto sstore = [&](int buf) {
+      float* As = As0 + buf * A_ELEMS;
+      float* Bs = Bs0 + buf * B_ELEMS;
+#pragma unroll
+      for (int it = 0; it < FA; ++it) *reinterpret_cast<float4*>(As + a_off[it]) = ra[it];
+#pragma unroll
+      for (int it = 0; it < FB; ++it) *reinterpret_cast<float4*>(Bs + b_off[it]) = rb[it];
+    };
+
+    f32x16 acc2;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc2[q] = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+    const int lr = lane & 31;   // fragment row / column
+    const int lh = lane >> 5;   // k half
+
+    // fragment fetch of a whole K tile from LDS buffer (As, Bs), issued as one burst so the
+    // LDS latency is paid once per tile
+    float av[R][TM][4], bv[R][TN][4];
+    auto fetch_all = [&](const float* As, const float* Bs) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wm * WTM + i * 32 + lr;
+          if constexpr (AK) {
+            const float4 t = *reinterpret_cast<const float4*>(As + row * SA + r * 8 + 4 * lh);
+            av[r][i][0] = t.x; av[r][i][1] = t.y; av[r][i][2] = t.z; av[r][i][3] = t.w;
+          } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) av[r][i][s] = As[(r * 8 + 4 * lh + s) * SA + row];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = wn * WTN + j * 32 + lr;
+          if constexpr (BKC) {
+            const float4 t = *reinterpret_cast<const float4*>(Bs + col * SB + r * 8 + 4 * lh);
+            bv[r][j][0] = t.x; bv[r][j][1] = t.y; bv[r][j][2] = t.z; bv[r][j][3] = t.w;
+          } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) bv[r][j][s] = Bs[(r * 8 + 4 * lh + s) * SB + col];
+          }
+        }
+      }
+    };
+
+    if (nk > 0) {
+      gload(kb);
+      sstore(0);
+      if (nk > 1) gload(kb + BK);
+    }
+    if constexpr (!SOLO) __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = SOLO ? 0 : (kt & 1);
+      fetch_all(As0 + cur * A_ELEMS, Bs0 + cur * B_ELEMS);
+      // (SOLO) overwriting the buffer just read is safe: a wave's LDS ops run in order;
+      // with two buffers the previous iteration's barrier freed buffer cur^1.
+      if (kt + 1 < nk) sstore(SOLO ? 0 : (cur ^ 1));
+      if (kt + 2 < nk) gload(kb + (kt + 2) * BK);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          if constexpr (NCH == 2) {
+            if (s & 1) acc2 = mfma32x32x2(av[r][0][s], bv[r][0][s], acc2);
+            else acc[0][0] = mfma32x32x2(av[r][0][s], bv[r][0][s], acc[0][0]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+                acc[i][j] = mfma32x32x2(av[r][i][s], bv[r][j][s], acc[i][j]);
+          }
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!SOLO) __syncthreads();
+    }
+    if constexpr (NCH == 2) acc[0][0] += acc2;
   }
 
-  float4 ra[FA], rb[FB];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int it = 0; it < FA; ++it) ra[it] = p.loadA(ai[it], k0);
-#pragma unroll
-    for (int it = 0; it < FB; ++it) rb[it] = p.loadB(bi[it], k0);
-  };
-  auto sstore = [&](int buf) {
-    float* As = As0 + buf * A_ELEMS;
-    float* Bs = Bs0 + buf * B_ELEMS;
-#pragma unroll
-    for (int it = 0; it < FA; ++it) *reinterpret_cast<float4*>(As + a_off[it]) = ra[it];
-#pragma unroll
-    for (int it = 0; it < FB; ++it) *reinterpret_cast<float4*>(Bs + b_off[it]) = rb[it];
-  };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
-
-  const int lr = lane & 31;   // fragment row / column
-  const int lh = lane >> 5;   // k half
-
-  // fragment fetch of K sub-step r from LDS buffer (As, Bs)
-  auto fetch = [&](const float* As, const float* Bs, int r, float (&av)[TM][4], float (&bv)[TN][4]) {
+  // fused epilogue: each lane owns 4 groups of 4 consecutive rows of one column
+  static DDL_DEV void epilogue(const P& p, int m_blk, int n_blk, const f32x16 (&acc)[TM][TN]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int lr = lane & 31, lh = lane >> 5;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int row = wm * WTM + i * 32 + lr;
-      if constexpr (AK) {
-        const float4 t = *reinterpret_cast<const float4*>(As + row * SA + r * 8 + 4 * lh);
-        av[i][0] = t.x; av[i][1] = t.y; av[i][2] = t.z; av[i][3] = t.w;
-      } else {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) av[i][s] = As[(r * 8 + 4 * lh + s) * SA + row];
+      for (int j = 0; j < TN; ++j) {
+        const int n = n_blk + wn * WTN + j * 32 + lr;
+        if (n >= p.N) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int m0 = m_blk + wm * WTM + i * 32 + 8 * g + 4 * lh;
+          if (m0 < p.M) {
+            const f32x16& v = acc[i][j];
+            p.epi(m0, n, f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]});
+          }
+        }
       }
     }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wn * WTN + j * 32 + lr;
-      if constexpr (BKC) {
-        const float4 t = *reinterpret_cast<const float4*>(Bs + col * SB + r * 8 + 4 * lh);
-        bv[j][0] = t.x; bv[j][1] = t.y; bv[j][2] = t.z; bv[j][3] = t.w;
-      } else {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) bv[j][s] = Bs[(r * 8 + 4 * lh + s) * SB + col];
-      }
-    }
-  };
-
-  if (nk > 0) {
-    gload(kb);
-    sstore(0);
-  }
-  if constexpr (!SOLO) __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = SOLO ? 0 : (kt & 1);
-    if (kt + 1 < nk) gload(kb + (kt + 1) * BK);
-    const float* As = As0 + cur * A_ELEMS;
-    const float* Bs = Bs0 + cur * B_ELEMS;
-    float av[2][TM][4], bv[2][TN][4];
-    fetch(As, Bs, 0, av[0], bv[0]);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (r + 1 < R) fetch(As, Bs, r + 1, av[(r + 1) & 1], bv[(r + 1) & 1]);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = mfma32x32x2(av[r & 1][i][s], bv[r & 1][j][s], acc[i][j]);
-    }
-    if (kt + 1 < nk) sstore(SOLO ? 0 : (cur ^ 1));
-    if constexpr (!SOLO) __syncthreads();
   }
 
-  if (mode != 0) {
-    // ---- split-K: publish this split's partial fragments ------------------------------------
-    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-    const int ntiles = gridDim.x * gridDim.y;
-    const int S = gridDim.z;
-    constexpr int WPART = TM * TN * 4 * 64;  // float4 per wave
-    float4* mine = slab + ((size_t)blockIdx.z * ntiles + tile) * G::PART4 + wave * WPART + lane;
+  // partial-fragment image of one block: [wave][frag][g][lane] float4 (coalesced per wave),
+  // at float4 index `base` of the slab.  Written and read write-through (sc1): see arrive().
+  static DDL_DEV void store_partial(brsrc_t slab, size_t base, const f32x16 (&acc)[TM][TN]) {
+    const int mine = (int)base + (threadIdx.x >> 6) * WPART + (threadIdx.x & 63);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -223,66 +264,138 @@ gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __res
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const f32x16& v = acc[i][j];
-          mine[((i * TN + j) * 4 + g) * 64] =
-              make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+          bstore4_sc1(slab, (mine + ((i * TN + j) * 4 + g) * 64) * 16,
+                      make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]));
         }
-    if (mode == 2) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(lds4);
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int prev = __hip_atomic_fetch_add(&tickets[tile], 1, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-      const int last = prev == S - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        tickets[tile] = 0;  // re-arm for the next launch (kernel boundary orders it)
-      }
-      flag[0] = last;
-    }
-    __syncthreads();
-    if (!flag[0]) return;
-    const float4* base = slab + (size_t)tile * G::PART4 + wave * WPART + lane;
-    const size_t zstride = (size_t)ntiles * G::PART4;
+  }
+  static DDL_DEV void add_partial(brsrc_t slab, size_t base, f32x16 (&acc)[TM][TN]) {
+    const int src = (int)base + (threadIdx.x >> 6) * WPART + (threadIdx.x & 63);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 t = bload4_sc1(slab, (src + ((i * TN + j) * 4 + g) * 64) * 16);
+          acc[i][j][4 * g] += t.x; acc[i][j][4 * g + 1] += t.y;
+          acc[i][j][4 * g + 2] += t.z; acc[i][j][4 * g + 3] += t.w;
+        }
+  }
+  static DDL_DEV void zero(f32x16 (&acc)[TM][TN]) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
-    for (int z = 0; z < S; ++z) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const float4 t = base[z * zstride + ((i * TN + j) * 4 + g) * 64];
-            acc[i][j][4 * g] += t.x; acc[i][j][4 * g + 1] += t.y;
-            acc[i][j][4 * g + 2] += t.z; acc[i][j][4 * g + 3] += t.w;
-          }
-    }
   }
 
-  // ---- fused epilogue: each lane owns 4 groups of 4 consecutive rows of one column ----------
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n_blk + wn * WTN + j * 32 + lr;
-      if (n >= p.N) continue;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int m0 = m_blk + wm * WTM + i * 32 + 8 * g + 4 * lh;
-        if (m0 < p.M) {
-          const f32x16& v = acc[i][j];
-          p.epi(m0, n, f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]});
-        }
-      }
+  // In-launch hand-off of partial tiles (MI355X guide §6 Guideline 16, sc1 form): the
+  // partials were stored write-through (sc1), so publishing is just every wave draining its
+  // stores, the block barrier and ONE relaxed agent-scope ticket add — no release fence
+  // (an agent release writes back the XCD's whole L2, which serialised many-worker launches).
+  // The last of `count` arrivers reads every partial with sc1 loads (they bypass this CU's
+  // L1), so it needs no acquire fence; it re-arms the ticket and tells its block via LDS
+  // (the flag lives in the kernel's single __shared__ array: guide §5 trap 4a).
+  static DDL_DEV bool arrive(int* ticket, int count, int* flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int prev = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == count - 1;
+      if (last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
     }
+    __syncthreads();
+    const bool last = *flag != 0;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the slab loads below
+    __syncthreads();  // flag may be rewritten by the next arrive of this block
+    return last;
+  }
+};
+
+// Classic split-K driver: grid (tiles_m, tiles_n, S); split z covers K range
+// [z*kchunk, (z+1)*kchunk).  mode 0: no split; mode 1: in-launch last-arriver reduction of
+// the S partials (in z order, deterministic); mode 2: partials only (splitk_wide_reduce).
+template <int BM, int BN, int BK, int WM, int WN, class P>
+__global__ void __launch_bounds__(WM * WN * 64)
+gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets) {
+  using T = GemmTile<BM, BN, BK, WM, WN, P>;
+  using G = typename T::G;
+  __shared__ float4 lds4[T::LDS_F4 + 1];  // staging images + last-arriver flag
+  int* const flag = reinterpret_cast<int*>(lds4 + T::LDS_F4);
+  const int m_blk = blockIdx.x * BM;
+  const int n_blk = blockIdx.y * BN;
+  const int kb = blockIdx.z * kchunk;
+  const int ke = min(p.K, kb + kchunk);
+  f32x16 acc[T::TM][T::TN];
+  T::mainloop(p, m_blk, n_blk, kb, ke, reinterpret_cast<float*>(lds4), acc);
+  if (mode != 0) {
+    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const int ntiles = gridDim.x * gridDim.y;
+    const brsrc_t sr = make_rsrc(slab, (uint32_t)(gridDim.z * ntiles * G::PART4 * 16u));
+    T::store_partial(sr, ((size_t)blockIdx.z * ntiles + tile) * G::PART4, acc);
+    if (mode == 2) return;
+    if (!T::arrive(&tickets[tile], gridDim.z, flag)) return;
+    T::zero(acc);
+    for (int z = 0; z < (int)gridDim.z; ++z)
+      T::add_partial(sr, ((size_t)z * ntiles + tile) * G::PART4, acc);
+  }
+  T::epilogue(p, m_blk, n_blk, acc);
+}
+
+// Stream-K driver (balanced persistent schedule).  The iteration space is I = tiles * KI
+// (KI = K tiles of BK per output tile), tiles ordered m-fastest.  Worker w of the W launched
+// one-block workers owns iterations [w*I/W, (w+1)*I/W): every SIMD gets the same MFMA work
+// (+-1 K tile) whatever the tile count, instead of whole tiles/splits quantised over the
+// 1024 SIMDs.  A worker finishes whole tiles with the fused epilogue directly; its first and
+// last tile may be partial: those partials go to slab slot (w, 0|1) and the last of the
+// tile's contributors sums them in worker order (deterministic) and runs the epilogue — the
+// split-K reduction happens inside the same launch, with no separate reduce kernel.
+// Workers are numbered XCD-major (hardware dispatches block b to XCD b % 8), so the
+// neighbours that share a boundary tile, and adjacent tiles' operands, stay in one L2.
+template <int BM, int BN, int BK, int WM, int WN, class P>
+__global__ void __launch_bounds__(WM * WN * 64)
+gemm_streamk_kernel(P p, int KI, int gx, long long I, float4* __restrict__ slab,
+                    int* __restrict__ tickets) {
+  using T = GemmTile<BM, BN, BK, WM, WN, P>;
+  using G = typename T::G;
+  __shared__ float4 lds4[T::LDS_F4 + 1];  // staging images + last-arriver flag
+  int* const flag = reinterpret_cast<int*>(lds4 + T::LDS_F4);
+  const int W = gridDim.x;
+  const brsrc_t sr = make_rsrc(slab, (uint32_t)W * 2u * G::PART4 * 16u);
+  const int w = (blockIdx.x & 7) * (W >> 3) + (blockIdx.x >> 3);  // W % 8 == 0 (host)
+  auto first_iter = [&](int ww) -> long long { return (long long)ww * I / W; };
+  // worker owning iteration x: the largest ww with first_iter(ww) <= x
+  auto owner = [&](long long x) -> int { return (int)(((x + 1) * W + I - 1) / I) - 1; };
+  long long it = first_iter(w);
+  const long long end = first_iter(w + 1);
+  const int start_tile = (int)(it / KI);
+  f32x16 acc[T::TM][T::TN];
+  while (it < end) {
+    const int tile = (int)(it / KI);
+    const int klo = (int)(it - (long long)tile * KI);
+    const int khi = (int)min((long long)KI, (long long)klo + (end - it));
+    const int m_blk = (tile % gx) * BM, n_blk = (tile / gx) * BN;
+    T::mainloop(p, m_blk, n_blk, klo * BK, min(p.K, khi * BK), reinterpret_cast<float*>(lds4),
+                acc);
+    it += khi - klo;
+    if (klo == 0 && khi == KI) {
+      T::epilogue(p, m_blk, n_blk, acc);
+      continue;
+    }
+    const int slot = (tile == start_tile) ? 0 : 1;
+    T::store_partial(sr, ((size_t)w * 2 + slot) * G::PART4, acc);
+    const long long t0 = (long long)tile * KI;
+    const int wf = owner(t0), wl = owner(t0 + KI - 1);
+    if (!T::arrive(&tickets[tile], wl - wf + 1, flag)) continue;
+    T::zero(acc);
+    for (int ww = wf; ww <= wl; ++ww) {
+      const int s = (first_iter(ww) / KI == tile) ? 0 : 1;
+      T::add_partial(sr, ((size_t)ww * 2 + s) * G::PART4, acc);
+    }
+    T::epilogue(p, m_blk, n_blk, acc);
   }
 }
 
@@ -351,11 +464,42 @@ inline size_t splitk_slab_f4(int M, int N, int K, int splits) {
   return (size_t)z * tiles * TileGeo<BM, BN, WM, WN>::PART4;
 }
 
-// wide_thr: z > wide_thr uses mode 2 (separate wide reduce), else mode 1 (last arriver).
+// Stream-K worker count actually launched for a requested `workers` (0 = stream-K off):
+// a multiple of 8 (XCD-major numbering), at most one worker per K iteration.
+template <int BM, int BN, int BK>
+inline int streamk_workers(int M, int N, int K, int workers) {
+  if (workers <= 0) return 0;
+  const long long I = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN) * ((K + BK - 1) / BK);
+  long long w = workers < I ? workers : I;
+  w &= ~7LL;
+  return w < 8 ? 0 : (int)w;
+}
+
+// float4 partial-slab elements a launch needs (stream-K when workers > 0, else split-K)
+template <int BM, int BN, int BK, int WM, int WN>
+inline size_t gemm_slab_f4(int M, int N, int K, int splits, int workers) {
+  // (max of both: a stream-K launch with more tiles than tickets falls back to split-K)
+  const int w = streamk_workers<BM, BN, BK>(M, N, K, workers);
+  const size_t sk = (size_t)w * 2 * TileGeo<BM, BN, WM, WN>::PART4;
+  const size_t sp = splitk_slab_f4<BM, BN, BK, WM, WN>(M, N, K, splits);
+  return sk > sp ? sk : sp;
+}
+
+// workers > 0: stream-K launch (splits / wide_thr unused).  Otherwise split-K with `splits`:
+// z > wide_thr uses mode 2 (separate wide reduce), else mode 1 (last arriver).
 template <int BM, int BN, int BK, int WM, int WN, class P>
 inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch& sc,
-                        hipStream_t stream) {
+                        hipStream_t stream, int workers = 0) {
   if (p.M <= 0 || p.N <= 0) return;
+  const int W = streamk_workers<BM, BN, BK>(p.M, p.N, p.K, workers);
+  if (W > 0 && (long long)((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN) <= sc.max_tiles) {
+    const int gx = (p.M + BM - 1) / BM, gy = (p.N + BN - 1) / BN;
+    const int KI = (p.K + BK - 1) / BK;
+    const long long I = (long long)gx * gy * KI;
+    hipLaunchKernelGGL((gemm_streamk_kernel<BM, BN, BK, WM, WN, P>), dim3(W), dim3(WM * WN * 64),
+                       0, stream, p, KI, gx, I, reinterpret_cast<float4*>(sc.slab), sc.tickets);
+    return;
+  }
   const int z = splitk_z<BK>(p.K, splits);
   const int kchunk = z > 1 ? splitk_kchunk<BK>(p.K, splits) : p.K;
   const int gx = (p.M + BM - 1) / BM, gy = (p.N + BN - 1) / BN;

@@ -6,7 +6,7 @@
 //   w -= lr_t * m / (sqrt(v) + eps),  lr_t = lr * sqrt(1 - beta2^t) / (1 - beta1^t)
 // lr_t is computed on the host per PS step counter.  `scale` folds a 1/W gradient mean
 // (or 1.0 for the reference's sum) into the same pass.  HBM-bound: 5 streams of fp32;
-// 16-byte vector path when every operand is 16-B aligned.
+// 16-byte vector path (+ scalar tail) when every operand is 16-B aligned.
 #include "common.h"
 #include "api.h"
 
@@ -19,12 +19,14 @@ DDL_DEV void adam1(float& w, float g, float& m, float& v, float lr_t, float c1, 
   w -= lr_t * m / (sqrtf(v) + eps);
 }
 
+// 16-B body over n4 = n / 4 float4 elements; the n % 4 tail element(s) by the first lanes.
 __global__ void __launch_bounds__(256)
 adam_vec_kernel(float4* __restrict__ w, const float4* __restrict__ g, float4* __restrict__ m,
-                float4* __restrict__ v, int64_t n4, float lr_t, float c1, float c2, float eps,
+                float4* __restrict__ v, int64_t n, float lr_t, float c1, float c2, float eps,
                 float scale) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t n4 = n >> 2;
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (int64_t i = gid; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     float4 W = w[i], G = g[i], M = m[i], V = v[i];
     adam1(W.x, G.x * scale, M.x, V.x, lr_t, c1, c2, eps);
     adam1(W.y, G.y * scale, M.y, V.y, lr_t, c1, c2, eps);
@@ -32,8 +34,16 @@ adam_vec_kernel(float4* __restrict__ w, const float4* __restrict__ g, float4* __
     adam1(W.w, G.w * scale, M.w, V.w, lr_t, c1, c2, eps);
     w[i] = W; m[i] = M; v[i] = V;
   }
+  if (gid < (n & 3)) {
+    const int64_t e = 4 * n4 + gid;
+    float* wf = reinterpret_cast<float*>(w);
+    float* mf = reinterpret_cast<float*>(m);
+    float* vf = reinterpret_cast<float*>(v);
+    float W = wf[e], M = mf[e], V = vf[e];
+    adam1(W, reinterpret_cast<const float*>(g)[e] * scale, M, V, lr_t, c1, c2, eps);
+    wf[e] = W; mf[e] = M; vf[e] = V;
+  }
 }
-
 __global__ void __launch_bounds__(256)
 adam_scalar_kernel(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,
                    float* __restrict__ v, int64_t n, float lr_t, float c1, float c2, float eps,
@@ -68,9 +78,9 @@ void launch_adam(float* w, const float* g, float* m, float* v, int64_t n, float 
   if (n <= 0) return;
   const float c1 = 1.f - b1, c2 = 1.f - b2;
   const uintptr_t al = (uintptr_t)w | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v;
-  if ((al & 15) == 0 && (n & 3) == 0) {
-    hipLaunchKernelGGL(adam_vec_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, (float4*)w,
-                       (const float4*)g, (float4*)m, (float4*)v, n / 4, lr_t, c1, c2, eps, scale);
+  if ((al & 15) == 0) {
+    hipLaunchKernelGGL(adam_vec_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, (float4*)w,
+                       (const float4*)g, (float4*)m, (float4*)v, n, lr_t, c1, c2, eps, scale);
   } else {
     hipLaunchKernelGGL(adam_scalar_kernel, dim3(grid_for(n)), dim3(256), 0, st, w, g, m, v, n,
                        lr_t, c1, c2, eps, scale);

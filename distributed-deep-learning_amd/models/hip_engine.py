@@ -72,6 +72,14 @@ class HipEngine:
     def get_cfg(self) -> List[int]:
         return list(self.eng.get_cfg())
 
+    def set_workers(self, workers: List[int]) -> None:
+        """Per-op stream-K worker counts (0 = split-K by `splits`; csrc/kernels/gemm.h)."""
+        self.eng.set_workers(list(workers))
+        self.graphs = None
+
+    def get_workers(self) -> List[int]:
+        return list(self.eng.get_workers())
+
     def set_concurrent(self, on: bool) -> None:
         self.eng.set_concurrent(bool(on))
         self.graphs = None

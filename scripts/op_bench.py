@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--splits", default="1,2,4,8,16,32")
     ap.add_argument("--cfgs", default="0,1,2,3")
+    ap.add_argument("--workers", default="0", help="stream-K worker counts to sweep (0 = none)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     from ddl_amd.models.layout import CANON_OFFSETS, TOTAL_NUMEL
@@ -55,44 +56,53 @@ def main():
 
     res = {}
     sweep = [int(s) for s in a.splits.split(",")]
+    wsweep = [int(w) for w in a.workers.split(",") if int(w) > 0]
     cfgs = [int(c) for c in a.cfgs.split(",")]
     base_cfg = eng.get_cfg()
-    best_cfg, best_split = list(base_cfg), list(base)
+    base_w = eng.get_workers()
+    best_cfg, best_split, best_w = list(base_cfg), list(base), list(base_w)
     for op, name in enumerate(OPS):
         M, N, K = eng.eng.op_shape(op, B)
         flop = 2.0 * M * N * K
         row = {}
-        for c in cfgs:
-            for s in sweep:
-                cf = list(base_cfg)
-                cf[op] = c
-                sp = list(base)
-                sp[op] = s
-                eng.set_splits(sp)
-                eng.set_cfg(cf)
-                row[(c, s)] = time_op(op, a.iters)
+        # (cfg, splits, workers): split-K points have workers 0, stream-K points splits 1
+        points = [(c, s, 0) for c in cfgs for s in sweep] + [(c, 1, w) for c in cfgs for w in wsweep]
+        for c, s, w in points:
+            cf, sp, wk = list(base_cfg), list(base), list(base_w)
+            cf[op], sp[op], wk[op] = c, s, w
+            eng.set_splits(sp)
+            eng.set_cfg(cf)
+            eng.set_workers(wk)
+            row[(c, s, w)] = time_op(op, a.iters)
         eng.set_splits(base)
         eng.set_cfg(base_cfg)
+        eng.set_workers(base_w)
         best = min(row, key=row.get)
-        best_cfg[op], best_split[op] = best
-        res[name] = {"M": M, "N": N, "K": K, "us": {f"c{c}s{s}": v for (c, s), v in row.items()},
-                     "best": f"c{best[0]}s{best[1]}", "best_us": row[best],
-                     "default_us": row.get((base_cfg[op], base[op])),
+        best_cfg[op], best_split[op], best_w[op] = best
+        key = lambda t: f"c{t[0]}w{t[2]}" if t[2] else f"c{t[0]}s{t[1]}"
+        dflt = (base_cfg[op], base[op] if not base_w[op] else 1, base_w[op])
+        res[name] = {"M": M, "N": N, "K": K, "us": {key(t): v for t, v in row.items()},
+                     "best": key(best), "best_us": row[best],
+                     "default_us": row.get(dflt),
                      "best_tflops": flop / row[best] / 1e6}
-        print(f"{name:12s} M={M:6d} N={N:5d} K={K:6d} default c{base_cfg[op]}s{base[op]}="
-              f"{row.get((base_cfg[op], base[op]), float('nan')):7.1f}  best c{best[0]}s{best[1]}="
+        print(f"{name:12s} M={M:6d} N={N:5d} K={K:6d} default {key(dflt)}="
+              f"{row.get(dflt, float('nan')):7.1f}  best {key(best)}="
               f"{row[best]:7.1f} us {flop / row[best] / 1e6:6.1f} TF", flush=True)
         for c in cfgs:
-            print("      c%d " % c + " ".join(f"s{s}:{row[(c, s)]:7.1f}" for s in sweep), flush=True)
+            print("      c%d " % c + " ".join(f"{key(t)[len(str(c)) + 1:]}:{v:7.1f}"
+                                          for t, v in row.items() if t[0] == c), flush=True)
     print("BEST_CFG", ",".join(map(str, best_cfg)))
     print("BEST_SPLITS", ",".join(map(str, best_split)))
+    print("BEST_WORKERS", ",".join(map(str, best_w)))
     eng.set_cfg(best_cfg)
     eng.set_splits(best_split)
+    eng.set_workers(best_w)
     # whole step eager vs graph
     for g in (False, True):
         e2 = HipEngine(params, grads, CANON_OFFSETS, batch=B, graph=g, eval_chunk=B)
         e2.set_cfg(best_cfg)
         e2.set_splits(best_split)
+        e2.set_workers(best_w)
         for _ in range(5):
             e2.forward_backward(x, y, 0.5, 7)
         torch.cuda.synchronize()
