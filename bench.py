@@ -42,6 +42,8 @@ def main(argv=None):
                          "stream launches on MI355X: 0.600 vs 0.552 ms/step)")
     ap.add_argument("--no-graph", action="store_true", help="(default; kept for compatibility)")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--no-native-exchange", action="store_true",
+                    help="Python-driven exchange instead of the C++ SyncRunner")
     ap.add_argument("--splits", default=None, help="comma-separated split-K factors per op")
     ap.add_argument("--tta", type=float, default=None,
                     help="also run one full epoch with evals and report time to this test accuracy")
@@ -63,7 +65,8 @@ def main(argv=None):
     total_steps = a.warmup + a.steps
     cfg = TrainConfig(mode=a.mode, shard=a.shard, steps=total_steps, batch_size=a.batch_size,
                       eval_every=0, engine=a.engine, graph=a.graph and not a.no_graph,
-                      overlap=not a.no_overlap, quiet=True, data_sharding="stride")
+                      overlap=not a.no_overlap, quiet=True, data_sharding="stride",
+                      native_exchange=not a.no_native_exchange)
     data = synthetic_mnist()
     tr = Trainer(cfg, env, dataset=data)
     if a.splits and hasattr(tr.engine, "set_splits"):
@@ -132,6 +135,7 @@ def main(argv=None):
                 "engine": engine_name,
                 "hip_graph": bool(a.graph and not a.no_graph),
                 "overlap": not a.no_overlap,
+                "exchange": "native" if getattr(tr.exchange, "native", False) else "python",
                 "optimizer": "adam(1e-4) on PS shards",
             },
             "test_acc_after_run": round(acc, 4),

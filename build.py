@@ -92,7 +92,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
     if steps or not os.path.exists(OUT):
         link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs,
                 f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-                "-ltorch_python", f"-Wl,-rpath,{tlib}", "-lrt"]
+                "-ltorch_python", "-ldl", f"-Wl,-rpath,{tlib}", "-lrt"]
         if verbose:
             print(" ".join(link))
         _run(link)

@@ -82,6 +82,7 @@ class PyEngine {
     return std::vector<int64_t>(e_.cfg, e_.cfg + ddl::OP_COUNT);
   }
   void set_concurrent(bool on) { e_.concurrent = on; }
+  void set_dual(bool on) { e_.dual = on; }
   void set_wide_thr(int64_t t) { e_.wide_thr = (int)std::max<int64_t>(1, t); }
 
   void set_keep_prob(double keep) {
@@ -165,6 +166,8 @@ class PyEngine {
   }
 
   int64_t max_batch() const { return e_.max_batch; }
+  ddl::Engine* raw() { return &e_; }
+  void check_batch(const at::Tensor& x) { check_x(x); }
   int64_t workspace_bytes() const { return (int64_t)e_.workspace_bytes(); }
   static std::vector<int64_t> op_shape(int64_t op, int64_t B) {
     int M, N, K;
@@ -196,6 +199,98 @@ class PyEngine {
   std::vector<at::Tensor> params_, grads_;
   at::Tensor ws_;
   at::Device device_{at::kCPU};
+};
+
+// Python-facing wrapper of ddl::SyncRunner (native sync step: engine + exchange + update).
+class PyRunner {
+ public:
+  PyRunner(PyEngine& eng, at::Tensor params, at::Tensor grads, int64_t world, int64_t rank)
+      : eng_(eng), params_(params), grads_(grads) {
+    check_f32_cuda(params, "params");
+    check_f32_cuda(grads, "grads");
+    TORCH_CHECK(params.numel() == grads.numel(), "params/grads size mismatch");
+    r_ = std::make_unique<ddl::SyncRunner>(eng.raw(), params.data_ptr<float>(),
+                                           grads.data_ptr<float>(), (int)world, (int)rank);
+  }
+  static py::bytes unique_id() {
+    char id[128];
+    ddl::SyncRunner::unique_id(id);
+    return py::bytes(id, 128);
+  }
+  void init_comm(py::bytes id) {
+    std::string s = id;
+    TORCH_CHECK(s.size() == 128, "RCCL unique id must be 128 bytes");
+    py::gil_scoped_release nogil;  // collective: blocks until every rank joins
+    r_->init_comm(s.data());
+  }
+  // units: list of (seg, kind, host, ps, [(lo, hi, state_off)], m|None, v|None, shard|None)
+  void set_units(py::list units) {
+    std::vector<ddl::RunnerUnit> out;
+    keep_.clear();
+    const int64_t n = params_.numel();
+    for (auto item : units) {
+      auto t = item.cast<py::tuple>();
+      TORCH_CHECK(t.size() == 8, "unit tuple must have 8 fields");
+      ddl::RunnerUnit u;
+      u.seg = t[0].cast<int>();
+      u.kind = t[1].cast<int>();
+      u.host = t[2].cast<int>();
+      u.ps = t[3].cast<int>();
+      auto opt_ptr = [&](py::handle h, int64_t need, const char* what) -> float* {
+        if (h.is_none()) return nullptr;
+        at::Tensor x = h.cast<at::Tensor>();
+        check_f32_cuda(x, what);
+        TORCH_CHECK(x.numel() >= need, what, " too small");
+        keep_.push_back(x);
+        return x.data_ptr<float>();
+      };
+      int64_t need_state = 0;
+      for (auto r : t[4].cast<py::list>()) {
+        auto rr = r.cast<py::tuple>();
+        ddl::RunnerRange range{rr[0].cast<int64_t>(), rr[1].cast<int64_t>(), rr[2].cast<int64_t>()};
+        TORCH_CHECK(0 <= range.lo && range.lo <= range.hi && range.hi <= n, "range out of bounds");
+        const int64_t len = u.kind == ddl::RunnerUnit::RS ? 0 : range.hi - range.lo;
+        need_state = std::max(need_state, range.state_off + len);
+        u.ranges.push_back(range);
+      }
+      u.m = opt_ptr(t[5], need_state, "m");
+      u.v = opt_ptr(t[6], need_state, "v");
+      u.shard = opt_ptr(t[7], 0, "shard");
+      out.push_back(std::move(u));
+    }
+    r_->set_units(out);
+  }
+  void set_optimizer(int64_t kind, double lr, double b1, double b2, double eps, double mu) {
+    r_->set_optimizer((int)kind, (float)lr, (float)b1, (float)b2, (float)eps, (float)mu);
+  }
+  void set_scale(double grad_scale, double coef) { r_->set_scale((float)grad_scale, (float)coef); }
+  void set_local_on_main(bool on) { r_->set_local_on_main(on); }
+  void step(at::Tensor x, at::Tensor labels, at::Tensor seed, std::vector<double> lr_t) {
+    eng_.check_batch(x);
+    TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_cuda(), "labels must be int64 GPU");
+    TORCH_CHECK(seed.is_cuda() && seed.scalar_type() == at::kInt && seed.numel() == 1,
+                "seed must be a 1-element int32 GPU tensor");
+    lr_.assign(lr_t.begin(), lr_t.end());
+    if (lr_.empty()) lr_.push_back(0.f);
+    r_->step(x.data_ptr<float>(), labels.data_ptr<int64_t>(), (int)x.size(0),
+             reinterpret_cast<const uint32_t*>(seed.data_ptr<int32_t>()), lr_.data(), cur_stream());
+  }
+  py::tuple selftest() {
+    std::string why;
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = r_->selftest(&why);
+    }
+    return py::make_tuple(ok, why);
+  }
+
+ private:
+  PyEngine& eng_;
+  at::Tensor params_, grads_;
+  std::vector<at::Tensor> keep_;
+  std::vector<float> lr_;
+  std::unique_ptr<ddl::SyncRunner> r_;
 };
 
 }  // namespace
@@ -230,6 +325,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_cfg", &PyEngine::set_cfg)
       .def("get_cfg", &PyEngine::get_cfg)
       .def("set_concurrent", &PyEngine::set_concurrent)
+      .def("set_dual", &PyEngine::set_dual)
       .def("set_wide_thr", &PyEngine::set_wide_thr)
       .def("forward", &PyEngine::forward)
       .def("backward_segment", &PyEngine::backward_segment)
@@ -241,6 +337,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("max_batch", &PyEngine::max_batch)
       .def("workspace_bytes", &PyEngine::workspace_bytes)
       .def_static("op_shape", &PyEngine::op_shape);
+
+  py::class_<PyRunner>(m, "SyncRunner")
+      .def(py::init<PyEngine&, at::Tensor, at::Tensor, int64_t, int64_t>(), py::arg("engine"),
+           py::arg("params"), py::arg("grads"), py::arg("world"), py::arg("rank"),
+           py::keep_alive<1, 2>())
+      .def_static("unique_id", &PyRunner::unique_id)
+      .def("init_comm", &PyRunner::init_comm)
+      .def("set_units", &PyRunner::set_units)
+      .def("set_optimizer", &PyRunner::set_optimizer)
+      .def("set_scale", &PyRunner::set_scale)
+      .def("set_local_on_main", &PyRunner::set_local_on_main)
+      .def("step", &PyRunner::step)
+      .def("selftest", &PyRunner::selftest);
 
   py::class_<ddl::ShmMailbox>(m, "ShmMailbox")
       .def(py::init<const std::string&, int64_t, bool>(), py::arg("name"), py::arg("capacity"),

@@ -3,6 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
 
 #include "scratch.h"
 
@@ -13,6 +17,7 @@ void launch_adam(float* w, const float* g, float* m, float* v, int64_t n, float 
                  float b2, float eps, float scale, hipStream_t st);
 void launch_momentum(float* w, const float* g, float* m, int64_t n, float lr, float mu,
                      float scale, hipStream_t st);
+void launch_scale(float* p, int64_t n, float a, hipStream_t st);
 
 // ---- classifier head (head.hip) --------------------------------------------------------------
 void launch_head_fwd(const float* h2, const float* w, const float* bias, const int64_t* labels,
@@ -52,7 +57,11 @@ struct Engine {
   int wide_thr = 1;          // split count above which the separate wide reduce is used
   uint32_t thr24 = 0;        // dropout threshold (train)
   float inv_keep = 1.f;
-  bool concurrent = true;    // weight-gradient GEMMs on a second stream
+  // weight-gradient GEMMs on a second stream.  Off by default: a cross-queue event wait costs
+  // tens of microseconds of GPU idle on MI355X/ROCm (step timelines), more than the overlap
+  // gains; dgrad/wgrad concurrency comes from fused dual-problem launches instead.
+  bool concurrent = false;
+  bool dual = true;          // single stream: dgrad + wgrad of a layer in one launch
 
   // workspace carve-out
   float *p1 = nullptr, *p2 = nullptr, *p3 = nullptr, *p4 = nullptr, *h1 = nullptr, *h2 = nullptr;
@@ -92,6 +101,60 @@ struct Engine {
   void fork(hipStream_t st);
   void join(hipStream_t st);
   void wgrad(int op, const float* x, int B, const uint32_t* seed, hipStream_t st);
+};
+
+// ---- native synchronous step runner (runner.hip) -------------------------------------------
+struct RunnerRange {
+  int64_t lo, hi;       // plan-buffer element range [lo, hi)
+  int64_t state_off;    // offset of the range's optimizer state in the unit's m / v
+};
+struct RunnerUnit {
+  enum Kind { LOCAL = 0, RS = 1, REDUCE = 2 };
+  int seg = 0;          // backward segment after which the unit's gradients are complete
+  int kind = LOCAL;
+  int host = 0;         // REDUCE: rank that owns the PS
+  int ps = 0;           // index into the per-step lr_t table (RS: this rank's PS)
+  std::vector<RunnerRange> ranges;
+  float* m = nullptr;   // optimizer state base of the owning PS (null where not hosted)
+  float* v = nullptr;
+  float* shard = nullptr;  // RS: 1/W chunk buffer
+};
+
+class SyncRunner {
+ public:
+  static constexpr int kSegments = 4;
+  SyncRunner(Engine* eng, float* params, float* grads, int world, int rank);
+  ~SyncRunner();
+  static void unique_id(char out[128]);
+  void init_comm(const char id[128]);  // collective over all ranks (W > 1)
+  bool has_comm() const { return comm_ != nullptr; }
+  void set_units(const std::vector<RunnerUnit>& units);
+  void set_optimizer(int kind, float lr, float b1, float b2, float eps, float mu);
+  void set_scale(float grad_scale, float coef) { grad_scale_ = grad_scale; coef_ = coef; }
+  // one synchronous training step on stream `st`; lr_t indexed by RunnerUnit::ps
+  void step(const float* x, const int64_t* labels, int B, const uint32_t* seed,
+            const float* lr_t, hipStream_t st);
+  bool selftest(std::string* why);
+  void set_local_on_main(bool on) { local_on_main_ = on; }
+  hipStream_t comm_stream() const { return cs_; }
+
+ private:
+  void issue(const RunnerUnit& u, const float* lr_t, hipStream_t st);
+  void update(float* w, const float* g, float* m, float* v, int64_t n, float lr_t,
+              hipStream_t st);
+  Engine* eng_;
+  float* w_;
+  float* g_;
+  int world_, rank_;
+  void* comm_ = nullptr;  // ncclComm_t
+  hipStream_t cs_ = nullptr;
+  hipEvent_t seg_ev_[kSegments] = {};
+  hipEvent_t done_ev_ = nullptr;
+  std::vector<RunnerUnit> units_;
+  int opt_ = 0;
+  float lr_ = 1e-4f, b1_ = 0.9f, b2_ = 0.999f, eps_ = 1e-8f, mu_ = 0.9f;
+  float grad_scale_ = 1.f, coef_ = 1.f;
+  bool local_on_main_ = true;
 };
 
 }  // namespace ddl

@@ -9,6 +9,8 @@
 // next segment (fork/join events, captured as parallel graph branches).
 #include <string.h>
 
+#include <type_traits>
+
 #include "api.h"
 #include "layers.h"
 
@@ -139,85 +141,103 @@ void Engine::bind_workspace(void* base) {
   }
 }
 
+// Problem policy of op OP (layers.h) bound to this engine's buffers, at batch B.
+template <int OP>
+static auto make_policy(const Engine& e, int B, const float* x, const uint32_t* seed,
+                        bool train) {
+  int M, N, K;
+  Engine::op_shape(OP, B, &M, &N, &K);
+  const uint32_t thr = train ? e.thr24 : 0u;
+  const float* const* P = e.P;
+  float* const* G = e.G;
+  if constexpr (OP == OP_CONV1_FWD) return ConvFwd<28, 1, 32>{M, N, K, x, P[0], P[1], e.p1, e.c1};
+  else if constexpr (OP == OP_CONV2_FWD)
+    return ConvFwd<14, 32, 64>{M, N, K, e.p1, P[2], P[3], e.p2, e.c2};
+  else if constexpr (OP == OP_CONV3_FWD)
+    return ConvFwd<7, 64, 128>{M, N, K, e.p2, P[4], P[5], e.p3, e.c3};
+  else if constexpr (OP == OP_CONV4_FWD)
+    return ConvFwd<4, 128, 256>{M, N, K, e.p3, P[6], P[7], e.p4, e.c4};
+  else if constexpr (OP == OP_FC1_FWD)
+    return FcFwd<true>{M, N, K, e.p4, P[8], P[9], e.h1, seed, 1u, thr, e.inv_keep};
+  else if constexpr (OP == OP_FC2_FWD)
+    return FcFwd<false>{M, N, K, e.h1, P[10], P[11], e.h2, seed, 2u, thr, e.inv_keep};
+  else if constexpr (OP == OP_FC2_DGRAD)
+    return FcDgradAct{{M, N, K, e.dpre2fc, P[10]}, e.h1, e.inv_keep, e.dpre1fc};
+  else if constexpr (OP == OP_FC2_WGRAD)
+    return FcWgrad{M, N, K, 1024, e.h1, e.dpre2fc, G[10], G[11]};
+  else if constexpr (OP == OP_FC1_DGRAD)
+    return FcDgradPool<2, 256>{{M, N, K, e.dpre1fc, P[8]}, e.c4, e.d4};
+  else if constexpr (OP == OP_FC1_WGRAD)
+    return FcWgrad{M, N, K, 1024, e.p4, e.dpre1fc, G[8], G[9]};
+  else if constexpr (OP == OP_CONV4_DGRAD)
+    return ConvDgrad<4, 128, 256, 7>{M, N, K, e.d4, P[6], e.c3, e.d3};
+  else if constexpr (OP == OP_CONV4_WGRAD)
+    return ConvWgrad<4, 128, 256>{M, N, K, e.p3, e.d4, G[6], G[7]};
+  else if constexpr (OP == OP_CONV3_DGRAD)
+    return ConvDgrad<7, 64, 128, 14>{M, N, K, e.d3, P[4], e.c2, e.d2};
+  else if constexpr (OP == OP_CONV3_WGRAD)
+    return ConvWgrad<7, 64, 128>{M, N, K, e.p2, e.d3, G[4], G[5]};
+  else if constexpr (OP == OP_CONV2_DGRAD)
+    return ConvDgrad<14, 32, 64, 28>{M, N, K, e.d2, P[2], e.c1, e.d1};
+  else if constexpr (OP == OP_CONV2_WGRAD)
+    return ConvWgrad<14, 32, 64>{M, N, K, e.p1, e.d2, G[2], G[3]};
+  else
+    return ConvWgrad<28, 1, 32>{M, N, K, x, e.d1, G[0], G[1]};
+}
+
+template <int OP>
+static void run_op_t(Engine& e, const float* x, int B, const uint32_t* seed, bool train,
+                     hipStream_t st, int si) {
+  const auto p = make_policy<OP>(e, B, x, seed, train);
+  launch_cfg(e.cfg[OP], p, train ? e.splits[OP] : 1, train ? e.workers[OP] : 0, e.wide_thr,
+             e.scratch[si], st);
+}
+
 void Engine::run_op(int op, const float* x, int B, const uint32_t* seed, bool train,
                     hipStream_t st, int si) {
-  int M, N, K;
-  op_shape(op, B, &M, &N, &K);
-  const int s = train ? splits[op] : 1;
-  const int w = train ? workers[op] : 0;
-  const int c = cfg[op];
-  const uint32_t thr = train ? thr24 : 0u;
-  const SplitScratch& sc = scratch[si];
   switch (op) {
-    case OP_CONV1_FWD: {
-      ConvFwd<28, 1, 32> p{M, N, K, x, P[0], P[1], p1, c1};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_CONV2_FWD: {
-      ConvFwd<14, 32, 64> p{M, N, K, p1, P[2], P[3], p2, c2};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_CONV3_FWD: {
-      ConvFwd<7, 64, 128> p{M, N, K, p2, P[4], P[5], p3, c3};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_CONV4_FWD: {
-      ConvFwd<4, 128, 256> p{M, N, K, p3, P[6], P[7], p4, c4};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_FC1_FWD: {
-      FcFwd<true> p{M, N, K, p4, P[8], P[9], h1, seed, 1u, thr, inv_keep};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_FC2_FWD: {
-      FcFwd<false> p{M, N, K, h1, P[10], P[11], h2, seed, 2u, thr, inv_keep};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_FC2_DGRAD: {
-      FcDgradAct p{{M, N, K, dpre2fc, P[10]}, h1, inv_keep, dpre1fc};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_FC2_WGRAD: {
-      FcWgrad p{M, N, K, 1024, h1, dpre2fc, G[10], G[11]};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_FC1_DGRAD: {
-      FcDgradPool<2, 256> p{{M, N, K, dpre1fc, P[8]}, c4, d4};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_FC1_WGRAD: {
-      FcWgrad p{M, N, K, 1024, p4, dpre1fc, G[8], G[9]};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_CONV4_DGRAD: {
-      ConvDgrad<4, 128, 256, 7> p{M, N, K, d4, P[6], c3, d3};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_CONV4_WGRAD: {
-      ConvWgrad<4, 128, 256> p{M, N, K, p3, d4, G[6], G[7]};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_CONV3_DGRAD: {
-      ConvDgrad<7, 64, 128, 14> p{M, N, K, d3, P[4], c2, d2};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_CONV3_WGRAD: {
-      ConvWgrad<7, 64, 128> p{M, N, K, p2, d3, G[4], G[5]};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_CONV2_DGRAD: {
-      ConvDgrad<14, 32, 64, 28> p{M, N, K, d2, P[2], c1, d1};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_CONV2_WGRAD: {
-      ConvWgrad<14, 32, 64> p{M, N, K, p1, d2, G[2], G[3]};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
-    case OP_CONV1_WGRAD: {
-      ConvWgrad<28, 1, 32> p{M, N, K, x, d1, G[0], G[1]};
-      launch_cfg(c, p, s, w, wide_thr, sc, st);
-    } break;
+#define DDL_RUN(OPC) \
+  case OPC: run_op_t<OPC>(*this, x, B, seed, train, st, si); break;
+    DDL_RUN(OP_CONV1_FWD) DDL_RUN(OP_CONV2_FWD) DDL_RUN(OP_CONV3_FWD) DDL_RUN(OP_CONV4_FWD)
+    DDL_RUN(OP_FC1_FWD) DDL_RUN(OP_FC2_FWD) DDL_RUN(OP_FC2_DGRAD) DDL_RUN(OP_FC2_WGRAD)
+    DDL_RUN(OP_FC1_DGRAD) DDL_RUN(OP_FC1_WGRAD) DDL_RUN(OP_CONV4_DGRAD) DDL_RUN(OP_CONV4_WGRAD)
+    DDL_RUN(OP_CONV3_DGRAD) DDL_RUN(OP_CONV3_WGRAD) DDL_RUN(OP_CONV2_DGRAD)
+    DDL_RUN(OP_CONV2_WGRAD) DDL_RUN(OP_CONV1_WGRAD)
+#undef DDL_RUN
     default: break;
+  }
+}
+
+// ---- dual launches: data- and weight-gradient GEMM of one layer in one kernel -----------------
+static bool one_wave_cfg(int c) { return c == 0 || c == 2 || c == 3 || c == 4; }
+
+template <class CA, int OA, int OB, class PA, class PB>
+static void dual_b(Engine& e, const PA& pa, const PB& pb, hipStream_t st) {
+  switch (e.cfg[OB]) {
+    case 0: launch_gemm_dual<CA, PA, TileCfg<TILE_0>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide_thr, st); break;
+    case 2: launch_gemm_dual<CA, PA, TileCfg<TILE_2>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide_thr, st); break;
+    case 3: launch_gemm_dual<CA, PA, TileCfg<TILE_3>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide_thr, st); break;
+    default: launch_gemm_dual<CA, PA, TileCfg<TILE_4>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide_thr, st); break;
+  }
+}
+
+// Ops OA and OB (independent) in one launch if both use one-wave tiles, else back to back.
+template <int OA, int OB>
+static void run_dual(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
+  if (!e.dual || !one_wave_cfg(e.cfg[OA]) || !one_wave_cfg(e.cfg[OB])) {
+    run_op_t<OA>(e, x, B, seed, true, st, 0);
+    run_op_t<OB>(e, x, B, seed, true, st, 0);
+    return;
+  }
+  const auto pa = make_policy<OA>(e, B, x, seed, true);
+  const auto pb = make_policy<OB>(e, B, x, seed, true);
+  using PA = std::decay_t<decltype(pa)>;
+  using PB = std::decay_t<decltype(pb)>;
+  switch (e.cfg[OA]) {
+    case 0: dual_b<TileCfg<TILE_0>, OA, OB, PA, PB>(e, pa, pb, st); break;
+    case 2: dual_b<TileCfg<TILE_2>, OA, OB, PA, PB>(e, pa, pb, st); break;
+    case 3: dual_b<TileCfg<TILE_3>, OA, OB, PA, PB>(e, pa, pb, st); break;
+    default: dual_b<TileCfg<TILE_4>, OA, OB, PA, PB>(e, pa, pb, st); break;
   }
 }
 
@@ -238,41 +258,56 @@ void Engine::join(hipStream_t st) {
 }
 
 void Engine::wgrad(int op, const float* x, int B, const uint32_t* seed, hipStream_t st) {
-  if (concurrent && side) {
-    fork(st);
-    run_op(op, x, B, seed, true, side, 1);
-  } else {
-    run_op(op, x, B, seed, true, st, 0);
-  }
+  fork(st);
+  run_op(op, x, B, seed, true, side, 1);
 }
 
 void Engine::backward_segment(int s, const float* x, const int64_t* labels, int B,
                               const uint32_t* seed, hipStream_t st) {
+  if (concurrent && side) {  // weight gradients on the side stream (fork/join per segment)
+    switch (s) {
+      case 0:
+        launch_head_fwd(h2, P[12], P[13], labels, B, dlog, loss, nullptr, st);
+        launch_head_bwd(h2, P[12], dlog, B, seed, thr24, inv_keep, G[12], G[13], dpre2fc, st);
+        wgrad(OP_FC2_WGRAD, x, B, seed, st);
+        run_op(OP_FC2_DGRAD, x, B, seed, true, st, 0);
+        wgrad(OP_FC1_WGRAD, x, B, seed, st);
+        run_op(OP_FC1_DGRAD, x, B, seed, true, st, 0);
+        break;
+      case 1:
+        wgrad(OP_CONV4_WGRAD, x, B, seed, st);
+        run_op(OP_CONV4_DGRAD, x, B, seed, true, st, 0);
+        break;
+      case 2:
+        wgrad(OP_CONV3_WGRAD, x, B, seed, st);
+        run_op(OP_CONV3_DGRAD, x, B, seed, true, st, 0);
+        break;
+      case 3:
+        wgrad(OP_CONV2_WGRAD, x, B, seed, st);
+        run_op(OP_CONV2_DGRAD, x, B, seed, true, st, 0);
+        wgrad(OP_CONV1_WGRAD, x, B, seed, st);
+        break;
+      default: break;
+    }
+    join(st);
+    return;
+  }
+  // single stream: each layer's dgrad + wgrad as one dual launch
   switch (s) {
     case 0:
       launch_head_fwd(h2, P[12], P[13], labels, B, dlog, loss, nullptr, st);
       launch_head_bwd(h2, P[12], dlog, B, seed, thr24, inv_keep, G[12], G[13], dpre2fc, st);
-      wgrad(OP_FC2_WGRAD, x, B, seed, st);
-      run_op(OP_FC2_DGRAD, x, B, seed, true, st, 0);
-      wgrad(OP_FC1_WGRAD, x, B, seed, st);
-      run_op(OP_FC1_DGRAD, x, B, seed, true, st, 0);
+      run_dual<OP_FC2_DGRAD, OP_FC2_WGRAD>(*this, x, B, seed, st);
+      run_dual<OP_FC1_DGRAD, OP_FC1_WGRAD>(*this, x, B, seed, st);
       break;
-    case 1:
-      wgrad(OP_CONV4_WGRAD, x, B, seed, st);
-      run_op(OP_CONV4_DGRAD, x, B, seed, true, st, 0);
-      break;
-    case 2:
-      wgrad(OP_CONV3_WGRAD, x, B, seed, st);
-      run_op(OP_CONV3_DGRAD, x, B, seed, true, st, 0);
-      break;
+    case 1: run_dual<OP_CONV4_DGRAD, OP_CONV4_WGRAD>(*this, x, B, seed, st); break;
+    case 2: run_dual<OP_CONV3_DGRAD, OP_CONV3_WGRAD>(*this, x, B, seed, st); break;
     case 3:
-      wgrad(OP_CONV2_WGRAD, x, B, seed, st);
-      run_op(OP_CONV2_DGRAD, x, B, seed, true, st, 0);
-      wgrad(OP_CONV1_WGRAD, x, B, seed, st);
+      run_dual<OP_CONV2_DGRAD, OP_CONV2_WGRAD>(*this, x, B, seed, st);
+      run_op(OP_CONV1_WGRAD, x, B, seed, true, st, 0);
       break;
     default: break;
   }
-  if (concurrent && side) join(st);
 }
 
 void Engine::eval_count(const float* x, const int64_t* labels, int B, hipStream_t st) {

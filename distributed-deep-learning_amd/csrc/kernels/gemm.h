@@ -315,38 +315,43 @@ struct GemmTile {
   }
 };
 
-// Classic split-K driver: grid (tiles_m, tiles_n, S); split z covers K range
-// [z*kchunk, (z+1)*kchunk).  mode 0: no split; mode 1: in-launch last-arriver reduction of
-// the S partials (in z order, deterministic); mode 2: partials only (splitk_wide_reduce).
+// ---- drivers ------------------------------------------------------------------------------
+// Each driver is a device-function body over a *virtual* block id, so a kernel can host one
+// problem (gemm_f32_kernel / gemm_streamk_kernel) or two independent problems side by side
+// (gemm_dual_kernel: the data- and weight-gradient GEMMs of one layer in ONE launch — their
+// concurrency without a second stream, whose cross-queue event waits cost tens of us).
+// `lds` is the block's staging array (>= GemmTile::LDS_F4 float4), `flag` one int of LDS.
+
+// Classic split-K: virtual grid (gx, gy, gz); split bz covers K range
+// [bz*kchunk, (bz+1)*kchunk).  mode 0: no split; mode 1: in-launch last-arriver reduction of
+// the gz partials (in z order, deterministic); mode 2: partials only (splitk_wide_reduce).
 template <int BM, int BN, int BK, int WM, int WN, class P>
-__global__ void __launch_bounds__(WM * WN * 64)
-gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets) {
+DDL_DEV void splitk_body(const P& p, int kchunk, int mode, float4* __restrict__ slab,
+                         int* __restrict__ tickets, int bx, int by, int bz, int gx, int gy,
+                         int gz, float* lds, int* flag) {
   using T = GemmTile<BM, BN, BK, WM, WN, P>;
   using G = typename T::G;
-  __shared__ float4 lds4[T::LDS_F4 + 1];  // staging images + last-arriver flag
-  int* const flag = reinterpret_cast<int*>(lds4 + T::LDS_F4);
-  const int m_blk = blockIdx.x * BM;
-  const int n_blk = blockIdx.y * BN;
-  const int kb = blockIdx.z * kchunk;
+  const int m_blk = bx * BM;
+  const int n_blk = by * BN;
+  const int kb = bz * kchunk;
   const int ke = min(p.K, kb + kchunk);
   f32x16 acc[T::TM][T::TN];
-  T::mainloop(p, m_blk, n_blk, kb, ke, reinterpret_cast<float*>(lds4), acc);
+  T::mainloop(p, m_blk, n_blk, kb, ke, lds, acc);
   if (mode != 0) {
-    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-    const int ntiles = gridDim.x * gridDim.y;
-    const brsrc_t sr = make_rsrc(slab, (uint32_t)(gridDim.z * ntiles * G::PART4 * 16u));
-    T::store_partial(sr, ((size_t)blockIdx.z * ntiles + tile) * G::PART4, acc);
+    const int tile = by * gx + bx;
+    const int ntiles = gx * gy;
+    const brsrc_t sr = make_rsrc(slab, (uint32_t)(gz * ntiles * G::PART4 * 16u));
+    T::store_partial(sr, ((size_t)bz * ntiles + tile) * G::PART4, acc);
     if (mode == 2) return;
-    if (!T::arrive(&tickets[tile], gridDim.z, flag)) return;
+    if (!T::arrive(&tickets[tile], gz, flag)) return;
     T::zero(acc);
-    for (int z = 0; z < (int)gridDim.z; ++z)
-      T::add_partial(sr, ((size_t)z * ntiles + tile) * G::PART4, acc);
+    for (int z = 0; z < gz; ++z) T::add_partial(sr, ((size_t)z * ntiles + tile) * G::PART4, acc);
   }
   T::epilogue(p, m_blk, n_blk, acc);
 }
 
-// Stream-K driver (balanced persistent schedule).  The iteration space is I = tiles * KI
-// (KI = K tiles of BK per output tile), tiles ordered m-fastest.  Worker w of the W launched
+// Stream-K (balanced persistent schedule).  The iteration space is I = tiles * KI
+// (KI = K tiles of BK per output tile), tiles ordered m-fastest.  Worker w of the W
 // one-block workers owns iterations [w*I/W, (w+1)*I/W): every SIMD gets the same MFMA work
 // (+-1 K tile) whatever the tile count, instead of whole tiles/splits quantised over the
 // 1024 SIMDs.  A worker finishes whole tiles with the fused epilogue directly; its first and
@@ -356,16 +361,12 @@ gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __res
 // Workers are numbered XCD-major (hardware dispatches block b to XCD b % 8), so the
 // neighbours that share a boundary tile, and adjacent tiles' operands, stay in one L2.
 template <int BM, int BN, int BK, int WM, int WN, class P>
-__global__ void __launch_bounds__(WM * WN * 64)
-gemm_streamk_kernel(P p, int KI, int gx, long long I, float4* __restrict__ slab,
-                    int* __restrict__ tickets) {
+DDL_DEV void streamk_body(const P& p, int KI, int gx, long long I, float4* __restrict__ slab,
+                          int* __restrict__ tickets, int bid, int W, float* lds, int* flag) {
   using T = GemmTile<BM, BN, BK, WM, WN, P>;
   using G = typename T::G;
-  __shared__ float4 lds4[T::LDS_F4 + 1];  // staging images + last-arriver flag
-  int* const flag = reinterpret_cast<int*>(lds4 + T::LDS_F4);
-  const int W = gridDim.x;
+  const int w = (bid & 7) * (W >> 3) + (bid >> 3);  // W % 8 == 0 (host)
   const brsrc_t sr = make_rsrc(slab, (uint32_t)W * 2u * G::PART4 * 16u);
-  const int w = (blockIdx.x & 7) * (W >> 3) + (blockIdx.x >> 3);  // W % 8 == 0 (host)
   auto first_iter = [&](int ww) -> long long { return (long long)ww * I / W; };
   // worker owning iteration x: the largest ww with first_iter(ww) <= x
   auto owner = [&](long long x) -> int { return (int)(((x + 1) * W + I - 1) / I) - 1; };
@@ -378,8 +379,7 @@ gemm_streamk_kernel(P p, int KI, int gx, long long I, float4* __restrict__ slab,
     const int klo = (int)(it - (long long)tile * KI);
     const int khi = (int)min((long long)KI, (long long)klo + (end - it));
     const int m_blk = (tile % gx) * BM, n_blk = (tile / gx) * BN;
-    T::mainloop(p, m_blk, n_blk, klo * BK, min(p.K, khi * BK), reinterpret_cast<float*>(lds4),
-                acc);
+    T::mainloop(p, m_blk, n_blk, klo * BK, min(p.K, khi * BK), lds, acc);
     it += khi - klo;
     if (klo == 0 && khi == KI) {
       T::epilogue(p, m_blk, n_blk, acc);
@@ -397,6 +397,78 @@ gemm_streamk_kernel(P p, int KI, int gx, long long I, float4* __restrict__ slab,
     }
     T::epilogue(p, m_blk, n_blk, acc);
   }
+}
+
+// Launch geometry of one GEMM problem under its schedule (host-computed, passed by value).
+struct SubGrid {
+  int nblocks = 0;   // blocks (virtual ids 0..nblocks-1)
+  int streamk = 0;   // 1: stream-K with W = nblocks workers
+  int gx = 1, gy = 1, gz = 1;
+  int kchunk = 0, mode = 0;  // split-K
+  int KI = 0;                // stream-K
+  long long I = 0;
+  float4* slab = nullptr;
+  int* tickets = nullptr;
+};
+
+template <int BM, int BN, int BK, int WM, int WN, class P>
+DDL_DEV void run_sub(const P& p, const SubGrid& g, int vb, float* lds, int* flag) {
+  if (g.streamk) {
+    streamk_body<BM, BN, BK, WM, WN, P>(p, g.KI, g.gx, g.I, g.slab, g.tickets, vb, g.nblocks,
+                                        lds, flag);
+  } else {
+    const int bx = vb % g.gx, t = vb / g.gx;
+    splitk_body<BM, BN, BK, WM, WN, P>(p, g.kchunk, g.mode, g.slab, g.tickets, bx, t % g.gy,
+                                       t / g.gy, g.gx, g.gy, g.gz, lds, flag);
+  }
+}
+
+template <int BM, int BN, int BK, int WM, int WN, class P>
+__global__ void __launch_bounds__(WM * WN * 64)
+gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets) {
+  using T = GemmTile<BM, BN, BK, WM, WN, P>;
+  __shared__ float4 lds4[T::LDS_F4 + 1];  // staging images + last-arriver flag (one array:
+                                          // guide §5 trap 4a)
+  splitk_body<BM, BN, BK, WM, WN, P>(p, kchunk, mode, slab, tickets, blockIdx.x, blockIdx.y,
+                                     blockIdx.z, gridDim.x, gridDim.y, gridDim.z,
+                                     reinterpret_cast<float*>(lds4),
+                                     reinterpret_cast<int*>(lds4 + T::LDS_F4));
+}
+
+template <int BM, int BN, int BK, int WM, int WN, class P>
+__global__ void __launch_bounds__(WM * WN * 64)
+gemm_streamk_kernel(P p, int KI, int gx, long long I, float4* __restrict__ slab,
+                    int* __restrict__ tickets) {
+  using T = GemmTile<BM, BN, BK, WM, WN, P>;
+  __shared__ float4 lds4[T::LDS_F4 + 1];
+  streamk_body<BM, BN, BK, WM, WN, P>(p, KI, gx, I, slab, tickets, blockIdx.x, gridDim.x,
+                                      reinterpret_cast<float*>(lds4),
+                                      reinterpret_cast<int*>(lds4 + T::LDS_F4));
+}
+
+template <int BM_, int BN_, int BK_, int WM_, int WN_>
+struct TileCfg {
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_;
+  static constexpr int NT = WM * WN * 64;
+};
+
+// Two independent GEMM problems in one launch: blocks [0, ga.nblocks) run problem A, the
+// rest problem B.  Both must use one-wave blocks.
+template <class CA, class PA, class CB, class PB>
+__global__ void __launch_bounds__(64)
+gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb) {
+  static_assert(CA::NT == 64 && CB::NT == 64, "dual launch needs one-wave blocks");
+  using TA = GemmTile<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>;
+  using TB = GemmTile<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>;
+  constexpr int L = TA::LDS_F4 > TB::LDS_F4 ? TA::LDS_F4 : TB::LDS_F4;
+  __shared__ float4 lds4[L + 1];
+  float* lds = reinterpret_cast<float*>(lds4);
+  int* flag = reinterpret_cast<int*>(lds4 + L);
+  const int b = blockIdx.x;
+  if (b < ga.nblocks)
+    run_sub<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, b, lds, flag);
+  else
+    run_sub<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, b - ga.nblocks, lds, flag);
 }
 
 // Wide split-K reduce (mode 2): RL lanes cooperate on one float4 output element.
@@ -485,47 +557,85 @@ inline size_t gemm_slab_f4(int M, int N, int K, int splits, int workers) {
   return sk > sp ? sk : sp;
 }
 
-// workers > 0: stream-K launch (splits / wide_thr unused).  Otherwise split-K with `splits`:
-// z > wide_thr uses mode 2 (separate wide reduce), else mode 1 (last arriver).
+// Schedule of one launch: stream-K when workers > 0 (and the tile count fits the tickets),
+// else split-K with `splits`: z > wide_thr uses mode 2 (separate wide reduce), else mode 1
+// (last arriver).
+template <int BM, int BN, int BK, class P>
+inline SubGrid plan_gemm(const P& p, int splits, int workers, int wide_thr,
+                         const SplitScratch& sc) {
+  SubGrid g;
+  g.slab = reinterpret_cast<float4*>(sc.slab);
+  g.tickets = sc.tickets;
+  if (p.M <= 0 || p.N <= 0) return g;
+  g.gx = (p.M + BM - 1) / BM;
+  g.gy = (p.N + BN - 1) / BN;
+  const int W = streamk_workers<BM, BN, BK>(p.M, p.N, p.K, workers);
+  if (W > 0 && (long long)g.gx * g.gy <= sc.max_tiles) {
+    g.streamk = 1;
+    g.nblocks = W;
+    g.KI = (p.K + BK - 1) / BK;
+    g.I = (long long)g.gx * g.gy * g.KI;
+    return g;
+  }
+  g.gz = splitk_z<BK>(p.K, splits);
+  g.kchunk = g.gz > 1 ? splitk_kchunk<BK>(p.K, splits) : p.K;
+  g.mode = g.gz == 1 ? 0 : (g.gz > wide_thr ? 2 : 1);
+  g.nblocks = g.gx * g.gy * g.gz;
+  return g;
+}
+
+// The separate reduce of a mode-2 split-K launch (no-op otherwise).
+template <int BM, int BN, int BK, int WM, int WN, class P>
+inline void launch_reduce(const P& p, const SubGrid& g, hipStream_t stream) {
+  if (g.streamk || g.mode != 2 || g.nblocks == 0) return;
+  using G = TileGeo<BM, BN, WM, WN>;
+  const int ntiles = g.gx * g.gy, z = g.gz;
+  const size_t nelem = (size_t)ntiles * G::PART4;
+  const float4* s4 = g.slab;
+  if (z > 32) {
+    const size_t th = nelem * 64;
+    hipLaunchKernelGGL((splitk_wide_reduce<BM, BN, WM, WN, 64, P>), dim3((th + 255) / 256),
+                       dim3(256), 0, stream, p, s4, z, g.gx, ntiles);
+  } else if (z > 4) {
+    const size_t th = nelem * 16;
+    hipLaunchKernelGGL((splitk_wide_reduce<BM, BN, WM, WN, 16, P>), dim3((th + 255) / 256),
+                       dim3(256), 0, stream, p, s4, z, g.gx, ntiles);
+  } else {
+    const size_t th = nelem * 4;
+    hipLaunchKernelGGL((splitk_wide_reduce<BM, BN, WM, WN, 4, P>), dim3((th + 255) / 256),
+                       dim3(256), 0, stream, p, s4, z, g.gx, ntiles);
+  }
+}
+
 template <int BM, int BN, int BK, int WM, int WN, class P>
 inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch& sc,
                         hipStream_t stream, int workers = 0) {
-  if (p.M <= 0 || p.N <= 0) return;
-  const int W = streamk_workers<BM, BN, BK>(p.M, p.N, p.K, workers);
-  if (W > 0 && (long long)((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN) <= sc.max_tiles) {
-    const int gx = (p.M + BM - 1) / BM, gy = (p.N + BN - 1) / BN;
-    const int KI = (p.K + BK - 1) / BK;
-    const long long I = (long long)gx * gy * KI;
-    hipLaunchKernelGGL((gemm_streamk_kernel<BM, BN, BK, WM, WN, P>), dim3(W), dim3(WM * WN * 64),
-                       0, stream, p, KI, gx, I, reinterpret_cast<float4*>(sc.slab), sc.tickets);
+  const SubGrid g = plan_gemm<BM, BN, BK>(p, splits, workers, wide_thr, sc);
+  if (g.nblocks == 0) return;
+  if (g.streamk) {
+    hipLaunchKernelGGL((gemm_streamk_kernel<BM, BN, BK, WM, WN, P>), dim3(g.nblocks),
+                       dim3(WM * WN * 64), 0, stream, p, g.KI, g.gx, g.I, g.slab, g.tickets);
     return;
   }
-  const int z = splitk_z<BK>(p.K, splits);
-  const int kchunk = z > 1 ? splitk_kchunk<BK>(p.K, splits) : p.K;
-  const int gx = (p.M + BM - 1) / BM, gy = (p.N + BN - 1) / BN;
-  const int mode = z == 1 ? 0 : (z > wide_thr ? 2 : 1);
-  dim3 grid(gx, gy, z);
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, WM, WN, P>), grid, dim3(WM * WN * 64), 0,
-                     stream, p, kchunk, mode, reinterpret_cast<float4*>(sc.slab), sc.tickets);
-  if (mode == 2) {
-    using G = TileGeo<BM, BN, WM, WN>;
-    const int ntiles = gx * gy;
-    const size_t nelem = (size_t)ntiles * G::PART4;
-    const float4* s4 = reinterpret_cast<const float4*>(sc.slab);
-    if (z > 32) {
-      const size_t th = nelem * 64;
-      hipLaunchKernelGGL((splitk_wide_reduce<BM, BN, WM, WN, 64, P>), dim3((th + 255) / 256),
-                         dim3(256), 0, stream, p, s4, z, gx, ntiles);
-    } else if (z > 4) {
-      const size_t th = nelem * 16;
-      hipLaunchKernelGGL((splitk_wide_reduce<BM, BN, WM, WN, 16, P>), dim3((th + 255) / 256),
-                         dim3(256), 0, stream, p, s4, z, gx, ntiles);
-    } else {
-      const size_t th = nelem * 4;
-      hipLaunchKernelGGL((splitk_wide_reduce<BM, BN, WM, WN, 4, P>), dim3((th + 255) / 256),
-                         dim3(256), 0, stream, p, s4, z, gx, ntiles);
-    }
-  }
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, WM, WN, P>), dim3(g.gx, g.gy, g.gz),
+                     dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets);
+  launch_reduce<BM, BN, BK, WM, WN, P>(p, g, stream);
+}
+
+// Problems A and B (one-wave tile configs CA / CB) in one launch, each with its own schedule
+// and its own scratch (slab + tickets); mode-2 reduces follow on the same stream.
+template <class CA, class PA, class CB, class PB>
+inline void launch_gemm_dual(const PA& pa, int sa, int wa, const SplitScratch& sca,
+                             const PB& pb, int sb, int wb, const SplitScratch& scb,
+                             int wide_thr, hipStream_t stream) {
+  const SubGrid ga = plan_gemm<CA::BM, CA::BN, CA::BK>(pa, sa, wa, wide_thr, sca);
+  const SubGrid gb = plan_gemm<CB::BM, CB::BN, CB::BK>(pb, sb, wb, wide_thr, scb);
+  const int n = ga.nblocks + gb.nblocks;
+  if (n > 0)
+    hipLaunchKernelGGL((gemm_dual_kernel<CA, PA, CB, PB>), dim3(n), dim3(64), 0, stream, pa, ga,
+                       pb, gb);
+  launch_reduce<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, stream);
+  launch_reduce<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, stream);
 }
 
 }  // namespace ddl

@@ -67,6 +67,11 @@ momentum_kernel(float* __restrict__ w, const float* __restrict__ g, float* __res
   }
 }
 
+__global__ void __launch_bounds__(256) scale_kernel(float* __restrict__ p, int64_t n, float a) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] *= a;
+}
 static int grid_for(int64_t n) {
   int64_t b = (n + 255) / 256;
   if (b > 2048) b = 2048;  // 8 blocks per CU, grid-stride beyond
@@ -94,4 +99,8 @@ void launch_momentum(float* w, const float* g, float* m, int64_t n, float lr, fl
                      scale);
 }
 
+void launch_scale(float* p, int64_t n, float a, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, n, a);
+}
 }  // namespace ddl

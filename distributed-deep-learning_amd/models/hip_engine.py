@@ -81,7 +81,13 @@ class HipEngine:
         return list(self.eng.get_workers())
 
     def set_concurrent(self, on: bool) -> None:
+        """Weight-gradient GEMMs on a second stream (fork/join per backward segment)."""
         self.eng.set_concurrent(bool(on))
+        self.graphs = None
+
+    def set_dual(self, on: bool) -> None:
+        """Single stream: each layer's data- and weight-gradient GEMMs in one launch."""
+        self.eng.set_dual(bool(on))
         self.graphs = None
 
     def _set_keep(self, keep: float) -> None:
@@ -122,10 +128,13 @@ class HipEngine:
         self._set_keep(keep_prob)
         B = x.shape[0]
         if B != self.batch or not self.use_graph:
-            seed_t = torch.tensor([_i32(seed)], dtype=torch.int32, device=x.device)
             if B > self.batch:
                 raise ValueError(f"batch {B} > engine batch {self.batch}")
-            self._eager(x.contiguous(), labels, seed_t, on_segment)
+            # fill_ enqueues the value by argument: no host<->device sync, so the host keeps
+            # running ahead of the GPU across steps (a torch.tensor(..., device=) H2D copy
+            # here blocked the host every step until the GPU drained).
+            self.seed_static.fill_(_i32(seed))
+            self._eager(x.contiguous(), labels, self.seed_static, on_segment)
             return
         self.x_static.copy_(x)
         self.y_static.copy_(labels)

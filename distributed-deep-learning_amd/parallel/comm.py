@@ -117,7 +117,10 @@ class SyncExchange:
         self.world = env.world
         self.grad_scale = 1.0 / env.world if grad_reduce == "mean" else 1.0
         self.coef = quirk_coefficient(plan, env.rank, env.world, ref_quirks)
-        # Without overlap every unit is issued after the whole backward.
+        # Without overlap every unit is issued after the whole backward (the last engine
+        # segment), as one merged segment.
+        self.overlap = overlap
+        self.n_engine_segments = len(segments)
         self.segments = [set(s) for s in segments] if overlap else [set().union(*map(set, segments))]
         self.units = self._build_units()
         cuda = params.is_cuda
@@ -191,6 +194,8 @@ class SyncExchange:
     def grads_ready(self, seg_index: int) -> None:
         """Called (host side, in stream order) after the engine enqueued the kernels of
         backward segment ``seg_index``."""
+        if not self.overlap and seg_index < self.n_engine_segments - 1:
+            return  # the merged segment is complete only after the last engine segment
         self._ready |= self.segments[min(seg_index, len(self.segments) - 1)]
         for k, u in enumerate(self.units):
             if k in self._issued or not u.tensors <= self._ready:
@@ -239,7 +244,7 @@ class SyncExchange:
 
     def finish_step(self) -> None:
         if len(self._issued) != len(self.units):
-            self.grads_ready(len(self.segments) - 1)
+            self.grads_ready(self.n_engine_segments - 1)
             # any unit still not issued covers tensors of no segment: issue now
             for k, u in enumerate(self.units):
                 if k not in self._issued:

@@ -31,6 +31,7 @@ from ..utils.watchdog import Watchdog
 from ..utils import checkpoint as ckpt
 from ..utils.tracing import trace_range
 from .comm import DistEnv, SyncExchange, AsyncExchange, init_distributed
+from .native_exchange import make_sync_exchange
 from .ps import ParameterServer
 from .sharding import make_plan
 
@@ -89,9 +90,8 @@ class Trainer:
                                           steps_per_worker=self.steps * cfg.epochs,
                                           grad_reduce=cfg.grad_reduce)
         else:
-            self.exchange = SyncExchange(self.plan, env, self.params, self.grads, segs,
-                                         self.servers, cfg.grad_reduce, cfg.ref_quirks,
-                                         overlap=cfg.overlap)
+            self.exchange = make_sync_exchange(self.plan, env, self.params, self.grads, segs,
+                                               self.servers, self.engine, cfg, hyper)
         self.log = metrics.JsonlLogger(cfg.log_jsonl, r)
         self.global_step = 0
         self.history: List[dict] = []
@@ -111,6 +111,9 @@ class Trainer:
                 self.engine.forward_backward(x, y, cfg.keep_prob, seed)
             with trace_range("push_pull"):
                 self.exchange.push_pull()
+        elif getattr(self.exchange, "native", False):
+            with trace_range("step_native"):
+                self.exchange.step(x, y, cfg.keep_prob, seed)
         else:
             ex = self.exchange
             ex.begin_step()

@@ -100,6 +100,7 @@ def main():
     # whole step eager vs graph
     for g in (False, True):
         e2 = HipEngine(params, grads, CANON_OFFSETS, batch=B, graph=g, eval_chunk=B)
+        e2.set_concurrent(False)
         e2.set_cfg(best_cfg)
         e2.set_splits(best_split)
         e2.set_workers(best_w)

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--passes", type=int, default=2)
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--graph", action="store_true")
+    ap.add_argument("--concurrent", action="store_true", help="tune for the two-stream backward")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     from ddl_amd.models.layout import CANON_OFFSETS, TOTAL_NUMEL
@@ -47,6 +48,7 @@ def main():
     grads = torch.zeros_like(params)
     B = a.batch
     eng = HipEngine(params, grads, CANON_OFFSETS, batch=B, graph=a.graph, eval_chunk=B)
+    eng.set_concurrent(a.concurrent)
     x = torch.rand(B, 784, device=dev)
     y = torch.randint(0, 10, (B,), device=dev)
 

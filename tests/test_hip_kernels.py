@@ -173,6 +173,27 @@ def test_stream_k_matches_reference(setup, cfg):
         eng.set_workers(base_w)
 
 
+@pytest.mark.parametrize("conc,dual", [(False, True), (False, False), (True, False)])
+def test_backward_modes_match(setup, conc, dual):
+    """Single-stream dual launches, single-stream back-to-back and the two-stream backward
+    compute the same (bitwise: same schedules, same reduction orders) gradients."""
+    eng, flat, params, grads, x, y = setup
+    grads.zero_()
+    eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 55)
+    torch.cuda.synchronize()
+    ref = grads.clone()
+    eng.set_concurrent(conc)
+    eng.set_dual(dual)
+    try:
+        grads.zero_()
+        eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 55)
+        torch.cuda.synchronize()
+        assert torch.equal(grads, ref)
+    finally:
+        eng.set_concurrent(False)
+        eng.set_dual(True)
+
+
 def test_graph_replay_matches_eager(setup):
     from ddl_amd.models.hip_engine import HipEngine
     eng, flat, params, grads, x, y = setup
