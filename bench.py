@@ -45,8 +45,10 @@ def main(argv=None):
     ap.add_argument("--no-native-exchange", action="store_true",
                     help="Python-driven exchange instead of the C++ SyncRunner")
     ap.add_argument("--splits", default=None, help="comma-separated split-K factors per op")
-    ap.add_argument("--tta", type=float, default=None,
-                    help="also run one full epoch with evals and report time to this test accuracy")
+    ap.add_argument("--tta", type=float, default=0.95,
+                    help="after the throughput run, train one reference epoch (500 steps/worker, "
+                         "full test-set eval every 10 steps, eval time included) and report the "
+                         "wall time to this test accuracy; <= 0 skips it")
     a = ap.parse_args(argv)
 
     import torch
@@ -101,14 +103,17 @@ def main(argv=None):
     acc = tr.evaluate()
 
     tta = None
-    if a.tta is not None:
+    if a.tta is not None and a.tta > 0:
         cfg2 = TrainConfig(mode=a.mode, shard=a.shard, batch_size=a.batch_size, eval_every=10,
-                           engine=a.engine, graph=a.graph and not a.no_graph, overlap=not a.no_overlap,
-                           quiet=True, target_acc=a.tta)
+                           engine=a.engine, graph=a.graph and not a.no_graph,
+                           overlap=not a.no_overlap, quiet=True, target_acc=a.tta,
+                           data_sharding="stride", native_exchange=not a.no_native_exchange)
         tr2 = Trainer(cfg2, env, dataset=data)
         s = tr2.train()
         tta = {"target_acc": a.tta, "time_to_target_s": s["time_to_target"],
-               "final_acc": s["final_acc"], "epoch_wall_s": s["wall_time"]}
+               "final_acc": round(s["final_acc"], 4), "epoch_wall_s": round(s["wall_time"], 4),
+               "steps_per_worker": s["steps"], "eval_every": 10,
+               "eval": "distributed over ranks" if world > 1 and a.mode == "sync" else "full"}
 
     if env.rank == 0:
         base = BASELINE_IMG_PER_S_PER_GPU

@@ -37,6 +37,7 @@ class TrainConfig:
     graph: bool = False             # replay the compute step as HIP graphs (eager is faster)
     overlap: bool = True            # bucketed grad push overlapped with backward
     native_exchange: bool = True    # sync step in the C++ SyncRunner (HIP engine on GPU)
+    dist_eval: bool = True          # sync, W > 1: each rank scores 1/W of the test set
     log_jsonl: Optional[str] = None
     checkpoint_dir: Optional[str] = None
     checkpoint_every: int = 0
@@ -75,6 +76,8 @@ def add_args(p: argparse.ArgumentParser, mode_default: str = "sync") -> argparse
     p.add_argument("--engine", default=d.engine, choices=["auto", "hip", "torch"])
     p.add_argument("--graph", action="store_true", help="replay the engine step as HIP graphs")
     p.add_argument("--no-graph", action="store_true", help="(default)")
+    p.add_argument("--no-dist-eval", action="store_true",
+                   help="every worker scores the full test set (reference behaviour)")
     p.add_argument("--no-native-exchange", action="store_true",
                    help="drive the sync exchange from Python instead of the C++ SyncRunner")
     p.add_argument("--no-overlap", action="store_true")
@@ -97,6 +100,7 @@ def from_args(a: argparse.Namespace) -> TrainConfig:
         steps=a.steps, lr=a.lr, optimizer=a.optimizer, keep_prob=a.keep_prob,
         eval_every=a.eval_every, data=a.data, data_sharding=a.data_sharding,
         grad_reduce=a.grad_reduce, ref_quirks=a.ref_quirks, seed=a.seed, engine=a.engine,
-        graph=a.graph and not a.no_graph, native_exchange=not a.no_native_exchange, overlap=not a.no_overlap, log_jsonl=a.log_jsonl,
+        graph=a.graph and not a.no_graph, native_exchange=not a.no_native_exchange,
+        dist_eval=not a.no_dist_eval, overlap=not a.no_overlap, log_jsonl=a.log_jsonl,
         checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
         resume=a.resume, target_acc=a.target_acc, quiet=a.quiet, watchdog_s=a.watchdog_s)

@@ -83,7 +83,18 @@ class PyEngine {
   }
   void set_concurrent(bool on) { e_.concurrent = on; }
   void set_dual(bool on) { e_.dual = on; }
-  void set_wide_thr(int64_t t) { e_.wide_thr = (int)std::max<int64_t>(1, t); }
+  void set_wide_thr(int64_t t) {
+    e_.wide_thr = (int)std::max<int64_t>(1, t);
+    for (int i = 0; i < ddl::OP_COUNT; ++i) e_.wide[i] = e_.wide_thr;
+  }
+  // per-op split-K reduce threshold: z > wide[op] -> separate reduce kernel, else in-launch
+  void set_wide(std::vector<int64_t> w) {
+    TORCH_CHECK((int)w.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " thresholds");
+    for (int i = 0; i < ddl::OP_COUNT; ++i) e_.wide[i] = (int)std::max<int64_t>(1, w[i]);
+  }
+  std::vector<int64_t> get_wide() const {
+    return std::vector<int64_t>(e_.wide, e_.wide + ddl::OP_COUNT);
+  }
 
   void set_keep_prob(double keep) {
     const double rate = 1.0 - keep;
@@ -265,15 +276,14 @@ class PyRunner {
   }
   void set_scale(double grad_scale, double coef) { r_->set_scale((float)grad_scale, (float)coef); }
   void set_local_on_main(bool on) { r_->set_local_on_main(on); }
-  void step(at::Tensor x, at::Tensor labels, at::Tensor seed, std::vector<double> lr_t) {
+  void step(at::Tensor x, at::Tensor labels, int64_t seed, std::vector<double> lr_t) {
     eng_.check_batch(x);
     TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_cuda(), "labels must be int64 GPU");
-    TORCH_CHECK(seed.is_cuda() && seed.scalar_type() == at::kInt && seed.numel() == 1,
-                "seed must be a 1-element int32 GPU tensor");
+    TORCH_CHECK(labels.numel() == x.size(0), "labels/batch size mismatch");
     lr_.assign(lr_t.begin(), lr_t.end());
     if (lr_.empty()) lr_.push_back(0.f);
     r_->step(x.data_ptr<float>(), labels.data_ptr<int64_t>(), (int)x.size(0),
-             reinterpret_cast<const uint32_t*>(seed.data_ptr<int32_t>()), lr_.data(), cur_stream());
+             (uint32_t)(seed & 0xFFFFFFFF), lr_.data(), cur_stream());
   }
   py::tuple selftest() {
     std::string why;
@@ -327,6 +337,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_concurrent", &PyEngine::set_concurrent)
       .def("set_dual", &PyEngine::set_dual)
       .def("set_wide_thr", &PyEngine::set_wide_thr)
+      .def("set_wide", &PyEngine::set_wide)
+      .def("get_wide", &PyEngine::get_wide)
       .def("forward", &PyEngine::forward)
       .def("backward_segment", &PyEngine::backward_segment)
       .def("run_op", &PyEngine::run_op)

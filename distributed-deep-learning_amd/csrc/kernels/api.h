@@ -23,8 +23,8 @@ void launch_scale(float* p, int64_t n, float a, hipStream_t st);
 void launch_head_fwd(const float* h2, const float* w, const float* bias, const int64_t* labels,
                      int B, float* dlog, float* loss, int* correct, hipStream_t st);
 void launch_head_bwd(const float* h2, const float* w, const float* dlog, int B,
-                     const uint32_t* seed, uint32_t thr24, float inv_keep, float* gw, float* gb,
-                     float* dpre2, hipStream_t st);
+                     const uint32_t* seed, uint32_t seed_v, uint32_t thr24, float inv_keep,
+                     float* gw, float* gb, float* dpre2, hipStream_t st);
 
 // ---- diagnostics (diag.hip) -------------------------------------------------------------------
 void launch_mfma_peak(float* out, int blocks, int iters, hipStream_t st);
@@ -54,8 +54,11 @@ struct Engine {
   int splits[OP_COUNT];
   int cfg[OP_COUNT];
   int workers[OP_COUNT];     // > 0: stream-K with this many workers (overrides splits)
-  int wide_thr = 1;          // split count above which the separate wide reduce is used
+  int wide_thr = 1;          // default split count above which the separate wide reduce is used
+  int wide[OP_COUNT];        // per op: z > wide[op] -> separate wide reduce (mode 2), else the
+                             // in-launch last-arriver reduction (mode 1)
   uint32_t thr24 = 0;        // dropout threshold (train)
+  uint32_t seed_value = 0;   // dropout seed used when a step is given no device seed word
   float inv_keep = 1.f;
   // weight-gradient GEMMs on a second stream.  Off by default: a cross-queue event wait costs
   // tens of microseconds of GPU idle on MI355X/ROCm (step timelines), more than the overlap
@@ -132,8 +135,8 @@ class SyncRunner {
   void set_optimizer(int kind, float lr, float b1, float b2, float eps, float mu);
   void set_scale(float grad_scale, float coef) { grad_scale_ = grad_scale; coef_ = coef; }
   // one synchronous training step on stream `st`; lr_t indexed by RunnerUnit::ps
-  void step(const float* x, const int64_t* labels, int B, const uint32_t* seed,
-            const float* lr_t, hipStream_t st);
+  void step(const float* x, const int64_t* labels, int B, uint32_t seed, const float* lr_t,
+            hipStream_t st);
   bool selftest(std::string* why);
   void set_local_on_main(bool on) { local_on_main_ = on; }
   hipStream_t comm_stream() const { return cs_; }
@@ -155,6 +158,14 @@ class SyncRunner {
   float lr_ = 1e-4f, b1_ = 0.9f, b2_ = 0.999f, eps_ = 1e-8f, mu_ = 0.9f;
   float grad_scale_ = 1.f, coef_ = 1.f;
   bool local_on_main_ = true;
+  struct Piece {
+    RunnerRange r;
+    int ps;
+    float* m;
+    float* v;
+  };
+  bool all_local_ = false;
+  std::vector<Piece> merged_;  // coalesced LOCAL update ranges (all_local_)
 };
 
 }  // namespace ddl

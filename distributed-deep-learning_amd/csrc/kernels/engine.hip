@@ -19,13 +19,16 @@ namespace ddl {
 Engine::Engine() {
   // {tile config, split-K, stream-K workers} per op: whole-step coordinate-descent tune
   // (scripts/step_tune.py over the scripts/op_bench.py per-op sweep) on one MI355X, batch 100,
-  // single-stream backward with dual dgrad+wgrad launches: fwd+bwd 396 us (was 449 us)
-  static const int defc[OP_COUNT] = {3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3};
-  static const int defs[OP_COUNT] = {1, 1, 1, 1, 8, 16, 4, 1, 4, 1, 16, 1, 1, 32, 1, 64, 1024};
-  static const int defw[OP_COUNT] = {0, 2048, 3072, 3072, 0, 0, 0, 0, 0, 0, 0, 3072, 2048, 0, 2048, 0, 0};
+  // single-stream backward with dual dgrad+wgrad launches: fwd+bwd 394 us (was 449 us)
+  static const int defc[OP_COUNT] = {3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 0, 3, 3, 3, 3, 3};
+  static const int defs[OP_COUNT] = {1, 2, 1, 8, 8, 16, 4, 1, 4, 1, 32, 1, 1, 32, 4, 64, 1024};
+  static const int defw[OP_COUNT] = {0, 0, 3072, 0, 0, 0, 0, 0, 0, 0, 0, 2048, 2048, 0, 0, 0, 0};
+  // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
+  static const bool inl[OP_COUNT] = {0, 1, 0, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0};
   memcpy(cfg, defc, sizeof(defc));
   memcpy(splits, defs, sizeof(defs));
   memcpy(workers, defw, sizeof(defw));
+  for (int op = 0; op < OP_COUNT; ++op) wide[op] = inl[op] ? (1 << 20) : 1;
 }
 
 Engine::~Engine() {
@@ -159,9 +162,9 @@ static auto make_policy(const Engine& e, int B, const float* x, const uint32_t* 
   else if constexpr (OP == OP_CONV4_FWD)
     return ConvFwd<4, 128, 256>{M, N, K, e.p3, P[6], P[7], e.p4, e.c4};
   else if constexpr (OP == OP_FC1_FWD)
-    return FcFwd<true>{M, N, K, e.p4, P[8], P[9], e.h1, seed, 1u, thr, e.inv_keep};
+    return FcFwd<true>{M, N, K, e.p4, P[8], P[9], e.h1, seed, 1u, thr, e.inv_keep, e.seed_value};
   else if constexpr (OP == OP_FC2_FWD)
-    return FcFwd<false>{M, N, K, e.h1, P[10], P[11], e.h2, seed, 2u, thr, e.inv_keep};
+    return FcFwd<false>{M, N, K, e.h1, P[10], P[11], e.h2, seed, 2u, thr, e.inv_keep, e.seed_value};
   else if constexpr (OP == OP_FC2_DGRAD)
     return FcDgradAct{{M, N, K, e.dpre2fc, P[10]}, e.h1, e.inv_keep, e.dpre1fc};
   else if constexpr (OP == OP_FC2_WGRAD)
@@ -190,7 +193,7 @@ template <int OP>
 static void run_op_t(Engine& e, const float* x, int B, const uint32_t* seed, bool train,
                      hipStream_t st, int si) {
   const auto p = make_policy<OP>(e, B, x, seed, train);
-  launch_cfg(e.cfg[OP], p, train ? e.splits[OP] : 1, train ? e.workers[OP] : 0, e.wide_thr,
+  launch_cfg(e.cfg[OP], p, train ? e.splits[OP] : 1, train ? e.workers[OP] : 0, e.wide[OP],
              e.scratch[si], st);
 }
 
@@ -215,10 +218,10 @@ static bool one_wave_cfg(int c) { return c == 0 || c == 2 || c == 3 || c == 4; }
 template <class CA, int OA, int OB, class PA, class PB>
 static void dual_b(Engine& e, const PA& pa, const PB& pb, hipStream_t st) {
   switch (e.cfg[OB]) {
-    case 0: launch_gemm_dual<CA, PA, TileCfg<TILE_0>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide_thr, st); break;
-    case 2: launch_gemm_dual<CA, PA, TileCfg<TILE_2>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide_thr, st); break;
-    case 3: launch_gemm_dual<CA, PA, TileCfg<TILE_3>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide_thr, st); break;
-    default: launch_gemm_dual<CA, PA, TileCfg<TILE_4>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide_thr, st); break;
+    case 0: launch_gemm_dual<CA, PA, TileCfg<TILE_0>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st); break;
+    case 2: launch_gemm_dual<CA, PA, TileCfg<TILE_2>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st); break;
+    case 3: launch_gemm_dual<CA, PA, TileCfg<TILE_3>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st); break;
+    default: launch_gemm_dual<CA, PA, TileCfg<TILE_4>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st); break;
   }
 }
 
@@ -269,7 +272,8 @@ void Engine::backward_segment(int s, const float* x, const int64_t* labels, int 
     switch (s) {
       case 0:
         launch_head_fwd(h2, P[12], P[13], labels, B, dlog, loss, nullptr, st);
-        launch_head_bwd(h2, P[12], dlog, B, seed, thr24, inv_keep, G[12], G[13], dpre2fc, st);
+        launch_head_bwd(h2, P[12], dlog, B, seed, seed_value, thr24, inv_keep, G[12], G[13],
+                        dpre2fc, st);
         wgrad(OP_FC2_WGRAD, x, B, seed, st);
         run_op(OP_FC2_DGRAD, x, B, seed, true, st, 0);
         wgrad(OP_FC1_WGRAD, x, B, seed, st);
@@ -297,7 +301,8 @@ void Engine::backward_segment(int s, const float* x, const int64_t* labels, int 
   switch (s) {
     case 0:
       launch_head_fwd(h2, P[12], P[13], labels, B, dlog, loss, nullptr, st);
-      launch_head_bwd(h2, P[12], dlog, B, seed, thr24, inv_keep, G[12], G[13], dpre2fc, st);
+      launch_head_bwd(h2, P[12], dlog, B, seed, seed_value, thr24, inv_keep, G[12], G[13],
+                        dpre2fc, st);
       run_dual<OP_FC2_DGRAD, OP_FC2_WGRAD>(*this, x, B, seed, st);
       run_dual<OP_FC1_DGRAD, OP_FC1_WGRAD>(*this, x, B, seed, st);
       break;

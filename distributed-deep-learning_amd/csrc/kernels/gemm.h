@@ -580,6 +580,7 @@ inline SubGrid plan_gemm(const P& p, int splits, int workers, int wide_thr,
   g.gz = splitk_z<BK>(p.K, splits);
   g.kchunk = g.gz > 1 ? splitk_kchunk<BK>(p.K, splits) : p.K;
   g.mode = g.gz == 1 ? 0 : (g.gz > wide_thr ? 2 : 1);
+  if (g.mode == 1 && (long long)g.gx * g.gy > sc.max_tiles) g.mode = 2;  // ticket capacity
   g.nblocks = g.gx * g.gy * g.gz;
   return g;
 }
@@ -625,11 +626,11 @@ inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch
 // Problems A and B (one-wave tile configs CA / CB) in one launch, each with its own schedule
 // and its own scratch (slab + tickets); mode-2 reduces follow on the same stream.
 template <class CA, class PA, class CB, class PB>
-inline void launch_gemm_dual(const PA& pa, int sa, int wa, const SplitScratch& sca,
-                             const PB& pb, int sb, int wb, const SplitScratch& scb,
-                             int wide_thr, hipStream_t stream) {
-  const SubGrid ga = plan_gemm<CA::BM, CA::BN, CA::BK>(pa, sa, wa, wide_thr, sca);
-  const SubGrid gb = plan_gemm<CB::BM, CB::BN, CB::BK>(pb, sb, wb, wide_thr, scb);
+inline void launch_gemm_dual(const PA& pa, int sa, int wa, const SplitScratch& sca, int wide_a,
+                             const PB& pb, int sb, int wb, const SplitScratch& scb, int wide_b,
+                             hipStream_t stream) {
+  const SubGrid ga = plan_gemm<CA::BM, CA::BN, CA::BK>(pa, sa, wa, wide_a, sca);
+  const SubGrid gb = plan_gemm<CB::BM, CB::BN, CB::BK>(pb, sb, wb, wide_b, scb);
   const int n = ga.nblocks + gb.nblocks;
   if (n > 0)
     hipLaunchKernelGGL((gemm_dual_kernel<CA, PA, CB, PB>), dim3(n), dim3(64), 0, stream, pa, ga,

@@ -70,6 +70,7 @@ head_fwd_kernel(const float* __restrict__ h2, const float* __restrict__ w,
 __global__ void __launch_bounds__(256)
 head_bwd_kernel(const float* __restrict__ h2, const float* __restrict__ w,
                 const float* __restrict__ dlog, int B, int wblocks, const uint32_t* __restrict__ seed,
+                uint32_t seed_v,
                 uint32_t thr24, float inv_keep, float* __restrict__ gw, float* __restrict__ gb,
                 float* __restrict__ dpre2) {
   if ((int)blockIdx.x < wblocks) {
@@ -111,7 +112,7 @@ head_bwd_kernel(const float* __restrict__ h2, const float* __restrict__ w,
 #pragma unroll
   for (int c = 0; c < HC; ++c) g = fmaf(dlog[(size_t)b * HC + c], w[i * HC + c], g);
   if (thr24) {
-    const uint32_t key = ddl_mix32(*seed + 2u * 0x9E3779B9u);
+    const uint32_t key = ddl_mix32((seed ? *seed : seed_v) + 2u * 0x9E3779B9u);
     g = ddl_keep(key, (uint32_t)idx, thr24) ? g * inv_keep : 0.f;
   }
   dpre2[idx] = g;
@@ -124,12 +125,13 @@ void launch_head_fwd(const float* h2, const float* w, const float* bias, const i
 }
 
 void launch_head_bwd(const float* h2, const float* w, const float* dlog, int B,
-                     const uint32_t* seed, uint32_t thr24, float inv_keep, float* gw, float* gb,
+                     const uint32_t* seed, uint32_t seed_v, uint32_t thr24, float inv_keep,
+                     float* gw, float* gb,
                      float* dpre2, hipStream_t st) {
   const int wblocks = (HK + 1 + 3) / 4;  // one wave per dW_aug row
   const int dblocks = (B * HK + 255) / 256;
   hipLaunchKernelGGL(head_bwd_kernel, dim3(wblocks + dblocks), dim3(256), 0, st, h2, w, dlog, B,
-                     wblocks, seed, thr24, inv_keep, gw, gb, dpre2);
+                     wblocks, seed, seed_v, thr24, inv_keep, gw, gb, dpre2);
 }
 
 }  // namespace ddl

@@ -271,7 +271,8 @@ struct ConvWgrad {
 
 // ---------------------------------------------------------------------------------------------
 // fully connected forward (model.py:70 fc1: +b, ReLU, dropout; :79,82 fc2: +b, dropout)
-// M = B, N = NOUT, K = KIN.  Dropout key derived on device from *seed (graph-replayable).
+// M = B, N = NOUT, K = KIN.  Dropout key derived on device from *seed (graph-replayable),
+// or from seed_v when no seed word is given (the native step runner: no seed-upload kernel).
 // ---------------------------------------------------------------------------------------------
 template <bool RELU>
 struct FcFwd {
@@ -286,6 +287,7 @@ struct FcFwd {
   uint32_t layer;
   uint32_t thr24;                  // 0 => no dropout
   float inv_keep;
+  uint32_t seed_v;                 // dropout seed by value when `seed` is null
 
   using AInfo = LinInfo;
   using BInfo = LinInfo;
@@ -302,7 +304,7 @@ struct FcFwd {
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
     const float bb = bias[n];
     uint32_t key = 0;
-    if (thr24) key = ddl_mix32(*seed + layer * 0x9E3779B9u);
+    if (thr24) key = ddl_mix32((seed ? *seed : seed_v) + layer * 0x9E3779B9u);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = m0 + r;

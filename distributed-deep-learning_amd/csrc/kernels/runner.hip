@@ -21,6 +21,7 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -132,6 +133,32 @@ void SyncRunner::set_units(const std::vector<RunnerUnit>& units) {
       throw std::invalid_argument("RS unit needs exactly one range and a shard buffer");
   }
   units_ = units;
+  // W = 1 (every unit LOCAL): one stream, so per-segment updates buy no overlap — coalesce
+  // all updates into as few launches as possible at the end of the step (ranges adjacent in
+  // both the parameter buffer and the PS state merge).  Same result: no backward GEMM reads a
+  // tensor after its update either way.
+  merged_.clear();
+  all_local_ = true;
+  for (const auto& u : units_) all_local_ &= (u.kind == RunnerUnit::LOCAL);
+  if (!all_local_) return;
+  for (const auto& u : units_)
+    for (const auto& r : u.ranges) merged_.push_back({r, u.ps, u.m, u.v});
+  std::sort(merged_.begin(), merged_.end(), [](const Piece& a, const Piece& b) {
+    return a.r.lo < b.r.lo;
+  });
+  std::vector<Piece> out;
+  for (const auto& p : merged_) {
+    if (!out.empty()) {
+      Piece& q = out.back();
+      if (q.r.hi == p.r.lo && q.ps == p.ps && q.m == p.m && q.v == p.v &&
+          q.r.state_off + (q.r.hi - q.r.lo) == p.r.state_off) {
+        q.r.hi = p.r.hi;
+        continue;
+      }
+    }
+    out.push_back(p);
+  }
+  merged_.swap(out);
 }
 
 void SyncRunner::set_optimizer(int kind, float lr, float b1, float b2, float eps, float mu) {
@@ -185,13 +212,24 @@ void SyncRunner::issue(const RunnerUnit& u, const float* lr_t, hipStream_t st) {
   }
 }
 
-void SyncRunner::step(const float* x, const int64_t* labels, int B, const uint32_t* seed,
+void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t seed_value,
                       const float* lr_t, hipStream_t st) {
+  eng_->seed_value = seed_value;  // dropout seed by kernel argument: no seed-upload kernel
+  const uint32_t* seed = nullptr;
   // Cross-queue dependencies (event record -> stream wait) cost tens of microseconds of GPU
   // idle each on this stack (measured), so LOCAL updates go straight onto the compute
   // stream in order; only units with collectives use the comm stream, which then overlaps
   // the remaining backward segments.
   eng_->forward(x, B, seed, true, st);
+  if (all_local_ && local_on_main_) {
+    for (int s = 0; s < kSegments; ++s) eng_->backward_segment(s, x, labels, B, seed, st);
+    if (coef_ != 1.f)
+      for (const auto& p : merged_) launch_scale(g_ + p.r.lo, p.r.hi - p.r.lo, coef_, st);
+    for (const auto& p : merged_)
+      update(w_ + p.r.lo, g_ + p.r.lo, p.m + p.r.state_off, p.v ? p.v + p.r.state_off : nullptr,
+             p.r.hi - p.r.lo, lr_t[p.ps], st);
+    return;
+  }
   bool comm_used = false;
   for (int s = 0; s < kSegments; ++s) {
     eng_->backward_segment(s, x, labels, B, seed, st);

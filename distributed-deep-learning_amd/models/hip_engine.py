@@ -80,6 +80,14 @@ class HipEngine:
     def get_workers(self) -> List[int]:
         return list(self.eng.get_workers())
 
+    def set_wide(self, wide: List[int]) -> None:
+        """Per-op split-K reduce threshold: splits > wide[op] use the separate wide-reduce
+        kernel, otherwise the in-launch last-arriver reduction (csrc/kernels/gemm.h)."""
+        self.eng.set_wide(list(wide))
+
+    def get_wide(self) -> List[int]:
+        return list(self.eng.get_wide())
+
     def set_concurrent(self, on: bool) -> None:
         """Weight-gradient GEMMs on a second stream (fork/join per backward segment)."""
         self.eng.set_concurrent(bool(on))

@@ -23,7 +23,6 @@ from typing import Dict, Sequence
 import torch
 import torch.distributed as dist
 
-from ..models.hip_engine import _i32
 from ..ops import native
 from ..ops.adam import adam_coeffs
 from .comm import DistEnv, SyncExchange
@@ -95,12 +94,11 @@ class NativeSyncExchange(SyncExchange):
         compute + exchange + update."""
         eng = self.engine
         eng._set_keep(keep_prob)
-        eng.seed_static.fill_(_i32(seed))
         lr = self._lr
         for p, ps in self.servers.items():
             ps.begin()
             lr[p] = adam_coeffs(ps.h, ps.t) if self.optimizer == "adam" else ps.h.lr
-        self.runner.step(x if x.is_contiguous() else x.contiguous(), labels, eng.seed_static, lr)
+        self.runner.step(x if x.is_contiguous() else x.contiguous(), labels, seed & 0xFFFFFFFF, lr)
 
 
 def make_sync_exchange(plan, env, params, grads, segments, servers, engine, cfg, hyper):

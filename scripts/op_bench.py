@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--splits", default="1,2,4,8,16,32")
     ap.add_argument("--cfgs", default="0,1,2,3")
     ap.add_argument("--workers", default="0", help="stream-K worker counts to sweep (0 = none)")
+    ap.add_argument("--m1-max", type=int, default=32,
+                    help="also sweep split-K with the in-launch reduce for splits <= this")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     from ddl_amd.models.layout import CANON_OFFSETS, TOTAL_NUMEL
@@ -66,20 +68,29 @@ def main():
         flop = 2.0 * M * N * K
         row = {}
         # (cfg, splits, workers): split-K points have workers 0, stream-K points splits 1
-        points = [(c, s, 0) for c in cfgs for s in sweep] + [(c, 1, w) for c in cfgs for w in wsweep]
+        # (cfg, splits, workers): split-K points have workers 0 (workers -1: split-K with the
+        # in-launch last-arriver reduce), stream-K points splits 1
+        points = ([(c, s, 0) for c in cfgs for s in sweep]
+                  + [(c, s, -1) for c in cfgs for s in sweep if 1 < s <= a.m1_max]
+                  + [(c, 1, w) for c in cfgs for w in wsweep])
+        base_wide = eng.get_wide()
         for c, s, w in points:
-            cf, sp, wk = list(base_cfg), list(base), list(base_w)
-            cf[op], sp[op], wk[op] = c, s, w
+            cf, sp, wk, wd = list(base_cfg), list(base), list(base_w), list(base_wide)
+            cf[op], sp[op], wk[op] = c, s, max(w, 0)
+            wd[op] = 1 << 20 if w < 0 else 1
             eng.set_splits(sp)
             eng.set_cfg(cf)
             eng.set_workers(wk)
+            eng.set_wide(wd)
             row[(c, s, w)] = time_op(op, a.iters)
         eng.set_splits(base)
         eng.set_cfg(base_cfg)
         eng.set_workers(base_w)
+        eng.set_wide(base_wide)
         best = min(row, key=row.get)
-        best_cfg[op], best_split[op], best_w[op] = best
-        key = lambda t: f"c{t[0]}w{t[2]}" if t[2] else f"c{t[0]}s{t[1]}"
+        best_cfg[op], best_split[op], best_w[op] = best[0], best[1], best[2]
+        key = lambda t: (f"c{t[0]}w{t[2]}" if t[2] > 0 else
+                         f"c{t[0]}s{t[1]}m1" if t[2] < 0 else f"c{t[0]}s{t[1]}")
         dflt = (base_cfg[op], base[op] if not base_w[op] else 1, base_w[op])
         res[name] = {"M": M, "N": N, "K": K, "us": {key(t): v for t, v in row.items()},
                      "best": key(best), "best_us": row[best],
@@ -93,10 +104,14 @@ def main():
                                           for t, v in row.items() if t[0] == c), flush=True)
     print("BEST_CFG", ",".join(map(str, best_cfg)))
     print("BEST_SPLITS", ",".join(map(str, best_split)))
+    best_wide = [1 << 20 if w < 0 else 1 for w in best_w]
+    best_w = [max(w, 0) for w in best_w]
     print("BEST_WORKERS", ",".join(map(str, best_w)))
+    print("BEST_WIDE", ",".join(map(str, best_wide)))
     eng.set_cfg(best_cfg)
     eng.set_splits(best_split)
     eng.set_workers(best_w)
+    eng.set_wide(best_wide)
     # whole step eager vs graph
     for g in (False, True):
         e2 = HipEngine(params, grads, CANON_OFFSETS, batch=B, graph=g, eval_chunk=B)
@@ -104,6 +119,7 @@ def main():
         e2.set_cfg(best_cfg)
         e2.set_splits(best_split)
         e2.set_workers(best_w)
+        e2.set_wide(best_wide)
         for _ in range(5):
             e2.forward_backward(x, y, 0.5, 7)
         torch.cuda.synchronize()

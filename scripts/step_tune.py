@@ -22,9 +22,13 @@ from op_bench import OPS  # noqa: E402  (scripts/ is on sys.path when run as a s
 
 
 def parse_key(k):
-    m = re.fullmatch(r"c(\d+)([sw])(\d+)", k)
+    """c3s16 -> split-K 16 (separate reduce); c3s16m1 -> split-K 16 with the in-launch
+    reduce (workers -1); c3w2048 -> stream-K 2048 workers."""
+    m = re.fullmatch(r"c(\d+)([sw])(\d+)(m1)?", k)
     c, kind, v = int(m.group(1)), m.group(2), int(m.group(3))
-    return (c, v, 0) if kind == "s" else (c, 1, v)
+    if kind == "w":
+        return (c, 1, v)
+    return (c, v, -1 if m.group(4) else 0)
 
 
 def main():
@@ -65,7 +69,8 @@ def main():
     def apply():
         eng.set_cfg(cfg)
         eng.set_splits(spl)
-        eng.set_workers(wk)
+        eng.set_workers([max(w, 0) for w in wk])
+        eng.set_wide([1 << 20 if w < 0 else 1 for w in wk])
 
     def step_us():
         apply()
@@ -106,10 +111,12 @@ def main():
                   flush=True)
     print("DEFAULT_CFG", ",".join(map(str, cfg)))
     print("DEFAULT_SPLITS", ",".join(map(str, spl)))
-    print("DEFAULT_WORKERS", ",".join(map(str, wk)))
+    print("DEFAULT_WORKERS", ",".join(str(max(w, 0)) for w in wk))
+    print("DEFAULT_WIDE", ",".join(str(1 << 20 if w < 0 else 1) for w in wk))
     print(f"final step {cur:.1f} us (default {t_default:.1f} us)")
     if a.json:
-        json.dump({"cfg": cfg, "splits": spl, "workers": wk, "step_us": cur,
+        json.dump({"cfg": cfg, "splits": spl, "workers": [max(w, 0) for w in wk],
+                   "wide": [1 << 20 if w < 0 else 1 for w in wk], "step_us": cur,
                    "default_step_us": t_default}, open(a.json, "w"), indent=1)
 
 

@@ -83,3 +83,28 @@ def simulate_sync(cfg_kw, world, n_train=600):
             acc.div_(world)
         adam_torch_(params, acc, m, v, h, step + 1)
     return params
+
+
+def eval_rank(rank, world, port, outdir):
+    """Distributed (1/W per rank + all-reduce) vs full test-set accuracy after a few steps."""
+    _setup(rank, world, port)
+    try:
+        import torch.distributed as dist
+        from ddl_amd.config import TrainConfig
+        from ddl_amd.parallel.comm import init_distributed
+        from ddl_amd.parallel.roles import Trainer
+        from ddl_amd.utils.data import synthetic_mnist
+        env = init_distributed(device="cpu")
+        tr = Trainer(TrainConfig(mode="sync", shard="contiguous", steps=3, eval_every=0,
+                                 quiet=True), env, dataset=synthetic_mnist(600, 301, seed=9))
+        for i in range(3):
+            tr.train_step(i)
+        dist_acc = tr.evaluate()
+        tr.cfg.dist_eval = False
+        full_acc = tr.evaluate()
+        torch.save({"dist": dist_acc, "full": full_acc}, os.path.join(outdir, f"eval{rank}.pt"))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        traceback.print_exc()
+        raise

@@ -85,3 +85,14 @@ def test_async_single_worker_equals_sync(tmp_path):
     a, cfg = _run(tmp_path, 1, mode="async", shard="contiguous")
     ref = simulate_sync(dict(cfg, mode="sync"), 1)
     assert torch.allclose(_canon(a[0]), ref, atol=2e-6, rtol=0)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_eval_equals_full_eval(tmp_path, world):
+    """Sync mode scores 1/W of the test set per rank (odd split: 301 images) and
+    all-reduces the counts: same accuracy as every rank scoring the whole set."""
+    from dist_helpers import eval_rank, spawn
+    spawn(eval_rank, world, free_port(), str(tmp_path))
+    res = [torch.load(tmp_path / f"eval{r}.pt") for r in range(world)]
+    for r in res:
+        assert r["dist"] == r["full"] == res[0]["full"]

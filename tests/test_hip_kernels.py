@@ -134,14 +134,19 @@ def test_split_k_variants_agree(setup):
     g2 = grads.clone()
     eng.set_splits(base)
     _, r64 = ref_grads(flat, x, y, 0.5, 99, torch.float64)
+    _, r32 = ref_grads(flat, x, y, 0.5, 99, torch.float32)
     for t in TENSORS:
         o = CANON_OFFSETS[t.index]
         ref = r64[t.index].reshape(-1)
-        # conv dW/db reduce 1,600-78,400 cancelling terms over the batch: a single fp32 MFMA
-        # chain (split 1) is legitimately ~1e-3 off fp64 there
-        tol = 5e-5 if t.index > 7 else 5e-3
-        for g in (g0, g1, g2):
-            assert rel_err(g[o:o + t.numel], ref) < tol, t.name
+        # conv dW/db reduce 1,600-78,400 cancelling terms over the batch; and an fp32 forward
+        # can take a different pool/ReLU branch than fp64 on near-ties (at this seed the CPU
+        # fp32 reference itself is 6.4e-3 off fp64 on conv2 dW): bound by the fp32
+        # reference's own error as well
+        e32 = rel_err(r32[t.index].reshape(-1), ref)
+        for name, g in (("default", g0), ("split1", g1), ("split2x", g2)):
+            tol = 5e-5 if t.index > 7 else max(5e-3, 2 * e32 + 1e-6)
+            err = rel_err(g[o:o + t.numel], ref)
+            assert err < tol, (t.name, name, err, e32)
 
 
 @pytest.mark.parametrize("cfg", [None, 0, 1, 2, 4])
@@ -171,6 +176,33 @@ def test_stream_k_matches_reference(setup, cfg):
     finally:
         eng.set_cfg(base_cfg)
         eng.set_workers(base_w)
+
+
+def test_inlaunch_splitk_reduce_matches_reference(setup):
+    """Split-K with the in-launch last-arriver reduce (sc1 hand-off) for every op: fp64
+    reference gradients, bit-deterministic across runs."""
+    eng, flat, params, grads, x, y = setup
+    base_w, base_s, base_wide = eng.get_workers(), eng.get_splits(), eng.get_wide()
+    _, r64 = ref_grads(flat, x, y, 0.5, 77, torch.float64)
+    try:
+        eng.set_workers([0] * len(base_w))
+        eng.set_splits([max(2, min(s, 64)) for s in base_s])
+        eng.set_wide([1 << 20] * len(base_w))
+        outs = []
+        for _ in range(2):
+            grads.zero_()
+            eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 77)
+            torch.cuda.synchronize()
+            outs.append(grads.clone())
+        assert torch.equal(outs[0], outs[1])
+        for t in TENSORS:
+            o = CANON_OFFSETS[t.index]
+            tol = 5e-5 if t.index > 7 else 5e-3
+            assert rel_err(outs[0][o:o + t.numel], r64[t.index].reshape(-1)) < tol, t.name
+    finally:
+        eng.set_workers(base_w)
+        eng.set_splits(base_s)
+        eng.set_wide(base_wide)
 
 
 @pytest.mark.parametrize("conc,dual", [(False, True), (False, False), (True, False)])
