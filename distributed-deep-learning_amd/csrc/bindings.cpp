@@ -285,6 +285,8 @@ class PyRunner {
     r_->step(x.data_ptr<float>(), labels.data_ptr<int64_t>(), (int)x.size(0),
              (uint32_t)(seed & 0xFFFFFFFF), lr_.data(), cur_stream());
   }
+  std::string async_error() { return r_->async_error(); }
+  void abort() { r_->abort(); }
   py::tuple selftest() {
     std::string why;
     bool ok;
@@ -361,7 +363,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_scale", &PyRunner::set_scale)
       .def("set_local_on_main", &PyRunner::set_local_on_main)
       .def("step", &PyRunner::step)
-      .def("selftest", &PyRunner::selftest);
+      .def("selftest", &PyRunner::selftest)
+      .def("async_error", &PyRunner::async_error)
+      .def("abort", &PyRunner::abort);
 
   py::class_<ddl::ShmMailbox>(m, "ShmMailbox")
       .def(py::init<const std::string&, int64_t, bool>(), py::arg("name"), py::arg("capacity"),

@@ -139,6 +139,8 @@ class SyncRunner {
             hipStream_t st);
   bool selftest(std::string* why);
   void set_local_on_main(bool on) { local_on_main_ = on; }
+  std::string async_error();  // "" while the communicator is healthy
+  void abort();               // ncclCommAbort: unblocks this rank's pending collectives
   hipStream_t comm_stream() const { return cs_; }
 
  private:

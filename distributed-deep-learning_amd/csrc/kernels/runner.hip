@@ -60,6 +60,8 @@ struct RcclApi {
   decltype(&ncclBroadcast) Broadcast = nullptr;
   decltype(&ncclGroupStart) GroupStart = nullptr;
   decltype(&ncclGroupEnd) GroupEnd = nullptr;
+  decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;
+  decltype(&ncclCommAbort) CommAbort = nullptr;
 };
 
 static const RcclApi& rccl() {
@@ -84,6 +86,8 @@ static const RcclApi& rccl() {
     a.Broadcast = (decltype(a.Broadcast))sym("ncclBroadcast");
     a.GroupStart = (decltype(a.GroupStart))sym("ncclGroupStart");
     a.GroupEnd = (decltype(a.GroupEnd))sym("ncclGroupEnd");
+    a.CommGetAsyncError = (decltype(a.CommGetAsyncError))sym("ncclCommGetAsyncError");
+    a.CommAbort = (decltype(a.CommAbort))sym("ncclCommAbort");
     return a;
   }();
   return api;
@@ -254,6 +258,23 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
     HIP_CHECK(hipEventRecord(done_ev_, cs_));
     HIP_CHECK(hipStreamWaitEvent(st, done_ev_, 0));
   }
+}
+
+// Failure detection: RCCL reports remote-peer / network failures
+// asynchronously; the trainer polls this between steps and the watchdog aborts the comm (so
+// blocked collectives on this rank return and the job can be torn down) on a hang.
+std::string SyncRunner::async_error() {
+  if (!comm_) return std::string();
+  ncclResult_t st = ncclSuccess;
+  RCCL_CHECK(rccl().CommGetAsyncError(as_comm(comm_), &st));
+  if (st == ncclSuccess || st == ncclInProgress) return std::string();
+  return rccl().GetErrorString(st);
+}
+
+void SyncRunner::abort() {
+  if (!comm_) return;
+  (void)rccl().CommAbort(as_comm(comm_));
+  comm_ = nullptr;
 }
 
 // Collective sanity check used before trusting the native path on a multi-GPU job: the RS

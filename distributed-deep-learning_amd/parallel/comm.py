@@ -280,7 +280,8 @@ class AsyncExchange:
 
     def __init__(self, plan: ShardPlan, env: DistEnv, params: torch.Tensor, grads: torch.Tensor,
                  servers: Dict[int, ParameterServer], steps_per_worker: int,
-                 grad_reduce: str = "sum", mailbox_kind: str = "auto", job_id: str = "ddl"):
+                 grad_reduce: str = "sum", mailbox_kind: str = "auto", job_id: str = "ddl",
+                 check_provenance: bool = False):
         for p in range(plan.num_ps):
             if len(plan.ps_segments(p)) != 1:
                 raise ValueError("async mode needs one contiguous range per PS "
@@ -316,6 +317,14 @@ class AsyncExchange:
         self._thread: Optional[threading.Thread] = None
         self._error: Optional[BaseException] = None
         self.served = 0
+        # Race detection: with check_provenance every push carries a
+        # (step, fp64 checksum) header; the PS verifies that the bytes it applies are exactly
+        # what that worker pushed for that step, that each worker's pushes to a PS arrive in
+        # order with none lost or duplicated, and logs (worker, ps, step, t) per update.
+        self.check_provenance = check_provenance
+        self.provenance: List[Tuple[int, int, int, int]] = []
+        self._last_step: Dict[Tuple[int, int], int] = {}
+        self._push_step: Dict[int, int] = {}
 
     # -- PS service thread -------------------------------------------------------------------------
     def _expected_remote(self) -> int:
@@ -343,13 +352,47 @@ class AsyncExchange:
                     w, p = mbox.decode(v)
                     ps = self.servers[p]
                     g = self.pair_groups[(w, self.env.rank)]
+                    hdr = None
+                    if self.check_provenance:
+                        hdr = torch.empty(2, dtype=torch.float64, device=dev)
+                        dist.recv(hdr, src=w, group=g)
                     dist.recv(ps.gbuf, src=w, group=g)
+                    if hdr is not None:
+                        self._verify(w, p, hdr, ps.gbuf)
                     with ps.exclusive():
                         ps.update_own(ps.gbuf, self.grad_scale)
+                        if hdr is not None:
+                            self.provenance.append((w, p, int(hdr[0].item()), ps.t))
                         dist.send(ps.params, dst=w, group=g)
                     self.served += 1
         except BaseException as e:  # surfaced by join()
             self._error = e
+
+    def _verify(self, w: int, p: int, hdr: torch.Tensor, g: torch.Tensor) -> None:
+        step, want = int(hdr[0].item()), float(hdr[1].item())
+        got = float(g.double().sum().item())
+        if got != want:
+            raise RuntimeError(f"provenance: PS {p} received gradient bytes from worker {w} "
+                               f"step {step} that differ from what it pushed ({got} != {want})")
+        last = self._last_step.get((w, p), -1)
+        if step != last + 1:
+            raise RuntimeError(f"provenance: PS {p} got worker {w} step {step} after step "
+                               f"{last} (lost, duplicated or reordered push)")
+        self._last_step[(w, p)] = step
+
+    def verify_provenance(self) -> None:
+        """After join(): every hosted PS applied exactly `steps` pushes of every remote
+        worker, each once, in step order, and its step counter advanced once per push."""
+        for p, ps in self.servers.items():
+            for w in range(self.env.world):
+                if w == self.env.rank:
+                    continue
+                steps = [s for (ww, pp, s, _) in self.provenance if ww == w and pp == p]
+                if steps != list(range(self.steps)):
+                    raise RuntimeError(f"provenance: PS {p} / worker {w} steps {steps[:5]}...")
+            ts = [t for (_, pp, _, t) in self.provenance if pp == p]
+            if ts != sorted(ts) or len(set(ts)) != len(ts):
+                raise RuntimeError(f"provenance: PS {p} step counter not strictly increasing")
 
     def join(self) -> None:
         if self._thread is not None:
@@ -372,6 +415,12 @@ class AsyncExchange:
             else:
                 g = self.pair_groups[(r, host)]
                 self.remote_boxes[host].push(mbox.encode(r, p))
+                if self.check_provenance:
+                    step = self._push_step.get(p, 0)
+                    self._push_step[p] = step + 1
+                    hdr = torch.tensor([float(step), float(self.grads[lo:hi].double().sum())],
+                                       dtype=torch.float64, device=self.grads.device)
+                    dist.send(hdr, dst=host, group=g)
                 dist.send(self.grads[lo:hi], dst=host, group=g)
                 dist.recv(self.params[lo:hi], src=host, group=g)
 

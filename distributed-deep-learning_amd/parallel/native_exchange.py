@@ -87,6 +87,7 @@ class NativeSyncExchange(SyncExchange):
                                   momentum)
         self.runner.set_scale(self.grad_scale, self.coef)
         self._lr = [0.0] * max(plan.num_ps, env.world)
+        self._n = 0
 
     def step(self, x: torch.Tensor, labels: torch.Tensor, keep_prob: float, seed: int) -> None:
         """One synchronous global step: every hosted PS advances its step counter (one
@@ -99,6 +100,19 @@ class NativeSyncExchange(SyncExchange):
             ps.begin()
             lr[p] = adam_coeffs(ps.h, ps.t) if self.optimizer == "adam" else ps.h.lr
         self.runner.step(x if x.is_contiguous() else x.contiguous(), labels, seed & 0xFFFFFFFF, lr)
+        self._n += 1
+        if self.env.world > 1 and self._n % 64 == 0:
+            self.check()
+
+    def check(self) -> None:
+        """Raise if RCCL reported an asynchronous communicator error."""
+        err = self.runner.async_error()
+        if err:
+            raise RuntimeError(f"RCCL communicator error on rank {self.env.rank}: {err}")
+
+    def abort(self) -> None:
+        """Watchdog hook: abort the communicator so blocked collectives return."""
+        self.runner.abort()
 
 
 def make_sync_exchange(plan, env, params, grads, segments, servers, engine, cfg, hyper):

@@ -88,7 +88,8 @@ class Trainer:
         if asyncm:
             self.exchange = AsyncExchange(self.plan, env, self.params, self.grads, self.servers,
                                           steps_per_worker=self.steps * cfg.epochs,
-                                          grad_reduce=cfg.grad_reduce)
+                                          grad_reduce=cfg.grad_reduce,
+                                          check_provenance=cfg.check_provenance)
         else:
             self.exchange = make_sync_exchange(self.plan, env, self.params, self.grads, segs,
                                                self.servers, self.engine, cfg, hyper)
@@ -141,6 +142,20 @@ class Trainer:
             dist.all_reduce(t)
             return float(t.item()) / n
 
+    def _on_hang(self) -> None:
+        """Watchdog fired: abort the native RCCL communicator (pending collectives return
+        with an error instead of spinning) and end the process so the launcher tears the
+        job down."""
+        import os
+        import sys
+        ab = getattr(self.exchange, "abort", None)
+        if ab is not None:
+            try:
+                ab()
+            except Exception as e:  # best effort: we are exiting anyway
+                sys.stderr.write(f"[watchdog] comm abort failed: {e}\n")
+        os._exit(124)
+
     # ---- reference main loop -----------------------------------------------------------------------
     def train(self) -> dict:
         cfg, env = self.cfg, self.env
@@ -150,7 +165,7 @@ class Trainer:
             ckpt.load(self, cfg.checkpoint_dir)
         if isinstance(self.exchange, AsyncExchange):
             self.exchange.start()
-        wd = Watchdog(cfg.watchdog_s, name=f"rank{env.rank}")
+        wd = Watchdog(cfg.watchdog_s, name=f"rank{env.rank}", on_timeout=self._on_hang)
         t_target = None
         train_wall = 0.0
         for epoch in range(cfg.epochs):
@@ -179,6 +194,10 @@ class Trainer:
                     ckpt.save(self, cfg.checkpoint_dir)
         if isinstance(self.exchange, AsyncExchange):
             self.exchange.join()
+            if cfg.check_provenance:
+                self.exchange.verify_provenance()
+        if getattr(self.exchange, "native", False) and env.world > 1:
+            self.exchange.check()
         if env.device.type == "cuda":
             torch.cuda.synchronize()
         if env.world > 1:

@@ -32,6 +32,7 @@ def train_rank(rank, world, port, cfg_kw, outdir, n_train=600):
         torch.save({"params": tr.params.clone(), "plan_offsets": tr.plan.tensor_offsets,
                     "ps_t": {p: s.t for p, s in tr.servers.items()},
                     "served": getattr(tr.exchange, "served", None),
+                    "provenance": list(getattr(tr.exchange, "provenance", []) or []),
                     "summary": summary},
                    os.path.join(outdir, f"rank{rank}.pt"))
         if world > 1:

@@ -80,6 +80,23 @@ def test_async_serves_every_push(tmp_path, world, shard):
         assert torch.isfinite(rec["params"]).all()
 
 
+@pytest.mark.parametrize("world,kw", [(3, dict(shard="greedy")), (3, dict(shard="contiguous",
+                                                                          num_ps=2))])
+def test_async_provenance_checked(tmp_path, world, kw):
+    """Race-detection mode: every remote push is checksummed and its
+    (worker, step) order verified at the PS (train() raises otherwise); the log holds one
+    entry per applied remote push."""
+    recs, cfg = _run(tmp_path, world, mode="async", check_provenance=True, **kw)
+    steps = cfg["steps"]
+    from ddl_amd.parallel.sharding import make_plan
+    plan = make_plan(kw["shard"], kw.get("num_ps", world))
+    for r, rec in enumerate(recs):
+        hosted = sum(1 for p in range(plan.num_ps) if plan.host_rank(p, world) == r)
+        prov = rec["provenance"]
+        assert len(prov) == hosted * (world - 1) * steps
+        assert all(w != r for (w, _, _, _) in prov)
+
+
 def test_async_single_worker_equals_sync(tmp_path):
     """W=1: async and sync PS do the same math."""
     a, cfg = _run(tmp_path, 1, mode="async", shard="contiguous")
