@@ -62,7 +62,8 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
     cpp_srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     bind = os.path.join(CSRC, "bindings.cpp")
     py_inc = sysconfig.get_paths()["include"]
-    common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", f"-D_GLIBCXX_USE_CXX11_ABI={abi}"]
+    common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+              *os.environ.get("DDL_EXTRA_CFLAGS", "").split()]
     steps = []
     objs = []
     for s in hip_srcs:

@@ -43,8 +43,9 @@ enum Op {
 
 // Block-tile configurations selectable per op at run time (gemm.h template args
 // <BM, BN, BK=32, WM, WN>): 0 = 64x64 (1 wave 64x64), 1 = 128x64 (2 waves 64x64),
-// 2 = 64x32 (1 wave), 3 = 32x32 (1 wave), 4 = 32x64 (1 wave).
-constexpr int NUM_TILE_CFGS = 5;
+// 2 = 64x32 (1 wave), 3 = 32x32 (1 wave), 4 = 32x64 (1 wave),
+// 5 = 32x32 with BK = 16 and the software-pipelined main loop (1 wave).
+constexpr int NUM_TILE_CFGS = 6;
 
 struct Engine {
   const float* P[14] = {};   // parameter tensors v0..v13 (any flat layout)

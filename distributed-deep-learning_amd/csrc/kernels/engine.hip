@@ -19,12 +19,12 @@ namespace ddl {
 Engine::Engine() {
   // {tile config, split-K, stream-K workers} per op: whole-step coordinate-descent tune
   // (scripts/step_tune.py over the scripts/op_bench.py per-op sweep) on one MI355X, batch 100,
-  // single-stream backward with dual dgrad+wgrad launches: fwd+bwd 394 us (was 449 us)
-  static const int defc[OP_COUNT] = {3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 0, 3, 3, 3, 3, 3};
-  static const int defs[OP_COUNT] = {1, 2, 1, 8, 8, 16, 4, 1, 4, 1, 32, 1, 1, 32, 4, 64, 1024};
-  static const int defw[OP_COUNT] = {0, 0, 3072, 0, 0, 0, 0, 0, 0, 0, 0, 2048, 2048, 0, 0, 0, 0};
+  // single-stream backward with dual dgrad+wgrad launches: fwd+bwd 367 us (was 449 us)
+  static const int defc[OP_COUNT] = {3, 3, 3, 3, 3, 3, 3, 5, 3, 5, 3, 3, 3, 3, 3, 5, 3};
+  static const int defs[OP_COUNT] = {1, 2, 1, 8, 8, 16, 4, 1, 4, 1, 1, 8, 8, 16, 4, 32, 1024};
+  static const int defw[OP_COUNT] = {0, 0, 3072, 0, 0, 0, 0, 0, 0, 0, 2048, 0, 0, 0, 0, 0, 0};
   // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
-  static const bool inl[OP_COUNT] = {0, 1, 0, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0};
+  static const bool inl[OP_COUNT] = {0, 1, 0, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0};
   memcpy(cfg, defc, sizeof(defc));
   memcpy(splits, defs, sizeof(defs));
   memcpy(workers, defw, sizeof(defw));
@@ -74,6 +74,7 @@ void Engine::op_shape(int op, int B, int* M, int* N, int* K) {
 #define TILE_2 64, 32, 32, 1, 1
 #define TILE_3 32, 32, 32, 1, 1
 #define TILE_4 32, 64, 32, 1, 1
+#define TILE_5 32, 32, 16, 1, 1   // software-pipelined main loop (gemm.h GemmTile::PIPE)
 
 static size_t slab_need(int c, int M, int N, int K, int s, int w) {
   switch (c) {
@@ -81,7 +82,8 @@ static size_t slab_need(int c, int M, int N, int K, int s, int w) {
     case 1: return gemm_slab_f4<TILE_1>(M, N, K, s, w);
     case 2: return gemm_slab_f4<TILE_2>(M, N, K, s, w);
     case 3: return gemm_slab_f4<TILE_3>(M, N, K, s, w);
-    default: return gemm_slab_f4<TILE_4>(M, N, K, s, w);
+    case 4: return gemm_slab_f4<TILE_4>(M, N, K, s, w);
+    default: return gemm_slab_f4<TILE_5>(M, N, K, s, w);
   }
 }
 
@@ -93,7 +95,8 @@ static void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const Spli
     case 1: launch_gemm<TILE_1>(p, s, wide_thr, sc, st, w); break;
     case 2: launch_gemm<TILE_2>(p, s, wide_thr, sc, st, w); break;
     case 3: launch_gemm<TILE_3>(p, s, wide_thr, sc, st, w); break;
-    default: launch_gemm<TILE_4>(p, s, wide_thr, sc, st, w); break;
+    case 4: launch_gemm<TILE_4>(p, s, wide_thr, sc, st, w); break;
+    default: launch_gemm<TILE_5>(p, s, wide_thr, sc, st, w); break;
   }
 }
 
@@ -213,16 +216,22 @@ void Engine::run_op(int op, const float* x, int B, const uint32_t* seed, bool tr
 }
 
 // ---- dual launches: data- and weight-gradient GEMM of one layer in one kernel -----------------
-static bool one_wave_cfg(int c) { return c == 0 || c == 2 || c == 3 || c == 4; }
+// dual launches are instantiated for these one-wave configs (others run back to back)
+static bool one_wave_cfg(int c) { return c == 0 || c == 3 || c == 4 || c == 5; }
 
 template <class CA, int OA, int OB, class PA, class PB>
 static void dual_b(Engine& e, const PA& pa, const PB& pb, hipStream_t st) {
+#define DDL_DUAL_B(CB) \
+  launch_gemm_dual<CA, PA, TileCfg<CB>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], \
+                                            e.wide[OA], pb, e.splits[OB], e.workers[OB], \
+                                            e.scratch[1], e.wide[OB], st)
   switch (e.cfg[OB]) {
-    case 0: launch_gemm_dual<CA, PA, TileCfg<TILE_0>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st); break;
-    case 2: launch_gemm_dual<CA, PA, TileCfg<TILE_2>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st); break;
-    case 3: launch_gemm_dual<CA, PA, TileCfg<TILE_3>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st); break;
-    default: launch_gemm_dual<CA, PA, TileCfg<TILE_4>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st); break;
+    case 0: DDL_DUAL_B(TILE_0); break;
+    case 3: DDL_DUAL_B(TILE_3); break;
+    case 4: DDL_DUAL_B(TILE_4); break;
+    default: DDL_DUAL_B(TILE_5); break;
   }
+#undef DDL_DUAL_B
 }
 
 // Ops OA and OB (independent) in one launch if both use one-wave tiles, else back to back.
@@ -239,9 +248,9 @@ static void run_dual(Engine& e, const float* x, int B, const uint32_t* seed, hip
   using PB = std::decay_t<decltype(pb)>;
   switch (e.cfg[OA]) {
     case 0: dual_b<TileCfg<TILE_0>, OA, OB, PA, PB>(e, pa, pb, st); break;
-    case 2: dual_b<TileCfg<TILE_2>, OA, OB, PA, PB>(e, pa, pb, st); break;
     case 3: dual_b<TileCfg<TILE_3>, OA, OB, PA, PB>(e, pa, pb, st); break;
-    default: dual_b<TileCfg<TILE_4>, OA, OB, PA, PB>(e, pa, pb, st); break;
+    case 4: dual_b<TileCfg<TILE_4>, OA, OB, PA, PB>(e, pa, pb, st); break;
+    default: dual_b<TileCfg<TILE_5>, OA, OB, PA, PB>(e, pa, pb, st); break;
   }
 }
 

@@ -90,8 +90,176 @@ struct GemmTile {
   static constexpr int WPART = TM * TN * 4 * 64;  // float4 of one wave's partial fragments
 
   // acc = sum over k in [kb, ke) of the (m_blk, n_blk) block tile; kb is a multiple of BK.
+  // One-wave single-fragment tiles with BK = 16 take the software-pipelined loop (its double
+  // register sets fit at 3 waves/SIMD only with the 16-deep K step: at BK = 32 it needed
+  // 256 VGPRs + 64 AGPRs, one wave per SIMD, and lost to the basic loop); others the basic loop.
+  static constexpr bool PIPE = SOLO && TM * TN == 1 && BK == 16;
   static DDL_DEV void mainloop(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
                                f32x16 (&acc)[TM][TN]) {
+    if constexpr (PIPE) mainloop_pipe(p, m_blk, n_blk, kb, ke, lds, acc);
+    else mainloop_basic(p, m_blk, n_blk, kb, ke, lds, acc);
+  }
+
+  // Software-pipelined main loop (one wave, one 32x32 fragment, single LDS buffer).
+  // Per K tile t the wave's 16 MFMAs on fragments F[t&1] (already in VGPRs) are interleaved
+  // with: the LDS store of tile t+1 from global-load registers G[(t+1)&1], the global loads
+  // of tile t+3 into that freed register set (two iterations of latency cover), and the LDS
+  // fragment reads of tile t+1 into F[(t+1)&1].  The LDS ops of a wave execute in order, so
+  // the stores of t+1 cannot overtake the (earlier-issued) reads of t, nor the reads of t+1
+  // the stores.  PMC on the unpipelined loop: MFMA pipe ~40 % busy with waves stalled on
+  // LDS-read latency and on global loads issued only one tile ahead.
+  static DDL_DEV void mainloop_pipe(const P& p, int m_blk, int n_blk, int kb, int ke,
+                                    float* lds, f32x16 (&acc)[TM][TN]) {
+    float* const As = lds;
+    float* const Bs = lds + A_ELEMS;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int nk = (ke - kb + BK - 1) / BK;
+    typename P::AInfo ai[FA];
+    typename P::BInfo bi[FB];
+    int a_off[FA], b_off[FB];
+#pragma unroll
+    for (int it = 0; it < FA; ++it) {
+      const int idx = tid + it * NT;
+      if constexpr (AK) {
+        const int kq = idx % (BK / 4), row = idx / (BK / 4);
+        ai[it] = p.prepA(m_blk + row, kq * 4);
+        a_off[it] = row * SA + kq * 4;
+      } else {
+        const int mq = idx % (BM / 4), kk = idx / (BM / 4);
+        ai[it] = p.prepA(m_blk + mq * 4, kk);
+        a_off[it] = kk * SA + mq * 4;
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < FB; ++it) {
+      const int idx = tid + it * NT;
+      if constexpr (BKC) {
+        const int kq = idx % (BK / 4), row = idx / (BK / 4);
+        bi[it] = p.prepB(n_blk + row, kq * 4);
+        b_off[it] = row * SB + kq * 4;
+      } else {
+        const int nq = idx % (BN / 4), kk = idx / (BN / 4);
+        bi[it] = p.prepB(n_blk + nq * 4, kk);
+        b_off[it] = kk * SB + nq * 4;
+      }
+    }
+    float4 ga0[FA], gb0[FB], ga1[FA], gb1[FB];     // global staging G[0], G[1]
+    float f0a[R][4], f0b[R][4], f1a[R][4], f1b[R][4];  // fragments F[0], F[1]
+    auto gload = [&](int k0, float4 (&ra)[FA], float4 (&rb)[FB]) {
+#pragma unroll
+      for (int it = 0; it < FA; ++it) ra[it] = p.loadA(ai[it], k0);
+#pragma unroll
+      for (int it = 0; it < FB; ++it) rb[it] = p.loadB(bi[it], k0);
+    };
+    auto sstore = [&](const float4 (&ra)[FA], const float4 (&rb)[FB]) {
+#pragma unroll
+      for (int it = 0; it < FA; ++it) *reinterpret_cast<float4*>(As + a_off[it]) = ra[it];
+#pragma unroll
+      for (int it = 0; it < FB; ++it) *reinterpret_cast<float4*>(Bs + b_off[it]) = rb[it];
+    };
+    const int lr = lane & 31, lh = lane >> 5;
+    auto fetch = [&](float (&fa)[R][4], float (&fb)[R][4]) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if constexpr (AK) {
+          const float4 t = *reinterpret_cast<const float4*>(As + lr * SA + r * 8 + 4 * lh);
+          fa[r][0] = t.x; fa[r][1] = t.y; fa[r][2] = t.z; fa[r][3] = t.w;
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) fa[r][s] = As[(r * 8 + 4 * lh + s) * SA + lr];
+        }
+        if constexpr (BKC) {
+          const float4 t = *reinterpret_cast<const float4*>(Bs + lr * SB + r * 8 + 4 * lh);
+          fb[r][0] = t.x; fb[r][1] = t.y; fb[r][2] = t.z; fb[r][3] = t.w;
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) fb[r][s] = Bs[(r * 8 + 4 * lh + s) * SB + lr];
+        }
+      }
+    };
+    f32x16 c0, c1;  // two independent accumulator chains
+#pragma unroll
+    for (int q = 0; q < 16; ++q) { c0[q] = 0.f; c1[q] = 0.f; }
+    auto mfmas = [&](const float (&fa)[R][4], const float (&fb)[R][4]) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          if (s & 1) c1 = mfma32x32x2(fa[r][s], fb[r][s], c1);
+          else c0 = mfma32x32x2(fa[r][s], fb[r][s], c0);
+        }
+    };
+    // Interleave pattern of one steady-state iteration (4R MFMAs, 64 cycles each): the DS
+    // stores of the next tile between the first FA+FB MFMAs, then the next tile's fragment
+    // reads (which must follow those stores) and the global loads between the rest.
+    constexpr int NMF = 4 * R, NST = FA + FB;
+    static_assert(NMF >= 2 * NST, "pipelined loop needs 2 MFMAs per staged float4");
+#ifndef DDL_PIPE_SCHED
+#define DDL_PIPE_SCHED 1
+#endif
+    auto interleave = [&]() {
+      if constexpr (!DDL_PIPE_SCHED) return;
+#pragma unroll
+      for (int i = 0; i < NST; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+      }
+#pragma unroll
+      for (int i = 0; i < NMF - NST; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+      }
+    };
+
+    if (nk > 0) {
+      gload(kb, ga0, gb0);
+      if (nk > 1) gload(kb + BK, ga1, gb1);
+      sstore(ga0, gb0);
+      if (nk > 2) gload(kb + 2 * BK, ga0, gb0);
+      fetch(f0a, f0b);
+    }
+    int kt = 0;
+    // steady state: tiles kt (F0) and kt+1 (F1) per trip; all of kt+1..kt+4 exist
+#ifndef DDL_PIPE_STEADY
+#define DDL_PIPE_STEADY 1
+#endif
+    for (; DDL_PIPE_STEADY && kt + 4 < nk; kt += 2) {
+      sstore(ga1, gb1);                       // tile kt+1
+      gload(kb + (kt + 3) * BK, ga1, gb1);    // tile kt+3
+      fetch(f1a, f1b);                        // fragments of kt+1
+      mfmas(f0a, f0b);                        // tile kt
+      interleave();
+      __builtin_amdgcn_sched_barrier(0);
+      sstore(ga0, gb0);                       // tile kt+2
+      gload(kb + (kt + 4) * BK, ga0, gb0);    // tile kt+4
+      fetch(f0a, f0b);                        // fragments of kt+2
+      mfmas(f1a, f1b);                        // tile kt+1
+      interleave();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // tail: at most 4 tiles left (kt .. nk-1), same rotation with guards
+    for (; kt < nk; ++kt) {
+      const bool odd = (kt & 1) != 0;
+      const bool has1 = kt + 1 < nk, has3 = kt + 3 < nk;
+      if (!odd) {
+        if (has1) sstore(ga1, gb1);
+        if (has3) gload(kb + (kt + 3) * BK, ga1, gb1);
+        if (has1) fetch(f1a, f1b);
+        mfmas(f0a, f0b);
+      } else {
+        if (has1) sstore(ga0, gb0);
+        if (has3) gload(kb + (kt + 3) * BK, ga0, gb0);
+        if (has1) fetch(f0a, f0b);
+        mfmas(f1a, f1b);
+      }
+    }
+    acc[0][0] = c0 + c1;
+  }
+
+  static DDL_DEV void mainloop_basic(const P& p, int m_blk, int n_blk, int kb, int ke,
+                                     float* lds, f32x16 (&acc)[TM][TN]) {
     float* const As0 = lds;
     float* const Bs0 = lds + NBUF * A_ELEMS;
     const int tid = threadIdx.x;

@@ -236,10 +236,14 @@ struct ConvWgrad {
     const int xx = k % H;
     const int t = k / H;
     const int y = t % H, b = t / H;
-    if (a.vec) {
+    if constexpr (CIN % 4 == 0) {
+      // KW = 25*CIN is a multiple of 4, so a 4-row group is either all weight rows (one
+      // 16-B gather) or starts at row >= KW: the ones row (db) then zeros.  Branch-free.
       const int iy = y + a.dy, ix = xx + a.dx;
-      const bool good = kin && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)H;
-      return bload4(r, good ? (((b * H + iy) * H + ix) * CIN + a.ci) * 4 : kOOB);
+      const bool good = a.vec && kin && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)H;
+      float4 v = bload4(r, good ? (((b * H + iy) * H + ix) * CIN + a.ci) * 4 : kOOB);
+      if (a.m == KW) v.x = kin ? 1.f : 0.f;
+      return v;
     }
     float v[4];
 #pragma unroll
@@ -394,7 +398,11 @@ struct FcWgrad {
     const brsrc_t r = make_rsrc(in, (uint32_t)K * KIN * 4u);
     const int k = k0 + a.kk;
     const bool kin = k < K;
-    if (a.ok) return bload4(r, kin ? (k * KIN + a.off) * 4 : kOOB);
+    if ((KIN & 3) == 0) {  // group = all weight rows, or [ones row, 0, 0, 0] / zeros: branch-free
+      float4 v = bload4(r, (a.ok && kin) ? (k * KIN + a.off) * 4 : kOOB);
+      if (a.off == KIN) v.x = kin ? 1.f : 0.f;
+      return v;
+    }
     float v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

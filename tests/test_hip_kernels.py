@@ -149,7 +149,7 @@ def test_split_k_variants_agree(setup):
             assert err < tol, (t.name, name, err, e32)
 
 
-@pytest.mark.parametrize("cfg", [None, 0, 1, 2, 4])
+@pytest.mark.parametrize("cfg", [None, 0, 1, 2, 4, 5])
 def test_stream_k_matches_reference(setup, cfg):
     """Stream-K schedules (several worker counts, every tile config) give the fp64-reference
     gradients, and a given schedule is bit-deterministic across runs."""
