@@ -2,7 +2,12 @@
 """Headline benchmark: MNIST CNN, synchronous sharded parameter server, images/s (whole job).
 
 Config (BASELINE.json): ``mnist_sync_sharding`` — W workers (one per MI355X), one PS shard
-per GPU co-located with the workers, batch 100 per worker (``mnist_sync/worker.py:42``),
+per GPU co-located with the workers, the parameters and Adam state sharded into contiguous
+byte-equal chunks of each gradient bucket so that push/pull are one RCCL reduce-scatter +
+all-gather per bucket (``--shard flat``; in sync mode every policy computes the same update,
+the policy only changes who applies it and the traffic pattern — the reference's
+tensor-granular ``contiguous``/``greedy`` planners are ``--shard contiguous|greedy``),
+batch 100 per worker (``mnist_sync/worker.py:42``),
 Adam 1e-4 on the PS (``model.py:93``), dropout keep 0.5, fp32 (the reference computes in
 fp32 throughout; gfx950 fp32 MFMA), synthetic MNIST-shaped data resident in HBM and
 random (TF1 glorot) init.  Weak scaling: per-GPU batch fixed at 100, so the global batch
@@ -33,8 +38,12 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch-size", type=int, default=100)
-    ap.add_argument("--shard", default="contiguous",
-                    choices=["none", "contiguous", "greedy", "lpt", "flat"])
+    ap.add_argument("--shard", default="flat",
+                    choices=["none", "contiguous", "greedy", "lpt", "flat"],
+                    help="PS shard policy (default flat: one PS per GPU owning a byte-equal "
+                         "contiguous chunk of every gradient bucket -> RCCL reduce-scatter + "
+                         "all-gather, BASELINE.json config; 'contiguous'/'greedy' are the "
+                         "reference's tensor-granular planners -> grouped reduce + broadcast)")
     ap.add_argument("--mode", default="sync", choices=["sync", "async"])
     ap.add_argument("--engine", default="auto", choices=["auto", "hip", "torch"])
     ap.add_argument("--graph", action="store_true",

@@ -37,6 +37,7 @@ class TrainConfig:
     graph: bool = False             # replay the compute step as HIP graphs (eager is faster)
     overlap: bool = True            # bucketed grad push overlapped with backward
     native_exchange: bool = True    # sync step in the C++ SyncRunner (HIP engine on GPU)
+    force_collectives: bool = False  # W = 1: native runner keeps RS/reduce units on a 1-rank comm
     dist_eval: bool = True          # sync, W > 1: each rank scores 1/W of the test set
     check_provenance: bool = False  # async: verify every applied push
     log_jsonl: Optional[str] = None

@@ -228,12 +228,14 @@ class PyRunner {
     ddl::SyncRunner::unique_id(id);
     return py::bytes(id, 128);
   }
-  void init_comm(py::bytes id) {
+  static std::string probe() { return ddl::SyncRunner::probe(); }
+  void init_comm(py::bytes id, bool force) {
     std::string s = id;
     TORCH_CHECK(s.size() == 128, "RCCL unique id must be 128 bytes");
     py::gil_scoped_release nogil;  // collective: blocks until every rank joins
-    r_->init_comm(s.data());
+    r_->init_comm(s.data(), force);
   }
+  bool has_comm() const { return r_->has_comm(); }
   // units: list of (seg, kind, host, ps, [(lo, hi, state_off)], m|None, v|None, shard|None)
   void set_units(py::list units) {
     std::vector<ddl::RunnerUnit> out;
@@ -357,7 +359,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("params"), py::arg("grads"), py::arg("world"), py::arg("rank"),
            py::keep_alive<1, 2>())
       .def_static("unique_id", &PyRunner::unique_id)
-      .def("init_comm", &PyRunner::init_comm)
+      .def_static("probe", &PyRunner::probe)
+      .def("init_comm", &PyRunner::init_comm, py::arg("id"), py::arg("force") = false)
+      .def("has_comm", &PyRunner::has_comm)
       .def("set_units", &PyRunner::set_units)
       .def("set_optimizer", &PyRunner::set_optimizer)
       .def("set_scale", &PyRunner::set_scale)

@@ -130,7 +130,11 @@ class SyncRunner {
   SyncRunner(Engine* eng, float* params, float* grads, int world, int rank);
   ~SyncRunner();
   static void unique_id(char out[128]);
-  void init_comm(const char id[128]);  // collective over all ranks (W > 1)
+  // "" when torch's librccl and every entry point the runner uses resolve, else the reason
+  static std::string probe();
+  // collective over all ranks; W = 1 only with `force` (1-rank communicator: the collective
+  // units then run as RCCL copies — the on-device test of the exchange path on one GPU)
+  void init_comm(const char id[128], bool force = false);
   bool has_comm() const { return comm_ != nullptr; }
   void set_units(const std::vector<RunnerUnit>& units);
   void set_optimizer(int kind, float lr, float b1, float b2, float eps, float mu);
@@ -146,6 +150,10 @@ class SyncRunner {
 
  private:
   void issue(const RunnerUnit& u, const float* lr_t, hipStream_t st);
+  // all REDUCE units of one segment: one RCCL group of reduces, the hosted updates, one
+  // group of broadcasts (instead of two groups per unit)
+  void issue_reduce_group(const std::vector<const RunnerUnit*>& us, const float* lr_t,
+                          hipStream_t st);
   void update(float* w, const float* g, float* m, float* v, int64_t n, float lr_t,
               hipStream_t st);
   Engine* eng_;

@@ -40,8 +40,49 @@
 #pragma once
 #include "common.h"
 #include "scratch.h"
+#include "tail.h"
 
 namespace ddl {
+
+// TF1 ApplyAdam update of one element (optim.hip documents the form).
+DDL_DEV void adam1(float& w, float g, float& m, float& v, float lr_t, float c1, float c2,
+                   float eps) {
+  m += (g - m) * c1;
+  v += (g * g - v) * c2;
+  w -= lr_t * m / (sqrtf(v) + eps);
+}
+
+// One optimizer-tail block (tail.h): kTailF4PerLane float4 of one piece per lane, all loads
+// issued before any math (HBM-bound: memory-level parallelism is the whole game).
+DDL_DEV void tail_body(const UpdTail& t, int b) {
+  int i = 0;
+#pragma unroll
+  for (int q = 1; q < kTailPieces; ++q)
+    if (q < t.npieces && b >= t.p[q].blk0) i = q;
+  const UpdPiece& P = t.p[i];
+  const int64_t n4 = P.n >> 2;
+  const int64_t base = (int64_t)(b - P.blk0) * kTailF4PerBlock + (threadIdx.x & 63);
+  float4* w = reinterpret_cast<float4*>(P.w);
+  const float4* g = reinterpret_cast<const float4*>(P.g);
+  float4* m = reinterpret_cast<float4*>(P.m);
+  float4* v = reinterpret_cast<float4*>(P.v);
+  float4 W[kTailF4PerLane], G[kTailF4PerLane], M[kTailF4PerLane], V[kTailF4PerLane];
+#pragma unroll
+  for (int j = 0; j < kTailF4PerLane; ++j) {
+    const int64_t e = base + j * 64;
+    if (e < n4) { W[j] = w[e]; G[j] = g[e]; M[j] = m[e]; V[j] = v[e]; }
+  }
+#pragma unroll
+  for (int j = 0; j < kTailF4PerLane; ++j) {
+    const int64_t e = base + j * 64;
+    if (e >= n4) continue;
+    adam1(W[j].x, G[j].x * t.scale, M[j].x, V[j].x, P.lr_t, t.c1, t.c2, t.eps);
+    adam1(W[j].y, G[j].y * t.scale, M[j].y, V[j].y, P.lr_t, t.c1, t.c2, t.eps);
+    adam1(W[j].z, G[j].z * t.scale, M[j].z, V[j].z, P.lr_t, t.c1, t.c2, t.eps);
+    adam1(W[j].w, G[j].w * t.scale, M[j].w, V[j].w, P.lr_t, t.c1, t.c2, t.eps);
+    w[e] = W[j]; m[e] = M[j]; v[e] = V[j];
+  }
+}
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -621,10 +662,12 @@ struct TileCfg {
 };
 
 // Two independent GEMM problems in one launch: blocks [0, ga.nblocks) run problem A, the
-// rest problem B.  Both must use one-wave blocks.
+// rest problem B.  Both must use one-wave blocks.  An optional optimizer tail (tail.h) takes
+// the first ut.nblocks blocks (dispatched first, so the HBM-bound update overlaps the GEMM
+// blocks instead of trailing them; a multiple of 8 so the GEMMs' XCD-major numbering holds).
 template <class CA, class PA, class CB, class PB>
 __global__ void __launch_bounds__(64)
-gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb) {
+gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, UpdTail ut) {
   static_assert(CA::NT == 64 && CB::NT == 64, "dual launch needs one-wave blocks");
   using TA = GemmTile<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>;
   using TB = GemmTile<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>;
@@ -632,7 +675,11 @@ gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb) {
   __shared__ float4 lds4[L + 1];
   float* lds = reinterpret_cast<float*>(lds4);
   int* flag = reinterpret_cast<int*>(lds4 + L);
-  const int b = blockIdx.x;
+  if ((int)blockIdx.x < ut.nblocks) {
+    tail_body(ut, blockIdx.x);
+    return;
+  }
+  const int b = blockIdx.x - ut.nblocks;
   if (b < ga.nblocks)
     run_sub<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, b, lds, flag);
   else
@@ -796,13 +843,13 @@ inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch
 template <class CA, class PA, class CB, class PB>
 inline void launch_gemm_dual(const PA& pa, int sa, int wa, const SplitScratch& sca, int wide_a,
                              const PB& pb, int sb, int wb, const SplitScratch& scb, int wide_b,
-                             hipStream_t stream) {
+                             hipStream_t stream, const UpdTail& ut = UpdTail()) {
   const SubGrid ga = plan_gemm<CA::BM, CA::BN, CA::BK>(pa, sa, wa, wide_a, sca);
   const SubGrid gb = plan_gemm<CB::BM, CB::BN, CB::BK>(pb, sb, wb, wide_b, scb);
-  const int n = ga.nblocks + gb.nblocks;
+  const int n = ut.nblocks + ga.nblocks + gb.nblocks;
   if (n > 0)
     hipLaunchKernelGGL((gemm_dual_kernel<CA, PA, CB, PB>), dim3(n), dim3(64), 0, stream, pa, ga,
-                       pb, gb);
+                       pb, gb, ut);
   launch_reduce<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, stream);
   launch_reduce<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, stream);
 }

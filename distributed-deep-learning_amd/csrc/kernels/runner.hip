@@ -119,8 +119,17 @@ void SyncRunner::unique_id(char out[128]) {
   memcpy(out, &id, 128);
 }
 
-void SyncRunner::init_comm(const char id_bytes[128]) {
-  if (world_ <= 1) return;
+std::string SyncRunner::probe() {
+  try {
+    (void)rccl();
+  } catch (const std::exception& e) {
+    return e.what();
+  }
+  return std::string();
+}
+
+void SyncRunner::init_comm(const char id_bytes[128], bool force) {
+  if (world_ <= 1 && !force) return;
   ncclUniqueId id;
   memcpy(&id, id_bytes, 128);
   ncclComm_t c;
@@ -177,6 +186,10 @@ void SyncRunner::update(float* w, const float* g, float* m, float* v, int64_t n,
 }
 
 void SyncRunner::issue(const RunnerUnit& u, const float* lr_t, hipStream_t st) {
+  if (u.kind == RunnerUnit::REDUCE) {
+    issue_reduce_group({&u}, lr_t, st);
+    return;
+  }
   if (coef_ != 1.f)
     for (const auto& r : u.ranges) launch_scale(g_ + r.lo, r.hi - r.lo, coef_, st);
   const float lt = lr_t[u.ps];
@@ -195,25 +208,38 @@ void SyncRunner::issue(const RunnerUnit& u, const float* lr_t, hipStream_t st) {
       update(mine, u.shard, u.m + r.state_off, u.v ? u.v + r.state_off : nullptr, c, lt, st);
       RCCL_CHECK(rccl().AllGather(mine, w_ + r.lo, (size_t)c, ncclFloat32, as_comm(comm_), st));
     } break;
-    case RunnerUnit::REDUCE: {
-      RCCL_CHECK(rccl().GroupStart());
-      for (const auto& r : u.ranges)
-        RCCL_CHECK(rccl().Reduce(g_ + r.lo, g_ + r.lo, (size_t)(r.hi - r.lo), ncclFloat32, ncclSum,
-                              u.host, as_comm(comm_), st));
-      RCCL_CHECK(rccl().GroupEnd());
-      if (rank_ == u.host)
-        for (const auto& r : u.ranges)
-          update(w_ + r.lo, g_ + r.lo, u.m + r.state_off, u.v ? u.v + r.state_off : nullptr,
-                 r.hi - r.lo, lt, st);
-      RCCL_CHECK(rccl().GroupStart());
-      for (const auto& r : u.ranges)
-        RCCL_CHECK(rccl().Broadcast(w_ + r.lo, w_ + r.lo, (size_t)(r.hi - r.lo), ncclFloat32,
-                                 u.host, as_comm(comm_), st));
-      RCCL_CHECK(rccl().GroupEnd());
-    } break;
     default:
       throw std::invalid_argument("unknown unit kind");
   }
+}
+
+// Tensor-granular plans put the units of one backward segment on different hosts (e.g. at
+// W = 8 contiguous: conv4 weight on PS 6, its bias on PS 7).  Grouping every reduce of the
+// segment lets RCCL run them as one launch with the roots' transfers concurrent on
+// different xGMI links, then every broadcast likewise: 2 collective launches per segment
+// instead of 2 per unit (each launch costs ~10-20 us of latency on an 8-GPU ring).
+void SyncRunner::issue_reduce_group(const std::vector<const RunnerUnit*>& us, const float* lr_t,
+                                    hipStream_t st) {
+  for (const RunnerUnit* u : us)
+    if (coef_ != 1.f)
+      for (const auto& r : u->ranges) launch_scale(g_ + r.lo, r.hi - r.lo, coef_, st);
+  RCCL_CHECK(rccl().GroupStart());
+  for (const RunnerUnit* u : us)
+    for (const auto& r : u->ranges)
+      RCCL_CHECK(rccl().Reduce(g_ + r.lo, g_ + r.lo, (size_t)(r.hi - r.lo), ncclFloat32, ncclSum,
+                               u->host, as_comm(comm_), st));
+  RCCL_CHECK(rccl().GroupEnd());
+  for (const RunnerUnit* u : us)
+    if (rank_ == u->host)
+      for (const auto& r : u->ranges)
+        update(w_ + r.lo, g_ + r.lo, u->m + r.state_off, u->v ? u->v + r.state_off : nullptr,
+               r.hi - r.lo, lr_t[u->ps], st);
+  RCCL_CHECK(rccl().GroupStart());
+  for (const RunnerUnit* u : us)
+    for (const auto& r : u->ranges)
+      RCCL_CHECK(rccl().Broadcast(w_ + r.lo, w_ + r.lo, (size_t)(r.hi - r.lo), ncclFloat32,
+                                  u->host, as_comm(comm_), st));
+  RCCL_CHECK(rccl().GroupEnd());
 }
 
 void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t seed_value,
@@ -235,9 +261,11 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
     return;
   }
   bool comm_used = false;
+  std::vector<const RunnerUnit*> reduces;
   for (int s = 0; s < kSegments; ++s) {
     eng_->backward_segment(s, x, labels, B, seed, st);
     bool waited = false;
+    reduces.clear();
     for (const auto& u : units_) {
       if (u.seg != s) continue;
       if (u.kind == RunnerUnit::LOCAL && local_on_main_) {
@@ -249,9 +277,11 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
         HIP_CHECK(hipStreamWaitEvent(cs_, seg_ev_[s], 0));
         waited = true;
       }
-      issue(u, lr_t, cs_);
       comm_used = true;
+      if (u.kind == RunnerUnit::REDUCE) reduces.push_back(&u);
+      else issue(u, lr_t, cs_);
     }
+    if (!reduces.empty()) issue_reduce_group(reduces, lr_t, cs_);
   }
   if (comm_used) {
     // the next step's forward reads the updated parameters
@@ -280,7 +310,7 @@ void SyncRunner::abort() {
 // Collective sanity check used before trusting the native path on a multi-GPU job: the RS
 // and REDUCE patterns on a known pattern, compared on the host.
 bool SyncRunner::selftest(std::string* why) {
-  if (world_ <= 1) return true;
+  if (!comm_) return world_ <= 1;
   const int64_t c = 1031, n = c * world_;
   float *buf = nullptr, *shard = nullptr;
   HIP_CHECK(hipMalloc(&buf, n * sizeof(float)));

@@ -1,0 +1,37 @@
+// Optimizer "tail" riding in a GEMM launch (host-visible descriptor; device body in gemm.h).
+//
+// With one worker (W = 1) every PS update is local and the step is one packed queue, so a
+// stand-alone Adam launch at the end of the step is pure critical path: an HBM-bound pass
+// over w, g, m, v (≈74 MB for the 2.66 M parameters, 18.5 us measured) after the last
+// backward GEMM.  A segment's gradients are final once its backward launches have run, and
+// no later backward launch reads that segment's parameters, so the update of segment s can
+// run as extra blocks of segment s+1's dual dgrad+wgrad launch: memory-bound blocks beside
+// MFMA-bound ones, hidden instead of serialised.  Only the last segment's (conv1 + conv2,
+// 52 k parameters) update remains a launch of its own.
+#pragma once
+#include <stdint.h>
+
+namespace ddl {
+
+constexpr int kTailPieces = 4;
+constexpr int kTailF4PerLane = 8;                    // float4 per lane per tail block
+constexpr int kTailF4PerBlock = 64 * kTailF4PerLane;  // one-wave blocks
+
+struct UpdPiece {
+  float* w = nullptr;      // 16-B aligned, n % 4 == 0 (checked by the host)
+  const float* g = nullptr;
+  float* m = nullptr;
+  float* v = nullptr;
+  int64_t n = 0;           // elements
+  float lr_t = 0.f;        // TF1 Adam step size of the owning PS
+  int blk0 = 0;            // first tail block of this piece
+};
+
+struct UpdTail {
+  int nblocks = 0;         // tail blocks (multiple of 8: keeps the GEMM blocks' XCD mapping)
+  int npieces = 0;
+  UpdPiece p[kTailPieces];
+  float c1 = 0.f, c2 = 0.f, eps = 0.f, scale = 1.f;  // 1 - beta1, 1 - beta2, epsilon, grad scale
+};
+
+}  // namespace ddl

@@ -109,8 +109,12 @@ class SyncExchange:
     def __init__(self, plan: ShardPlan, env: DistEnv, params: torch.Tensor,
                  grads: torch.Tensor, segments: Sequence[Sequence[int]],
                  servers: Dict[int, ParameterServer], grad_reduce: str = "sum",
-                 ref_quirks: bool = False, overlap: bool = True, group=None):
+                 ref_quirks: bool = False, overlap: bool = True, group=None,
+                 force_collectives: bool = False):
         self.plan, self.env = plan, env
+        # W = 1 normally updates locally; forcing keeps the collective unit kinds (run by the
+        # native runner on a 1-rank RCCL communicator: the exchange path tested on one GPU)
+        self.collective = env.world > 1 or force_collectives
         self.params, self.grads = params, grads
         self.servers = servers
         self.group = group
@@ -146,7 +150,7 @@ class SyncExchange:
         if plan.bucket_ranges is not None:
             for bi, (lo, hi) in enumerate(plan.bucket_ranges):
                 ts = tensors_in(lo, hi)
-                if W > 1 and plan.num_ps == W:
+                if self.collective and plan.num_ps == W:
                     u = Unit("rs", ts, [(lo, hi)])
                     c = (hi - lo) // W
                     u.shard_buf = torch.empty(c, dtype=torch.float32, device=self.params.device)
@@ -157,7 +161,7 @@ class SyncExchange:
                     for p in range(plan.num_ps):
                         seg = plan.ps_segments(p)[bi]
                         host = plan.host_rank(p, W)
-                        u = Unit("reduce" if W > 1 else "local", ts, [seg], p, host)
+                        u = Unit("reduce" if self.collective else "local", ts, [seg], p, host)
                         if p in self.servers:
                             u.state_offs = [self.servers[p].seg_off[bi]]
                         units.append(u)
@@ -178,7 +182,7 @@ class SyncExchange:
                         runs[-1] = (runs[-1][0], hi)
                     else:
                         runs.append((lo, hi))
-                u = Unit("reduce" if W > 1 else "local", set(ids), runs, p, host)
+                u = Unit("reduce" if self.collective else "local", set(ids), runs, p, host)
                 u.state_offs = [lo - ps_lo for lo, _ in runs]
                 units.append(u)
         return units

@@ -42,7 +42,8 @@ class NativeSyncExchange(SyncExchange):
     def __init__(self, plan: ShardPlan, env: DistEnv, params: torch.Tensor, grads: torch.Tensor,
                  segments: Sequence[Sequence[int]], servers: Dict[int, ParameterServer], engine,
                  grad_reduce: str = "sum", ref_quirks: bool = False, overlap: bool = True,
-                 optimizer: str = "adam", hyper=None, momentum: float = 0.9):
+                 optimizer: str = "adam", hyper=None, momentum: float = 0.9,
+                 force_collectives: bool = False):
         if optimizer not in ("adam", "momentum"):
             raise NativeUnavailable(f"native runner has no '{optimizer}' update")
         if not params.is_cuda or getattr(engine, "name", "") != "hip":
@@ -50,21 +51,18 @@ class NativeSyncExchange(SyncExchange):
         if len(segments) != 4:
             raise NativeUnavailable("native runner expects the engine's 4 backward segments")
         super().__init__(plan, env, params, grads, segments, servers, grad_reduce, ref_quirks,
-                         overlap=overlap)
+                         overlap=overlap, force_collectives=force_collectives)
         self.engine = engine
         self.optimizer = optimizer
         ops = native.ops()
         self.runner = ops.SyncRunner(engine.eng, params, grads, env.world, env.rank)
         if env.world > 1:
-            ids = [ops.SyncRunner.unique_id() if env.rank == 0 else None]
-            dist.broadcast_object_list(ids, src=0)
-            self.runner.init_comm(ids[0])
+            self._init_comm_collectively(ops, env)
+        elif force_collectives:
+            self.runner.init_comm(ops.SyncRunner.unique_id(), True)
             ok, why = self.runner.selftest()
-            votes = [None] * env.world
-            dist.all_gather_object(votes, (bool(ok), why))
-            bad = [(r, w) for r, (o, w) in enumerate(votes) if not o]
-            if bad:
-                raise NativeUnavailable(f"RCCL self-test failed on ranks {bad}")
+            if not ok:
+                raise RuntimeError(f"RCCL 1-rank self-test failed: {why}")
         seg_sets = [set(s) for s in segments]
 
         def seg_of(tensors):
@@ -88,6 +86,32 @@ class NativeSyncExchange(SyncExchange):
         self.runner.set_scale(self.grad_scale, self.coef)
         self._lr = [0.0] * max(plan.num_ps, env.world)
         self._n = 0
+
+    def _init_comm_collectively(self, ops, env: DistEnv) -> None:
+        """Every go/no-go decision is voted on over the default process group BEFORE any rank
+        enters a blocking RCCL call, so a rank that cannot use the native path makes all ranks
+        fall back together instead of leaving the others stuck in ``ncclCommInitRank``."""
+        def agree(ok: bool, why: str, what: str) -> None:
+            votes = [None] * env.world
+            dist.all_gather_object(votes, (bool(ok), why))
+            bad = [(r, w) for r, (o, w) in enumerate(votes) if not o]
+            if bad:
+                raise NativeUnavailable(f"{what} failed on ranks {bad}")
+
+        why = ops.SyncRunner.probe()
+        agree(not why, why, "RCCL symbol probe")
+        ids = [None, ""]
+        if env.rank == 0:
+            try:
+                ids[0] = ops.SyncRunner.unique_id()
+            except RuntimeError as e:
+                ids[1] = str(e)
+        dist.broadcast_object_list(ids, src=0)
+        if ids[0] is None:
+            raise NativeUnavailable(f"ncclGetUniqueId failed on rank 0: {ids[1]}")
+        self.runner.init_comm(ids[0])
+        ok, why = self.runner.selftest()
+        agree(ok, why, "RCCL self-test")
 
     def step(self, x: torch.Tensor, labels: torch.Tensor, keep_prob: float, seed: int) -> None:
         """One synchronous global step: every hosted PS advances its step counter (one
@@ -122,7 +146,8 @@ def make_sync_exchange(plan, env, params, grads, segments, servers, engine, cfg,
         try:
             return NativeSyncExchange(plan, env, params, grads, segments, servers, engine,
                                       cfg.grad_reduce, cfg.ref_quirks, cfg.overlap,
-                                      cfg.optimizer, hyper, cfg.momentum)
+                                      cfg.optimizer, hyper, cfg.momentum,
+                                      force_collectives=cfg.force_collectives)
         except NativeUnavailable as e:
             if env.rank == 0 and getattr(engine, "name", "") == "hip":
                 print(f"[ddl_amd] native sync runner unavailable ({e}); using the Python "

@@ -27,6 +27,9 @@ def _run(data, native, steps=6, **kw):
                       quiet=True, native_exchange=native, **kw)
     tr = Trainer(cfg, env, dataset=data)
     assert getattr(tr.exchange, "native", False) == native
+    if kw.get("force_collectives"):
+        assert tr.exchange.runner.has_comm()
+        assert any(u.kind != "local" for u in tr.exchange.units)
     for i in range(steps):
         tr.train_step(i)
     torch.cuda.synchronize()
@@ -63,3 +66,28 @@ def test_native_runner_trains(data):
     for i in range(60):
         tr.train_step(i)
     assert tr.evaluate() > max(0.5, acc0 + 0.2)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(shard="flat"),                       # RS unit -> ncclReduceScatter/AllGather
+    dict(shard="contiguous"),                 # REDUCE units -> grouped ncclReduce/Broadcast
+    dict(shard="greedy", num_ps=3),           # several PS hosts, several ranges per unit
+    dict(shard="contiguous", num_ps=2, overlap=False),
+])
+def test_forced_collectives_on_one_rank_match_local(data, kw):
+    """The multi-GPU exchange path on one GPU: torch's librccl resolved by dlsym, a 1-rank
+    communicator, the comm stream waiting on per-segment events, RS/AG and grouped
+    reduce/broadcast units.  With one rank every collective is a copy, so the result must be
+    bit-identical to the local-update path."""
+    p_loc, s_loc = _run(data, True, **kw)
+    p_col, s_col = _run(data, True, force_collectives=True, **kw)
+    assert torch.equal(p_loc, p_col)
+    for p in s_loc:
+        assert s_loc[p][0] == s_col[p][0]
+        assert torch.equal(s_loc[p][1], s_col[p][1])
+        assert torch.equal(s_loc[p][2], s_col[p][2])
+
+
+def test_rccl_probe_resolves_torch_librccl():
+    from ddl_amd.ops import native
+    assert native.ops().SyncRunner.probe() == ""
