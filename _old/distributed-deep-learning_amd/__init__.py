@@ -1,0 +1,27 @@
+"""ddl_amd — MI355X-native parameter-server training framework.
+
+Capabilities mirror epikjjh/DIstributed-Deep-Learning (six ``mnist_*`` variants:
+sync/async parameter servers, single/contiguous/greedy sharding), re-designed for
+MI355X: hand-written gfx950 HIP kernels for the CNN forward/backward and the fused
+TF1-Adam shard update, RCCL (``torch.distributed`` backend ``nccl``) over xGMI for
+gradient push / parameter pull, HIP graphs for the step, and a native shared-memory
+mailbox for the asynchronous control plane.
+
+Sub-packages:
+  models/    layout table of the 14 tensors, the CNN (torch oracle + HIP engine)
+  ops/       native extension loader, kernel wrappers, TF1 Adam, dropout hash
+  parallel/  shard planners, communication plans, PS / worker roles, launcher
+  utils/     data (mnist.pkl / npz / synthetic), metrics, checkpoint, tracing
+"""
+__version__ = "0.1.0"
+
+# Presets named after the reference's six variant directories
+# (reference: mnist_*/run.sh:3).
+VARIANTS = {
+    "mnist_sync": dict(mode="sync", shard="none"),
+    "mnist_async": dict(mode="async", shard="none"),
+    "mnist_sync_sharding": dict(mode="sync", shard="contiguous"),
+    "mnist_async_sharding": dict(mode="async", shard="contiguous"),
+    "mnist_sync_sharding_greedy": dict(mode="sync", shard="greedy"),
+    "mnist_async_sharding_greedy": dict(mode="async", shard="greedy"),
+}

@@ -1,0 +1,378 @@
+// Python bindings of the native extension ``_C`` (kernels launch on torch's current HIP
+// stream so they compose with RCCL collectives and hipGraph capture).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kernels/api.h"
+#include "runtime/mailbox.h"
+
+namespace py = pybind11;
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_f32_cuda(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void adam_flat(at::Tensor w, at::Tensor g, at::Tensor m, at::Tensor v, double lr_t, double b1,
+               double b2, double eps, double scale) {
+  check_f32_cuda(w, "w");
+  check_f32_cuda(g, "g");
+  check_f32_cuda(m, "m");
+  check_f32_cuda(v, "v");
+  const int64_t n = w.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adam_flat: size mismatch");
+  ddl::launch_adam(w.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
+                   v.data_ptr<float>(), n, (float)lr_t, (float)b1, (float)b2, (float)eps,
+                   (float)scale, cur_stream());
+}
+
+void momentum_flat(at::Tensor w, at::Tensor g, at::Tensor m, double lr, double mu, double scale) {
+  check_f32_cuda(w, "w");
+  check_f32_cuda(g, "g");
+  check_f32_cuda(m, "m");
+  const int64_t n = w.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n, "momentum_flat: size mismatch");
+  ddl::launch_momentum(w.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), n,
+                       (float)lr, (float)mu, (float)scale, cur_stream());
+}
+
+// Python-facing wrapper of ddl::Engine: owns the workspace tensor.
+class PyEngine {
+ public:
+  PyEngine(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, int64_t max_batch,
+           int64_t train_batch, double keep_prob)
+      : params_(params), grads_(grads) {
+    TORCH_CHECK(params.size() == 14 && grads.size() == 14, "need 14 parameter/gradient tensors");
+    for (int i = 0; i < 14; ++i) {
+      check_f32_cuda(params[i], "param");
+      check_f32_cuda(grads[i], "grad");
+      e_.P[i] = params[i].data_ptr<float>();
+      e_.G[i] = grads[i].data_ptr<float>();
+    }
+    device_ = params[0].device();
+    e_.max_batch = (int)std::max(max_batch, train_batch);
+    e_.train_batch = (int)train_batch;
+    set_keep_prob(keep_prob);
+    {
+      c10::hip::HIPGuard guard(device_.index());
+      e_.init_streams();
+    }
+    realloc();
+  }
+
+  void set_cfg(std::vector<int64_t> c) {
+    TORCH_CHECK((int)c.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " tile configs");
+    for (int i = 0; i < ddl::OP_COUNT; ++i) {
+      TORCH_CHECK(c[i] >= 0 && c[i] < ddl::NUM_TILE_CFGS, "tile config out of range");
+      e_.cfg[i] = (int)c[i];
+    }
+    realloc();
+  }
+  std::vector<int64_t> get_cfg() const {
+    return std::vector<int64_t>(e_.cfg, e_.cfg + ddl::OP_COUNT);
+  }
+  void set_concurrent(bool on) { e_.concurrent = on; }
+  void set_dual(bool on) { e_.dual = on; }
+  void set_wide_thr(int64_t t) {
+    e_.wide_thr = (int)std::max<int64_t>(1, t);
+    for (int i = 0; i < ddl::OP_COUNT; ++i) e_.wide[i] = e_.wide_thr;
+  }
+  // per-op split-K reduce threshold: z > wide[op] -> separate reduce kernel, else in-launch
+  void set_wide(std::vector<int64_t> w) {
+    TORCH_CHECK((int)w.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " thresholds");
+    for (int i = 0; i < ddl::OP_COUNT; ++i) e_.wide[i] = (int)std::max<int64_t>(1, w[i]);
+  }
+  std::vector<int64_t> get_wide() const {
+    return std::vector<int64_t>(e_.wide, e_.wide + ddl::OP_COUNT);
+  }
+
+  void set_keep_prob(double keep) {
+    const double rate = 1.0 - keep;
+    e_.thr24 = (uint32_t)std::llround(rate * 16777216.0);
+    e_.inv_keep = keep > 0.0 ? (float)(1.0 / keep) : 0.f;
+  }
+
+  void set_splits(std::vector<int64_t> s) {
+    TORCH_CHECK((int)s.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " split factors");
+    for (int i = 0; i < ddl::OP_COUNT; ++i) e_.splits[i] = (int)std::max<int64_t>(1, s[i]);
+    realloc();
+  }
+  std::vector<int64_t> get_splits() const {
+    return std::vector<int64_t>(e_.splits, e_.splits + ddl::OP_COUNT);
+  }
+  // stream-K worker counts per op (0 = split-K by `splits`)
+  void set_workers(std::vector<int64_t> w) {
+    TORCH_CHECK((int)w.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " worker counts");
+    for (int i = 0; i < ddl::OP_COUNT; ++i) {
+      TORCH_CHECK(w[i] >= 0 && w[i] <= (1 << 20), "worker count out of range");
+      e_.workers[i] = (int)w[i];
+    }
+    realloc();
+  }
+  std::vector<int64_t> get_workers() const {
+    return std::vector<int64_t>(e_.workers, e_.workers + ddl::OP_COUNT);
+  }
+
+  void forward(at::Tensor x, at::Tensor seed, bool train) {
+    check_x(x);
+    e_.forward(x.data_ptr<float>(), (int)x.size(0), seed_ptr(seed), train, cur_stream());
+  }
+  void backward_segment(int64_t s, at::Tensor x, at::Tensor labels, at::Tensor seed) {
+    check_x(x);
+    TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_cuda(), "labels must be int64 GPU");
+    e_.backward_segment((int)s, x.data_ptr<float>(), labels.data_ptr<int64_t>(), (int)x.size(0),
+                        seed_ptr(seed), cur_stream());
+  }
+  void run_op(int64_t op, at::Tensor x, at::Tensor seed, bool train) {
+    check_x(x);
+    e_.run_op((int)op, x.data_ptr<float>(), (int)x.size(0), seed_ptr(seed), train, cur_stream());
+  }
+  void zero_correct() {
+    TORCH_CHECK(hipMemsetAsync(e_.correct, 0, sizeof(int), cur_stream()) == hipSuccess);
+  }
+  void eval_count(at::Tensor x, at::Tensor labels) {
+    check_x(x);
+    e_.eval_count(x.data_ptr<float>(), labels.data_ptr<int64_t>(), (int)x.size(0), cur_stream());
+  }
+  void head_fwd(at::Tensor labels, int64_t B) {
+    ddl::launch_head_fwd(e_.h2, e_.P[12], e_.P[13], labels.data_ptr<int64_t>(), (int)B, e_.dlog,
+                         e_.loss, nullptr, cur_stream());
+  }
+
+  // Views of internal buffers (testing / debugging).  Shapes are for batch B.
+  at::Tensor buffer(const std::string& name, int64_t B) {
+    auto f = at::TensorOptions().dtype(at::kFloat).device(device_);
+    auto u8 = at::TensorOptions().dtype(at::kByte).device(device_);
+    auto i32 = at::TensorOptions().dtype(at::kInt).device(device_);
+    if (name == "p1") return torch::from_blob(e_.p1, {B, 14, 14, 32}, f);
+    if (name == "p2") return torch::from_blob(e_.p2, {B, 7, 7, 64}, f);
+    if (name == "p3") return torch::from_blob(e_.p3, {B, 4, 4, 128}, f);
+    if (name == "p4") return torch::from_blob(e_.p4, {B, 1024}, f);
+    if (name == "h1") return torch::from_blob(e_.h1, {B, 1024}, f);
+    if (name == "h2") return torch::from_blob(e_.h2, {B, 512}, f);
+    if (name == "dlog") return torch::from_blob(e_.dlog, {B, 10}, f);
+    if (name == "loss") return torch::from_blob(e_.loss, {B}, f);
+    if (name == "dpre2fc") return torch::from_blob(e_.dpre2fc, {B, 512}, f);
+    if (name == "dpre1fc") return torch::from_blob(e_.dpre1fc, {B, 1024}, f);
+    if (name == "d4") return torch::from_blob(e_.d4, {B, 4, 4, 256}, f);
+    if (name == "d3") return torch::from_blob(e_.d3, {B, 7, 7, 128}, f);
+    if (name == "d2") return torch::from_blob(e_.d2, {B, 14, 14, 64}, f);
+    if (name == "d1") return torch::from_blob(e_.d1, {B, 28, 28, 32}, f);
+    if (name == "c1") return torch::from_blob(e_.c1, {B, 14, 14, 32}, u8);
+    if (name == "c2") return torch::from_blob(e_.c2, {B, 7, 7, 64}, u8);
+    if (name == "c3") return torch::from_blob(e_.c3, {B, 4, 4, 128}, u8);
+    if (name == "c4") return torch::from_blob(e_.c4, {B, 1024}, u8);
+    if (name == "correct") return torch::from_blob(e_.correct, {1}, i32);
+    TORCH_CHECK(false, "unknown buffer ", name);
+  }
+
+  int64_t max_batch() const { return e_.max_batch; }
+  ddl::Engine* raw() { return &e_; }
+  void check_batch(const at::Tensor& x) { check_x(x); }
+  int64_t workspace_bytes() const { return (int64_t)e_.workspace_bytes(); }
+  static std::vector<int64_t> op_shape(int64_t op, int64_t B) {
+    int M, N, K;
+    ddl::Engine::op_shape((int)op, (int)B, &M, &N, &K);
+    return {M, N, K};
+  }
+
+ private:
+  void realloc() {
+    e_.slab_floats = e_.slab_floats_needed(e_.train_batch);
+    const size_t bytes = e_.workspace_bytes();
+    // zeroed once: the split-K arrival tickets must start at 0 (reducers re-arm them)
+    ws_ = at::zeros({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).device(device_));
+    e_.bind_workspace(ws_.data_ptr());
+  }
+  void check_x(const at::Tensor& x) {
+    check_f32_cuda(x, "x");
+    TORCH_CHECK(x.dim() == 2 && x.size(1) == 784, "x must be [B,784]");
+    TORCH_CHECK(x.size(0) <= e_.max_batch, "batch ", x.size(0), " exceeds engine max_batch ",
+                e_.max_batch);
+  }
+  static const uint32_t* seed_ptr(const at::Tensor& s) {
+    if (!s.defined() || s.numel() == 0) return nullptr;
+    TORCH_CHECK(s.is_cuda() && s.scalar_type() == at::kInt, "seed must be an int32 GPU tensor");
+    return reinterpret_cast<const uint32_t*>(s.data_ptr<int32_t>());
+  }
+
+  ddl::Engine e_;
+  std::vector<at::Tensor> params_, grads_;
+  at::Tensor ws_;
+  at::Device device_{at::kCPU};
+};
+
+// Python-facing wrapper of ddl::SyncRunner (native sync step: engine + exchange + update).
+class PyRunner {
+ public:
+  PyRunner(PyEngine& eng, at::Tensor params, at::Tensor grads, int64_t world, int64_t rank)
+      : eng_(eng), params_(params), grads_(grads) {
+    check_f32_cuda(params, "params");
+    check_f32_cuda(grads, "grads");
+    TORCH_CHECK(params.numel() == grads.numel(), "params/grads size mismatch");
+    r_ = std::make_unique<ddl::SyncRunner>(eng.raw(), params.data_ptr<float>(),
+                                           grads.data_ptr<float>(), (int)world, (int)rank);
+  }
+  static py::bytes unique_id() {
+    char id[128];
+    ddl::SyncRunner::unique_id(id);
+    return py::bytes(id, 128);
+  }
+  void init_comm(py::bytes id) {
+    std::string s = id;
+    TORCH_CHECK(s.size() == 128, "RCCL unique id must be 128 bytes");
+    py::gil_scoped_release nogil;  // collective: blocks until every rank joins
+    r_->init_comm(s.data());
+  }
+  // units: list of (seg, kind, host, ps, [(lo, hi, state_off)], m|None, v|None, shard|None)
+  void set_units(py::list units) {
+    std::vector<ddl::RunnerUnit> out;
+    keep_.clear();
+    const int64_t n = params_.numel();
+    for (auto item : units) {
+      auto t = item.cast<py::tuple>();
+      TORCH_CHECK(t.size() == 8, "unit tuple must have 8 fields");
+      ddl::RunnerUnit u;
+      u.seg = t[0].cast<int>();
+      u.kind = t[1].cast<int>();
+      u.host = t[2].cast<int>();
+      u.ps = t[3].cast<int>();
+      auto opt_ptr = [&](py::handle h, int64_t need, const char* what) -> float* {
+        if (h.is_none()) return nullptr;
+        at::Tensor x = h.cast<at::Tensor>();
+        check_f32_cuda(x, what);
+        TORCH_CHECK(x.numel() >= need, what, " too small");
+        keep_.push_back(x);
+        return x.data_ptr<float>();
+      };
+      int64_t need_state = 0;
+      for (auto r : t[4].cast<py::list>()) {
+        auto rr = r.cast<py::tuple>();
+        ddl::RunnerRange range{rr[0].cast<int64_t>(), rr[1].cast<int64_t>(), rr[2].cast<int64_t>()};
+        TORCH_CHECK(0 <= range.lo && range.lo <= range.hi && range.hi <= n, "range out of bounds");
+        const int64_t len = u.kind == ddl::RunnerUnit::RS ? 0 : range.hi - range.lo;
+        need_state = std::max(need_state, range.state_off + len);
+        u.ranges.push_back(range);
+      }
+      u.m = opt_ptr(t[5], need_state, "m");
+      u.v = opt_ptr(t[6], need_state, "v");
+      u.shard = opt_ptr(t[7], 0, "shard");
+      out.push_back(std::move(u));
+    }
+    r_->set_units(out);
+  }
+  void set_optimizer(int64_t kind, double lr, double b1, double b2, double eps, double mu) {
+    r_->set_optimizer((int)kind, (float)lr, (float)b1, (float)b2, (float)eps, (float)mu);
+  }
+  void set_scale(double grad_scale, double coef) { r_->set_scale((float)grad_scale, (float)coef); }
+  void set_local_on_main(bool on) { r_->set_local_on_main(on); }
+  void step(at::Tensor x, at::Tensor labels, int64_t seed, std::vector<double> lr_t) {
+    eng_.check_batch(x);
+    TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_cuda(), "labels must be int64 GPU");
+    TORCH_CHECK(labels.numel() == x.size(0), "labels/batch size mismatch");
+    lr_.assign(lr_t.begin(), lr_t.end());
+    if (lr_.empty()) lr_.push_back(0.f);
+    r_->step(x.data_ptr<float>(), labels.data_ptr<int64_t>(), (int)x.size(0),
+             (uint32_t)(seed & 0xFFFFFFFF), lr_.data(), cur_stream());
+  }
+  std::string async_error() { return r_->async_error(); }
+  void abort() { r_->abort(); }
+  py::tuple selftest() {
+    std::string why;
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = r_->selftest(&why);
+    }
+    return py::make_tuple(ok, why);
+  }
+
+ private:
+  PyEngine& eng_;
+  at::Tensor params_, grads_;
+  std::vector<at::Tensor> keep_;
+  std::vector<float> lr_;
+  std::unique_ptr<ddl::SyncRunner> r_;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "ddl_amd native extension: gfx950 HIP kernels + C++ runtime";
+  m.def("adam_flat", &adam_flat, "Fused TF1 Adam on a flat shard",
+        py::arg("w"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr_t"), py::arg("b1"),
+        py::arg("b2"), py::arg("eps"), py::arg("scale") = 1.0);
+  m.def("momentum_flat", &momentum_flat, "Fused momentum SGD on a flat shard");
+  m.def("mfma_peak", [](at::Tensor out, int64_t blocks, int64_t iters) {
+    check_f32_cuda(out, "out");
+    TORCH_CHECK(out.numel() >= blocks * 64, "out too small");
+    ddl::launch_mfma_peak(out.data_ptr<float>(), (int)blocks, (int)iters, cur_stream());
+  }, "diagnostic: 2 chains of v_mfma_f32_32x32x2_f32 per wave (2*iters MFMAs)");
+  m.def("gemm_nomem", [](at::Tensor out, at::Tensor slab, int64_t M, int64_t N, int64_t K,
+                         int64_t splits) {
+    ddl::launch_gemm_nomem(out.data_ptr<float>(), (int)M, (int)N, (int)K, (int)splits,
+                           slab.data_ptr(), nullptr, cur_stream());
+  }, "diagnostic: engine GEMM structure with register-only operand loads");
+  m.attr("OP_COUNT") = (int)ddl::OP_COUNT;
+
+  py::class_<PyEngine>(m, "Engine")
+      .def(py::init<std::vector<at::Tensor>, std::vector<at::Tensor>, int64_t, int64_t, double>(),
+           py::arg("params"), py::arg("grads"), py::arg("max_batch"), py::arg("train_batch"),
+           py::arg("keep_prob"))
+      .def("set_keep_prob", &PyEngine::set_keep_prob)
+      .def("set_splits", &PyEngine::set_splits)
+      .def("get_splits", &PyEngine::get_splits)
+      .def("set_workers", &PyEngine::set_workers)
+      .def("get_workers", &PyEngine::get_workers)
+      .def("set_cfg", &PyEngine::set_cfg)
+      .def("get_cfg", &PyEngine::get_cfg)
+      .def("set_concurrent", &PyEngine::set_concurrent)
+      .def("set_dual", &PyEngine::set_dual)
+      .def("set_wide_thr", &PyEngine::set_wide_thr)
+      .def("set_wide", &PyEngine::set_wide)
+      .def("get_wide", &PyEngine::get_wide)
+      .def("forward", &PyEngine::forward)
+      .def("backward_segment", &PyEngine::backward_segment)
+      .def("run_op", &PyEngine::run_op)
+      .def("zero_correct", &PyEngine::zero_correct)
+      .def("eval_count", &PyEngine::eval_count)
+      .def("head_fwd", &PyEngine::head_fwd)
+      .def("buffer", &PyEngine::buffer)
+      .def("max_batch", &PyEngine::max_batch)
+      .def("workspace_bytes", &PyEngine::workspace_bytes)
+      .def_static("op_shape", &PyEngine::op_shape);
+
+  py::class_<PyRunner>(m, "SyncRunner")
+      .def(py::init<PyEngine&, at::Tensor, at::Tensor, int64_t, int64_t>(), py::arg("engine"),
+           py::arg("params"), py::arg("grads"), py::arg("world"), py::arg("rank"),
+           py::keep_alive<1, 2>())
+      .def_static("unique_id", &PyRunner::unique_id)
+      .def("init_comm", &PyRunner::init_comm)
+      .def("set_units", &PyRunner::set_units)
+      .def("set_optimizer", &PyRunner::set_optimizer)
+      .def("set_scale", &PyRunner::set_scale)
+      .def("set_local_on_main", &PyRunner::set_local_on_main)
+      .def("step", &PyRunner::step)
+      .def("selftest", &PyRunner::selftest)
+      .def("async_error", &PyRunner::async_error)
+      .def("abort", &PyRunner::abort);
+
+  py::class_<ddl::ShmMailbox>(m, "ShmMailbox")
+      .def(py::init<const std::string&, int64_t, bool>(), py::arg("name"), py::arg("capacity"),
+           py::arg("create"))
+      .def("push", &ddl::ShmMailbox::push, py::call_guard<py::gil_scoped_release>())
+      .def("pop", &ddl::ShmMailbox::pop, py::call_guard<py::gil_scoped_release>())
+      .def("size", &ddl::ShmMailbox::size)
+      .def("capacity", &ddl::ShmMailbox::capacity)
+      .def("unlink", &ddl::ShmMailbox::unlink);
+}

@@ -1,0 +1,174 @@
+// Host-side launch API of the gfx950 kernels (raw device pointers + hipStream_t; no torch).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "scratch.h"
+
+namespace ddl {
+
+// ---- optimizer (optim.hip) -------------------------------------------------------------------
+void launch_adam(float* w, const float* g, float* m, float* v, int64_t n, float lr_t, float b1,
+                 float b2, float eps, float scale, hipStream_t st);
+void launch_momentum(float* w, const float* g, float* m, int64_t n, float lr, float mu,
+                     float scale, hipStream_t st);
+void launch_scale(float* p, int64_t n, float a, hipStream_t st);
+
+// ---- classifier head (head.hip) --------------------------------------------------------------
+void launch_head_fwd(const float* h2, const float* w, const float* bias, const int64_t* labels,
+                     int B, float* dlog, float* loss, int* correct, hipStream_t st);
+void launch_head_bwd(const float* h2, const float* w, const float* dlog, int B,
+                     const uint32_t* seed, uint32_t seed_v, uint32_t thr24, float inv_keep,
+                     float* gw, float* gb, float* dpre2, hipStream_t st);
+
+// ---- diagnostics (diag.hip) -------------------------------------------------------------------
+void launch_mfma_peak(float* out, int blocks, int iters, hipStream_t st);
+void launch_gemm_nomem(float* out, int M, int N, int K, int splits, void* slab, int* tickets,
+                       hipStream_t st);
+
+// ---- the CNN step engine (engine.hip) --------------------------------------------------------
+// GEMM-shaped ops, in SURVEY.md §2.6 order.  Index into Engine::splits / Engine::cfg.
+enum Op {
+  OP_CONV1_FWD = 0, OP_CONV2_FWD, OP_CONV3_FWD, OP_CONV4_FWD, OP_FC1_FWD, OP_FC2_FWD,
+  OP_FC2_DGRAD, OP_FC2_WGRAD, OP_FC1_DGRAD, OP_FC1_WGRAD,
+  OP_CONV4_DGRAD, OP_CONV4_WGRAD, OP_CONV3_DGRAD, OP_CONV3_WGRAD,
+  OP_CONV2_DGRAD, OP_CONV2_WGRAD, OP_CONV1_WGRAD,
+  OP_COUNT
+};
+
+// Block-tile configurations selectable per op at run time (gemm.h template args
+// <BM, BN, BK=32, WM, WN>): 0 = 64x64 (1 wave 64x64), 1 = 128x64 (2 waves 64x64),
+// 2 = 64x32 (1 wave), 3 = 32x32 (1 wave), 4 = 32x64 (1 wave),
+// 5 = 32x32 with BK = 16 and the software-pipelined main loop (1 wave).
+constexpr int NUM_TILE_CFGS = 6;
+
+struct Engine {
+  const float* P[14] = {};   // parameter tensors v0..v13 (any flat layout)
+  float* G[14] = {};         // gradient tensors v0..v13
+  int max_batch = 0;         // activation buffers sized for this batch
+  int train_batch = 0;       // slab sized for this batch with the current splits/cfgs
+  int splits[OP_COUNT];
+  int cfg[OP_COUNT];
+  int workers[OP_COUNT];     // > 0: stream-K with this many workers (overrides splits)
+  int wide_thr = 1;          // default split count above which the separate wide reduce is used
+  int wide[OP_COUNT];        // per op: z > wide[op] -> separate wide reduce (mode 2), else the
+                             // in-launch last-arriver reduction (mode 1)
+  uint32_t thr24 = 0;        // dropout threshold (train)
+  uint32_t seed_value = 0;   // dropout seed used when a step is given no device seed word
+  float inv_keep = 1.f;
+  // weight-gradient GEMMs on a second stream.  Off by default: a cross-queue event wait costs
+  // tens of microseconds of GPU idle on MI355X/ROCm (step timelines), more than the overlap
+  // gains; dgrad/wgrad concurrency comes from fused dual-problem launches instead.
+  bool concurrent = false;
+  bool dual = true;          // single stream: dgrad + wgrad of a layer in one launch
+
+  // workspace carve-out
+  float *p1 = nullptr, *p2 = nullptr, *p3 = nullptr, *p4 = nullptr, *h1 = nullptr, *h2 = nullptr;
+  float *dlog = nullptr, *loss = nullptr, *dpre2fc = nullptr, *dpre1fc = nullptr;
+  float *d4 = nullptr, *d3 = nullptr, *d2 = nullptr, *d1 = nullptr;
+  uint8_t *c1 = nullptr, *c2 = nullptr, *c3 = nullptr, *c4 = nullptr;
+  int* correct = nullptr;
+  size_t slab_floats = 0;
+  SplitScratch scratch[2];   // [0] main stream, [1] weight-gradient stream
+  static constexpr int kMaxTickets = 8192;
+
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+
+  Engine();
+  ~Engine();
+  void init_streams();
+  // M, N, K of op `op` at batch B (used for slab sizing and by tests)
+  static void op_shape(int op, int B, int* M, int* N, int* K);
+  size_t slab_floats_needed(int B) const;
+  size_t workspace_bytes() const;
+  void bind_workspace(void* base);
+
+  // forward through fc2 (train: dropout on, configured split-K; eval: no dropout, no split)
+  void forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st);
+  // backward segment s (0: head+fc, 1: conv4, 2: conv3, 3: conv2+conv1); weight-gradient
+  // GEMMs fork onto the side stream and join back at the end of the segment
+  void backward_segment(int s, const float* x, const int64_t* labels, int B,
+                        const uint32_t* seed, hipStream_t st);
+  // eval: forward(train=false) + correct-count accumulation into *correct
+  void eval_count(const float* x, const int64_t* labels, int B, hipStream_t st);
+  // run a single GEMM op on `st` with scratch `si` (tests / tuning)
+  void run_op(int op, const float* x, int B, const uint32_t* seed, bool train, hipStream_t st,
+              int si = 0);
+
+ private:
+  void fork(hipStream_t st);
+  void join(hipStream_t st);
+  void wgrad(int op, const float* x, int B, const uint32_t* seed, hipStream_t st);
+};
+
+// ---- native synchronous step runner (runner.hip) -------------------------------------------
+struct RunnerRange {
+  int64_t lo, hi;       // plan-buffer element range [lo, hi)
+  int64_t state_off;    // offset of the range's optimizer state in the unit's m / v
+};
+struct RunnerUnit {
+  enum Kind { LOCAL = 0, RS = 1, REDUCE = 2 };
+  int seg = 0;          // backward segment after which the unit's gradients are complete
+  int kind = LOCAL;
+  int host = 0;         // REDUCE: rank that owns the PS
+  int ps = 0;           // index into the per-step lr_t table (RS: this rank's PS)
+  std::vector<RunnerRange> ranges;
+  float* m = nullptr;   // optimizer state base of the owning PS (null where not hosted)
+  float* v = nullptr;
+  float* shard = nullptr;  // RS: 1/W chunk buffer
+};
+
+class SyncRunner {
+ public:
+  static constexpr int kSegments = 4;
+  SyncRunner(Engine* eng, float* params, float* grads, int world, int rank);
+  ~SyncRunner();
+  static void unique_id(char out[128]);
+  void init_comm(const char id[128]);  // collective over all ranks (W > 1)
+  bool has_comm() const { return comm_ != nullptr; }
+  void set_units(const std::vector<RunnerUnit>& units);
+  void set_optimizer(int kind, float lr, float b1, float b2, float eps, float mu);
+  void set_scale(float grad_scale, float coef) { grad_scale_ = grad_scale; coef_ = coef; }
+  // one synchronous training step on stream `st`; lr_t indexed by RunnerUnit::ps
+  void step(const float* x, const int64_t* labels, int B, uint32_t seed, const float* lr_t,
+            hipStream_t st);
+  bool selftest(std::string* why);
+  void set_local_on_main(bool on) { local_on_main_ = on; }
+  std::string async_error();  // "" while the communicator is healthy
+  void abort();               // ncclCommAbort: unblocks this rank's pending collectives
+  hipStream_t comm_stream() const { return cs_; }
+
+ private:
+  void issue(const RunnerUnit& u, const float* lr_t, hipStream_t st);
+  void update(float* w, const float* g, float* m, float* v, int64_t n, float lr_t,
+              hipStream_t st);
+  Engine* eng_;
+  float* w_;
+  float* g_;
+  int world_, rank_;
+  void* comm_ = nullptr;  // ncclComm_t
+  hipStream_t cs_ = nullptr;
+  hipEvent_t seg_ev_[kSegments] = {};
+  hipEvent_t done_ev_ = nullptr;
+  std::vector<RunnerUnit> units_;
+  int opt_ = 0;
+  float lr_ = 1e-4f, b1_ = 0.9f, b2_ = 0.999f, eps_ = 1e-8f, mu_ = 0.9f;
+  float grad_scale_ = 1.f, coef_ = 1.f;
+  bool local_on_main_ = true;
+  struct Piece {
+    RunnerRange r;
+    int ps;
+    float* m;
+    float* v;
+  };
+  bool all_local_ = false;
+  std::vector<Piece> merged_;  // coalesced LOCAL update ranges (all_local_)
+};
+
+}  // namespace ddl

@@ -1,0 +1,78 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DDL_DEV __device__ __forceinline__
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------------------------
+// Dropout RNG — bit-identical to ops/rng.py (lowbias32 finalizer on (index ^ layer_key)).
+// TF1 tf.nn.dropout keeps an element when uniform >= rate (mnist_sync/model/model.py:73-74).
+// ---------------------------------------------------------------------------------------------
+DDL_DEV uint32_t ddl_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// key = mix(seed + layer * 0x9E3779B9) is computed on the host (ops/rng.py:layer_key).
+DDL_DEV bool ddl_keep(uint32_t key, uint32_t idx, uint32_t thr24) {
+  return (ddl_mix32(idx ^ key) >> 8) >= thr24;
+}
+
+// f32-input / f32-accumulate MFMA, 16x16x4 (exact fp32, 64 FLOP/clk/SIMD on gfx950).
+// Lane l holds A[l&15][k=l>>4] and B[k=l>>4][l&15]; C/D: col = l&15, row = (l>>4)*4 + reg.
+DDL_DEV f32x4 mfma16x16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+DDL_DEV float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+// ---------------------------------------------------------------------------------------------
+// Raw buffer loads (MI355X guide T8): 32-bit offsets against a wave-uniform descriptor, and
+// the hardware range check returns 0 for any offset past num_records.  Gathers with padding
+// (SAME conv halos, tile edges) therefore need no branches or predicated zero-fill: an
+// out-of-range element simply gets offset kOOB.  Descriptors are built from kernel
+// arguments only, so they stay in SGPRs (guide T20).
+// ---------------------------------------------------------------------------------------------
+typedef __amdgpu_buffer_rsrc_t brsrc_t;
+constexpr int kOOB = 0x7FFFFFF0;
+
+DDL_DEV brsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes,
+                                           0x00020000);
+}
+DDL_DEV float4 bload4(brsrc_t r, int byte_off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
+  return *reinterpret_cast<float4*>(&v);
+}
+DDL_DEV float bload1(brsrc_t r, int byte_off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0);
+  return __builtin_bit_cast(float, v);
+}
+
+// Write-through (sc1) 16-B store / load pair for data handed to another workgroup inside
+// one launch (MI355X guide §6 Guideline 16, R1): the stores need no agent-scope release (an
+// L2 writeback) and the consumer's sc1 loads bypass its possibly-stale L1, so it needs no
+// acquire either.  aux bit 16 = sc1.
+DDL_DEV void bstore4_sc1(brsrc_t r, int byte_off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
+                                         r, byte_off, 0, 16);
+}
+DDL_DEV float4 bload4_sc1(brsrc_t r, int byte_off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
+  return *reinterpret_cast<float4*>(&v);
+}
+
+DDL_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+DDL_DEV float f4get(const float4& v, int i) {
+  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+#define DDL_CHECK_LAUNCH() (void)hipGetLastError()

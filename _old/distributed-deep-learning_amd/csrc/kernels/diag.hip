@@ -1,0 +1,65 @@
+// Diagnostics: sustained FP32-MFMA issue rate on this chip (no memory traffic), used to
+// calibrate what fraction of the *achievable* matrix rate the GEMM engine reaches.
+#include "common.h"
+#include "api.h"
+
+namespace ddl {
+
+typedef float f32x16d __attribute__((ext_vector_type(16)));
+
+__global__ void __launch_bounds__(64) mfma_peak_kernel(float* out, int iters) {
+  f32x16d acc0 = {}, acc1 = {};
+  float a = 1.0f + 1e-7f * threadIdx.x, b = 0.999f;
+  for (int i = 0; i < iters; ++i) {
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b, a, acc1, 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) s += acc0[q] + acc1[q];
+  out[blockIdx.x * 64 + threadIdx.x] = s;
+}
+
+void launch_mfma_peak(float* out, int blocks, int iters, hipStream_t st) {
+  hipLaunchKernelGGL(mfma_peak_kernel, dim3(blocks), dim3(64), 0, st, out, iters);
+}
+
+}  // namespace ddl
+
+// ---- GEMM-structure ablation: the engine kernel with register-only "loads" -------------------
+#include "gemm.h"
+
+namespace ddl {
+
+struct NoMemPolicy {   // same K loop / LDS / MFMA structure, no global memory traffic
+  static constexpr bool A_KCONTIG = true;
+  static constexpr bool B_KCONTIG = false;
+  int M, N, K;
+  float* out;
+  struct AInfo { int m; int kk; };
+  using BInfo = AInfo;
+  DDL_DEV AInfo prepA(int m, int kk) const { return {m, kk}; }
+  DDL_DEV AInfo prepB(int n, int kk) const { return {n, kk}; }
+  DDL_DEV float4 loadA(const AInfo& a, int k0) const {
+    const float v = (float)(a.m + k0 + a.kk) * 1e-6f;
+    return make_float4(v, v, v, v);
+  }
+  DDL_DEV float4 loadB(const BInfo& b, int k0) const {
+    const float v = (float)(b.m - k0 + b.kk) * 1e-6f;
+    return make_float4(v, v, v, v);
+  }
+  DDL_DEV void epi(int m0, int n, f32x4 v) const {
+    if (v[0] + v[1] + v[2] + v[3] == 12345.f) out[n] = 1.f;  // keep live, ~never stores
+  }
+};
+
+void launch_gemm_nomem(float* out, int M, int N, int K, int splits, void* slab, int* tickets,
+                       hipStream_t st) {
+  NoMemPolicy p{M, N, K, out};
+  SplitScratch sc;
+  sc.slab = slab;
+  sc.tickets = tickets;
+  launch_gemm<32, 32, 32, 1, 1>(p, splits, 1, sc, st);
+}
+
+}  // namespace ddl

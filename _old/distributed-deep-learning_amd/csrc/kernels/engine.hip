@@ -1,0 +1,333 @@
+// The CNN step engine: every forward / backward kernel launch of one worker step.
+//
+// Reference step: sess.run(grads) on the TF runtime, 14 host round trips
+// to push, 14 to pull.  Here a step is ~20 GEMM-engine launches + 2 head kernels, all
+// buffers preallocated (graph-capturable: no malloc, no sync).  The backward is split
+// into 4 segments so the host can push a segment's gradients on a side stream while the
+// next segment computes (SURVEY.md §5.8 bucket plan); inside a segment the weight-gradient
+// GEMM runs on a second stream concurrently with the data-gradient GEMM that feeds the
+// next segment (fork/join events, captured as parallel graph branches).
+#include <string.h>
+
+#include <type_traits>
+
+#include "api.h"
+#include "layers.h"
+
+namespace ddl {
+
+Engine::Engine() {
+  // {tile config, split-K, stream-K workers} per op: whole-step coordinate-descent tune
+  // (scripts/step_tune.py over the scripts/op_bench.py per-op sweep) on one MI355X, batch 100,
+  // single-stream backward with dual dgrad+wgrad launches: fwd+bwd 367 us (was 449 us)
+  static const int defc[OP_COUNT] = {3, 3, 3, 3, 3, 3, 3, 5, 3, 5, 3, 3, 3, 3, 3, 5, 3};
+  static const int defs[OP_COUNT] = {1, 2, 1, 8, 8, 16, 4, 1, 4, 1, 1, 8, 8, 16, 4, 32, 1024};
+  static const int defw[OP_COUNT] = {0, 0, 3072, 0, 0, 0, 0, 0, 0, 0, 2048, 0, 0, 0, 0, 0, 0};
+  // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
+  static const bool inl[OP_COUNT] = {0, 1, 0, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0};
+  memcpy(cfg, defc, sizeof(defc));
+  memcpy(splits, defs, sizeof(defs));
+  memcpy(workers, defw, sizeof(defw));
+  for (int op = 0; op < OP_COUNT; ++op) wide[op] = inl[op] ? (1 << 20) : 1;
+}
+
+Engine::~Engine() {
+  if (ev_fork) (void)hipEventDestroy(ev_fork);
+  if (ev_join) (void)hipEventDestroy(ev_join);
+  if (side) (void)hipStreamDestroy(side);
+}
+
+void Engine::init_streams() {
+  if (side) return;
+  (void)hipStreamCreateWithFlags(&side, hipStreamNonBlocking);
+  (void)hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming);
+  (void)hipEventCreateWithFlags(&ev_join, hipEventDisableTiming);
+}
+
+void Engine::op_shape(int op, int B, int* M, int* N, int* K) {
+  int m = 0, n = 0, k = 0;
+  switch (op) {
+    case OP_CONV1_FWD: m = B * 14 * 14 * 4; n = 32; k = 25; break;
+    case OP_CONV2_FWD: m = B * 7 * 7 * 4; n = 64; k = 800; break;
+    case OP_CONV3_FWD: m = B * 4 * 4 * 4; n = 128; k = 1600; break;
+    case OP_CONV4_FWD: m = B * 2 * 2 * 4; n = 256; k = 3200; break;
+    case OP_FC1_FWD: m = B; n = 1024; k = 1024; break;
+    case OP_FC2_FWD: m = B; n = 512; k = 1024; break;
+    case OP_FC2_DGRAD: m = B; n = 1024; k = 512; break;
+    case OP_FC2_WGRAD: m = 1025; n = 512; k = B; break;
+    case OP_FC1_DGRAD: m = B; n = 1024; k = 1024; break;
+    case OP_FC1_WGRAD: m = 1025; n = 1024; k = B; break;
+    case OP_CONV4_DGRAD: m = B * 16; n = 128; k = 6400; break;
+    case OP_CONV4_WGRAD: m = 3201; n = 256; k = B * 16; break;
+    case OP_CONV3_DGRAD: m = B * 49; n = 64; k = 3200; break;
+    case OP_CONV3_WGRAD: m = 1601; n = 128; k = B * 49; break;
+    case OP_CONV2_DGRAD: m = B * 196; n = 32; k = 1600; break;
+    case OP_CONV2_WGRAD: m = 801; n = 64; k = B * 196; break;
+    case OP_CONV1_WGRAD: m = 26; n = 32; k = B * 784; break;
+    default: break;
+  }
+  *M = m; *N = n; *K = k;
+}
+
+#define TILE_0 64, 64, 32, 1, 1
+#define TILE_1 128, 64, 32, 2, 1
+#define TILE_2 64, 32, 32, 1, 1
+#define TILE_3 32, 32, 32, 1, 1
+#define TILE_4 32, 64, 32, 1, 1
+#define TILE_5 32, 32, 16, 1, 1   // software-pipelined main loop (gemm.h GemmTile::PIPE)
+
+static size_t slab_need(int c, int M, int N, int K, int s, int w) {
+  switch (c) {
+    case 0: return gemm_slab_f4<TILE_0>(M, N, K, s, w);
+    case 1: return gemm_slab_f4<TILE_1>(M, N, K, s, w);
+    case 2: return gemm_slab_f4<TILE_2>(M, N, K, s, w);
+    case 3: return gemm_slab_f4<TILE_3>(M, N, K, s, w);
+    case 4: return gemm_slab_f4<TILE_4>(M, N, K, s, w);
+    default: return gemm_slab_f4<TILE_5>(M, N, K, s, w);
+  }
+}
+
+template <class P>
+static void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const SplitScratch& sc,
+                       hipStream_t st) {
+  switch (c) {
+    case 0: launch_gemm<TILE_0>(p, s, wide_thr, sc, st, w); break;
+    case 1: launch_gemm<TILE_1>(p, s, wide_thr, sc, st, w); break;
+    case 2: launch_gemm<TILE_2>(p, s, wide_thr, sc, st, w); break;
+    case 3: launch_gemm<TILE_3>(p, s, wide_thr, sc, st, w); break;
+    case 4: launch_gemm<TILE_4>(p, s, wide_thr, sc, st, w); break;
+    default: launch_gemm<TILE_5>(p, s, wide_thr, sc, st, w); break;
+  }
+}
+
+size_t Engine::slab_floats_needed(int B) const {
+  size_t mx = 0;
+  for (int op = 0; op < OP_COUNT; ++op) {
+    int M, N, K;
+    op_shape(op, B, &M, &N, &K);
+    const size_t f = 4 * slab_need(cfg[op], M, N, K, splits[op], workers[op]);
+    if (f > mx) mx = f;
+  }
+  return mx;
+}
+
+static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+static const size_t kActPer[] = {6272, 3136, 2048, 1024, 1024, 512, 16, 1,
+                                 512, 1024, 4096, 6272, 12544, 25088};
+static const size_t kCodePer[] = {6272, 3136, 2048, 1024};
+
+size_t Engine::workspace_bytes() const {
+  const size_t B = (size_t)max_batch;
+  size_t f = 0;
+  for (size_t p : kActPer) f += al256(4 * B * p);
+  f += 2 * al256(4 * slab_floats);
+  for (size_t c : kCodePer) f += al256(B * c);
+  f += 256;                          // correct counter
+  f += 2 * al256(4 * kMaxTickets);   // split-K arrival tickets (two streams)
+  return f;
+}
+
+void Engine::bind_workspace(void* base) {
+  const size_t B = (size_t)max_batch;
+  char* p = (char*)base;
+  auto take = [&](size_t bytes) { char* r = p; p += al256(bytes); return r; };
+  float** acts[] = {&p1, &p2, &p3, &p4, &h1, &h2, &dlog, &loss,
+                    &dpre2fc, &dpre1fc, &d4, &d3, &d2, &d1};
+  for (int i = 0; i < 14; ++i) *acts[i] = (float*)take(4 * B * kActPer[i]);
+  for (int s = 0; s < 2; ++s) {
+    scratch[s].slab = take(4 * slab_floats);
+    scratch[s].slab_f4 = slab_floats / 4;
+  }
+  uint8_t** codes[] = {&c1, &c2, &c3, &c4};
+  for (int i = 0; i < 4; ++i) *codes[i] = (uint8_t*)take(B * kCodePer[i]);
+  correct = (int*)take(256);
+  for (int s = 0; s < 2; ++s) {
+    scratch[s].tickets = (int*)take(4 * kMaxTickets);
+    scratch[s].max_tiles = kMaxTickets;
+  }
+}
+
+// Problem policy of op OP (layers.h) bound to this engine's buffers, at batch B.
+template <int OP>
+static auto make_policy(const Engine& e, int B, const float* x, const uint32_t* seed,
+                        bool train) {
+  int M, N, K;
+  Engine::op_shape(OP, B, &M, &N, &K);
+  const uint32_t thr = train ? e.thr24 : 0u;
+  const float* const* P = e.P;
+  float* const* G = e.G;
+  if constexpr (OP == OP_CONV1_FWD) return ConvFwd<28, 1, 32>{M, N, K, x, P[0], P[1], e.p1, e.c1};
+  else if constexpr (OP == OP_CONV2_FWD)
+    return ConvFwd<14, 32, 64>{M, N, K, e.p1, P[2], P[3], e.p2, e.c2};
+  else if constexpr (OP == OP_CONV3_FWD)
+    return ConvFwd<7, 64, 128>{M, N, K, e.p2, P[4], P[5], e.p3, e.c3};
+  else if constexpr (OP == OP_CONV4_FWD)
+    return ConvFwd<4, 128, 256>{M, N, K, e.p3, P[6], P[7], e.p4, e.c4};
+  else if constexpr (OP == OP_FC1_FWD)
+    return FcFwd<true>{M, N, K, e.p4, P[8], P[9], e.h1, seed, 1u, thr, e.inv_keep, e.seed_value};
+  else if constexpr (OP == OP_FC2_FWD)
+    return FcFwd<false>{M, N, K, e.h1, P[10], P[11], e.h2, seed, 2u, thr, e.inv_keep, e.seed_value};
+  else if constexpr (OP == OP_FC2_DGRAD)
+    return FcDgradAct{{M, N, K, e.dpre2fc, P[10]}, e.h1, e.inv_keep, e.dpre1fc};
+  else if constexpr (OP == OP_FC2_WGRAD)
+    return FcWgrad{M, N, K, 1024, e.h1, e.dpre2fc, G[10], G[11]};
+  else if constexpr (OP == OP_FC1_DGRAD)
+    return FcDgradPool<2, 256>{{M, N, K, e.dpre1fc, P[8]}, e.c4, e.d4};
+  else if constexpr (OP == OP_FC1_WGRAD)
+    return FcWgrad{M, N, K, 1024, e.p4, e.dpre1fc, G[8], G[9]};
+  else if constexpr (OP == OP_CONV4_DGRAD)
+    return ConvDgrad<4, 128, 256, 7>{M, N, K, e.d4, P[6], e.c3, e.d3};
+  else if constexpr (OP == OP_CONV4_WGRAD)
+    return ConvWgrad<4, 128, 256>{M, N, K, e.p3, e.d4, G[6], G[7]};
+  else if constexpr (OP == OP_CONV3_DGRAD)
+    return ConvDgrad<7, 64, 128, 14>{M, N, K, e.d3, P[4], e.c2, e.d2};
+  else if constexpr (OP == OP_CONV3_WGRAD)
+    return ConvWgrad<7, 64, 128>{M, N, K, e.p2, e.d3, G[4], G[5]};
+  else if constexpr (OP == OP_CONV2_DGRAD)
+    return ConvDgrad<14, 32, 64, 28>{M, N, K, e.d2, P[2], e.c1, e.d1};
+  else if constexpr (OP == OP_CONV2_WGRAD)
+    return ConvWgrad<14, 32, 64>{M, N, K, e.p1, e.d2, G[2], G[3]};
+  else
+    return ConvWgrad<28, 1, 32>{M, N, K, x, e.d1, G[0], G[1]};
+}
+
+template <int OP>
+static void run_op_t(Engine& e, const float* x, int B, const uint32_t* seed, bool train,
+                     hipStream_t st, int si) {
+  const auto p = make_policy<OP>(e, B, x, seed, train);
+  launch_cfg(e.cfg[OP], p, train ? e.splits[OP] : 1, train ? e.workers[OP] : 0, e.wide[OP],
+             e.scratch[si], st);
+}
+
+void Engine::run_op(int op, const float* x, int B, const uint32_t* seed, bool train,
+                    hipStream_t st, int si) {
+  switch (op) {
+#define DDL_RUN(OPC) \
+  case OPC: run_op_t<OPC>(*this, x, B, seed, train, st, si); break;
+    DDL_RUN(OP_CONV1_FWD) DDL_RUN(OP_CONV2_FWD) DDL_RUN(OP_CONV3_FWD) DDL_RUN(OP_CONV4_FWD)
+    DDL_RUN(OP_FC1_FWD) DDL_RUN(OP_FC2_FWD) DDL_RUN(OP_FC2_DGRAD) DDL_RUN(OP_FC2_WGRAD)
+    DDL_RUN(OP_FC1_DGRAD) DDL_RUN(OP_FC1_WGRAD) DDL_RUN(OP_CONV4_DGRAD) DDL_RUN(OP_CONV4_WGRAD)
+    DDL_RUN(OP_CONV3_DGRAD) DDL_RUN(OP_CONV3_WGRAD) DDL_RUN(OP_CONV2_DGRAD)
+    DDL_RUN(OP_CONV2_WGRAD) DDL_RUN(OP_CONV1_WGRAD)
+#undef DDL_RUN
+    default: break;
+  }
+}
+
+// ---- dual launches: data- and weight-gradient GEMM of one layer in one kernel -----------------
+// dual launches are instantiated for these one-wave configs (others run back to back)
+static bool one_wave_cfg(int c) { return c == 0 || c == 3 || c == 4 || c == 5; }
+
+template <class CA, int OA, int OB, class PA, class PB>
+static void dual_b(Engine& e, const PA& pa, const PB& pb, hipStream_t st) {
+#define DDL_DUAL_B(CB) \
+  launch_gemm_dual<CA, PA, TileCfg<CB>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], \
+                                            e.wide[OA], pb, e.splits[OB], e.workers[OB], \
+                                            e.scratch[1], e.wide[OB], st)
+  switch (e.cfg[OB]) {
+    case 0: DDL_DUAL_B(TILE_0); break;
+    case 3: DDL_DUAL_B(TILE_3); break;
+    case 4: DDL_DUAL_B(TILE_4); break;
+    default: DDL_DUAL_B(TILE_5); break;
+  }
+#undef DDL_DUAL_B
+}
+
+// Ops OA and OB (independent) in one launch if both use one-wave tiles, else back to back.
+template <int OA, int OB>
+static void run_dual(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
+  if (!e.dual || !one_wave_cfg(e.cfg[OA]) || !one_wave_cfg(e.cfg[OB])) {
+    run_op_t<OA>(e, x, B, seed, true, st, 0);
+    run_op_t<OB>(e, x, B, seed, true, st, 0);
+    return;
+  }
+  const auto pa = make_policy<OA>(e, B, x, seed, true);
+  const auto pb = make_policy<OB>(e, B, x, seed, true);
+  using PA = std::decay_t<decltype(pa)>;
+  using PB = std::decay_t<decltype(pb)>;
+  switch (e.cfg[OA]) {
+    case 0: dual_b<TileCfg<TILE_0>, OA, OB, PA, PB>(e, pa, pb, st); break;
+    case 3: dual_b<TileCfg<TILE_3>, OA, OB, PA, PB>(e, pa, pb, st); break;
+    case 4: dual_b<TileCfg<TILE_4>, OA, OB, PA, PB>(e, pa, pb, st); break;
+    default: dual_b<TileCfg<TILE_5>, OA, OB, PA, PB>(e, pa, pb, st); break;
+  }
+}
+
+void Engine::forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st) {
+  for (int op = OP_CONV1_FWD; op <= OP_FC2_FWD; ++op) run_op(op, x, B, seed, train, st, 0);
+}
+
+// The side stream waits for everything enqueued on `st` so far.
+void Engine::fork(hipStream_t st) {
+  (void)hipEventRecord(ev_fork, st);
+  (void)hipStreamWaitEvent(side, ev_fork, 0);
+}
+
+// `st` waits for everything enqueued on the side stream so far.
+void Engine::join(hipStream_t st) {
+  (void)hipEventRecord(ev_join, side);
+  (void)hipStreamWaitEvent(st, ev_join, 0);
+}
+
+void Engine::wgrad(int op, const float* x, int B, const uint32_t* seed, hipStream_t st) {
+  fork(st);
+  run_op(op, x, B, seed, true, side, 1);
+}
+
+void Engine::backward_segment(int s, const float* x, const int64_t* labels, int B,
+                              const uint32_t* seed, hipStream_t st) {
+  if (concurrent && side) {  // weight gradients on the side stream (fork/join per segment)
+    switch (s) {
+      case 0:
+        launch_head_fwd(h2, P[12], P[13], labels, B, dlog, loss, nullptr, st);
+        launch_head_bwd(h2, P[12], dlog, B, seed, seed_value, thr24, inv_keep, G[12], G[13],
+                        dpre2fc, st);
+        wgrad(OP_FC2_WGRAD, x, B, seed, st);
+        run_op(OP_FC2_DGRAD, x, B, seed, true, st, 0);
+        wgrad(OP_FC1_WGRAD, x, B, seed, st);
+        run_op(OP_FC1_DGRAD, x, B, seed, true, st, 0);
+        break;
+      case 1:
+        wgrad(OP_CONV4_WGRAD, x, B, seed, st);
+        run_op(OP_CONV4_DGRAD, x, B, seed, true, st, 0);
+        break;
+      case 2:
+        wgrad(OP_CONV3_WGRAD, x, B, seed, st);
+        run_op(OP_CONV3_DGRAD, x, B, seed, true, st, 0);
+        break;
+      case 3:
+        wgrad(OP_CONV2_WGRAD, x, B, seed, st);
+        run_op(OP_CONV2_DGRAD, x, B, seed, true, st, 0);
+        wgrad(OP_CONV1_WGRAD, x, B, seed, st);
+        break;
+      default: break;
+    }
+    join(st);
+    return;
+  }
+  // single stream: each layer's dgrad + wgrad as one dual launch
+  switch (s) {
+    case 0:
+      launch_head_fwd(h2, P[12], P[13], labels, B, dlog, loss, nullptr, st);
+      launch_head_bwd(h2, P[12], dlog, B, seed, seed_value, thr24, inv_keep, G[12], G[13],
+                        dpre2fc, st);
+      run_dual<OP_FC2_DGRAD, OP_FC2_WGRAD>(*this, x, B, seed, st);
+      run_dual<OP_FC1_DGRAD, OP_FC1_WGRAD>(*this, x, B, seed, st);
+      break;
+    case 1: run_dual<OP_CONV4_DGRAD, OP_CONV4_WGRAD>(*this, x, B, seed, st); break;
+    case 2: run_dual<OP_CONV3_DGRAD, OP_CONV3_WGRAD>(*this, x, B, seed, st); break;
+    case 3:
+      run_dual<OP_CONV2_DGRAD, OP_CONV2_WGRAD>(*this, x, B, seed, st);
+      run_op(OP_CONV1_WGRAD, x, B, seed, true, st, 0);
+      break;
+    default: break;
+  }
+}
+
+void Engine::eval_count(const float* x, const int64_t* labels, int B, hipStream_t st) {
+  forward(x, B, nullptr, false, st);
+  launch_head_fwd(h2, P[12], P[13], labels, B, nullptr, nullptr, correct, st);
+}
+
+}  // namespace ddl

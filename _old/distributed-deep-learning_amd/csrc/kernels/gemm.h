@@ -1,0 +1,810 @@
+// Generic FP32 MFMA GEMM engine for gfx950: C[M,N] = sum_k A[m,k] * B[k,n].
+//
+// Every conv / fc forward, data-gradient and weight-gradient of the MNIST CNN is one
+// instantiation of this kernel with a *problem* policy P that supplies:
+//   * operand gathers: P::prepA(mn) -> per-thread info hoisted out of the K loop, then
+//     P::loadA(info, k) returning 4 consecutive elements along the operand's contiguous
+//     global direction (A_KCONTIG / B_KCONTIG); same for B.  Implicit-GEMM im2col,
+//     transposed weights and pool-window row orders are just address functions — nothing
+//     is materialised;
+//   * a fused epilogue P::epi(m0, n, f32x4 rows m0..m0+3) (bias / ReLU / max-pool with
+//     argmax code / dropout / pool-backward scatter / dW+db split).  The 32x32 MFMA C
+//     layout gives each lane 4 groups of 4 consecutive rows of one column; with M
+//     enumerated pool-window-major each group is exactly one 2x2 pool window.
+//
+// Math: v_mfma_f32_32x32x2_f32 (exact fp32; gfx950 has no xf32), 64-cycle issue; a wave
+// with a single fragment alternates two accumulator chains.
+// Tiling: BM x BN block tile, BK-deep K step, WM x WN waves (wave64), wave tile
+// (BM/WM) x (BN/WN) of 32x32 fragments.  One-wave blocks use a single LDS buffer (no
+// barriers), multi-wave blocks a double buffer; global loads run two K tiles ahead in
+// registers; a whole K tile's fragments are read from LDS in one burst before its MFMAs.  LDS operand images follow global contiguity so the
+// global->LDS copy is a straight float4 store:
+//   K-contiguous operand -> [mn][BK+4]   one ds_read_b128 per 4 MFMAs: lane half
+//                                        h = l>>5 owns k = 8r+4h .. 8r+4h+3 of every
+//                                        8-deep sub-step (MFMA s pairs k = 8r+s and
+//                                        8r+4+s); stride BK+4 is bank-conflict free for
+//                                        the four 16-lane b128 groups
+//   MN-contiguous operand -> [BK][mn+4]  ds_read_b32; the two 32-lane halves read rows
+//                                        4 apart (separate conflict groups)
+//
+// Two drivers share the per-tile main loop / epilogue (GemmTile):
+// Stream-K (gemm_streamk_kernel): W one-block workers split the (tile, K-tile) iteration
+//   space evenly; partial boundary tiles are reduced in-launch by their last contributor.
+// Split-K (gridDim.z = S > 1), deterministic, no float atomics:
+//   mode 1: every split stores its fp32 partial fragments (float4 per lane, coalesced,
+//     write-through sc1) and takes an arrival ticket; the last arriver of a tile sums the S
+//     partials in z order with sc1 loads and runs the fused epilogue (MI355X guide §5 /
+//     §6 G16 in-launch reduction, sc1 form: no release or acquire fence).
+//   mode 2: partials only; splitk_wide_reduce sums them with RL lanes per output element
+//     and runs the epilogue.
+#pragma once
+#include "common.h"
+#include "scratch.h"
+
+namespace ddl {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+DDL_DEV f32x16 mfma32x32x2(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+template <int BM, int BN, int WM, int WN>
+struct TileGeo {
+  static constexpr int NW = WM * WN;
+  static constexpr int WTM = BM / WM, WTN = BN / WN;
+  static constexpr int TM = WTM / 32, TN = WTN / 32;
+  static constexpr int FRAGS = TM * TN;
+  // float4 elements of one split's partial tile: 4 float4 per fragment per lane
+  static constexpr int PART4 = NW * FRAGS * 4 * 64;
+};
+
+// ---- per-tile building blocks shared by the split-K and stream-K drivers ---------------------
+template <int BM, int BN, int BK, int WM, int WN, class P>
+struct GemmTile {
+  using G = TileGeo<BM, BN, WM, WN>;
+  static constexpr int NT = WM * WN * 64;
+  static constexpr bool AK = P::A_KCONTIG;
+  static constexpr bool BKC = P::B_KCONTIG;
+  static constexpr int SA = AK ? (BK + 4) : (BM + 4);
+  static constexpr int A_ELEMS = AK ? BM * SA : BK * SA;
+  static constexpr int SB = BKC ? (BK + 4) : (BN + 4);
+  static constexpr int B_ELEMS = BKC ? BN * SB : BK * SB;
+  static constexpr int WTM = G::WTM, WTN = G::WTN, TM = G::TM, TN = G::TN;
+  static constexpr int FA = (BM * BK / 4) / NT;
+  static constexpr int FB = (BN * BK / 4) / NT;
+  static constexpr int R = BK / 8;
+  static_assert(FA >= 1 && FA * NT == BM * BK / 4, "A tile must split evenly over threads");
+  static_assert(FB >= 1 && FB * NT == BN * BK / 4, "B tile must split evenly over threads");
+  static_assert(TM * 32 == WTM && TN * 32 == WTN, "wave tile must be 32-multiples");
+  static_assert(BK % 8 == 0, "BK must be a multiple of 8");
+  // One-wave blocks need neither a second LDS buffer nor barriers: a wave's LDS ops execute
+  // in order, so the next tile's ds_writes cannot overtake this tile's ds_reads.  Halving
+  // the LDS footprint doubles the resident waves per CU (LDS was the occupancy limit).
+  static constexpr bool SOLO = (NT == 64);
+  static constexpr int NBUF = SOLO ? 1 : 2;
+  static constexpr int LDS_F4 = (NBUF * (A_ELEMS + B_ELEMS)) / 4;
+  // A wave with a single 32x32 fragment alternates two accumulator chains (summed at the
+  // end) so consecutive MFMAs are independent.
+  static constexpr int NCH = (TM * TN == 1) ? 2 : 1;
+  static constexpr int WPART = TM * TN * 4 * 64;  // float4 of one wave's partial fragments
+
+  // acc = sum over k in [kb, ke) of the (m_blk, n_blk) block tile; kb is a multiple of BK.
+  // One-wave single-fragment tiles with BK = 16 take the software-pipelined loop (its double
+  // register sets fit at 3 waves/SIMD only with the 16-deep K step: at BK = 32 it needed
+  // 256 VGPRs + 64 AGPRs, one wave per SIMD, and lost to the basic loop); others the basic loop.
+  static constexpr bool PIPE = SOLO && TM * TN == 1 && BK == 16;
+  static DDL_DEV void mainloop(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
+                               f32x16 (&acc)[TM][TN]) {
+    if constexpr (PIPE) mainloop_pipe(p, m_blk, n_blk, kb, ke, lds, acc);
+    else mainloop_basic(p, m_blk, n_blk, kb, ke, lds, acc);
+  }
+
+  // Software-pipelined main loop (one wave, one 32x32 fragment, single LDS buffer).
+  // Per K tile t the wave's 16 MFMAs on fragments F[t&1] (already in VGPRs) are interleaved
+  // with: the LDS store of tile t+1 from global-load registers G[(t+1)&1], the global loads
+  // of tile t+3 into that freed register set (two iterations of latency cover), and the LDS
+  // fragment reads of tile t+1 into F[(t+1)&1].  The LDS ops of a wave execute in order, so
+  // the stores of t+1 cannot overtake the (earlier-issued) reads of t, nor the reads of t+1
+  // the stores.  PMC on the unpipelined loop: MFMA pipe ~40 % busy with waves stalled on
+  // LDS-read latency and on global loads issued only one tile ahead.
+  static DDL_DEV void mainloop_pipe(const P& p, int m_blk, int n_blk, int kb, int ke,
+                                    float* lds, f32x16 (&acc)[TM][TN]) {
+    float* const As = lds;
+    float* const Bs = lds + A_ELEMS;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int nk = (ke - kb + BK - 1) / BK;
+    typename P::AInfo ai[FA];
+    typename P::BInfo bi[FB];
+    int a_off[FA], b_off[FB];
+#pragma unroll
+    for (int it = 0; it < FA; ++it) {
+      const int idx = tid + it * NT;
+      if constexpr (AK) {
+        const int kq = idx % (BK / 4), row = idx / (BK / 4);
+        ai[it] = p.prepA(m_blk + row, kq * 4);
+        a_off[it] = row * SA + kq * 4;
+      } else {
+        const int mq = idx % (BM / 4), kk = idx / (BM / 4);
+        ai[it] = p.prepA(m_blk + mq * 4, kk);
+        a_off[it] = kk * SA + mq * 4;
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < FB; ++it) {
+      const int idx = tid + it * NT;
+      if constexpr (BKC) {
+        const int kq = idx % (BK / 4), row = idx / (BK / 4);
+        bi[it] = p.prepB(n_blk + row, kq * 4);
+        b_off[it] = row * SB + kq * 4;
+      } else {
+        const int nq = idx % (BN / 4), kk = idx / (BN / 4);
+        bi[it] = p.prepB(n_blk + nq * 4, kk);
+        b_off[it] = kk * SB + nq * 4;
+      }
+    }
+    float4 ga0[FA], gb0[FB], ga1[FA], gb1[FB];     // global staging G[0], G[1]
+    float f0a[R][4], f0b[R][4], f1a[R][4], f1b[R][4];  // fragments F[0], F[1]
+    auto gload = [&](int k0, float4 (&ra)[FA], float4 (&rb)[FB]) {
+#pragma unroll
+      for (int it = 0; it < FA; ++it) ra[it] = p.loadA(ai[it], k0);
+#pragma unroll
+      for (int it = 0; it < FB; ++it) rb[it] = p.loadB(bi[it], k0);
+    };
+    auto sstore = [&](const float4 (&ra)[FA], const float4 (&rb)[FB]) {
+#pragma unroll
+      for (int it = 0; it < FA; ++it) *reinterpret_cast<float4*>(As + a_off[it]) = ra[it];
+#pragma unroll
+      for (int it = 0; it < FB; ++it) *reinterpret_cast<float4*>(Bs + b_off[it]) = rb[it];
+    };
+    const int lr = lane & 31, lh = lane >> 5;
+    auto fetch = [&](float (&fa)[R][4], float (&fb)[R][4]) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if constexpr (AK) {
+          const float4 t = *reinterpret_cast<const float4*>(As + lr * SA + r * 8 + 4 * lh);
+          fa[r][0] = t.x; fa[r][1] = t.y; fa[r][2] = t.z; fa[r][3] = t.w;
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) fa[r][s] = As[(r * 8 + 4 * lh + s) * SA + lr];
+        }
+        if constexpr (BKC) {
+          const float4 t = *reinterpret_cast<const float4*>(Bs + lr * SB + r * 8 + 4 * lh);
+          fb[r][0] = t.x; fb[r][1] = t.y; fb[r][2] = t.z; fb[r][3] = t.w;
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) fb[r][s] = Bs[(r * 8 + 4 * lh + s) * SB + lr];
+        }
+      }
+    };
+    f32x16 c0, c1;  // two independent accumulator chains
+#pragma unroll
+    for (int q = 0; q < 16; ++q) { c0[q] = 0.f; c1[q] = 0.f; }
+    auto mfmas = [&](const float (&fa)[R][4], const float (&fb)[R][4]) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          if (s & 1) c1 = mfma32x32x2(fa[r][s], fb[r][s], c1);
+          else c0 = mfma32x32x2(fa[r][s], fb[r][s], c0);
+        }
+    };
+    // Interleave pattern of one steady-state iteration (4R MFMAs, 64 cycles each): the DS
+    // stores of the next tile between the first FA+FB MFMAs, then the next tile's fragment
+    // reads (which must follow those stores) and the global loads between the rest.
+    constexpr int NMF = 4 * R, NST = FA + FB;
+    static_assert(NMF >= 2 * NST, "pipelined loop needs 2 MFMAs per staged float4");
+#ifndef DDL_PIPE_SCHED
+#define DDL_PIPE_SCHED 1
+#endif
+    auto interleave = [&]() {
+      if constexpr (!DDL_PIPE_SCHED) return;
+#pragma unroll
+      for (int i = 0; i < NST; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+      }
+#pragma unroll
+      for (int i = 0; i < NMF - NST; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+      }
+    };
+
+    if (nk > 0) {
+      gload(kb, ga0, gb0);
+      if (nk > 1) gload(kb + BK, ga1, gb1);
+      sstore(ga0, gb0);
+      if (nk > 2) gload(kb + 2 * BK, ga0, gb0);
+      fetch(f0a, f0b);
+    }
+    int kt = 0;
+    // steady state: tiles kt (F0) and kt+1 (F1) per trip; all of kt+1..kt+4 exist
+#ifndef DDL_PIPE_STEADY
+#define DDL_PIPE_STEADY 1
+#endif
+    for (; DDL_PIPE_STEADY && kt + 4 < nk; kt += 2) {
+      sstore(ga1, gb1);                       // tile kt+1
+      gload(kb + (kt + 3) * BK, ga1, gb1);    // tile kt+3
+      fetch(f1a, f1b);                        // fragments of kt+1
+      mfmas(f0a, f0b);                        // tile kt
+      interleave();
+      __builtin_amdgcn_sched_barrier(0);
+      sstore(ga0, gb0);                       // tile kt+2
+      gload(kb + (kt + 4) * BK, ga0, gb0);    // tile kt+4
+      fetch(f0a, f0b);                        // fragments of kt+2
+      mfmas(f1a, f1b);                        // tile kt+1
+      interleave();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // tail: at most 4 tiles left (kt .. nk-1), same rotation with guards
+    for (; kt < nk; ++kt) {
+      const bool odd = (kt & 1) != 0;
+      const bool has1 = kt + 1 < nk, has3 = kt + 3 < nk;
+      if (!odd) {
+        if (has1) sstore(ga1, gb1);
+        if (has3) gload(kb + (kt + 3) * BK, ga1, gb1);
+        if (has1) fetch(f1a, f1b);
+        mfmas(f0a, f0b);
+      } else {
+        if (has1) sstore(ga0, gb0);
+        if (has3) gload(kb + (kt + 3) * BK, ga0, gb0);
+        if (has1) fetch(f0a, f0b);
+        mfmas(f1a, f1b);
+      }
+    }
+    acc[0][0] = c0 + c1;
+  }
+
+  static DDL_DEV void mainloop_basic(const P& p, int m_blk, int n_blk, int kb, int ke,
+                                     float* lds, f32x16 (&acc)[TM][TN]) {
+    float* const As0 = lds;
+    float* const Bs0 = lds + NBUF * A_ELEMS;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int nk = (ke - kb + BK - 1) / BK;
+
+    // Loader protocol: prepX(mn, kk) fixes a thread's row/column (group) and its k offset
+    // inside every K tile; loadX(info, k0) gathers at tile base k0 (wave-uniform, a multiple
+    // of BK = 32), so per-tile index math that depends only on k0 runs on the scalar unit.
+    typename P::AInfo ai[FA];
+    typename P::BInfo bi[FB];
+    int a_off[FA], b_off[FB];
+#pragma unroll
+    for (int it = 0; it < FA; ++it) {
+      const int idx = tid + it * NT;
+      if constexpr (AK) {
+        const int kq = idx % (BK / 4), row = idx / (BK / 4);
+        ai[it] = p.prepA(m_blk + row, kq * 4);
+        a_off[it] = row * SA + kq * 4;
+      } else {
+        const int mq = idx % (BM / 4), kk = idx / (BM / 4);
+        ai[it] = p.prepA(m_blk + mq * 4, kk);
+        a_off[it] = kk * SA + mq * 4;
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < FB; ++it) {
+      const int idx = tid + it * NT;
+      if constexpr (BKC) {
+        const int kq = idx % (BK / 4), row = idx / (BK / 4);
+        bi[it] = p.prepB(n_blk + row, kq * 4);
+        b_off[it] = row * SB + kq * 4;
+      } else {
+        const int nq = idx % (BN / 4), kk = idx / (BN / 4);
+        bi[it] = p.prepB(n_blk + nq * 4, kk);
+        b_off[it] = kk * SB + nq * 4;
+      }
+    }
+
+    // Two register-prefetch stages of the global operands: K tile t+1 is stored to LDS
+    // while tile t's fragments are already in VGPRs, and tile t+2 loads during t's MFMAs.
+    float4 ra[FA], rb[FB];
+    auto gload = [&](int k0) {
+#pragma unroll
+      for (int it = 0; it < FA; ++it) ra[it] = p.loadA(ai[it], k0);
+#pragma unroll
+      for (int it = 0; it < FB; ++it) rb[it] = p.loadB(bi[it], k0);
+    };
+    auto sstore = [&](int buf) {
+      float* As = As0 + buf * A_ELEMS;
+      float* Bs = Bs0 + buf * B_ELEMS;
+#pragma unroll
+      for (int it = 0; it < FA; ++it) *reinterpret_cast<float4*>(As + a_off[it]) = ra[it];
+#pragma unroll
+      for (int it = 0; it < FB; ++it) *reinterpret_cast<float4*>(Bs + b_off[it]) = rb[it];
+    };
+
+    f32x16 acc2;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc2[q] = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+    const int lr = lane & 31;   // fragment row / column
+    const int lh = lane >> 5;   // k half
+
+    // fragment fetch of a whole K tile from LDS buffer (As, Bs), issued as one burst so the
+    // LDS latency is paid once per tile
+    float av[R][TM][4], bv[R][TN][4];
+    auto fetch_all = [&](const float* As, const float* Bs) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wm * WTM + i * 32 + lr;
+          if constexpr (AK) {
+            const float4 t = *reinterpret_cast<const float4*>(As + row * SA + r * 8 + 4 * lh);
+            av[r][i][0] = t.x; av[r][i][1] = t.y; av[r][i][2] = t.z; av[r][i][3] = t.w;
+          } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) av[r][i][s] = As[(r * 8 + 4 * lh + s) * SA + row];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = wn * WTN + j * 32 + lr;
+          if constexpr (BKC) {
+            const float4 t = *reinterpret_cast<const float4*>(Bs + col * SB + r * 8 + 4 * lh);
+            bv[r][j][0] = t.x; bv[r][j][1] = t.y; bv[r][j][2] = t.z; bv[r][j][3] = t.w;
+          } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) bv[r][j][s] = Bs[(r * 8 + 4 * lh + s) * SB + col];
+          }
+        }
+      }
+    };
+
+    if (nk > 0) {
+      gload(kb);
+      sstore(0);
+      if (nk > 1) gload(kb + BK);
+    }
+    if constexpr (!SOLO) __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = SOLO ? 0 : (kt & 1);
+      fetch_all(As0 + cur * A_ELEMS, Bs0 + cur * B_ELEMS);
+      // (SOLO) overwriting the buffer just read is safe: a wave's LDS ops run in order;
+      // with two buffers the previous iteration's barrier freed buffer cur^1.
+      if (kt + 1 < nk) sstore(SOLO ? 0 : (cur ^ 1));
+      if (kt + 2 < nk) gload(kb + (kt + 2) * BK);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          if constexpr (NCH == 2) {
+            if (s & 1) acc2 = mfma32x32x2(av[r][0][s], bv[r][0][s], acc2);
+            else acc[0][0] = mfma32x32x2(av[r][0][s], bv[r][0][s], acc[0][0]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+                acc[i][j] = mfma32x32x2(av[r][i][s], bv[r][j][s], acc[i][j]);
+          }
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!SOLO) __syncthreads();
+    }
+    if constexpr (NCH == 2) acc[0][0] += acc2;
+  }
+
+  // fused epilogue: each lane owns 4 groups of 4 consecutive rows of one column
+  static DDL_DEV void epilogue(const P& p, int m_blk, int n_blk, const f32x16 (&acc)[TM][TN]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n_blk + wn * WTN + j * 32 + lr;
+        if (n >= p.N) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int m0 = m_blk + wm * WTM + i * 32 + 8 * g + 4 * lh;
+          if (m0 < p.M) {
+            const f32x16& v = acc[i][j];
+            p.epi(m0, n, f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]});
+          }
+        }
+      }
+    }
+  }
+
+  // partial-fragment image of one block: [wave][frag][g][lane] float4 (coalesced per wave),
+  // at float4 index `base` of the slab.  Written and read write-through (sc1): see arrive().
+  static DDL_DEV void store_partial(brsrc_t slab, size_t base, const f32x16 (&acc)[TM][TN]) {
+    const int mine = (int)base + (threadIdx.x >> 6) * WPART + (threadIdx.x & 63);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x16& v = acc[i][j];
+          bstore4_sc1(slab, (mine + ((i * TN + j) * 4 + g) * 64) * 16,
+                      make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]));
+        }
+  }
+  static DDL_DEV void add_partial(brsrc_t slab, size_t base, f32x16 (&acc)[TM][TN]) {
+    const int src = (int)base + (threadIdx.x >> 6) * WPART + (threadIdx.x & 63);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 t = bload4_sc1(slab, (src + ((i * TN + j) * 4 + g) * 64) * 16);
+          acc[i][j][4 * g] += t.x; acc[i][j][4 * g + 1] += t.y;
+          acc[i][j][4 * g + 2] += t.z; acc[i][j][4 * g + 3] += t.w;
+        }
+  }
+  static DDL_DEV void zero(f32x16 (&acc)[TM][TN]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  }
+
+  // In-launch hand-off of partial tiles (MI355X guide §6 Guideline 16, sc1 form): the
+  // partials were stored write-through (sc1), so publishing is just every wave draining its
+  // stores, the block barrier and ONE relaxed agent-scope ticket add — no release fence
+  // (an agent release writes back the XCD's whole L2, which serialised many-worker launches).
+  // The last of `count` arrivers reads every partial with sc1 loads (they bypass this CU's
+  // L1), so it needs no acquire fence; it re-arms the ticket and tells its block via LDS
+  // (the flag lives in the kernel's single __shared__ array: guide §5 trap 4a).
+  static DDL_DEV bool arrive(int* ticket, int count, int* flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int prev = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == count - 1;
+      if (last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    const bool last = *flag != 0;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the slab loads below
+    __syncthreads();  // flag may be rewritten by the next arrive of this block
+    return last;
+  }
+};
+
+// ---- drivers ------------------------------------------------------------------------------
+// Each driver is a device-function body over a *virtual* block id, so a kernel can host one
+// problem (gemm_f32_kernel / gemm_streamk_kernel) or two independent problems side by side
+// (gemm_dual_kernel: the data- and weight-gradient GEMMs of one layer in ONE launch — their
+// concurrency without a second stream, whose cross-queue event waits cost tens of us).
+// `lds` is the block's staging array (>= GemmTile::LDS_F4 float4), `flag` one int of LDS.
+
+// Classic split-K: virtual grid (gx, gy, gz); split bz covers K range
+// [bz*kchunk, (bz+1)*kchunk).  mode 0: no split; mode 1: in-launch last-arriver reduction of
+// the gz partials (in z order, deterministic); mode 2: partials only (splitk_wide_reduce).
+template <int BM, int BN, int BK, int WM, int WN, class P>
+DDL_DEV void splitk_body(const P& p, int kchunk, int mode, float4* __restrict__ slab,
+                         int* __restrict__ tickets, int bx, int by, int bz, int gx, int gy,
+                         int gz, float* lds, int* flag) {
+  using T = GemmTile<BM, BN, BK, WM, WN, P>;
+  using G = typename T::G;
+  const int m_blk = bx * BM;
+  const int n_blk = by * BN;
+  const int kb = bz * kchunk;
+  const int ke = min(p.K, kb + kchunk);
+  f32x16 acc[T::TM][T::TN];
+  T::mainloop(p, m_blk, n_blk, kb, ke, lds, acc);
+  if (mode != 0) {
+    const int tile = by * gx + bx;
+    const int ntiles = gx * gy;
+    const brsrc_t sr = make_rsrc(slab, (uint32_t)(gz * ntiles * G::PART4 * 16u));
+    T::store_partial(sr, ((size_t)bz * ntiles + tile) * G::PART4, acc);
+    if (mode == 2) return;
+    if (!T::arrive(&tickets[tile], gz, flag)) return;
+    T::zero(acc);
+    for (int z = 0; z < gz; ++z) T::add_partial(sr, ((size_t)z * ntiles + tile) * G::PART4, acc);
+  }
+  T::epilogue(p, m_blk, n_blk, acc);
+}
+
+// Stream-K (balanced persistent schedule).  The iteration space is I = tiles * KI
+// (KI = K tiles of BK per output tile), tiles ordered m-fastest.  Worker w of the W
+// one-block workers owns iterations [w*I/W, (w+1)*I/W): every SIMD gets the same MFMA work
+// (+-1 K tile) whatever the tile count, instead of whole tiles/splits quantised over the
+// 1024 SIMDs.  A worker finishes whole tiles with the fused epilogue directly; its first and
+// last tile may be partial: those partials go to slab slot (w, 0|1) and the last of the
+// tile's contributors sums them in worker order (deterministic) and runs the epilogue — the
+// split-K reduction happens inside the same launch, with no separate reduce kernel.
+// Workers are numbered XCD-major (hardware dispatches block b to XCD b % 8), so the
+// neighbours that share a boundary tile, and adjacent tiles' operands, stay in one L2.
+template <int BM, int BN, int BK, int WM, int WN, class P>
+DDL_DEV void streamk_body(const P& p, int KI, int gx, long long I, float4* __restrict__ slab,
+                          int* __restrict__ tickets, int bid, int W, float* lds, int* flag) {
+  using T = GemmTile<BM, BN, BK, WM, WN, P>;
+  using G = typename T::G;
+  const int w = (bid & 7) * (W >> 3) + (bid >> 3);  // W % 8 == 0 (host)
+  const brsrc_t sr = make_rsrc(slab, (uint32_t)W * 2u * G::PART4 * 16u);
+  auto first_iter = [&](int ww) -> long long { return (long long)ww * I / W; };
+  // worker owning iteration x: the largest ww with first_iter(ww) <= x
+  auto owner = [&](long long x) -> int { return (int)(((x + 1) * W + I - 1) / I) - 1; };
+  long long it = first_iter(w);
+  const long long end = first_iter(w + 1);
+  const int start_tile = (int)(it / KI);
+  f32x16 acc[T::TM][T::TN];
+  while (it < end) {
+    const int tile = (int)(it / KI);
+    const int klo = (int)(it - (long long)tile * KI);
+    const int khi = (int)min((long long)KI, (long long)klo + (end - it));
+    const int m_blk = (tile % gx) * BM, n_blk = (tile / gx) * BN;
+    T::mainloop(p, m_blk, n_blk, klo * BK, min(p.K, khi * BK), lds, acc);
+    it += khi - klo;
+    if (klo == 0 && khi == KI) {
+      T::epilogue(p, m_blk, n_blk, acc);
+      continue;
+    }
+    const int slot = (tile == start_tile) ? 0 : 1;
+    T::store_partial(sr, ((size_t)w * 2 + slot) * G::PART4, acc);
+    const long long t0 = (long long)tile * KI;
+    const int wf = owner(t0), wl = owner(t0 + KI - 1);
+    if (!T::arrive(&tickets[tile], wl - wf + 1, flag)) continue;
+    T::zero(acc);
+    for (int ww = wf; ww <= wl; ++ww) {
+      const int s = (first_iter(ww) / KI == tile) ? 0 : 1;
+      T::add_partial(sr, ((size_t)ww * 2 + s) * G::PART4, acc);
+    }
+    T::epilogue(p, m_blk, n_blk, acc);
+  }
+}
+
+// Launch geometry of one GEMM problem under its schedule (host-computed, passed by value).
+struct SubGrid {
+  int nblocks = 0;   // blocks (virtual ids 0..nblocks-1)
+  int streamk = 0;   // 1: stream-K with W = nblocks workers
+  int gx = 1, gy = 1, gz = 1;
+  int kchunk = 0, mode = 0;  // split-K
+  int KI = 0;                // stream-K
+  long long I = 0;
+  float4* slab = nullptr;
+  int* tickets = nullptr;
+};
+
+template <int BM, int BN, int BK, int WM, int WN, class P>
+DDL_DEV void run_sub(const P& p, const SubGrid& g, int vb, float* lds, int* flag) {
+  if (g.streamk) {
+    streamk_body<BM, BN, BK, WM, WN, P>(p, g.KI, g.gx, g.I, g.slab, g.tickets, vb, g.nblocks,
+                                        lds, flag);
+  } else {
+    const int bx = vb % g.gx, t = vb / g.gx;
+    splitk_body<BM, BN, BK, WM, WN, P>(p, g.kchunk, g.mode, g.slab, g.tickets, bx, t % g.gy,
+                                       t / g.gy, g.gx, g.gy, g.gz, lds, flag);
+  }
+}
+
+template <int BM, int BN, int BK, int WM, int WN, class P>
+__global__ void __launch_bounds__(WM * WN * 64)
+gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets) {
+  using T = GemmTile<BM, BN, BK, WM, WN, P>;
+  __shared__ float4 lds4[T::LDS_F4 + 1];  // staging images + last-arriver flag (one array:
+                                          // guide §5 trap 4a)
+  splitk_body<BM, BN, BK, WM, WN, P>(p, kchunk, mode, slab, tickets, blockIdx.x, blockIdx.y,
+                                     blockIdx.z, gridDim.x, gridDim.y, gridDim.z,
+                                     reinterpret_cast<float*>(lds4),
+                                     reinterpret_cast<int*>(lds4 + T::LDS_F4));
+}
+
+template <int BM, int BN, int BK, int WM, int WN, class P>
+__global__ void __launch_bounds__(WM * WN * 64)
+gemm_streamk_kernel(P p, int KI, int gx, long long I, float4* __restrict__ slab,
+                    int* __restrict__ tickets) {
+  using T = GemmTile<BM, BN, BK, WM, WN, P>;
+  __shared__ float4 lds4[T::LDS_F4 + 1];
+  streamk_body<BM, BN, BK, WM, WN, P>(p, KI, gx, I, slab, tickets, blockIdx.x, gridDim.x,
+                                      reinterpret_cast<float*>(lds4),
+                                      reinterpret_cast<int*>(lds4 + T::LDS_F4));
+}
+
+template <int BM_, int BN_, int BK_, int WM_, int WN_>
+struct TileCfg {
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_;
+  static constexpr int NT = WM * WN * 64;
+};
+
+// Two independent GEMM problems in one launch: blocks [0, ga.nblocks) run problem A, the
+// rest problem B.  Both must use one-wave blocks.
+template <class CA, class PA, class CB, class PB>
+__global__ void __launch_bounds__(64)
+gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb) {
+  static_assert(CA::NT == 64 && CB::NT == 64, "dual launch needs one-wave blocks");
+  using TA = GemmTile<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>;
+  using TB = GemmTile<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>;
+  constexpr int L = TA::LDS_F4 > TB::LDS_F4 ? TA::LDS_F4 : TB::LDS_F4;
+  __shared__ float4 lds4[L + 1];
+  float* lds = reinterpret_cast<float*>(lds4);
+  int* flag = reinterpret_cast<int*>(lds4 + L);
+  const int b = blockIdx.x;
+  if (b < ga.nblocks)
+    run_sub<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, b, lds, flag);
+  else
+    run_sub<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, b - ga.nblocks, lds, flag);
+}
+
+// Wide split-K reduce (mode 2): RL lanes cooperate on one float4 output element.
+template <int BM, int BN, int WM, int WN, int RL, class P>
+__global__ void __launch_bounds__(256)
+splitk_wide_reduce(P p, const float4* __restrict__ slab, int S, int gx, int ntiles) {
+  using G = TileGeo<BM, BN, WM, WN>;
+  const int gid = blockIdx.x * 256 + threadIdx.x;
+  const int elem = gid / RL;
+  const int sub = gid % RL;
+  const int nelem = ntiles * G::PART4;
+  const bool valid = elem < nelem;
+  const int e = valid ? elem : 0;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  const size_t zstride = (size_t)ntiles * G::PART4;
+  for (int z = sub; z < S; z += RL) {
+    const float4 t = slab[z * zstride + e];
+    s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+  }
+#pragma unroll
+  for (int off = RL / 2; off > 0; off >>= 1) {
+    s.x += __shfl_xor(s.x, off, 64);
+    s.y += __shfl_xor(s.y, off, 64);
+    s.z += __shfl_xor(s.z, off, 64);
+    s.w += __shfl_xor(s.w, off, 64);
+  }
+  if (!valid || sub != 0) return;
+  const int tile = e / G::PART4;
+  int r = e % G::PART4;
+  constexpr int WPART = G::FRAGS * 4 * 64;
+  const int wave = r / WPART;
+  r %= WPART;
+  const int fg = r / 64, lane = r % 64;
+  const int frag = fg / 4, g = fg % 4;
+  const int i = frag / G::TN, j = frag % G::TN;
+  const int wm = wave / WN, wn = wave % WN;
+  const int bx = tile % gx, by = tile / gx;
+  const int m0 = bx * BM + wm * G::WTM + i * 32 + 8 * g + 4 * (lane >> 5);
+  const int n = by * BN + wn * G::WTN + j * 32 + (lane & 31);
+  if (n < p.N && m0 < p.M) p.epi(m0, n, f32x4{s.x, s.y, s.z, s.w});
+}
+
+template <int BK>
+inline int splitk_kchunk(int K, int splits) {
+  if (splits <= 1) return K;
+  const int per = (K + splits - 1) / splits;
+  const int kc = ((per + BK - 1) / BK) * BK;
+  return kc < BK ? BK : kc;
+}
+
+template <int BK>
+inline int splitk_z(int K, int splits) {
+  if (splits <= 1) return 1;
+  const int kc = splitk_kchunk<BK>(K, splits);
+  const int z = (K + kc - 1) / kc;
+  return z < 1 ? 1 : z;
+}
+
+// float4 partial-slab elements a launch needs
+template <int BM, int BN, int BK, int WM, int WN>
+inline size_t splitk_slab_f4(int M, int N, int K, int splits) {
+  const int z = splitk_z<BK>(K, splits);
+  if (z <= 1) return 0;
+  const size_t tiles = (size_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  return (size_t)z * tiles * TileGeo<BM, BN, WM, WN>::PART4;
+}
+
+// Stream-K worker count actually launched for a requested `workers` (0 = stream-K off):
+// a multiple of 8 (XCD-major numbering), at most one worker per K iteration.
+template <int BM, int BN, int BK>
+inline int streamk_workers(int M, int N, int K, int workers) {
+  if (workers <= 0) return 0;
+  const long long I = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN) * ((K + BK - 1) / BK);
+  long long w = workers < I ? workers : I;
+  w &= ~7LL;
+  return w < 8 ? 0 : (int)w;
+}
+
+// float4 partial-slab elements a launch needs (stream-K when workers > 0, else split-K)
+template <int BM, int BN, int BK, int WM, int WN>
+inline size_t gemm_slab_f4(int M, int N, int K, int splits, int workers) {
+  // (max of both: a stream-K launch with more tiles than tickets falls back to split-K)
+  const int w = streamk_workers<BM, BN, BK>(M, N, K, workers);
+  const size_t sk = (size_t)w * 2 * TileGeo<BM, BN, WM, WN>::PART4;
+  const size_t sp = splitk_slab_f4<BM, BN, BK, WM, WN>(M, N, K, splits);
+  return sk > sp ? sk : sp;
+}
+
+// Schedule of one launch: stream-K when workers > 0 (and the tile count fits the tickets),
+// else split-K with `splits`: z > wide_thr uses mode 2 (separate wide reduce), else mode 1
+// (last arriver).
+template <int BM, int BN, int BK, class P>
+inline SubGrid plan_gemm(const P& p, int splits, int workers, int wide_thr,
+                         const SplitScratch& sc) {
+  SubGrid g;
+  g.slab = reinterpret_cast<float4*>(sc.slab);
+  g.tickets = sc.tickets;
+  if (p.M <= 0 || p.N <= 0) return g;
+  g.gx = (p.M + BM - 1) / BM;
+  g.gy = (p.N + BN - 1) / BN;
+  const int W = streamk_workers<BM, BN, BK>(p.M, p.N, p.K, workers);
+  if (W > 0 && (long long)g.gx * g.gy <= sc.max_tiles) {
+    g.streamk = 1;
+    g.nblocks = W;
+    g.KI = (p.K + BK - 1) / BK;
+    g.I = (long long)g.gx * g.gy * g.KI;
+    return g;
+  }
+  g.gz = splitk_z<BK>(p.K, splits);
+  g.kchunk = g.gz > 1 ? splitk_kchunk<BK>(p.K, splits) : p.K;
+  g.mode = g.gz == 1 ? 0 : (g.gz > wide_thr ? 2 : 1);
+  if (g.mode == 1 && (long long)g.gx * g.gy > sc.max_tiles) g.mode = 2;  // ticket capacity
+  g.nblocks = g.gx * g.gy * g.gz;
+  return g;
+}
+
+// The separate reduce of a mode-2 split-K launch (no-op otherwise).
+template <int BM, int BN, int BK, int WM, int WN, class P>
+inline void launch_reduce(const P& p, const SubGrid& g, hipStream_t stream) {
+  if (g.streamk || g.mode != 2 || g.nblocks == 0) return;
+  using G = TileGeo<BM, BN, WM, WN>;
+  const int ntiles = g.gx * g.gy, z = g.gz;
+  const size_t nelem = (size_t)ntiles * G::PART4;
+  const float4* s4 = g.slab;
+  if (z > 32) {
+    const size_t th = nelem * 64;
+    hipLaunchKernelGGL((splitk_wide_reduce<BM, BN, WM, WN, 64, P>), dim3((th + 255) / 256),
+                       dim3(256), 0, stream, p, s4, z, g.gx, ntiles);
+  } else if (z > 4) {
+    const size_t th = nelem * 16;
+    hipLaunchKernelGGL((splitk_wide_reduce<BM, BN, WM, WN, 16, P>), dim3((th + 255) / 256),
+                       dim3(256), 0, stream, p, s4, z, g.gx, ntiles);
+  } else {
+    const size_t th = nelem * 4;
+    hipLaunchKernelGGL((splitk_wide_reduce<BM, BN, WM, WN, 4, P>), dim3((th + 255) / 256),
+                       dim3(256), 0, stream, p, s4, z, g.gx, ntiles);
+  }
+}
+
+template <int BM, int BN, int BK, int WM, int WN, class P>
+inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch& sc,
+                        hipStream_t stream, int workers = 0) {
+  const SubGrid g = plan_gemm<BM, BN, BK>(p, splits, workers, wide_thr, sc);
+  if (g.nblocks == 0) return;
+  if (g.streamk) {
+    hipLaunchKernelGGL((gemm_streamk_kernel<BM, BN, BK, WM, WN, P>), dim3(g.nblocks),
+                       dim3(WM * WN * 64), 0, stream, p, g.KI, g.gx, g.I, g.slab, g.tickets);
+    return;
+  }
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, WM, WN, P>), dim3(g.gx, g.gy, g.gz),
+                     dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets);
+  launch_reduce<BM, BN, BK, WM, WN, P>(p, g, stream);
+}
+
+// Problems A and B (one-wave tile configs CA / CB) in one launch, each with its own schedule
+// and its own scratch (slab + tickets); mode-2 reduces follow on the same stream.
+template <class CA, class PA, class CB, class PB>
+inline void launch_gemm_dual(const PA& pa, int sa, int wa, const SplitScratch& sca, int wide_a,
+                             const PB& pb, int sb, int wb, const SplitScratch& scb, int wide_b,
+                             hipStream_t stream) {
+  const SubGrid ga = plan_gemm<CA::BM, CA::BN, CA::BK>(pa, sa, wa, wide_a, sca);
+  const SubGrid gb = plan_gemm<CB::BM, CB::BN, CB::BK>(pb, sb, wb, wide_b, scb);
+  const int n = ga.nblocks + gb.nblocks;
+  if (n > 0)
+    hipLaunchKernelGGL((gemm_dual_kernel<CA, PA, CB, PB>), dim3(n), dim3(64), 0, stream, pa, ga,
+                       pb, gb);
+  launch_reduce<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, stream);
+  launch_reduce<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, stream);
+}
+
+}  // namespace ddl

@@ -1,0 +1,137 @@
+// Classifier head: fc3 (512->10) + softmax cross-entropy (model.py:85-92) and its backward.
+//
+// fc3 is too skinny (N = 10) for MFMA tiles to pay, so it is two small VALU kernels:
+//   head_fwd : one wave64 per sample: logits, loss, dlogits = (softmax - onehot)/B
+//              (SoftmaxCrossEntropyWithLogits + Mean fwd/bwd),
+//              or in eval mode the correct-prediction count (F22).
+//   head_bwd : dW3_aug[513,10] = [h2;1]^T dlogits and dh2 = dlogits W3^T, with the fc2
+//              dropout backward fused (mask regenerated from the seed, nothing stored).
+#include "common.h"
+#include "api.h"
+
+namespace ddl {
+
+constexpr int HK = 512;  // fc3 input width
+constexpr int HC = 10;   // classes
+
+__global__ void __launch_bounds__(256)
+head_fwd_kernel(const float* __restrict__ h2, const float* __restrict__ w,
+                const float* __restrict__ bias, const int64_t* __restrict__ labels, int B,
+                float inv_batch, float* __restrict__ dlog, float* __restrict__ loss,
+                int* __restrict__ correct) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  float acc[HC];
+#pragma unroll
+  for (int c = 0; c < HC; ++c) acc[c] = 0.f;
+  const float* hr = h2 + (size_t)row * HK;
+#pragma unroll 4
+  for (int k = lane; k < HK; k += 64) {
+    const float hv = hr[k];
+    const float* wr = w + k * HC;
+#pragma unroll
+    for (int c = 0; c < HC; ++c) acc[c] = fmaf(hv, wr[c], acc[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < HC; ++c) {
+    float v = acc[c];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    acc[c] = v + bias[c];
+  }
+  float mx = acc[0];
+  int arg = 0;
+#pragma unroll
+  for (int c = 1; c < HC; ++c)
+    if (acc[c] > mx) { mx = acc[c]; arg = c; }
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < HC; ++c) se += __expf(acc[c] - mx);
+  const int lab = (int)labels[row];
+  if (lane == 0) {
+    float ll = 0.f;
+#pragma unroll
+    for (int c = 0; c < HC; ++c)
+      if (c == lab) ll = acc[c];
+    if (loss) loss[row] = (mx + __logf(se)) - ll;
+    if (correct && arg == lab) atomicAdd(correct, 1);
+  }
+  if (dlog && lane < HC) {
+    float lc = 0.f;
+#pragma unroll
+    for (int c = 0; c < HC; ++c)
+      if (c == lane) lc = acc[c];
+    const float p = __expf(lc - mx) / se;
+    dlog[(size_t)row * HC + lane] = (p - (lane == lab ? 1.f : 0.f)) * inv_batch;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+head_bwd_kernel(const float* __restrict__ h2, const float* __restrict__ w,
+                const float* __restrict__ dlog, int B, int wblocks, const uint32_t* __restrict__ seed,
+                uint32_t seed_v,
+                uint32_t thr24, float inv_keep, float* __restrict__ gw, float* __restrict__ gb,
+                float* __restrict__ dpre2) {
+  if ((int)blockIdx.x < wblocks) {
+    // dW_aug row i (i == HK: bias row of ones): one wave per row, lanes stride the batch,
+    // 10 class partials reduced across the wave.
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i > HK) return;
+    float acc[HC];
+#pragma unroll
+    for (int c = 0; c < HC; ++c) acc[c] = 0.f;
+    for (int b = lane; b < B; b += 64) {
+      const float hv = i < HK ? h2[(size_t)b * HK + i] : 1.f;
+      const float* dl = dlog + (size_t)b * HC;
+#pragma unroll
+      for (int c = 0; c < HC; ++c) acc[c] = fmaf(hv, dl[c], acc[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < HC; ++c) {
+      float v = acc[c];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      acc[c] = v;
+    }
+    if (lane < HC) {
+      float v = 0.f;
+#pragma unroll
+      for (int c = 0; c < HC; ++c)
+        if (c == lane) v = acc[c];
+      if (i < HK) gw[i * HC + lane] = v;
+      else gb[lane] = v;
+    }
+    return;
+  }
+  const int idx = (blockIdx.x - wblocks) * 256 + threadIdx.x;
+  if (idx >= B * HK) return;
+  const int b = idx / HK, i = idx % HK;
+  float g = 0.f;
+#pragma unroll
+  for (int c = 0; c < HC; ++c) g = fmaf(dlog[(size_t)b * HC + c], w[i * HC + c], g);
+  if (thr24) {
+    const uint32_t key = ddl_mix32((seed ? *seed : seed_v) + 2u * 0x9E3779B9u);
+    g = ddl_keep(key, (uint32_t)idx, thr24) ? g * inv_keep : 0.f;
+  }
+  dpre2[idx] = g;
+}
+
+void launch_head_fwd(const float* h2, const float* w, const float* bias, const int64_t* labels,
+                     int B, float* dlog, float* loss, int* correct, hipStream_t st) {
+  hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, st, h2, w, bias, labels, B,
+                     1.f / (float)B, dlog, loss, correct);
+}
+
+void launch_head_bwd(const float* h2, const float* w, const float* dlog, int B,
+                     const uint32_t* seed, uint32_t seed_v, uint32_t thr24, float inv_keep,
+                     float* gw, float* gb,
+                     float* dpre2, hipStream_t st) {
+  const int wblocks = (HK + 1 + 3) / 4;  // one wave per dW_aug row
+  const int dblocks = (B * HK + 255) / 256;
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(wblocks + dblocks), dim3(256), 0, st, h2, w, dlog, B,
+                     wblocks, seed, seed_v, thr24, inv_keep, gw, gb, dpre2);
+}
+
+}  // namespace ddl

@@ -1,0 +1,430 @@
+// Problem policies for every GEMM-shaped op of the MNIST CNN.
+//
+// Activations NHWC fp32, weights HWIO flattened to [25*Cin, Cout] (model.py:24-86).
+// Each policy = per-thread gather info (prepA/prepB, fixed across K tiles) + 4-wide
+// gathers at a wave-uniform tile base k0 (loadA/loadB, raw buffer loads: padding and
+// tile edges read as 0 via the hardware range check) + fused epilogue for
+// ddl::gemm_f32_kernel (gemm.h).  Tiles are BK = 32 deep and every Cin/Cout >= 32 is a
+// multiple of 32, so a K tile never straddles two 5x5 taps: tap = k0 / C is uniform.
+#pragma once
+#include <math.h>
+#include "gemm.h"
+
+namespace ddl {
+
+constexpr int kBK = 32;
+
+struct LinInfo {   // linear operand: element offset of (row, k = 0 + kk), validity
+  int off;
+  int kk;
+  bool ok;
+};
+
+// ---------------------------------------------------------------------------------------------
+// conv 5x5 SAME + bias + ReLU + max-pool 2x2/2 SAME, forward (model.py:28-31 etc.)
+// M enumerates conv output positions pool-window-major: m = ((b*HP+py)*HP+px)*4 + q,
+// q = dy*2+dx, so a lane's 4 consecutive C rows are one pool window.  N = COUT,
+// K = 25*CIN (k = tap*CIN + ci, tap = ky*5+kx).  Positions outside an odd-sized map
+// (SAME pool 7->4) are -inf for the max.  Epilogue writes the pooled output and a 1-byte
+// code: argmax q, or 0xFF when the max is <= 0 (ReLU inactive => no gradient).
+// ---------------------------------------------------------------------------------------------
+template <int H, int CIN, int COUT>
+struct ConvFwd {
+  static constexpr int HP = (H + 1) / 2;
+  static constexpr bool A_KCONTIG = true;
+  static constexpr bool B_KCONTIG = false;
+  static_assert(CIN == 1 || CIN % kBK == 0, "tap must be tile-uniform");
+  int M, N, K;
+  const float* __restrict__ x;     // [B,H,H,CIN]
+  const float* __restrict__ w;     // [25*CIN, COUT]
+  const float* __restrict__ bias;  // [COUT]
+  float* __restrict__ out;         // [B,HP,HP,COUT]
+  uint8_t* __restrict__ code;      // [B,HP,HP,COUT] or nullptr
+
+  struct AInfo {
+    int base;   // element offset of the image
+    int y, x;
+    int kk;
+    bool ok;
+  };
+  using BInfo = LinInfo;
+
+  DDL_DEV uint32_t x_bytes() const { return (uint32_t)((M / (HP * HP * 4)) * H * H * CIN) * 4u; }
+
+  DDL_DEV AInfo prepA(int m, int kk) const {
+    AInfo a;
+    const int q = m & 3;
+    int t = m >> 2;
+    const int px = t % HP;
+    t /= HP;
+    const int py = t % HP;
+    const int b = t / HP;
+    a.y = 2 * py + (q >> 1);
+    a.x = 2 * px + (q & 1);
+    a.ok = m < M && a.y < H && a.x < H;
+    a.base = b * H * H * CIN;
+    a.kk = kk;
+    return a;
+  }
+  DDL_DEV float4 loadA(const AInfo& a, int k0) const {
+    const brsrc_t r = make_rsrc(x, x_bytes());
+    if constexpr (CIN % kBK == 0) {
+      const int tap = k0 / CIN, cib = k0 - tap * CIN;
+      const int ky = tap / 5, kx = tap - ky * 5;
+      const int iy = a.y + ky - 2, ix = a.x + kx - 2;
+      const bool good = a.ok && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)H;
+      const int off = a.base + (iy * H + ix) * CIN + cib + a.kk;
+      return bload4(r, good ? off * 4 : kOOB);
+    } else {  // CIN == 1: k = tap, 4 taps per float4
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + a.kk + j;
+        const int ky = k / 5, kx = k - ky * 5;
+        const int iy = a.y + ky - 2, ix = a.x + kx - 2;
+        const bool good =
+            a.ok && k < K && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)H;
+        v[j] = bload1(r, good ? (a.base + iy * H + ix) * 4 : kOOB);
+      }
+      return make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+  DDL_DEV BInfo prepB(int n, int kk) const { return {kk * COUT + n, kk, n < N}; }
+  DDL_DEV float4 loadB(const BInfo& b, int k0) const {
+    const brsrc_t r = make_rsrc(w, 25u * CIN * COUT * 4u);
+    const bool good = b.ok && k0 + b.kk < K;
+    return bload4(r, good ? (b.off + k0 * COUT) * 4 : kOOB);
+  }
+  DDL_DEV void epi(int m0, int n, f32x4 v) const {
+    const int t = m0 >> 2;
+    const int px = t % HP;
+    const int py = (t / HP) % HP;
+    const float bb = bias[n];
+    float best = -INFINITY;
+    int arg = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int y = 2 * py + (q >> 1), xx = 2 * px + (q & 1);
+      if (y < H && xx < H) {
+        const float val = v[q] + bb;
+        if (val > best) { best = val; arg = q; }
+      }
+    }
+    const size_t o = (size_t)t * COUT + n;
+    out[o] = best > 0.f ? best : 0.f;
+    if (code) code[o] = best > 0.f ? (uint8_t)arg : (uint8_t)0xFF;
+  }
+};
+
+// Scatter one pooled-output gradient g into the 2x2 window of the pre-pool gradient:
+// dpre[b, 2y+dy, 2x+dx, c] = (code == dy*2+dx) ? g : 0  (ReLU folded in via code 0xFF).
+template <int HPREV, int C>
+DDL_DEV void pool_bwd_scatter(float* __restrict__ dpre, int b, int y, int x, int c, uint8_t code,
+                              float g) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int yy = 2 * y + (q >> 1), xx = 2 * x + (q & 1);
+    if (yy < HPREV && xx < HPREV)
+      dpre[((size_t)(b * HPREV + yy) * HPREV + xx) * C + c] = (code == q) ? g : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// conv data gradient (Conv2DBackpropInput) fused with the previous
+// layer's MaxPoolGrad + ReluGrad (B7/B8): M = B*H*H (b,y,x), N = CIN, K = 25*COUT
+// (k = tap*COUT + co).  dX[b,y,x,ci] = sum dpre[b, y-ky+2, x-kx+2, co] * W[ky,kx,ci,co];
+// the epilogue scatters dX through the previous pool's codes into dpre_prev.
+// ---------------------------------------------------------------------------------------------
+template <int H, int CIN, int COUT, int HPREV>
+struct ConvDgrad {
+  static constexpr bool A_KCONTIG = true;
+  static constexpr bool B_KCONTIG = true;
+  static_assert(COUT % kBK == 0, "tap must be tile-uniform");
+  int M, N, K;
+  const float* __restrict__ dpre;        // [B,H,H,COUT]
+  const float* __restrict__ w;           // [25*CIN, COUT]
+  const uint8_t* __restrict__ code_prev; // [B,H,H,CIN]
+  float* __restrict__ dpre_prev;         // [B,HPREV,HPREV,CIN]
+
+  struct AInfo {
+    int base;
+    int y, x;
+    int kk;
+    bool ok;
+  };
+  using BInfo = LinInfo;
+
+  DDL_DEV AInfo prepA(int m, int kk) const {
+    AInfo a;
+    a.ok = m < M;
+    const int mm = a.ok ? m : 0;
+    a.x = mm % H;
+    const int t = mm / H;
+    a.y = t % H;
+    a.base = (t / H) * H * H * COUT;
+    a.kk = kk;
+    return a;
+  }
+  DDL_DEV float4 loadA(const AInfo& a, int k0) const {
+    const brsrc_t r = make_rsrc(dpre, (uint32_t)M * COUT * 4u);
+    const int tap = k0 / COUT, cob = k0 - tap * COUT;
+    const int ky = tap / 5, kx = tap - ky * 5;
+    const int oy = a.y - ky + 2, ox = a.x - kx + 2;
+    const bool good = a.ok && (unsigned)oy < (unsigned)H && (unsigned)ox < (unsigned)H;
+    return bload4(r, good ? (a.base + (oy * H + ox) * COUT + cob + a.kk) * 4 : kOOB);
+  }
+  DDL_DEV BInfo prepB(int n, int kk) const { return {n * COUT + kk, kk, n < N}; }
+  DDL_DEV float4 loadB(const BInfo& b, int k0) const {
+    const brsrc_t r = make_rsrc(w, 25u * CIN * COUT * 4u);
+    const int tap = k0 / COUT, cob = k0 - tap * COUT;
+    return bload4(r, b.ok ? (b.off + tap * CIN * COUT + cob) * 4 : kOOB);
+  }
+  DDL_DEV void epi(int m0, int n, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + r;
+      if (m >= M) break;
+      const int xx = m % H;
+      const int t = m / H;
+      const int y = t % H, b = t / H;
+      pool_bwd_scatter<HPREV, CIN>(dpre_prev, b, y, xx, n, code_prev[(size_t)m * CIN + n], v[r]);
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// conv weight gradient (Conv2DBackpropFilter + bias grad, B10/B8): dW_aug[25*CIN+1, COUT].
+// M = 25*CIN + 1 (row 25*CIN is a row of ones -> db), N = COUT, K = B*H*H.
+// A[m=(tap,ci)][k=(b,y,x)] = x[b, y+ky-2, x+kx-2, ci] (ci contiguous => MN-contiguous),
+// B[n=co][k] = dpre[k*COUT + co] (MN-contiguous).
+// ---------------------------------------------------------------------------------------------
+template <int H, int CIN, int COUT>
+struct ConvWgrad {
+  static constexpr bool A_KCONTIG = false;
+  static constexpr bool B_KCONTIG = false;
+  static constexpr int KW = 25 * CIN;
+  int M, N, K;
+  const float* __restrict__ x;     // [B,H,H,CIN]
+  const float* __restrict__ dpre;  // [B,H,H,COUT]
+  float* __restrict__ gw;          // [25*CIN, COUT]
+  float* __restrict__ gb;          // [COUT]
+
+  struct AInfo {
+    int m;      // first of the 4 rows
+    int dy, dx; // tap offsets of row m (vector path)
+    int ci;
+    int kk;
+    bool vec;   // all 4 rows are weight rows of one tap
+  };
+  using BInfo = LinInfo;
+
+  DDL_DEV AInfo prepA(int m, int kk) const {
+    AInfo a;
+    a.m = m;
+    const int tap = m / CIN;
+    a.ci = m - tap * CIN;
+    a.dy = tap / 5 - 2;
+    a.dx = tap % 5 - 2;
+    a.kk = kk;
+    a.vec = (CIN % 4 == 0) && (m + 3 < KW);
+    return a;
+  }
+  DDL_DEV float4 loadA(const AInfo& a, int k0) const {
+    const brsrc_t r = make_rsrc(x, (uint32_t)K * CIN * 4u);
+    const int k = k0 + a.kk;
+    const bool kin = k < K;
+    const int xx = k % H;
+    const int t = k / H;
+    const int y = t % H, b = t / H;
+    if constexpr (CIN % 4 == 0) {
+      // KW = 25*CIN is a multiple of 4, so a 4-row group is either all weight rows (one
+      // 16-B gather) or starts at row >= KW: the ones row (db) then zeros.  Branch-free.
+      const int iy = y + a.dy, ix = xx + a.dx;
+      const bool good = a.vec && kin && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)H;
+      float4 v = bload4(r, good ? (((b * H + iy) * H + ix) * CIN + a.ci) * 4 : kOOB);
+      if (a.m == KW) v.x = kin ? 1.f : 0.f;
+      return v;
+    }
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = a.m + j;
+      const int tap = e / CIN, ci = e - tap * CIN;
+      const int iy = y + tap / 5 - 2, ix = xx + tap % 5 - 2;
+      const bool good = kin && e < KW && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)H;
+      const float val = bload1(r, good ? (((b * H + iy) * H + ix) * CIN + ci) * 4 : kOOB);
+      v[j] = (e == KW && kin) ? 1.f : val;
+    }
+    return make_float4(v[0], v[1], v[2], v[3]);
+  }
+  DDL_DEV BInfo prepB(int n, int kk) const { return {kk * COUT + n, kk, n < N}; }
+  DDL_DEV float4 loadB(const BInfo& b, int k0) const {
+    const brsrc_t r = make_rsrc(dpre, (uint32_t)K * COUT * 4u);
+    const bool good = b.ok && k0 + b.kk < K;
+    return bload4(r, good ? (b.off + k0 * COUT) * 4 : kOOB);
+  }
+  DDL_DEV void epi(int m0, int n, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + r;
+      if (m < KW) gw[(size_t)m * COUT + n] = v[r];
+      else if (m == KW) gb[n] = v[r];
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// fully connected forward (model.py:70 fc1: +b, ReLU, dropout; :79,82 fc2: +b, dropout)
+// M = B, N = NOUT, K = KIN.  Dropout key derived on device from *seed (graph-replayable),
+// or from seed_v when no seed word is given (the native step runner: no seed-upload kernel).
+// ---------------------------------------------------------------------------------------------
+template <bool RELU>
+struct FcFwd {
+  static constexpr bool A_KCONTIG = true;
+  static constexpr bool B_KCONTIG = false;
+  int M, N, K;
+  const float* __restrict__ in;    // [B,KIN]
+  const float* __restrict__ w;     // [KIN,NOUT]
+  const float* __restrict__ bias;  // [NOUT]
+  float* __restrict__ out;         // [B,NOUT]
+  const uint32_t* __restrict__ seed;
+  uint32_t layer;
+  uint32_t thr24;                  // 0 => no dropout
+  float inv_keep;
+  uint32_t seed_v;                 // dropout seed by value when `seed` is null
+
+  using AInfo = LinInfo;
+  using BInfo = LinInfo;
+  DDL_DEV AInfo prepA(int m, int kk) const { return {m * K + kk, kk, m < M}; }
+  DDL_DEV float4 loadA(const AInfo& a, int k0) const {
+    const brsrc_t r = make_rsrc(in, (uint32_t)M * K * 4u);
+    return bload4(r, a.ok && k0 + a.kk < K ? (a.off + k0) * 4 : kOOB);
+  }
+  DDL_DEV BInfo prepB(int n, int kk) const { return {kk * N + n, kk, n < N}; }
+  DDL_DEV float4 loadB(const BInfo& b, int k0) const {
+    const brsrc_t r = make_rsrc(w, (uint32_t)K * N * 4u);
+    return bload4(r, b.ok && k0 + b.kk < K ? (b.off + k0 * N) * 4 : kOOB);
+  }
+  DDL_DEV void epi(int m0, int n, f32x4 v) const {
+    const float bb = bias[n];
+    uint32_t key = 0;
+    if (thr24) key = ddl_mix32((seed ? *seed : seed_v) + layer * 0x9E3779B9u);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + r;
+      if (m >= M) break;
+      float val = v[r] + bb;
+      if (RELU) val = val > 0.f ? val : 0.f;
+      const uint32_t idx = (uint32_t)(m * N + n);
+      if (thr24) val = ddl_keep(key, idx, thr24) ? val * inv_keep : 0.f;
+      out[idx] = val;
+    }
+  }
+};
+
+// fc data gradient dX = dY W^T (B2/B4/B6).  A = dY [B,NOUT] (K-contig), B[n=i][k=o] =
+// W[i][o] (K-contig).  Epilogue variants:
+//   FcDgradAct  : previous layer was ReLU+dropout (fc1): dpre = hpost > 0 ? g/keep : 0
+//   FcDgradPool : previous layer was the conv4 max-pool (flatten of [B,2,2,256])
+struct FcDgradBase {
+  static constexpr bool A_KCONTIG = true;
+  static constexpr bool B_KCONTIG = true;
+  int M, N, K;
+  const float* __restrict__ dy;     // [B,K]
+  const float* __restrict__ w;      // [N,K]
+  using AInfo = LinInfo;
+  using BInfo = LinInfo;
+  DDL_DEV AInfo prepA(int m, int kk) const { return {m * K + kk, kk, m < M}; }
+  DDL_DEV float4 loadA(const AInfo& a, int k0) const {
+    const brsrc_t r = make_rsrc(dy, (uint32_t)M * K * 4u);
+    return bload4(r, a.ok && k0 + a.kk < K ? (a.off + k0) * 4 : kOOB);
+  }
+  DDL_DEV BInfo prepB(int n, int kk) const { return {n * K + kk, kk, n < N}; }
+  DDL_DEV float4 loadB(const BInfo& b, int k0) const {
+    const brsrc_t r = make_rsrc(w, (uint32_t)N * K * 4u);
+    return bload4(r, b.ok && k0 + b.kk < K ? (b.off + k0) * 4 : kOOB);
+  }
+};
+
+struct FcDgradAct : FcDgradBase {
+  const float* __restrict__ hpost;  // [B,N] post ReLU+dropout activation
+  float inv_keep;
+  float* __restrict__ dx;           // [B,N]
+  DDL_DEV void epi(int m0, int n, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + r;
+      if (m >= M) break;
+      const size_t o = (size_t)m * N + n;
+      dx[o] = hpost[o] > 0.f ? v[r] * inv_keep : 0.f;
+    }
+  }
+};
+
+template <int HP, int C>
+struct FcDgradPool : FcDgradBase {
+  static constexpr int HPREV = 2 * HP;
+  const uint8_t* __restrict__ code;    // [B,HP,HP,C] == [B,N]
+  float* __restrict__ dpre_prev;       // [B,HPREV,HPREV,C]
+  DDL_DEV void epi(int m0, int n, f32x4 v) const {
+    const int c = n % C;
+    const int t = n / C;
+    const int px = t % HP, py = t / HP;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + r;
+      if (m >= M) break;
+      pool_bwd_scatter<HPREV, C>(dpre_prev, m, py, px, c, code[(size_t)m * N + n], v[r]);
+    }
+  }
+};
+
+// fc weight gradient dW_aug[KIN+1, NOUT] = [X;1]^T dY (B2/B4/B6): M = KIN+1, N = NOUT, K = B.
+struct FcWgrad {
+  static constexpr bool A_KCONTIG = false;
+  static constexpr bool B_KCONTIG = false;
+  int M, N, K;
+  int KIN;
+  const float* __restrict__ in;  // [B,KIN]
+  const float* __restrict__ dy;  // [B,NOUT]
+  float* __restrict__ gw;        // [KIN,NOUT]
+  float* __restrict__ gb;        // [NOUT]
+
+  using AInfo = LinInfo;
+  using BInfo = LinInfo;
+  // A info: off = first row m, kk = k offset, ok = the 4 rows are all weight rows
+  DDL_DEV AInfo prepA(int m, int kk) const { return {m, kk, m + 3 < KIN}; }
+  DDL_DEV float4 loadA(const AInfo& a, int k0) const {
+    const brsrc_t r = make_rsrc(in, (uint32_t)K * KIN * 4u);
+    const int k = k0 + a.kk;
+    const bool kin = k < K;
+    if ((KIN & 3) == 0) {  // group = all weight rows, or [ones row, 0, 0, 0] / zeros: branch-free
+      float4 v = bload4(r, (a.ok && kin) ? (k * KIN + a.off) * 4 : kOOB);
+      if (a.off == KIN) v.x = kin ? 1.f : 0.f;
+      return v;
+    }
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = a.off + j;
+      const float val = bload1(r, kin && e < KIN ? (k * KIN + e) * 4 : kOOB);
+      v[j] = (e == KIN && kin) ? 1.f : val;
+    }
+    return make_float4(v[0], v[1], v[2], v[3]);
+  }
+  DDL_DEV BInfo prepB(int n, int kk) const { return {kk * N + n, kk, n < N}; }
+  DDL_DEV float4 loadB(const BInfo& b, int k0) const {
+    const brsrc_t r = make_rsrc(dy, (uint32_t)K * N * 4u);
+    return bload4(r, b.ok && k0 + b.kk < K ? (b.off + k0 * N) * 4 : kOOB);
+  }
+  DDL_DEV void epi(int m0, int n, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + r;
+      if (m < KIN) gw[(size_t)m * N + n] = v[r];
+      else if (m == KIN) gb[n] = v[r];
+    }
+  }
+};
+
+}  // namespace ddl

@@ -1,0 +1,330 @@
+// Native synchronous training-step runner: forward, the four backward segments, and the
+// per-unit gradient exchange + PS update, all enqueued from C++ (one Python call per step).
+//
+// Reference behaviour (SURVEY.md §2.7 sync data plane; mnist_sync_sharding/worker.py:95-120,
+// parameter_server.py:108-126): every worker pushes its gradients to the owning PS, the PS
+// applies Adam once per global step and every worker pulls the new parameters.  Here:
+//
+//  * a unit = a set of plan-buffer ranges whose gradients are complete after backward segment
+//    `seg`; the comm stream waits on that segment's event, so the exchange of the fc layers
+//    runs while the conv backward is still computing (bucketed overlap);
+//  * kind LOCAL  : this rank owns the PS of the ranges (W = 1, or co-located) -> fused Adam;
+//  * kind RS     : flat plan with one PS per GPU: ncclReduceScatter -> fused Adam on this
+//                  rank's 1/W chunk -> in-place ncclAllGather (ring-optimal on xGMI);
+//  * kind REDUCE : tensor-granular plans: ncclReduce(dst=host) -> Adam at the host ->
+//                  ncclBroadcast(src=host), ranges of a unit grouped in one RCCL group.
+//
+// The communicator is our own RCCL comm (torch's librccl instance, id exchanged through
+// torch.distributed), so the per-step host cost is a few launches instead of one Python
+// ProcessGroup call per collective — the Python exchange was host-bound (step timeline:
+// 20-45 us GPU idle at every segment boundary).
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "api.h"
+
+namespace ddl {
+
+#define RCCL_CHECK(x)                                                                 \
+  do {                                                                                \
+    ncclResult_t r_ = (x);                                                            \
+    if (r_ != ncclSuccess)                                                            \
+      throw std::runtime_error(std::string("RCCL: ") + #x + ": " + rccl().GetErrorString(r_)); \
+  } while (0)
+#define HIP_CHECK(x)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess)                                                             \
+      throw std::runtime_error(std::string("HIP: ") + #x + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+static ncclComm_t as_comm(void* c) { return reinterpret_cast<ncclComm_t>(c); }
+
+// RCCL entry points resolved from the librccl instance torch already loaded (torch's
+// ProcessGroupNCCL and this runner must share ONE RCCL: a second copy from /opt/rocm would
+// run its own proxy threads / shm / device state).  Declarations come from the header; the
+// NCCL API of these calls is identical across the 2.26 (torch) / 2.27 (ROCm 7.2) builds.
+struct RcclApi {
+  decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+  decltype(&ncclCommInitRank) CommInitRank = nullptr;
+  decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclGetErrorString) GetErrorString = nullptr;
+  decltype(&ncclReduceScatter) ReduceScatter = nullptr;
+  decltype(&ncclAllGather) AllGather = nullptr;
+  decltype(&ncclReduce) Reduce = nullptr;
+  decltype(&ncclBroadcast) Broadcast = nullptr;
+  decltype(&ncclGroupStart) GroupStart = nullptr;
+  decltype(&ncclGroupEnd) GroupEnd = nullptr;
+  decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;
+  decltype(&ncclCommAbort) CommAbort = nullptr;
+};
+
+static const RcclApi& rccl() {
+  static RcclApi api = [] {
+    RcclApi a;
+    void* h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) throw std::runtime_error(std::string("cannot locate librccl: ") + dlerror());
+    auto sym = [&](const char* n) {
+      void* f = dlsym(h, n);
+      if (!f) throw std::runtime_error(std::string("librccl lacks ") + n);
+      return f;
+    };
+    a.GetUniqueId = (decltype(a.GetUniqueId))sym("ncclGetUniqueId");
+    a.CommInitRank = (decltype(a.CommInitRank))sym("ncclCommInitRank");
+    a.CommDestroy = (decltype(a.CommDestroy))sym("ncclCommDestroy");
+    a.GetErrorString = (decltype(a.GetErrorString))sym("ncclGetErrorString");
+    a.ReduceScatter = (decltype(a.ReduceScatter))sym("ncclReduceScatter");
+    a.AllGather = (decltype(a.AllGather))sym("ncclAllGather");
+    a.Reduce = (decltype(a.Reduce))sym("ncclReduce");
+    a.Broadcast = (decltype(a.Broadcast))sym("ncclBroadcast");
+    a.GroupStart = (decltype(a.GroupStart))sym("ncclGroupStart");
+    a.GroupEnd = (decltype(a.GroupEnd))sym("ncclGroupEnd");
+    a.CommGetAsyncError = (decltype(a.CommGetAsyncError))sym("ncclCommGetAsyncError");
+    a.CommAbort = (decltype(a.CommAbort))sym("ncclCommAbort");
+    return a;
+  }();
+  return api;
+}
+
+SyncRunner::SyncRunner(Engine* eng, float* params, float* grads, int world, int rank)
+    : eng_(eng), w_(params), g_(grads), world_(world), rank_(rank) {
+  int lo = 0, hi = 0;
+  HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  // collectives + optimizer on a high-priority stream so they are not starved by the GEMMs
+  HIP_CHECK(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, hi));
+  for (int s = 0; s < kSegments; ++s)
+    HIP_CHECK(hipEventCreateWithFlags(&seg_ev_[s], hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&done_ev_, hipEventDisableTiming));
+}
+
+SyncRunner::~SyncRunner() {
+  if (comm_) (void)rccl().CommDestroy(as_comm(comm_));
+  for (int s = 0; s < kSegments; ++s)
+    if (seg_ev_[s]) (void)hipEventDestroy(seg_ev_[s]);
+  if (done_ev_) (void)hipEventDestroy(done_ev_);
+  if (cs_) (void)hipStreamDestroy(cs_);
+}
+
+void SyncRunner::unique_id(char out[128]) {
+  ncclUniqueId id;
+  RCCL_CHECK(rccl().GetUniqueId(&id));
+  static_assert(sizeof(id) == 128, "ncclUniqueId size");
+  memcpy(out, &id, 128);
+}
+
+void SyncRunner::init_comm(const char id_bytes[128]) {
+  if (world_ <= 1) return;
+  ncclUniqueId id;
+  memcpy(&id, id_bytes, 128);
+  ncclComm_t c;
+  RCCL_CHECK(rccl().CommInitRank(&c, world_, id, rank_));
+  comm_ = c;
+}
+
+void SyncRunner::set_units(const std::vector<RunnerUnit>& units) {
+  for (const auto& u : units) {
+    if (u.seg < 0 || u.seg >= kSegments) throw std::invalid_argument("unit segment out of range");
+    if (u.kind != RunnerUnit::LOCAL && !comm_)
+      throw std::invalid_argument("collective unit without an RCCL communicator");
+    if (u.kind == RunnerUnit::RS && (u.ranges.size() != 1 || !u.shard))
+      throw std::invalid_argument("RS unit needs exactly one range and a shard buffer");
+  }
+  units_ = units;
+  // W = 1 (every unit LOCAL): one stream, so per-segment updates buy no overlap — coalesce
+  // all updates into as few launches as possible at the end of the step (ranges adjacent in
+  // both the parameter buffer and the PS state merge).  Same result: no backward GEMM reads a
+  // tensor after its update either way.
+  merged_.clear();
+  all_local_ = true;
+  for (const auto& u : units_) all_local_ &= (u.kind == RunnerUnit::LOCAL);
+  if (!all_local_) return;
+  for (const auto& u : units_)
+    for (const auto& r : u.ranges) merged_.push_back({r, u.ps, u.m, u.v});
+  std::sort(merged_.begin(), merged_.end(), [](const Piece& a, const Piece& b) {
+    return a.r.lo < b.r.lo;
+  });
+  std::vector<Piece> out;
+  for (const auto& p : merged_) {
+    if (!out.empty()) {
+      Piece& q = out.back();
+      if (q.r.hi == p.r.lo && q.ps == p.ps && q.m == p.m && q.v == p.v &&
+          q.r.state_off + (q.r.hi - q.r.lo) == p.r.state_off) {
+        q.r.hi = p.r.hi;
+        continue;
+      }
+    }
+    out.push_back(p);
+  }
+  merged_.swap(out);
+}
+
+void SyncRunner::set_optimizer(int kind, float lr, float b1, float b2, float eps, float mu) {
+  if (kind != 0 && kind != 1) throw std::invalid_argument("native runner: adam or momentum");
+  opt_ = kind; lr_ = lr; b1_ = b1; b2_ = b2; eps_ = eps; mu_ = mu;
+}
+
+void SyncRunner::update(float* w, const float* g, float* m, float* v, int64_t n, float lr_t,
+                        hipStream_t st) {
+  if (opt_ == 0) launch_adam(w, g, m, v, n, lr_t, b1_, b2_, eps_, grad_scale_, st);
+  else launch_momentum(w, g, m, n, lr_, mu_, grad_scale_, st);
+}
+
+void SyncRunner::issue(const RunnerUnit& u, const float* lr_t, hipStream_t st) {
+  if (coef_ != 1.f)
+    for (const auto& r : u.ranges) launch_scale(g_ + r.lo, r.hi - r.lo, coef_, st);
+  const float lt = lr_t[u.ps];
+  switch (u.kind) {
+    case RunnerUnit::LOCAL:
+      for (const auto& r : u.ranges)
+        update(w_ + r.lo, g_ + r.lo, u.m + r.state_off, u.v ? u.v + r.state_off : nullptr,
+               r.hi - r.lo, lt, st);
+      break;
+    case RunnerUnit::RS: {
+      const auto& r = u.ranges[0];
+      const int64_t c = (r.hi - r.lo) / world_;
+      float* mine = w_ + r.lo + rank_ * c;
+      RCCL_CHECK(rccl().ReduceScatter(g_ + r.lo, u.shard, (size_t)c, ncclFloat32, ncclSum,
+                                   as_comm(comm_), st));
+      update(mine, u.shard, u.m + r.state_off, u.v ? u.v + r.state_off : nullptr, c, lt, st);
+      RCCL_CHECK(rccl().AllGather(mine, w_ + r.lo, (size_t)c, ncclFloat32, as_comm(comm_), st));
+    } break;
+    case RunnerUnit::REDUCE: {
+      RCCL_CHECK(rccl().GroupStart());
+      for (const auto& r : u.ranges)
+        RCCL_CHECK(rccl().Reduce(g_ + r.lo, g_ + r.lo, (size_t)(r.hi - r.lo), ncclFloat32, ncclSum,
+                              u.host, as_comm(comm_), st));
+      RCCL_CHECK(rccl().GroupEnd());
+      if (rank_ == u.host)
+        for (const auto& r : u.ranges)
+          update(w_ + r.lo, g_ + r.lo, u.m + r.state_off, u.v ? u.v + r.state_off : nullptr,
+                 r.hi - r.lo, lt, st);
+      RCCL_CHECK(rccl().GroupStart());
+      for (const auto& r : u.ranges)
+        RCCL_CHECK(rccl().Broadcast(w_ + r.lo, w_ + r.lo, (size_t)(r.hi - r.lo), ncclFloat32,
+                                 u.host, as_comm(comm_), st));
+      RCCL_CHECK(rccl().GroupEnd());
+    } break;
+    default:
+      throw std::invalid_argument("unknown unit kind");
+  }
+}
+
+void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t seed_value,
+                      const float* lr_t, hipStream_t st) {
+  eng_->seed_value = seed_value;  // dropout seed by kernel argument: no seed-upload kernel
+  const uint32_t* seed = nullptr;
+  // Cross-queue dependencies (event record -> stream wait) cost tens of microseconds of GPU
+  // idle each on this stack (measured), so LOCAL updates go straight onto the compute
+  // stream in order; only units with collectives use the comm stream, which then overlaps
+  // the remaining backward segments.
+  eng_->forward(x, B, seed, true, st);
+  if (all_local_ && local_on_main_) {
+    for (int s = 0; s < kSegments; ++s) eng_->backward_segment(s, x, labels, B, seed, st);
+    if (coef_ != 1.f)
+      for (const auto& p : merged_) launch_scale(g_ + p.r.lo, p.r.hi - p.r.lo, coef_, st);
+    for (const auto& p : merged_)
+      update(w_ + p.r.lo, g_ + p.r.lo, p.m + p.r.state_off, p.v ? p.v + p.r.state_off : nullptr,
+             p.r.hi - p.r.lo, lr_t[p.ps], st);
+    return;
+  }
+  bool comm_used = false;
+  for (int s = 0; s < kSegments; ++s) {
+    eng_->backward_segment(s, x, labels, B, seed, st);
+    bool waited = false;
+    for (const auto& u : units_) {
+      if (u.seg != s) continue;
+      if (u.kind == RunnerUnit::LOCAL && local_on_main_) {
+        issue(u, lr_t, st);
+        continue;
+      }
+      if (!waited) {
+        HIP_CHECK(hipEventRecord(seg_ev_[s], st));
+        HIP_CHECK(hipStreamWaitEvent(cs_, seg_ev_[s], 0));
+        waited = true;
+      }
+      issue(u, lr_t, cs_);
+      comm_used = true;
+    }
+  }
+  if (comm_used) {
+    // the next step's forward reads the updated parameters
+    HIP_CHECK(hipEventRecord(done_ev_, cs_));
+    HIP_CHECK(hipStreamWaitEvent(st, done_ev_, 0));
+  }
+}
+
+// Failure detection: RCCL reports remote-peer / network failures
+// asynchronously; the trainer polls this between steps and the watchdog aborts the comm (so
+// blocked collectives on this rank return and the job can be torn down) on a hang.
+std::string SyncRunner::async_error() {
+  if (!comm_) return std::string();
+  ncclResult_t st = ncclSuccess;
+  RCCL_CHECK(rccl().CommGetAsyncError(as_comm(comm_), &st));
+  if (st == ncclSuccess || st == ncclInProgress) return std::string();
+  return rccl().GetErrorString(st);
+}
+
+void SyncRunner::abort() {
+  if (!comm_) return;
+  (void)rccl().CommAbort(as_comm(comm_));
+  comm_ = nullptr;
+}
+
+// Collective sanity check used before trusting the native path on a multi-GPU job: the RS
+// and REDUCE patterns on a known pattern, compared on the host.
+bool SyncRunner::selftest(std::string* why) {
+  if (world_ <= 1) return true;
+  const int64_t c = 1031, n = c * world_;
+  float *buf = nullptr, *shard = nullptr;
+  HIP_CHECK(hipMalloc(&buf, n * sizeof(float)));
+  HIP_CHECK(hipMalloc(&shard, c * sizeof(float)));
+  std::vector<float> h(n), out(n);
+  auto val = [&](int r, int64_t i) { return (float)((r + 1) * ((i % 13) + 1)); };
+  for (int64_t i = 0; i < n; ++i) h[i] = val(rank_, i);
+  bool ok = true;
+  try {
+    HIP_CHECK(hipMemcpy(buf, h.data(), n * sizeof(float), hipMemcpyHostToDevice));
+    // RS then AG of the reduced chunk: every element = sum_r val(r, i)
+    RCCL_CHECK(rccl().ReduceScatter(buf, shard, (size_t)c, ncclFloat32, ncclSum, as_comm(comm_), cs_));
+    RCCL_CHECK(rccl().AllGather(shard, buf, (size_t)c, ncclFloat32, as_comm(comm_), cs_));
+    HIP_CHECK(hipStreamSynchronize(cs_));
+    HIP_CHECK(hipMemcpy(out.data(), buf, n * sizeof(float), hipMemcpyDeviceToHost));
+    const float rs = (float)(world_ * (world_ + 1) / 2);
+    for (int64_t i = 0; i < n && ok; ++i)
+      if (out[i] != rs * (float)((i % 13) + 1)) {
+        ok = false;
+        if (why) *why = "reduce_scatter/all_gather mismatch at " + std::to_string(i);
+      }
+    // REDUCE to the last rank, then BROADCAST from it
+    const int root = world_ - 1;
+    HIP_CHECK(hipMemcpy(buf, h.data(), n * sizeof(float), hipMemcpyHostToDevice));
+    RCCL_CHECK(rccl().GroupStart());
+    RCCL_CHECK(rccl().Reduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, root, as_comm(comm_), cs_));
+    RCCL_CHECK(rccl().GroupEnd());
+    RCCL_CHECK(rccl().GroupStart());
+    RCCL_CHECK(rccl().Broadcast(buf, buf, (size_t)n, ncclFloat32, root, as_comm(comm_), cs_));
+    RCCL_CHECK(rccl().GroupEnd());
+    HIP_CHECK(hipStreamSynchronize(cs_));
+    HIP_CHECK(hipMemcpy(out.data(), buf, n * sizeof(float), hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n && ok; ++i)
+      if (out[i] != rs * (float)((i % 13) + 1)) {
+        ok = false;
+        if (why) *why = "reduce/broadcast mismatch at " + std::to_string(i);
+      }
+  } catch (const std::exception& e) {
+    ok = false;
+    if (why) *why = e.what();
+  }
+  (void)hipFree(buf);
+  (void)hipFree(shard);
+  return ok;
+}
+
+}  // namespace ddl

@@ -1,0 +1,131 @@
+"""Native synchronous exchange: the whole sync training step in the C++ ``SyncRunner``.
+
+Same plan and the same units as :class:`~.comm.SyncExchange` (whose planner this reuses);
+the per-step work — forward, the four backward segments, and per unit
+reduce-scatter/Adam/all-gather (flat plan) or reduce/Adam/broadcast (tensor-granular plans)
+or a local Adam (W = 1) — is enqueued by ``csrc/kernels/runner.hip`` in one call, on a
+high-priority comm stream that waits per backward segment.  The Python exchange spends
+tens of microseconds of host time per collective and per update, which left the GPU idle
+at every segment boundary; here the host issues the step in ~one launch per kernel.
+
+RCCL: the runner owns its own communicator on torch's librccl instance; the unique id is
+broadcast over the default process group.  Before the native path is trusted on a
+multi-GPU job, a collective self-test (reduce-scatter/all-gather and reduce/broadcast on a
+known pattern) runs on every rank and the decision to use it is agreed by all ranks.
+PS state (``m``/``v``/step counter ``t``) stays in the Python ``ParameterServer`` objects, so
+checkpointing and inspection are unchanged.
+"""
+from __future__ import annotations
+
+import sys
+from typing import Dict, Sequence
+
+import torch
+import torch.distributed as dist
+
+from ..ops import native
+from ..ops.adam import adam_coeffs
+from .comm import DistEnv, SyncExchange
+from .ps import ParameterServer
+from .sharding import ShardPlan
+
+_KIND = {"local": 0, "rs": 1, "reduce": 2}
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class NativeSyncExchange(SyncExchange):
+    native = True
+
+    def __init__(self, plan: ShardPlan, env: DistEnv, params: torch.Tensor, grads: torch.Tensor,
+                 segments: Sequence[Sequence[int]], servers: Dict[int, ParameterServer], engine,
+                 grad_reduce: str = "sum", ref_quirks: bool = False, overlap: bool = True,
+                 optimizer: str = "adam", hyper=None, momentum: float = 0.9):
+        if optimizer not in ("adam", "momentum"):
+            raise NativeUnavailable(f"native runner has no '{optimizer}' update")
+        if not params.is_cuda or getattr(engine, "name", "") != "hip":
+            raise NativeUnavailable("native runner needs the HIP engine on a GPU")
+        if len(segments) != 4:
+            raise NativeUnavailable("native runner expects the engine's 4 backward segments")
+        super().__init__(plan, env, params, grads, segments, servers, grad_reduce, ref_quirks,
+                         overlap=overlap)
+        self.engine = engine
+        self.optimizer = optimizer
+        ops = native.ops()
+        self.runner = ops.SyncRunner(engine.eng, params, grads, env.world, env.rank)
+        if env.world > 1:
+            ids = [ops.SyncRunner.unique_id() if env.rank == 0 else None]
+            dist.broadcast_object_list(ids, src=0)
+            self.runner.init_comm(ids[0])
+            ok, why = self.runner.selftest()
+            votes = [None] * env.world
+            dist.all_gather_object(votes, (bool(ok), why))
+            bad = [(r, w) for r, (o, w) in enumerate(votes) if not o]
+            if bad:
+                raise NativeUnavailable(f"RCCL self-test failed on ranks {bad}")
+        seg_sets = [set(s) for s in segments]
+
+        def seg_of(tensors):
+            if not overlap:
+                return len(seg_sets) - 1
+            return max(next(i for i, s in enumerate(seg_sets) if t in s) for t in tensors)
+
+        units = []
+        for u in self.units:
+            ps = env.rank if u.kind == "rs" else u.ps
+            srv = servers.get(ps)
+            offs = u.state_offs or [0] * len(u.ranges)
+            ranges = [(int(lo), int(hi), int(off)) for (lo, hi), off in zip(u.ranges, offs)]
+            units.append((seg_of(u.tensors), _KIND[u.kind], int(u.host), int(ps), ranges,
+                          srv.m if srv is not None else None,
+                          srv.v if srv is not None else None, u.shard_buf))
+        self.runner.set_units(units)
+        h = hyper if hyper is not None else next(iter(servers.values())).h
+        self.runner.set_optimizer(0 if optimizer == "adam" else 1, h.lr, h.beta1, h.beta2, h.eps,
+                                  momentum)
+        self.runner.set_scale(self.grad_scale, self.coef)
+        self._lr = [0.0] * max(plan.num_ps, env.world)
+        self._n = 0
+
+    def step(self, x: torch.Tensor, labels: torch.Tensor, keep_prob: float, seed: int) -> None:
+        """One synchronous global step: every hosted PS advances its step counter (one
+        ``apply_gradients`` per global step, like the reference PS) and the runner enqueues
+        compute + exchange + update."""
+        eng = self.engine
+        eng._set_keep(keep_prob)
+        lr = self._lr
+        for p, ps in self.servers.items():
+            ps.begin()
+            lr[p] = adam_coeffs(ps.h, ps.t) if self.optimizer == "adam" else ps.h.lr
+        self.runner.step(x if x.is_contiguous() else x.contiguous(), labels, seed & 0xFFFFFFFF, lr)
+        self._n += 1
+        if self.env.world > 1 and self._n % 64 == 0:
+            self.check()
+
+    def check(self) -> None:
+        """Raise if RCCL reported an asynchronous communicator error."""
+        err = self.runner.async_error()
+        if err:
+            raise RuntimeError(f"RCCL communicator error on rank {self.env.rank}: {err}")
+
+    def abort(self) -> None:
+        """Watchdog hook: abort the communicator so blocked collectives return."""
+        self.runner.abort()
+
+
+def make_sync_exchange(plan, env, params, grads, segments, servers, engine, cfg, hyper):
+    """Native runner when it applies (HIP engine, sync, adam/momentum), else the Python
+    exchange.  On a multi-GPU job the choice is collective (self-test votes)."""
+    if cfg.native_exchange:
+        try:
+            return NativeSyncExchange(plan, env, params, grads, segments, servers, engine,
+                                      cfg.grad_reduce, cfg.ref_quirks, cfg.overlap,
+                                      cfg.optimizer, hyper, cfg.momentum)
+        except NativeUnavailable as e:
+            if env.rank == 0 and getattr(engine, "name", "") == "hip":
+                print(f"[ddl_amd] native sync runner unavailable ({e}); using the Python "
+                      f"exchange", file=sys.stderr)
+    return SyncExchange(plan, env, params, grads, segments, servers, cfg.grad_reduce,
+                        cfg.ref_quirks, overlap=cfg.overlap)

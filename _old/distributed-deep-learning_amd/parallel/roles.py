@@ -1,0 +1,229 @@
+"""Training roles: ``Single``, ``SyncWorker``/``AsyncWorker`` with co-located ``ParameterServer``s.
+
+Reference roles: ``Single(epoch, batch).train()`` (``*/single.py:3-21``),
+``SyncWorker(batch[, rank, num_ps, num_workers]).work(cnt)`` (``*/worker.py``) and
+``ParameterServer(params[, rank, num_ps, num_workers]).update()``
+(``*/parameter_server.py``), launched MPMD as P PS ranks + W worker ranks.
+
+MI355X layout: one process per GPU.  Every process is a worker; PS ``p`` is hosted by
+process ``p % W`` (RCCL cannot place two ranks of one communicator on one GPU).  The
+``Trainer`` below wires an engine (HIP kernels, or the torch oracle on CPU), a shard
+plan, the hosted ``ParameterServer`` objects and a sync or async exchange, and runs the
+reference's loop: 1 epoch x 500 steps of batch 100, test-set accuracy every 10 steps,
+final accuracy and ``Time``.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..config import TrainConfig
+from ..models import make_engine, engine_segments
+from ..models.mnist_cnn import init_params_
+from ..ops import rng
+from ..ops.adam import AdamHyper
+from ..utils import metrics
+from ..utils.data import Dataset, get_dataset, batch_indices
+from ..utils.watchdog import Watchdog
+from ..utils import checkpoint as ckpt
+from ..utils.tracing import trace_range
+from .comm import DistEnv, SyncExchange, AsyncExchange, init_distributed
+from .native_exchange import make_sync_exchange
+from .ps import ParameterServer
+from .sharding import make_plan
+
+
+def resolve_num_ps(cfg: TrainConfig, world: int) -> int:
+    if cfg.mode == "single" or cfg.shard == "none":
+        return 1
+    return cfg.num_ps or world
+
+
+class Trainer:
+    """One process = one GPU = one worker (+ the PS shards it hosts)."""
+
+    def __init__(self, cfg: TrainConfig, env: Optional[DistEnv] = None,
+                 dataset: Optional[Dataset] = None):
+        self.cfg = cfg
+        self.env = env or init_distributed()
+        env = self.env
+        W, r = env.world, env.rank
+        if cfg.mode == "single" and W != 1:
+            raise ValueError("mode 'single' runs in one process")
+        self.num_ps = resolve_num_ps(cfg, W)
+        segs = engine_segments(cfg.engine, env.device)
+        buckets = segs if (cfg.shard == "flat" and cfg.overlap and cfg.mode == "sync") else None
+        shard = "none" if cfg.mode == "single" else cfg.shard
+        self.plan = make_plan(shard, self.num_ps, buckets=buckets)
+        dev = env.device
+        self.params = torch.zeros(self.plan.total, dtype=torch.float32, device=dev)
+        self.grads = torch.zeros(self.plan.total, dtype=torch.float32, device=dev)
+        # Same seed on every rank -> identical initial parameters (the reference
+        # initialises every process independently; --ref-quirks).
+        init_seed = cfg.seed + (r if cfg.ref_quirks else 0)
+        init_params_(self.params, self.plan.tensor_offsets, init_seed)
+        self.engine = make_engine(cfg.engine, self.params, self.grads, self.plan.tensor_offsets,
+                                  dev, cfg.batch_size, graph=cfg.graph)
+        hyper = AdamHyper(lr=cfg.lr)
+        hosted = [p for p in range(self.num_ps) if self.plan.host_rank(p, W) == r]
+        asyncm = cfg.mode == "async"
+        self.servers: Dict[int, ParameterServer] = {}
+        for p in hosted:
+            own = None
+            if asyncm:
+                own = self.params
+                if cfg.ref_quirks:  # PS initialised independently of the workers (Q4)
+                    tmp = torch.zeros_like(self.params)
+                    init_params_(tmp, self.plan.tensor_offsets, cfg.seed + 10007 + p)
+                    own = tmp
+            self.servers[p] = ParameterServer(self.plan, p, dev, hyper, cfg.optimizer,
+                                              cfg.momentum, own_params=own,
+                                              native_optim=self.engine.name != "torch")
+        self.data = dataset if dataset is not None else get_dataset(cfg.data, seed=1234)
+        self.data = self.data.to(dev)
+        self.steps = cfg.steps or (self.data.total_batch // cfg.batch_size)
+        if asyncm:
+            self.exchange = AsyncExchange(self.plan, env, self.params, self.grads, self.servers,
+                                          steps_per_worker=self.steps * cfg.epochs,
+                                          grad_reduce=cfg.grad_reduce,
+                                          check_provenance=cfg.check_provenance)
+        else:
+            self.exchange = make_sync_exchange(self.plan, env, self.params, self.grads, segs,
+                                               self.servers, self.engine, cfg, hyper)
+        self.log = metrics.JsonlLogger(cfg.log_jsonl, r)
+        self.global_step = 0
+        self.history: List[dict] = []
+
+    # ---- one worker step (reference SyncWorker.work + pull + assign) -----------------------------
+    def batch(self, step: int):
+        lo, hi = batch_indices(step, self.cfg.batch_size, self.data.total_batch, self.env.rank,
+                               self.env.world, self.cfg.data_sharding)
+        return self.data.x_train[lo:hi], self.data.y_train[lo:hi]
+
+    def train_step(self, step: int) -> None:
+        cfg = self.cfg
+        x, y = self.batch(step)
+        seed = rng.step_seed(cfg.seed, self.env.rank, self.global_step)
+        if cfg.mode == "async":
+            with trace_range("fwd_bwd"):
+                self.engine.forward_backward(x, y, cfg.keep_prob, seed)
+            with trace_range("push_pull"):
+                self.exchange.push_pull()
+        elif getattr(self.exchange, "native", False):
+            with trace_range("step_native"):
+                self.exchange.step(x, y, cfg.keep_prob, seed)
+        else:
+            ex = self.exchange
+            ex.begin_step()
+            with trace_range("fwd_bwd"):
+                self.engine.forward_backward(x, y, cfg.keep_prob, seed, on_segment=ex.grads_ready)
+            with trace_range("exchange"):
+                ex.finish_step()
+        self.global_step += 1
+
+    def evaluate(self) -> float:
+        """Test-set accuracy.  The reference has every worker score the full 10k test set
+        (``mnist_sync/worker.py:71-72``); in sync mode the ranks run in lockstep anyway, so
+        each scores 1/W of it and one all-reduce of the correct counts gives the identical
+        number W times faster (eval dominates time-to-accuracy)."""
+        with trace_range("eval"):
+            x, y = self.data.x_test, self.data.y_test
+            env = self.env
+            if not (self.cfg.dist_eval and self.cfg.mode == "sync" and env.world > 1):
+                return self.engine.accuracy(x, y)
+            n = x.shape[0]
+            per = (n + env.world - 1) // env.world
+            lo, hi = min(n, env.rank * per), min(n, (env.rank + 1) * per)
+            c = self.engine.correct(x[lo:hi], y[lo:hi]) if hi > lo else 0
+            t = torch.tensor([float(c)], dtype=torch.float64, device=env.device)
+            dist.all_reduce(t)
+            return float(t.item()) / n
+
+    def _on_hang(self) -> None:
+        """Watchdog fired: abort the native RCCL communicator (pending collectives return
+        with an error instead of spinning) and end the process so the launcher tears the
+        job down."""
+        import os
+        import sys
+        ab = getattr(self.exchange, "abort", None)
+        if ab is not None:
+            try:
+                ab()
+            except Exception as e:  # best effort: we are exiting anyway
+                sys.stderr.write(f"[watchdog] comm abort failed: {e}\n")
+        os._exit(124)
+
+    # ---- reference main loop -----------------------------------------------------------------------
+    def train(self) -> dict:
+        cfg, env = self.cfg, self.env
+        clock = metrics.Clock()
+        single = cfg.mode == "single"
+        if cfg.resume and cfg.checkpoint_dir:
+            ckpt.load(self, cfg.checkpoint_dir)
+        if isinstance(self.exchange, AsyncExchange):
+            self.exchange.start()
+        wd = Watchdog(cfg.watchdog_s, name=f"rank{env.rank}", on_timeout=self._on_hang)
+        t_target = None
+        train_wall = 0.0
+        for epoch in range(cfg.epochs):
+            for cnt in range(self.steps):
+                t0 = time.perf_counter()
+                self.train_step(cnt)
+                wd.kick()
+                if cfg.eval_every and cnt % cfg.eval_every == 0:
+                    if env.device.type == "cuda":
+                        torch.cuda.synchronize()
+                    train_wall += time.perf_counter() - t0
+                    acc = self.evaluate()
+                    if not cfg.quiet:
+                        line = (metrics.single_progress(epoch, cnt, acc) if single else
+                                metrics.worker_progress(env.rank, epoch, cnt, acc))
+                        metrics.emit(line)
+                    self.log.log(event="eval", epoch=epoch, batch=cnt, acc=acc,
+                                 wall=clock.wall(), step=self.global_step)
+                    self.history.append({"step": self.global_step, "acc": acc, "wall": clock.wall()})
+                    if cfg.target_acc is not None and t_target is None and acc >= cfg.target_acc:
+                        t_target = clock.wall()
+                else:
+                    train_wall += time.perf_counter() - t0
+                if cfg.checkpoint_dir and cfg.checkpoint_every and \
+                        self.global_step % cfg.checkpoint_every == 0:
+                    ckpt.save(self, cfg.checkpoint_dir)
+        if isinstance(self.exchange, AsyncExchange):
+            self.exchange.join()
+            if cfg.check_provenance:
+                self.exchange.verify_provenance()
+        if getattr(self.exchange, "native", False) and env.world > 1:
+            self.exchange.check()
+        if env.device.type == "cuda":
+            torch.cuda.synchronize()
+        if env.world > 1:
+            dist.barrier()
+        cpu_t, wall_t = clock.cpu(), clock.wall()
+        acc = self.evaluate()
+        if not cfg.quiet:
+            metrics.emit(metrics.single_final(acc) if single else metrics.worker_final(env.rank, acc))
+            metrics.emit(metrics.time_line(cpu_t))
+        wd.stop()
+        if cfg.checkpoint_dir:
+            ckpt.save(self, cfg.checkpoint_dir)
+        imgs = self.global_step * cfg.batch_size
+        summary = dict(final_acc=acc, cpu_time=cpu_t, wall_time=wall_t, train_wall=train_wall,
+                       images=imgs, images_per_s=imgs / max(train_wall, 1e-9),
+                       time_to_target=t_target, steps=self.global_step, plan=self.plan.describe())
+        self.log.log(event="final", **summary)
+        if isinstance(self.exchange, AsyncExchange):
+            self.exchange.close()
+        return summary
+
+
+class Single(Trainer):
+    """``Single(epoch, batch_size).train()`` — reference ``mnist_sync/single.py:3-21``."""
+
+    def __init__(self, epoch: int = 1, batch_size: int = 100, **kw):
+        cfg = TrainConfig(mode="single", shard="none", epochs=epoch, batch_size=batch_size, **kw)
+        super().__init__(cfg, DistEnv(device=torch.device("cuda") if torch.cuda.is_available()
+                                      else torch.device("cpu")))

@@ -1,0 +1,20 @@
+#!/usr/bin/env python3
+"""Run N default native-runner training steps (for rocprofv3 --pmc collection)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ddl_amd.config import TrainConfig  # noqa: E402
+from ddl_amd.parallel.comm import DistEnv  # noqa: E402
+from ddl_amd.parallel.roles import Trainer  # noqa: E402
+from ddl_amd.utils.data import synthetic_mnist  # noqa: E402
+
+data = synthetic_mnist(n_train=5000, n_test=500)
+tr = Trainer(TrainConfig(mode="sync", shard="contiguous", steps=50, eval_every=0, engine="hip",
+                         quiet=True), DistEnv(0, 1, 0, torch.device("cuda", 0)), dataset=data)
+for i in range(int(os.environ.get("STEPS", "20"))):
+    tr.train_step(i)
+torch.cuda.synchronize()
+print("done")

@@ -1,0 +1,104 @@
+"""Shard planners vs the reference formulas and the SURVEY.md §2.8 golden tables."""
+import pytest
+
+from ddl_amd.models.layout import TENSORS, NUM_TENSORS, TOTAL_NUMEL, TOTAL_BYTES
+from ddl_amd.parallel.sharding import (make_plan, greedy_order, reference_route, balance_table,
+                                       contiguous_counts)
+
+
+def test_layout_constants():
+    # SURVEY.md §2.5
+    assert NUM_TENSORS == 14
+    assert TOTAL_NUMEL == 2_656_010
+    assert TOTAL_BYTES == 10_624_040
+    assert [t.numel for t in TENSORS][:4] == [800, 32, 51200, 64]
+
+
+def test_greedy_order_golden():
+    # mnist_sync_sharding_greedy/worker.py:13-37 replayed
+    assert greedy_order([t.numel for t in TENSORS]) == [13, 8, 1, 6, 3, 10, 5, 4, 7, 2, 11, 12, 0, 9]
+
+
+def test_greedy_order_odd_count():
+    assert greedy_order([5, 1, 3]) == [1, 0, 2]
+
+
+@pytest.mark.parametrize("P,expect", [
+    (1, [1.00, 1.00]), (2, [1.19, 1.80]), (3, [1.78, 2.11]), (4, [2.81, 2.02]),
+    (5, [2.97, 1.97]), (6, [2.37, 2.37]), (7, [2.77, 2.76]), (8, [4.76, 3.16])])
+def test_balance_table_matches_survey(P, expect):
+    c = make_plan("contiguous", P).imbalance()
+    g = make_plan("greedy", P).imbalance()
+    assert round(c, 2) == pytest.approx(expect[0], abs=0.011)
+    assert round(g, 2) == pytest.approx(expect[1], abs=0.011)
+
+
+def test_contiguous_p2_shard_sizes():
+    mib = [b / 2**20 for b in make_plan("contiguous", 2).shard_bytes()]
+    assert mib[0] == pytest.approx(4.11, abs=0.01) and mib[1] == pytest.approx(6.03, abs=0.01)
+
+
+@pytest.mark.parametrize("P", range(1, 15))
+def test_contiguous_matches_reference_routing(P):
+    plan = make_plan("contiguous", P)
+    for i in range(NUM_TENSORS):
+        owner, tag = reference_route(i, NUM_TENSORS, P)
+        assert plan.owner[i] == owner
+        # tag = index local to the owning PS, as the reference PS receives it
+        assert plan.tensors_of(owner).index(i) == tag
+
+
+@pytest.mark.parametrize("P", range(1, 15))
+def test_greedy_matches_reference_routing(P):
+    plan = make_plan("greedy", P)
+    order = plan.meta["reference_order"]
+    for pos, i in enumerate(order):
+        owner, _ = reference_route(pos, NUM_TENSORS, P)
+        assert plan.owner[i] == owner
+
+
+@pytest.mark.parametrize("policy", ["contiguous", "greedy", "lpt", "flat"])
+@pytest.mark.parametrize("P", [1, 2, 3, 8])
+def test_plan_is_a_partition(policy, P):
+    plan = make_plan(policy, P)
+    covered = []
+    for p in range(P):
+        for lo, hi in plan.ps_segments(p):
+            covered.extend(range(lo, hi))
+    assert sorted(covered) == list(range(plan.total))
+    # every tensor lies inside the buffer, tensors don't overlap
+    spans = sorted((plan.tensor_offsets[t.index], plan.tensor_offsets[t.index] + t.numel) for t in TENSORS)
+    for (a, b), (c, d) in zip(spans, spans[1:]):
+        assert b <= c
+    assert spans[-1][1] <= plan.total
+
+
+def test_flat_bucketed_plan():
+    buckets = [list(range(8, 14)), [6, 7], [4, 5], [0, 1, 2, 3]]
+    plan = make_plan("flat", 8, buckets=buckets)
+    assert plan.imbalance() == 1.0
+    assert len(plan.bucket_ranges) == 4
+    for lo, hi in plan.bucket_ranges:
+        assert (hi - lo) % (8 * 64) == 0
+    assert all(len(plan.ps_segments(p)) == 4 for p in range(8))
+
+
+def test_flat_balance_is_perfect():
+    for row in balance_table():
+        assert row["flat"] == 1.0
+
+
+def test_invalid_plans():
+    with pytest.raises(ValueError):
+        make_plan("contiguous", 15)      # reference divides by zero (Q8)
+    with pytest.raises(ValueError):
+        make_plan("none", 2)             # Q7
+    with pytest.raises(ValueError):
+        make_plan("bogus", 1)
+    assert contiguous_counts(14, 4) == [3, 3, 3, 5]
+
+
+def test_host_ranks_colocated():
+    plan = make_plan("contiguous", 8)
+    assert [plan.host_rank(p, 8) for p in range(8)] == list(range(8))
+    assert [plan.host_rank(p, 2) for p in range(4)] == [0, 1, 0, 1]

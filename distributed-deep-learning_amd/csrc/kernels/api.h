@@ -5,16 +5,21 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
 #include "scratch.h"
+#include "tail.h"
 
 namespace ddl {
 
 // ---- optimizer (optim.hip) -------------------------------------------------------------------
 void launch_adam(float* w, const float* g, float* m, float* v, int64_t n, float lr_t, float b1,
                  float b2, float eps, float scale, hipStream_t st);
+// same with c1 = 1 - beta1, c2 = 1 - beta2 precomputed (bit-identical to launch_adam)
+void launch_adam_c(float* w, const float* g, float* m, float* v, int64_t n, float lr_t, float c1,
+                   float c2, float eps, float scale, hipStream_t st);
 void launch_momentum(float* w, const float* g, float* m, int64_t n, float lr, float mu,
                      float scale, hipStream_t st);
 void launch_scale(float* p, int64_t n, float a, hipStream_t st);
@@ -79,6 +84,9 @@ struct Engine {
 
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // optimizer tail (tail.h) for the next dual launch; consumed (and cleared) by it, or by
+  // flush_tail() as a launch of its own when no dual launch takes it
+  UpdTail tail;
 
   Engine();
   ~Engine();
@@ -100,6 +108,8 @@ struct Engine {
   // run a single GEMM op on `st` with scratch `si` (tests / tuning)
   void run_op(int op, const float* x, int B, const uint32_t* seed, bool train, hipStream_t st,
               int si = 0);
+  // launch a pending optimizer tail on its own (no-op when none is pending)
+  void flush_tail(hipStream_t st);
 
  private:
   void fork(hipStream_t st);
@@ -177,6 +187,27 @@ class SyncRunner {
   };
   bool all_local_ = false;
   std::vector<Piece> merged_;  // coalesced LOCAL update ranges (all_local_)
+  // all_local_: the same ranges coalesced per backward segment; segment s's update rides as
+  // an optimizer tail (tail.h) in segment s+1's dual launch when every piece is 16-B vector
+  // shaped (tail_ok_), the last segment's is launched after the backward
+  std::vector<Piece> seg_pieces_[kSegments];
+  bool tail_ok_ = false;
+  bool use_tail_ = true;
+  void set_tail(int seg, const float* lr_t);
+
+ public:
+  void set_use_tail(bool on) { use_tail_ = on; }
+  // tail placement (1: before the GEMM blocks) and float4 per tail block (tuning)
+  void set_tail_cfg(int first, int f4_per_block) {
+    tail_first_ = first;
+    tail_f4_ = std::max(1, f4_per_block / kTailF4PerBlock) * kTailF4PerBlock;
+  }
+
+ private:
+  // measured (scripts/tail_probe.py, one MI355X): after the GEMM blocks, 512 float4 per
+  // block: 373 us/step vs 381 without the tail; before the GEMM blocks 375-378
+  int tail_first_ = 0;
+  int tail_f4_ = 4 * kTailF4PerBlock;
 };
 
 }  // namespace ddl

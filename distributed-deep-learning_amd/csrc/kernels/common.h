@@ -31,6 +31,14 @@ DDL_DEV f32x4 mfma16x16x4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// TF1 ApplyAdam update of one element (TF's update form, documented in optim.hip).
+DDL_DEV void adam1(float& w, float g, float& m, float& v, float lr_t, float c1, float c2,
+                   float eps) {
+  m += (g - m) * c1;
+  v += (g * g - v) * c2;
+  w -= lr_t * m / (sqrtf(v) + eps);
+}
+
 DDL_DEV float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
 // ---------------------------------------------------------------------------------------------

@@ -13,6 +13,7 @@
 
 #include "api.h"
 #include "layers.h"
+#include "engine_decl.h"
 
 namespace ddl {
 
@@ -87,19 +88,6 @@ static size_t slab_need(int c, int M, int N, int K, int s, int w) {
   }
 }
 
-template <class P>
-static void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const SplitScratch& sc,
-                       hipStream_t st) {
-  switch (c) {
-    case 0: launch_gemm<TILE_0>(p, s, wide_thr, sc, st, w); break;
-    case 1: launch_gemm<TILE_1>(p, s, wide_thr, sc, st, w); break;
-    case 2: launch_gemm<TILE_2>(p, s, wide_thr, sc, st, w); break;
-    case 3: launch_gemm<TILE_3>(p, s, wide_thr, sc, st, w); break;
-    case 4: launch_gemm<TILE_4>(p, s, wide_thr, sc, st, w); break;
-    default: launch_gemm<TILE_5>(p, s, wide_thr, sc, st, w); break;
-  }
-}
-
 size_t Engine::slab_floats_needed(int B) const {
   size_t mx = 0;
   for (int op = 0; op < OP_COUNT; ++op) {
@@ -148,63 +136,11 @@ void Engine::bind_workspace(void* base) {
   }
 }
 
-// Problem policy of op OP (layers.h) bound to this engine's buffers, at batch B.
-template <int OP>
-static auto make_policy(const Engine& e, int B, const float* x, const uint32_t* seed,
-                        bool train) {
-  int M, N, K;
-  Engine::op_shape(OP, B, &M, &N, &K);
-  const uint32_t thr = train ? e.thr24 : 0u;
-  const float* const* P = e.P;
-  float* const* G = e.G;
-  if constexpr (OP == OP_CONV1_FWD) return ConvFwd<28, 1, 32>{M, N, K, x, P[0], P[1], e.p1, e.c1};
-  else if constexpr (OP == OP_CONV2_FWD)
-    return ConvFwd<14, 32, 64>{M, N, K, e.p1, P[2], P[3], e.p2, e.c2};
-  else if constexpr (OP == OP_CONV3_FWD)
-    return ConvFwd<7, 64, 128>{M, N, K, e.p2, P[4], P[5], e.p3, e.c3};
-  else if constexpr (OP == OP_CONV4_FWD)
-    return ConvFwd<4, 128, 256>{M, N, K, e.p3, P[6], P[7], e.p4, e.c4};
-  else if constexpr (OP == OP_FC1_FWD)
-    return FcFwd<true>{M, N, K, e.p4, P[8], P[9], e.h1, seed, 1u, thr, e.inv_keep, e.seed_value};
-  else if constexpr (OP == OP_FC2_FWD)
-    return FcFwd<false>{M, N, K, e.h1, P[10], P[11], e.h2, seed, 2u, thr, e.inv_keep, e.seed_value};
-  else if constexpr (OP == OP_FC2_DGRAD)
-    return FcDgradAct{{M, N, K, e.dpre2fc, P[10]}, e.h1, e.inv_keep, e.dpre1fc};
-  else if constexpr (OP == OP_FC2_WGRAD)
-    return FcWgrad{M, N, K, 1024, e.h1, e.dpre2fc, G[10], G[11]};
-  else if constexpr (OP == OP_FC1_DGRAD)
-    return FcDgradPool<2, 256>{{M, N, K, e.dpre1fc, P[8]}, e.c4, e.d4};
-  else if constexpr (OP == OP_FC1_WGRAD)
-    return FcWgrad{M, N, K, 1024, e.p4, e.dpre1fc, G[8], G[9]};
-  else if constexpr (OP == OP_CONV4_DGRAD)
-    return ConvDgrad<4, 128, 256, 7>{M, N, K, e.d4, P[6], e.c3, e.d3};
-  else if constexpr (OP == OP_CONV4_WGRAD)
-    return ConvWgrad<4, 128, 256>{M, N, K, e.p3, e.d4, G[6], G[7]};
-  else if constexpr (OP == OP_CONV3_DGRAD)
-    return ConvDgrad<7, 64, 128, 14>{M, N, K, e.d3, P[4], e.c2, e.d2};
-  else if constexpr (OP == OP_CONV3_WGRAD)
-    return ConvWgrad<7, 64, 128>{M, N, K, e.p2, e.d3, G[4], G[5]};
-  else if constexpr (OP == OP_CONV2_DGRAD)
-    return ConvDgrad<14, 32, 64, 28>{M, N, K, e.d2, P[2], e.c1, e.d1};
-  else if constexpr (OP == OP_CONV2_WGRAD)
-    return ConvWgrad<14, 32, 64>{M, N, K, e.p1, e.d2, G[2], G[3]};
-  else
-    return ConvWgrad<28, 1, 32>{M, N, K, x, e.d1, G[0], G[1]};
-}
-
-template <int OP>
-static void run_op_t(Engine& e, const float* x, int B, const uint32_t* seed, bool train,
-                     hipStream_t st, int si) {
-  const auto p = make_policy<OP>(e, B, x, seed, train);
-  launch_cfg(e.cfg[OP], p, train ? e.splits[OP] : 1, train ? e.workers[OP] : 0, e.wide[OP],
-             e.scratch[si], st);
-}
-
 void Engine::run_op(int op, const float* x, int B, const uint32_t* seed, bool train,
                     hipStream_t st, int si) {
   switch (op) {
 #define DDL_RUN(OPC) \
-  case OPC: run_op_t<OPC>(*this, x, B, seed, train, st, si); break;
+  case OPC: run_op_inst<OPC>(*this, x, B, seed, train, st, si); break;
     DDL_RUN(OP_CONV1_FWD) DDL_RUN(OP_CONV2_FWD) DDL_RUN(OP_CONV3_FWD) DDL_RUN(OP_CONV4_FWD)
     DDL_RUN(OP_FC1_FWD) DDL_RUN(OP_FC2_FWD) DDL_RUN(OP_FC2_DGRAD) DDL_RUN(OP_FC2_WGRAD)
     DDL_RUN(OP_FC1_DGRAD) DDL_RUN(OP_FC1_WGRAD) DDL_RUN(OP_CONV4_DGRAD) DDL_RUN(OP_CONV4_WGRAD)
@@ -215,43 +151,12 @@ void Engine::run_op(int op, const float* x, int B, const uint32_t* seed, bool tr
   }
 }
 
-// ---- dual launches: data- and weight-gradient GEMM of one layer in one kernel -----------------
-// dual launches are instantiated for these one-wave configs (others run back to back)
-static bool one_wave_cfg(int c) { return c == 0 || c == 3 || c == 4 || c == 5; }
-
-template <class CA, int OA, int OB, class PA, class PB>
-static void dual_b(Engine& e, const PA& pa, const PB& pb, hipStream_t st) {
-#define DDL_DUAL_B(CB) \
-  launch_gemm_dual<CA, PA, TileCfg<CB>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], \
-                                            e.wide[OA], pb, e.splits[OB], e.workers[OB], \
-                                            e.scratch[1], e.wide[OB], st)
-  switch (e.cfg[OB]) {
-    case 0: DDL_DUAL_B(TILE_0); break;
-    case 3: DDL_DUAL_B(TILE_3); break;
-    case 4: DDL_DUAL_B(TILE_4); break;
-    default: DDL_DUAL_B(TILE_5); break;
+void Engine::flush_tail(hipStream_t st) {
+  for (int i = 0; i < tail.npieces; ++i) {
+    const UpdPiece& p = tail.p[i];
+    launch_adam_c(p.w, p.g, p.m, p.v, p.n, p.lr_t, tail.c1, tail.c2, tail.eps, tail.scale, st);
   }
-#undef DDL_DUAL_B
-}
-
-// Ops OA and OB (independent) in one launch if both use one-wave tiles, else back to back.
-template <int OA, int OB>
-static void run_dual(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
-  if (!e.dual || !one_wave_cfg(e.cfg[OA]) || !one_wave_cfg(e.cfg[OB])) {
-    run_op_t<OA>(e, x, B, seed, true, st, 0);
-    run_op_t<OB>(e, x, B, seed, true, st, 0);
-    return;
-  }
-  const auto pa = make_policy<OA>(e, B, x, seed, true);
-  const auto pb = make_policy<OB>(e, B, x, seed, true);
-  using PA = std::decay_t<decltype(pa)>;
-  using PB = std::decay_t<decltype(pb)>;
-  switch (e.cfg[OA]) {
-    case 0: dual_b<TileCfg<TILE_0>, OA, OB, PA, PB>(e, pa, pb, st); break;
-    case 3: dual_b<TileCfg<TILE_3>, OA, OB, PA, PB>(e, pa, pb, st); break;
-    case 4: dual_b<TileCfg<TILE_4>, OA, OB, PA, PB>(e, pa, pb, st); break;
-    default: dual_b<TileCfg<TILE_5>, OA, OB, PA, PB>(e, pa, pb, st); break;
-  }
+  tail = UpdTail();
 }
 
 void Engine::forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st) {
@@ -278,6 +183,7 @@ void Engine::wgrad(int op, const float* x, int B, const uint32_t* seed, hipStrea
 void Engine::backward_segment(int s, const float* x, const int64_t* labels, int B,
                               const uint32_t* seed, hipStream_t st) {
   if (concurrent && side) {  // weight gradients on the side stream (fork/join per segment)
+    flush_tail(st);
     switch (s) {
       case 0:
         launch_head_fwd(h2, P[12], P[13], labels, B, dlog, loss, nullptr, st);
@@ -312,13 +218,13 @@ void Engine::backward_segment(int s, const float* x, const int64_t* labels, int 
       launch_head_fwd(h2, P[12], P[13], labels, B, dlog, loss, nullptr, st);
       launch_head_bwd(h2, P[12], dlog, B, seed, seed_value, thr24, inv_keep, G[12], G[13],
                         dpre2fc, st);
-      run_dual<OP_FC2_DGRAD, OP_FC2_WGRAD>(*this, x, B, seed, st);
-      run_dual<OP_FC1_DGRAD, OP_FC1_WGRAD>(*this, x, B, seed, st);
+      run_dual_inst<OP_FC2_DGRAD, OP_FC2_WGRAD>(*this, x, B, seed, st);
+      run_dual_inst<OP_FC1_DGRAD, OP_FC1_WGRAD>(*this, x, B, seed, st);
       break;
-    case 1: run_dual<OP_CONV4_DGRAD, OP_CONV4_WGRAD>(*this, x, B, seed, st); break;
-    case 2: run_dual<OP_CONV3_DGRAD, OP_CONV3_WGRAD>(*this, x, B, seed, st); break;
+    case 1: run_dual_inst<OP_CONV4_DGRAD, OP_CONV4_WGRAD>(*this, x, B, seed, st); break;
+    case 2: run_dual_inst<OP_CONV3_DGRAD, OP_CONV3_WGRAD>(*this, x, B, seed, st); break;
     case 3:
-      run_dual<OP_CONV2_DGRAD, OP_CONV2_WGRAD>(*this, x, B, seed, st);
+      run_dual_inst<OP_CONV2_DGRAD, OP_CONV2_WGRAD>(*this, x, B, seed, st);
       run_op(OP_CONV1_WGRAD, x, B, seed, true, st, 0);
       break;
     default: break;

@@ -1,0 +1,14 @@
+// Declarations of the engine's kernel-instantiating entry points (defined in
+// engine_impl.h, explicitly instantiated in engine_ops_*.hip; called from engine.hip).
+#pragma once
+#include "api.h"
+
+namespace ddl {
+
+template <int OP>
+void run_op_inst(Engine& e, const float* x, int B, const uint32_t* seed, bool train,
+                 hipStream_t st, int si);
+template <int OA, int OB>
+void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st);
+
+}  // namespace ddl

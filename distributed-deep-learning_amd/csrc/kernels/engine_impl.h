@@ -1,0 +1,128 @@
+// Kernel-instantiating half of the CNN step engine (engine.hip holds the host logic).
+//
+// Every GEMM op instantiates its tile configs x schedules and every dual launch the cross
+// product of its two ops' one-wave configs, so the templates live here and are explicitly
+// instantiated in several translation units (engine_ops_*.hip) that compile in parallel.
+#pragma once
+#include <type_traits>
+
+#include "api.h"
+#include "layers.h"
+#include "engine_decl.h"
+
+namespace ddl {
+
+#define TILE_0 64, 64, 32, 1, 1
+#define TILE_1 128, 64, 32, 2, 1
+#define TILE_2 64, 32, 32, 1, 1
+#define TILE_3 32, 32, 32, 1, 1
+#define TILE_4 32, 64, 32, 1, 1
+#define TILE_5 32, 32, 16, 1, 1   // software-pipelined main loop (gemm.h GemmTile::PIPE)
+
+template <class P>
+inline void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const SplitScratch& sc,
+                       hipStream_t st) {
+  switch (c) {
+    case 0: launch_gemm<TILE_0>(p, s, wide_thr, sc, st, w); break;
+    case 1: launch_gemm<TILE_1>(p, s, wide_thr, sc, st, w); break;
+    case 2: launch_gemm<TILE_2>(p, s, wide_thr, sc, st, w); break;
+    case 3: launch_gemm<TILE_3>(p, s, wide_thr, sc, st, w); break;
+    case 4: launch_gemm<TILE_4>(p, s, wide_thr, sc, st, w); break;
+    default: launch_gemm<TILE_5>(p, s, wide_thr, sc, st, w); break;
+  }
+}
+
+// Problem policy of op OP (layers.h) bound to this engine's buffers, at batch B.
+template <int OP>
+inline auto make_policy(const Engine& e, int B, const float* x, const uint32_t* seed,
+                        bool train) {
+  int M, N, K;
+  Engine::op_shape(OP, B, &M, &N, &K);
+  const uint32_t thr = train ? e.thr24 : 0u;
+  const float* const* P = e.P;
+  float* const* G = e.G;
+  if constexpr (OP == OP_CONV1_FWD) return ConvFwd<28, 1, 32>{M, N, K, x, P[0], P[1], e.p1, e.c1};
+  else if constexpr (OP == OP_CONV2_FWD)
+    return ConvFwd<14, 32, 64>{M, N, K, e.p1, P[2], P[3], e.p2, e.c2};
+  else if constexpr (OP == OP_CONV3_FWD)
+    return ConvFwd<7, 64, 128>{M, N, K, e.p2, P[4], P[5], e.p3, e.c3};
+  else if constexpr (OP == OP_CONV4_FWD)
+    return ConvFwd<4, 128, 256>{M, N, K, e.p3, P[6], P[7], e.p4, e.c4};
+  else if constexpr (OP == OP_FC1_FWD)
+    return FcFwd<true>{M, N, K, e.p4, P[8], P[9], e.h1, seed, 1u, thr, e.inv_keep, e.seed_value};
+  else if constexpr (OP == OP_FC2_FWD)
+    return FcFwd<false>{M, N, K, e.h1, P[10], P[11], e.h2, seed, 2u, thr, e.inv_keep, e.seed_value};
+  else if constexpr (OP == OP_FC2_DGRAD)
+    return FcDgradAct{{M, N, K, e.dpre2fc, P[10]}, e.h1, e.inv_keep, e.dpre1fc};
+  else if constexpr (OP == OP_FC2_WGRAD)
+    return FcWgrad{M, N, K, 1024, e.h1, e.dpre2fc, G[10], G[11]};
+  else if constexpr (OP == OP_FC1_DGRAD)
+    return FcDgradPool<2, 256>{{M, N, K, e.dpre1fc, P[8]}, e.c4, e.d4};
+  else if constexpr (OP == OP_FC1_WGRAD)
+    return FcWgrad{M, N, K, 1024, e.p4, e.dpre1fc, G[8], G[9]};
+  else if constexpr (OP == OP_CONV4_DGRAD)
+    return ConvDgrad<4, 128, 256, 7>{M, N, K, e.d4, P[6], e.c3, e.d3};
+  else if constexpr (OP == OP_CONV4_WGRAD)
+    return ConvWgrad<4, 128, 256>{M, N, K, e.p3, e.d4, G[6], G[7]};
+  else if constexpr (OP == OP_CONV3_DGRAD)
+    return ConvDgrad<7, 64, 128, 14>{M, N, K, e.d3, P[4], e.c2, e.d2};
+  else if constexpr (OP == OP_CONV3_WGRAD)
+    return ConvWgrad<7, 64, 128>{M, N, K, e.p2, e.d3, G[4], G[5]};
+  else if constexpr (OP == OP_CONV2_DGRAD)
+    return ConvDgrad<14, 32, 64, 28>{M, N, K, e.d2, P[2], e.c1, e.d1};
+  else if constexpr (OP == OP_CONV2_WGRAD)
+    return ConvWgrad<14, 32, 64>{M, N, K, e.p1, e.d2, G[2], G[3]};
+  else
+    return ConvWgrad<28, 1, 32>{M, N, K, x, e.d1, G[0], G[1]};
+}
+
+template <int OP>
+void run_op_inst(Engine& e, const float* x, int B, const uint32_t* seed, bool train,
+                     hipStream_t st, int si) {
+  const auto p = make_policy<OP>(e, B, x, seed, train);
+  launch_cfg(e.cfg[OP], p, train ? e.splits[OP] : 1, train ? e.workers[OP] : 0, e.wide[OP],
+             e.scratch[si], st);
+}
+
+// ---- dual launches: data- and weight-gradient GEMM of one layer in one kernel -----------------
+// dual launches are instantiated for these one-wave configs (others run back to back)
+inline bool one_wave_cfg(int c) { return c == 0 || c == 3 || c == 4 || c == 5; }
+
+template <class CA, int OA, int OB, class PA, class PB>
+inline void dual_b(Engine& e, const PA& pa, const PB& pb, hipStream_t st) {
+#define DDL_DUAL_B(CB) \
+  launch_gemm_dual<CA, PA, TileCfg<CB>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], \
+                                            e.wide[OA], pb, e.splits[OB], e.workers[OB], \
+                                            e.scratch[1], e.wide[OB], st, e.tail)
+  switch (e.cfg[OB]) {
+    case 0: DDL_DUAL_B(TILE_0); break;
+    case 3: DDL_DUAL_B(TILE_3); break;
+    case 4: DDL_DUAL_B(TILE_4); break;
+    default: DDL_DUAL_B(TILE_5); break;
+  }
+#undef DDL_DUAL_B
+  e.tail = UpdTail();
+}
+
+// Ops OA and OB (independent) in one launch if both use one-wave tiles, else back to back.
+template <int OA, int OB>
+void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
+  if (!e.dual || !one_wave_cfg(e.cfg[OA]) || !one_wave_cfg(e.cfg[OB])) {
+    e.flush_tail(st);
+    run_op_inst<OA>(e, x, B, seed, true, st, 0);
+    run_op_inst<OB>(e, x, B, seed, true, st, 0);
+    return;
+  }
+  const auto pa = make_policy<OA>(e, B, x, seed, true);
+  const auto pb = make_policy<OB>(e, B, x, seed, true);
+  using PA = std::decay_t<decltype(pa)>;
+  using PB = std::decay_t<decltype(pb)>;
+  switch (e.cfg[OA]) {
+    case 0: dual_b<TileCfg<TILE_0>, OA, OB, PA, PB>(e, pa, pb, st); break;
+    case 3: dual_b<TileCfg<TILE_3>, OA, OB, PA, PB>(e, pa, pb, st); break;
+    case 4: dual_b<TileCfg<TILE_4>, OA, OB, PA, PB>(e, pa, pb, st); break;
+    default: dual_b<TileCfg<TILE_5>, OA, OB, PA, PB>(e, pa, pb, st); break;
+  }
+}
+
+}  // namespace ddl

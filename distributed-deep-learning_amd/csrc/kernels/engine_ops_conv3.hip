@@ -1,0 +1,13 @@
+// Explicit instantiations of the engine GEMM launches: OP_CONV3_DGRAD, OP_CONV3_WGRAD.
+#include "engine_impl.h"
+
+namespace ddl {
+
+template void run_op_inst<OP_CONV3_DGRAD>(Engine&, const float*, int, const uint32_t*, bool, hipStream_t,
+                                  int);
+template void run_op_inst<OP_CONV3_WGRAD>(Engine&, const float*, int, const uint32_t*, bool, hipStream_t,
+                                  int);
+template void run_dual_inst<OP_CONV3_DGRAD, OP_CONV3_WGRAD>(Engine&, const float*, int, const uint32_t*,
+                                                  hipStream_t);
+
+}  // namespace ddl

@@ -1,0 +1,19 @@
+// Explicit instantiations of the engine GEMM launches: OP_FC2_DGRAD, OP_FC2_WGRAD, OP_FC1_DGRAD, OP_FC1_WGRAD.
+#include "engine_impl.h"
+
+namespace ddl {
+
+template void run_op_inst<OP_FC2_DGRAD>(Engine&, const float*, int, const uint32_t*, bool, hipStream_t,
+                                  int);
+template void run_op_inst<OP_FC2_WGRAD>(Engine&, const float*, int, const uint32_t*, bool, hipStream_t,
+                                  int);
+template void run_op_inst<OP_FC1_DGRAD>(Engine&, const float*, int, const uint32_t*, bool, hipStream_t,
+                                  int);
+template void run_op_inst<OP_FC1_WGRAD>(Engine&, const float*, int, const uint32_t*, bool, hipStream_t,
+                                  int);
+template void run_dual_inst<OP_FC2_DGRAD, OP_FC2_WGRAD>(Engine&, const float*, int, const uint32_t*,
+                                                  hipStream_t);
+template void run_dual_inst<OP_FC1_DGRAD, OP_FC1_WGRAD>(Engine&, const float*, int, const uint32_t*,
+                                                  hipStream_t);
+
+}  // namespace ddl

@@ -44,14 +44,6 @@
 
 namespace ddl {
 
-// TF1 ApplyAdam update of one element (optim.hip documents the form).
-DDL_DEV void adam1(float& w, float g, float& m, float& v, float lr_t, float c1, float c2,
-                   float eps) {
-  m += (g - m) * c1;
-  v += (g * g - v) * c2;
-  w -= lr_t * m / (sqrtf(v) + eps);
-}
-
 // One optimizer-tail block (tail.h): kTailF4PerLane float4 of one piece per lane, all loads
 // issued before any math (HBM-bound: memory-level parallelism is the whole game).
 DDL_DEV void tail_body(const UpdTail& t, int b) {
@@ -61,26 +53,30 @@ DDL_DEV void tail_body(const UpdTail& t, int b) {
     if (q < t.npieces && b >= t.p[q].blk0) i = q;
   const UpdPiece& P = t.p[i];
   const int64_t n4 = P.n >> 2;
-  const int64_t base = (int64_t)(b - P.blk0) * kTailF4PerBlock + (threadIdx.x & 63);
+  const int64_t blk_base = (int64_t)(b - P.blk0) * t.f4_per_block + (threadIdx.x & 63);
   float4* w = reinterpret_cast<float4*>(P.w);
   const float4* g = reinterpret_cast<const float4*>(P.g);
   float4* m = reinterpret_cast<float4*>(P.m);
   float4* v = reinterpret_cast<float4*>(P.v);
-  float4 W[kTailF4PerLane], G[kTailF4PerLane], M[kTailF4PerLane], V[kTailF4PerLane];
+  for (int off = 0; off < t.f4_per_block; off += kTailF4PerBlock) {
+    const int64_t base = blk_base + off;
+    if (base >= n4) break;
+    float4 W[kTailF4PerLane], G[kTailF4PerLane], M[kTailF4PerLane], V[kTailF4PerLane];
 #pragma unroll
-  for (int j = 0; j < kTailF4PerLane; ++j) {
-    const int64_t e = base + j * 64;
-    if (e < n4) { W[j] = w[e]; G[j] = g[e]; M[j] = m[e]; V[j] = v[e]; }
-  }
+    for (int j = 0; j < kTailF4PerLane; ++j) {
+      const int64_t e = base + j * 64;
+      if (e < n4) { W[j] = w[e]; G[j] = g[e]; M[j] = m[e]; V[j] = v[e]; }
+    }
 #pragma unroll
-  for (int j = 0; j < kTailF4PerLane; ++j) {
-    const int64_t e = base + j * 64;
-    if (e >= n4) continue;
-    adam1(W[j].x, G[j].x * t.scale, M[j].x, V[j].x, P.lr_t, t.c1, t.c2, t.eps);
-    adam1(W[j].y, G[j].y * t.scale, M[j].y, V[j].y, P.lr_t, t.c1, t.c2, t.eps);
-    adam1(W[j].z, G[j].z * t.scale, M[j].z, V[j].z, P.lr_t, t.c1, t.c2, t.eps);
-    adam1(W[j].w, G[j].w * t.scale, M[j].w, V[j].w, P.lr_t, t.c1, t.c2, t.eps);
-    w[e] = W[j]; m[e] = M[j]; v[e] = V[j];
+    for (int j = 0; j < kTailF4PerLane; ++j) {
+      const int64_t e = base + j * 64;
+      if (e >= n4) continue;
+      adam1(W[j].x, G[j].x * t.scale, M[j].x, V[j].x, P.lr_t, t.c1, t.c2, t.eps);
+      adam1(W[j].y, G[j].y * t.scale, M[j].y, V[j].y, P.lr_t, t.c1, t.c2, t.eps);
+      adam1(W[j].z, G[j].z * t.scale, M[j].z, V[j].z, P.lr_t, t.c1, t.c2, t.eps);
+      adam1(W[j].w, G[j].w * t.scale, M[j].w, V[j].w, P.lr_t, t.c1, t.c2, t.eps);
+      w[e] = W[j]; m[e] = M[j]; v[e] = V[j];
+    }
   }
 }
 
@@ -663,8 +659,10 @@ struct TileCfg {
 
 // Two independent GEMM problems in one launch: blocks [0, ga.nblocks) run problem A, the
 // rest problem B.  Both must use one-wave blocks.  An optional optimizer tail (tail.h) takes
-// the first ut.nblocks blocks (dispatched first, so the HBM-bound update overlaps the GEMM
-// blocks instead of trailing them; a multiple of 8 so the GEMMs' XCD-major numbering holds).
+// ut.nblocks more blocks, after the GEMM blocks (ut.first = 0, measured faster: the update
+// fills CUs as GEMM blocks retire) or before them (a multiple of 8 so the GEMMs' XCD-major
+// numbering holds).  The tail path must stay under the GEMM paths' VGPR count: at 8 float4
+// per lane it raised the conv4 dual from 113 to 149 VGPRs (3 -> 2 waves/SIMD, +9 us).
 template <class CA, class PA, class CB, class PB>
 __global__ void __launch_bounds__(64)
 gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, UpdTail ut) {
@@ -675,11 +673,18 @@ gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, UpdTail ut) {
   __shared__ float4 lds4[L + 1];
   float* lds = reinterpret_cast<float*>(lds4);
   int* flag = reinterpret_cast<int*>(lds4 + L);
-  if ((int)blockIdx.x < ut.nblocks) {
-    tail_body(ut, blockIdx.x);
+  const int gemm_blocks = ga.nblocks + gb.nblocks;
+  int b = blockIdx.x;
+  if (ut.first) {
+    if (b < ut.nblocks) {
+      tail_body(ut, b);
+      return;
+    }
+    b -= ut.nblocks;
+  } else if (b >= gemm_blocks) {
+    tail_body(ut, b - gemm_blocks);
     return;
   }
-  const int b = blockIdx.x - ut.nblocks;
   if (b < ga.nblocks)
     run_sub<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, b, lds, flag);
   else

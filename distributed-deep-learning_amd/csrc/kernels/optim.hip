@@ -12,12 +12,6 @@
 
 namespace ddl {
 
-DDL_DEV void adam1(float& w, float g, float& m, float& v, float lr_t, float c1, float c2,
-                   float eps) {
-  m += (g - m) * c1;
-  v += (g * g - v) * c2;
-  w -= lr_t * m / (sqrtf(v) + eps);
-}
 
 // 16-B body over n4 = n / 4 float4 elements; the n % 4 tail element(s) by the first lanes.
 __global__ void __launch_bounds__(256)
@@ -80,8 +74,12 @@ static int grid_for(int64_t n) {
 
 void launch_adam(float* w, const float* g, float* m, float* v, int64_t n, float lr_t, float b1,
                  float b2, float eps, float scale, hipStream_t st) {
+  launch_adam_c(w, g, m, v, n, lr_t, 1.f - b1, 1.f - b2, eps, scale, st);
+}
+
+void launch_adam_c(float* w, const float* g, float* m, float* v, int64_t n, float lr_t, float c1,
+                   float c2, float eps, float scale, hipStream_t st) {
   if (n <= 0) return;
-  const float c1 = 1.f - b1, c2 = 1.f - b2;
   const uintptr_t al = (uintptr_t)w | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v;
   if ((al & 15) == 0) {
     hipLaunchKernelGGL(adam_vec_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, (float4*)w,

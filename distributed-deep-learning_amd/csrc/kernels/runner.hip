@@ -146,32 +146,72 @@ void SyncRunner::set_units(const std::vector<RunnerUnit>& units) {
       throw std::invalid_argument("RS unit needs exactly one range and a shard buffer");
   }
   units_ = units;
-  // W = 1 (every unit LOCAL): one stream, so per-segment updates buy no overlap — coalesce
-  // all updates into as few launches as possible at the end of the step (ranges adjacent in
-  // both the parameter buffer and the PS state merge).  Same result: no backward GEMM reads a
-  // tensor after its update either way.
+  // W = 1 (every unit LOCAL): one stream.  Ranges adjacent in both the parameter buffer and
+  // the PS state merge; per segment they become the optimizer tail of the next segment's dual
+  // launch (tail.h), else all of them one coalesced launch at the end of the step.  Same
+  // result either way: no backward GEMM reads a tensor after its update.
   merged_.clear();
+  for (auto& sp : seg_pieces_) sp.clear();
+  tail_ok_ = false;
   all_local_ = true;
   for (const auto& u : units_) all_local_ &= (u.kind == RunnerUnit::LOCAL);
   if (!all_local_) return;
-  for (const auto& u : units_)
-    for (const auto& r : u.ranges) merged_.push_back({r, u.ps, u.m, u.v});
-  std::sort(merged_.begin(), merged_.end(), [](const Piece& a, const Piece& b) {
-    return a.r.lo < b.r.lo;
-  });
-  std::vector<Piece> out;
-  for (const auto& p : merged_) {
-    if (!out.empty()) {
-      Piece& q = out.back();
-      if (q.r.hi == p.r.lo && q.ps == p.ps && q.m == p.m && q.v == p.v &&
-          q.r.state_off + (q.r.hi - q.r.lo) == p.r.state_off) {
-        q.r.hi = p.r.hi;
-        continue;
+  auto coalesce = [](std::vector<Piece>& v) {
+    std::sort(v.begin(), v.end(), [](const Piece& a, const Piece& b) { return a.r.lo < b.r.lo; });
+    std::vector<Piece> out;
+    for (const auto& p : v) {
+      if (!out.empty()) {
+        Piece& q = out.back();
+        if (q.r.hi == p.r.lo && q.ps == p.ps && q.m == p.m && q.v == p.v &&
+            q.r.state_off + (q.r.hi - q.r.lo) == p.r.state_off) {
+          q.r.hi = p.r.hi;
+          continue;
+        }
       }
+      out.push_back(p);
     }
-    out.push_back(p);
+    v.swap(out);
+  };
+  for (const auto& u : units_)
+    for (const auto& r : u.ranges) {
+      merged_.push_back({r, u.ps, u.m, u.v});
+      seg_pieces_[u.seg].push_back({r, u.ps, u.m, u.v});
+    }
+  coalesce(merged_);
+  tail_ok_ = true;
+  auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  for (auto& sp : seg_pieces_) {
+    coalesce(sp);
+    tail_ok_ &= sp.size() <= (size_t)kTailPieces;
+    for (const auto& p : sp)
+      tail_ok_ &= p.v && (p.r.hi - p.r.lo) % 4 == 0 && a16(w_ + p.r.lo) && a16(g_ + p.r.lo) &&
+                  a16(p.m + p.r.state_off) && a16(p.v + p.r.state_off);
   }
-  merged_.swap(out);
+}
+
+// Segment `seg`'s Adam as the optimizer tail of the engine's next dual launch.
+void SyncRunner::set_tail(int seg, const float* lr_t) {
+  UpdTail t;
+  t.first = tail_first_;
+  t.f4_per_block = tail_f4_;
+  t.c1 = 1.f - b1_;
+  t.c2 = 1.f - b2_;
+  t.eps = eps_;
+  t.scale = grad_scale_;
+  int blk = 0;
+  for (const auto& p : seg_pieces_[seg]) {
+    UpdPiece& q = t.p[t.npieces++];
+    q.w = w_ + p.r.lo;
+    q.g = g_ + p.r.lo;
+    q.m = p.m + p.r.state_off;
+    q.v = p.v + p.r.state_off;
+    q.n = p.r.hi - p.r.lo;
+    q.lr_t = lr_t[p.ps];
+    q.blk0 = blk;
+    blk += (int)((q.n / 4 + tail_f4_ - 1) / tail_f4_);
+  }
+  t.nblocks = (blk + 7) & ~7;
+  eng_->tail = t;
 }
 
 void SyncRunner::set_optimizer(int kind, float lr, float b1, float b2, float eps, float mu) {
@@ -251,6 +291,19 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
   // stream in order; only units with collectives use the comm stream, which then overlaps
   // the remaining backward segments.
   eng_->forward(x, B, seed, true, st);
+  if (all_local_ && local_on_main_ && use_tail_ && tail_ok_ && opt_ == 0 && coef_ == 1.f) {
+    // segment s-1's update rides in segment s's dual launch (flushed as a launch of its own
+    // if the segment had no dual launch to take it); the last segment's follows the backward
+    for (int s = 0; s < kSegments; ++s) {
+      if (s > 0 && !seg_pieces_[s - 1].empty()) set_tail(s - 1, lr_t);
+      eng_->backward_segment(s, x, labels, B, seed, st);
+      eng_->flush_tail(st);
+    }
+    for (const auto& p : seg_pieces_[kSegments - 1])
+      update(w_ + p.r.lo, g_ + p.r.lo, p.m + p.r.state_off, p.v + p.r.state_off,
+             p.r.hi - p.r.lo, lr_t[p.ps], st);
+    return;
+  }
   if (all_local_ && local_on_main_) {
     for (int s = 0; s < kSegments; ++s) eng_->backward_segment(s, x, labels, B, seed, st);
     if (coef_ != 1.f)

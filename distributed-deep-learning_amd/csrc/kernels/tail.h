@@ -14,7 +14,7 @@
 namespace ddl {
 
 constexpr int kTailPieces = 4;
-constexpr int kTailF4PerLane = 8;                    // float4 per lane per tail block
+constexpr int kTailF4PerLane = 2;  // float4 per lane per pass: keeps the tail path under the GEMM paths' VGPRs
 constexpr int kTailF4PerBlock = 64 * kTailF4PerLane;  // one-wave blocks
 
 struct UpdPiece {
@@ -30,6 +30,8 @@ struct UpdPiece {
 struct UpdTail {
   int nblocks = 0;         // tail blocks (multiple of 8: keeps the GEMM blocks' XCD mapping)
   int npieces = 0;
+  int first = 1;           // 1: tail blocks precede the GEMM blocks in the grid, 0: follow them
+  int f4_per_block = kTailF4PerBlock;  // float4 per tail block (multiple of kTailF4PerBlock)
   UpdPiece p[kTailPieces];
   float c1 = 0.f, c2 = 0.f, eps = 0.f, scale = 1.f;  // 1 - beta1, 1 - beta2, epsilon, grad scale
 };

@@ -91,3 +91,24 @@ def test_forced_collectives_on_one_rank_match_local(data, kw):
 def test_rccl_probe_resolves_torch_librccl():
     from ddl_amd.ops import native
     assert native.ops().SyncRunner.probe() == ""
+
+
+@pytest.mark.parametrize("shard", ["flat", "contiguous"])
+def test_optimizer_tail_matches_end_of_step_update(data, shard):
+    """W = 1: segment s's Adam riding as extra blocks of segment s+1's dual GEMM launch
+    (csrc/kernels/tail.h) gives bit-identical parameters and moments to one coalesced Adam
+    launch after the backward."""
+    out = []
+    for tail in (True, False):
+        env = DistEnv(0, 1, 0, torch.device("cuda", 0))
+        cfg = TrainConfig(mode="sync", shard=shard, steps=5, batch_size=100, eval_every=0,
+                          engine="hip", quiet=True)
+        tr = Trainer(cfg, env, dataset=data)
+        tr.exchange.runner.set_use_tail(tail)
+        for i in range(5):
+            tr.train_step(i)
+        torch.cuda.synchronize()
+        s = tr.servers[0]
+        out.append((tr.params.clone(), s.m.clone(), s.v.clone()))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
