@@ -49,8 +49,11 @@ enum Op {
 // Block-tile configurations selectable per op at run time (gemm.h template args
 // <BM, BN, BK=32, WM, WN>): 0 = 64x64 (1 wave 64x64), 1 = 128x64 (2 waves 64x64),
 // 2 = 64x32 (1 wave), 3 = 32x32 (1 wave), 4 = 32x64 (1 wave),
-// 5 = 32x32 with BK = 16 and the software-pipelined main loop (1 wave).
-constexpr int NUM_TILE_CFGS = 6;
+// 5 = 32x32 with BK = 16 and the software-pipelined main loop (1 wave),
+// 6 = 64x64 (4 waves of 32x32), 7 = 64x32 (2 waves of 32x32), 8 = 32x64 (2 waves of 32x32):
+// multi-wave blocks share each staged operand tile between waves (half the L1/L2 bytes per
+// MFMA of one-wave 32x32 blocks at 64x64), at one barrier per K tile.
+constexpr int NUM_TILE_CFGS = 9;
 
 struct Engine {
   const float* P[14] = {};   // parameter tensors v0..v13 (any flat layout)

@@ -59,12 +59,12 @@ void Engine::op_shape(int op, int B, int* M, int* N, int* K) {
     case OP_FC1_DGRAD: m = B; n = 1024; k = 1024; break;
     case OP_FC1_WGRAD: m = 1025; n = 1024; k = B; break;
     case OP_CONV4_DGRAD: m = B * 16; n = 128; k = 6400; break;
-    case OP_CONV4_WGRAD: m = 3201; n = 256; k = B * 16; break;
+    case OP_CONV4_WGRAD: m = 3201; n = 256; k = ConvWgrad<4, 128, 256>::padded_k(B); break;
     case OP_CONV3_DGRAD: m = B * 49; n = 64; k = 3200; break;
-    case OP_CONV3_WGRAD: m = 1601; n = 128; k = B * 49; break;
+    case OP_CONV3_WGRAD: m = 1601; n = 128; k = ConvWgrad<7, 64, 128>::padded_k(B); break;
     case OP_CONV2_DGRAD: m = B * 196; n = 32; k = 1600; break;
-    case OP_CONV2_WGRAD: m = 801; n = 64; k = B * 196; break;
-    case OP_CONV1_WGRAD: m = 26; n = 32; k = B * 784; break;
+    case OP_CONV2_WGRAD: m = 801; n = 64; k = ConvWgrad<14, 32, 64>::padded_k(B); break;
+    case OP_CONV1_WGRAD: m = 26; n = 32; k = ConvWgrad<28, 1, 32>::padded_k(B); break;
     default: break;
   }
   *M = m; *N = n; *K = k;
@@ -76,6 +76,9 @@ void Engine::op_shape(int op, int B, int* M, int* N, int* K) {
 #define TILE_3 32, 32, 32, 1, 1
 #define TILE_4 32, 64, 32, 1, 1
 #define TILE_5 32, 32, 16, 1, 1   // software-pipelined main loop (gemm.h GemmTile::PIPE)
+#define TILE_6 64, 64, 32, 2, 2   // 4 waves of 32x32 sharing one LDS-staged 64x64 block tile
+#define TILE_7 64, 32, 32, 2, 1   // 2 waves of 32x32 along M
+#define TILE_8 32, 64, 32, 1, 2   // 2 waves of 32x32 along N
 
 static size_t slab_need(int c, int M, int N, int K, int s, int w) {
   switch (c) {
@@ -84,7 +87,10 @@ static size_t slab_need(int c, int M, int N, int K, int s, int w) {
     case 2: return gemm_slab_f4<TILE_2>(M, N, K, s, w);
     case 3: return gemm_slab_f4<TILE_3>(M, N, K, s, w);
     case 4: return gemm_slab_f4<TILE_4>(M, N, K, s, w);
-    default: return gemm_slab_f4<TILE_5>(M, N, K, s, w);
+    case 5: return gemm_slab_f4<TILE_5>(M, N, K, s, w);
+    case 6: return gemm_slab_f4<TILE_6>(M, N, K, s, w);
+    case 7: return gemm_slab_f4<TILE_7>(M, N, K, s, w);
+    default: return gemm_slab_f4<TILE_8>(M, N, K, s, w);
   }
 }
 

@@ -18,6 +18,9 @@ namespace ddl {
 #define TILE_3 32, 32, 32, 1, 1
 #define TILE_4 32, 64, 32, 1, 1
 #define TILE_5 32, 32, 16, 1, 1   // software-pipelined main loop (gemm.h GemmTile::PIPE)
+#define TILE_6 64, 64, 32, 2, 2   // 4 waves of 32x32 sharing one LDS-staged 64x64 block tile
+#define TILE_7 64, 32, 32, 2, 1   // 2 waves of 32x32 along M
+#define TILE_8 32, 64, 32, 1, 2   // 2 waves of 32x32 along N
 
 template <class P>
 inline void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const SplitScratch& sc,
@@ -28,7 +31,10 @@ inline void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const Spli
     case 2: launch_gemm<TILE_2>(p, s, wide_thr, sc, st, w); break;
     case 3: launch_gemm<TILE_3>(p, s, wide_thr, sc, st, w); break;
     case 4: launch_gemm<TILE_4>(p, s, wide_thr, sc, st, w); break;
-    default: launch_gemm<TILE_5>(p, s, wide_thr, sc, st, w); break;
+    case 5: launch_gemm<TILE_5>(p, s, wide_thr, sc, st, w); break;
+    case 6: launch_gemm<TILE_6>(p, s, wide_thr, sc, st, w); break;
+    case 7: launch_gemm<TILE_7>(p, s, wide_thr, sc, st, w); break;
+    default: launch_gemm<TILE_8>(p, s, wide_thr, sc, st, w); break;
   }
 }
 

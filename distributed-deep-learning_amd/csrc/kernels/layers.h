@@ -194,29 +194,71 @@ struct ConvDgrad {
 
 // ---------------------------------------------------------------------------------------------
 // conv weight gradient (Conv2DBackpropFilter + bias grad, B10/B8): dW_aug[25*CIN+1, COUT].
-// M = 25*CIN + 1 (row 25*CIN is a row of ones -> db), N = COUT, K = B*H*H.
+// M = 25*CIN + 1 (row 25*CIN is a row of ones -> db), N = COUT.
+// K enumerates positions with each image row padded to WP = next power of two >= H columns:
+// k = ((b*H + y) << LWP) + x, K = B*H*WP (x >= H reads 0, so the padding adds zeros to the
+// sum).  A K tile then covers whole rows (WP <= BK) or an aligned part of one row, so the
+// row index (b, y) comes from the tile base on the scalar unit and a thread's column x from
+// its fixed offset in the tile: the per-element position decode (k / H, k % H, k / (H*H):
+// ~20 VALU per gather, 8.7 VALU per MFMA in the dual launches by PMC) drops to a few adds.
+// The price is WP/H more MFMA work on the H = 7, 14, 28 layers (8/7, 16/14, 32/28).
 // A[m=(tap,ci)][k=(b,y,x)] = x[b, y+ky-2, x+kx-2, ci] (ci contiguous => MN-contiguous),
-// B[n=co][k] = dpre[k*COUT + co] (MN-contiguous).
+// B[n=co][k] = dpre[((b*H + y)*H + x)*COUT + co] (MN-contiguous).
 // ---------------------------------------------------------------------------------------------
+constexpr int wgrad_wp(int h) { return h <= 4 ? 4 : h <= 8 ? 8 : h <= 16 ? 16 : 32; }
+constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v / 2); }
+
 template <int H, int CIN, int COUT>
 struct ConvWgrad {
   static constexpr bool A_KCONTIG = false;
   static constexpr bool B_KCONTIG = false;
   static constexpr int KW = 25 * CIN;
-  int M, N, K;
+  static constexpr int WP = wgrad_wp(H), LWP = ilog2(WP);
+  // rows a thread's offset can add to the tile's first row (BK <= 32)
+  static_assert((H & (H - 1)) == 0 || 32 / WP - 1 < H, "one row wrap at most");
+  static constexpr int padded_k(int batch) { return batch * H * WP; }
+  int M, N, K;                     // K = padded_k(batch)
   const float* __restrict__ x;     // [B,H,H,CIN]
   const float* __restrict__ dpre;  // [B,H,H,COUT]
   float* __restrict__ gw;          // [25*CIN, COUT]
   float* __restrict__ gb;          // [COUT]
 
+  struct Pos {  // a thread's fixed position offset inside every K tile
+    int dr;     // rows past the tile's first row
+    int xk;     // column offset (added to the tile's first column)
+  };
   struct AInfo {
     int m;      // first of the 4 rows
     int dy, dx; // tap offsets of row m (vector path)
     int ci;
-    int kk;
+    Pos p;
     bool vec;   // all 4 rows are weight rows of one tap
   };
-  using BInfo = LinInfo;
+  struct BInfo {
+    int n;
+    Pos p;
+    bool ok;
+  };
+
+  static DDL_DEV Pos pos(int kk) { return {kk >> LWP, kk & (WP - 1)}; }
+  // (b, y, x, valid) of a thread's element in the K tile at k0 (k0 % min(WP, BK) == 0)
+  DDL_DEV void decode(int k0, const Pos& p, int& b, int& y, int& xx, bool& ok) const {
+    const int r0 = k0 >> LWP;  // tile-uniform: scalar unit
+    const int x0 = k0 & (WP - 1);
+    int yy = r0 % H + p.dr;
+    b = r0 / H;
+    if constexpr ((H & (H - 1)) == 0) {
+      b += yy >> ilog2(H);
+      yy &= H - 1;
+    } else {
+      const bool wrap = yy >= H;
+      yy -= wrap ? H : 0;
+      b += wrap ? 1 : 0;
+    }
+    y = yy;
+    xx = x0 + p.xk;
+    ok = xx < H && ((r0 + p.dr) << LWP) < K;
+  }
 
   DDL_DEV AInfo prepA(int m, int kk) const {
     AInfo a;
@@ -225,17 +267,16 @@ struct ConvWgrad {
     a.ci = m - tap * CIN;
     a.dy = tap / 5 - 2;
     a.dx = tap % 5 - 2;
-    a.kk = kk;
+    a.p = pos(kk);
     a.vec = (CIN % 4 == 0) && (m + 3 < KW);
     return a;
   }
   DDL_DEV float4 loadA(const AInfo& a, int k0) const {
-    const brsrc_t r = make_rsrc(x, (uint32_t)K * CIN * 4u);
-    const int k = k0 + a.kk;
-    const bool kin = k < K;
-    const int xx = k % H;
-    const int t = k / H;
-    const int y = t % H, b = t / H;
+    const int nimg = (K >> LWP) / H;
+    const brsrc_t r = make_rsrc(x, (uint32_t)nimg * H * H * CIN * 4u);
+    int b, y, xx;
+    bool kin;
+    decode(k0, a.p, b, y, xx, kin);
     if constexpr (CIN % 4 == 0) {
       // KW = 25*CIN is a multiple of 4, so a 4-row group is either all weight rows (one
       // 16-B gather) or starts at row >= KW: the ones row (db) then zeros.  Branch-free.
@@ -257,11 +298,15 @@ struct ConvWgrad {
     }
     return make_float4(v[0], v[1], v[2], v[3]);
   }
-  DDL_DEV BInfo prepB(int n, int kk) const { return {kk * COUT + n, kk, n < N}; }
-  DDL_DEV float4 loadB(const BInfo& b, int k0) const {
-    const brsrc_t r = make_rsrc(dpre, (uint32_t)K * COUT * 4u);
-    const bool good = b.ok && k0 + b.kk < K;
-    return bload4(r, good ? (b.off + k0 * COUT) * 4 : kOOB);
+  DDL_DEV BInfo prepB(int n, int kk) const { return {n, pos(kk), n < N}; }
+  DDL_DEV float4 loadB(const BInfo& bi, int k0) const {
+    const int nimg = (K >> LWP) / H;
+    const brsrc_t r = make_rsrc(dpre, (uint32_t)nimg * H * H * COUT * 4u);
+    int b, y, xx;
+    bool kin;
+    decode(k0, bi.p, b, y, xx, kin);
+    const bool good = bi.ok && kin;
+    return bload4(r, good ? (((b * H + y) * H + xx) * COUT + bi.n) * 4 : kOOB);
   }
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
 #pragma unroll

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""A/B of per-op GEMM schedules on the real training step (native runner, W = 1): the
+engine defaults vs schedules from step_tune.py --json files, interleaved rounds, one process.
+
+usage: python scripts/sched_ab.py tuned1.json [tuned2.json ...] [--steps 300] [--rounds 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tuned", nargs="*")
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    from ddl_amd.config import TrainConfig
+    from ddl_amd.parallel.comm import DistEnv
+    from ddl_amd.parallel.roles import Trainer
+    from ddl_amd.utils.data import synthetic_mnist
+
+    env = DistEnv(0, 1, 0, torch.device("cuda", 0))
+    cfg = TrainConfig(mode="sync", shard="flat", steps=10 ** 6, batch_size=100, eval_every=0,
+                      engine="hip", quiet=True, data_sharding="stride")
+    tr = Trainer(cfg, env, dataset=synthetic_mnist())
+    e = tr.engine.eng
+    scheds = {"default": {"cfg": e.get_cfg(), "splits": e.get_splits(),
+                          "workers": e.get_workers(), "wide": e.get_wide()}}
+    for p in a.tuned:
+        scheds[os.path.basename(p)] = json.load(open(p))
+    res = {k: [] for k in scheds}
+    step = 0
+    for _ in range(a.rounds):
+        for name, s in scheds.items():
+            e.set_cfg(s["cfg"])
+            e.set_splits(s["splits"])
+            e.set_workers(s["workers"])
+            e.set_wide(s["wide"])
+            for _ in range(20):
+                tr.train_step(step)
+                step += 1
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                tr.train_step(step)
+                step += 1
+            torch.cuda.synchronize()
+            res[name].append(1e6 * (time.perf_counter() - t0) / a.steps)
+    for name, ts in res.items():
+        print(f"{name:24s} us/step min {min(ts):7.1f}  all {' '.join(f'{t:.1f}' for t in ts)}")
+
+
+if __name__ == "__main__":
+    main()

@@ -149,7 +149,7 @@ def test_split_k_variants_agree(setup):
             assert err < tol, (t.name, name, err, e32)
 
 
-@pytest.mark.parametrize("cfg", [None, 0, 1, 2, 4, 5])
+@pytest.mark.parametrize("cfg", [None, 0, 1, 2, 4, 5, 6, 7, 8])
 def test_stream_k_matches_reference(setup, cfg):
     """Stream-K schedules (several worker counts, every tile config) give the fp64-reference
     gradients, and a given schedule is bit-deterministic across runs."""
@@ -178,16 +178,22 @@ def test_stream_k_matches_reference(setup, cfg):
         eng.set_workers(base_w)
 
 
-def test_inlaunch_splitk_reduce_matches_reference(setup):
-    """Split-K with the in-launch last-arriver reduce (sc1 hand-off) for every op: fp64
-    reference gradients, bit-deterministic across runs."""
+@pytest.mark.parametrize("cfg", [None, 6, 7, 8])
+@pytest.mark.parametrize("wide", [1 << 20, 1])
+def test_inlaunch_splitk_reduce_matches_reference(setup, cfg, wide):
+    """Split-K with the in-launch last-arriver reduce (sc1 hand-off; wide = 1: the separate
+    wide-reduce kernel) for every op, default and multi-wave tile configs: fp64 reference
+    gradients, bit-deterministic across runs."""
     eng, flat, params, grads, x, y = setup
     base_w, base_s, base_wide = eng.get_workers(), eng.get_splits(), eng.get_wide()
+    base_cfg = eng.get_cfg()
     _, r64 = ref_grads(flat, x, y, 0.5, 77, torch.float64)
     try:
+        if cfg is not None:
+            eng.set_cfg([cfg] * len(base_cfg))
         eng.set_workers([0] * len(base_w))
         eng.set_splits([max(2, min(s, 64)) for s in base_s])
-        eng.set_wide([1 << 20] * len(base_w))
+        eng.set_wide([wide] * len(base_w))
         outs = []
         for _ in range(2):
             grads.zero_()
@@ -200,6 +206,7 @@ def test_inlaunch_splitk_reduce_matches_reference(setup):
             tol = 5e-5 if t.index > 7 else 5e-3
             assert rel_err(outs[0][o:o + t.numel], r64[t.index].reshape(-1)) < tol, t.name
     finally:
+        eng.set_cfg(base_cfg)
         eng.set_workers(base_w)
         eng.set_splits(base_s)
         eng.set_wide(base_wide)
