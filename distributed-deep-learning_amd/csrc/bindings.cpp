@@ -81,6 +81,17 @@ class PyEngine {
   std::vector<int64_t> get_cfg() const {
     return std::vector<int64_t>(e_.cfg, e_.cfg + ddl::OP_COUNT);
   }
+  // tile configs of the eval forward (no split-K, large batch chunks); no slab needed
+  void set_eval_cfg(std::vector<int64_t> c) {
+    TORCH_CHECK((int)c.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " tile configs");
+    for (int i = 0; i < ddl::OP_COUNT; ++i) {
+      TORCH_CHECK(c[i] >= 0 && c[i] < ddl::NUM_TILE_CFGS, "tile config out of range");
+      e_.eval_cfg[i] = (int)c[i];
+    }
+  }
+  std::vector<int64_t> get_eval_cfg() const {
+    return std::vector<int64_t>(e_.eval_cfg, e_.eval_cfg + ddl::OP_COUNT);
+  }
   void set_concurrent(bool on) { e_.concurrent = on; }
   void set_dual(bool on) { e_.dual = on; }
   void set_wide_thr(int64_t t) {
@@ -340,6 +351,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("get_workers", &PyEngine::get_workers)
       .def("set_cfg", &PyEngine::set_cfg)
       .def("get_cfg", &PyEngine::get_cfg)
+      .def("set_eval_cfg", &PyEngine::set_eval_cfg)
+      .def("get_eval_cfg", &PyEngine::get_eval_cfg)
       .def("set_concurrent", &PyEngine::set_concurrent)
       .def("set_dual", &PyEngine::set_dual)
       .def("set_wide_thr", &PyEngine::set_wide_thr)

@@ -62,6 +62,7 @@ struct Engine {
   int train_batch = 0;       // slab sized for this batch with the current splits/cfgs
   int splits[OP_COUNT];
   int cfg[OP_COUNT];
+  int eval_cfg[OP_COUNT];    // tile configs of the no-split eval forward (train = false)
   int workers[OP_COUNT];     // > 0: stream-K with this many workers (overrides splits)
   int wide_thr = 1;          // default split count above which the separate wide reduce is used
   int wide[OP_COUNT];        // per op: z > wide[op] -> separate wide reduce (mode 2), else the

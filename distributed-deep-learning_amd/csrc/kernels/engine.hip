@@ -27,6 +27,10 @@ Engine::Engine() {
   // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
   static const bool inl[OP_COUNT] = {0, 1, 0, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0};
   memcpy(cfg, defc, sizeof(defc));
+  memcpy(eval_cfg, defc, sizeof(defc));
+  // eval forward at 10k-row chunks (scripts/eval_sweep.py): conv3 on 4-wave 64x64 blocks,
+  // full test-set eval 7.25 -> 7.16 ms (the others measured best on 32x32 one-wave blocks)
+  eval_cfg[OP_CONV3_FWD] = 6;
   memcpy(splits, defs, sizeof(defs));
   memcpy(workers, defw, sizeof(defw));
   for (int op = 0; op < OP_COUNT; ++op) wide[op] = inl[op] ? (1 << 20) : 1;

@@ -86,7 +86,8 @@ template <int OP>
 void run_op_inst(Engine& e, const float* x, int B, const uint32_t* seed, bool train,
                      hipStream_t st, int si) {
   const auto p = make_policy<OP>(e, B, x, seed, train);
-  launch_cfg(e.cfg[OP], p, train ? e.splits[OP] : 1, train ? e.workers[OP] : 0, e.wide[OP],
+  launch_cfg(train ? e.cfg[OP] : e.eval_cfg[OP], p, train ? e.splits[OP] : 1,
+             train ? e.workers[OP] : 0, e.wide[OP],
              e.scratch[si], st);
 }
 

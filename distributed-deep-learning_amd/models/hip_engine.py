@@ -33,7 +33,7 @@ class HipEngine:
     segments = HIP_SEGMENTS
 
     def __init__(self, params: torch.Tensor, grads: torch.Tensor, offsets: Sequence[int],
-                 batch: int = 100, graph: bool = True, eval_chunk: int = 2000,
+                 batch: int = 100, graph: bool = True, eval_chunk: int = 10000,
                  keep_prob: float = 0.5, splits: Optional[List[int]] = None):
         if not params.is_cuda:
             raise ValueError("HipEngine needs GPU tensors")
@@ -42,6 +42,8 @@ class HipEngine:
         self.pv = param_views(params, offsets)
         self.gv = param_views(grads, offsets)
         self.batch = batch
+        # 10k rows = the reference's whole test set in one forward (7.25 ms vs 7.74 ms in 2k
+        # chunks, scripts/eval_sweep.py); the activations for it take ~2.6 GB of 288 GB HBM
         self.eval_chunk = eval_chunk
         self.keep = keep_prob
         self.eng = ext.Engine([v.reshape(-1) for v in self.pv], [g.reshape(-1) for g in self.gv],
