@@ -69,17 +69,17 @@ inline auto make_policy(const Engine& e, int B, const float* x, const uint32_t* 
   else if constexpr (OP == OP_CONV4_DGRAD)
     return ConvDgrad<4, 128, 256, 7>{M, N, K, e.d4, P[6], e.c3, e.d3};
   else if constexpr (OP == OP_CONV4_WGRAD)
-    return ConvWgrad<4, 128, 256>{M, N, K, e.p3, e.d4, G[6], G[7]};
+    return WgradConv4{M, N, K, e.p3, e.d4, G[6], G[7]};
   else if constexpr (OP == OP_CONV3_DGRAD)
     return ConvDgrad<7, 64, 128, 14>{M, N, K, e.d3, P[4], e.c2, e.d2};
   else if constexpr (OP == OP_CONV3_WGRAD)
-    return ConvWgrad<7, 64, 128>{M, N, K, e.p2, e.d3, G[4], G[5]};
+    return WgradConv3{M, N, K, e.p2, e.d3, G[4], G[5]};
   else if constexpr (OP == OP_CONV2_DGRAD)
     return ConvDgrad<14, 32, 64, 28>{M, N, K, e.d2, P[2], e.c1, e.d1};
   else if constexpr (OP == OP_CONV2_WGRAD)
-    return ConvWgrad<14, 32, 64>{M, N, K, e.p1, e.d2, G[2], G[3]};
+    return WgradConv2{M, N, K, e.p1, e.d2, G[2], G[3]};
   else
-    return ConvWgrad<28, 1, 32>{M, N, K, x, e.d1, G[0], G[1]};
+    return WgradConv1{M, N, K, x, e.d1, G[0], G[1]};
 }
 
 template <int OP>

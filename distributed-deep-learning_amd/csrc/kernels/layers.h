@@ -208,14 +208,19 @@ struct ConvDgrad {
 constexpr int wgrad_wp(int h) { return h <= 4 ? 4 : h <= 8 ? 8 : h <= 16 ? 16 : 32; }
 constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v / 2); }
 
-template <int H, int CIN, int COUT>
+// WP: row width of the K enumeration — wgrad_wp(H) (padded to a power of two) or H (exact;
+// a thread's column then may wrap into the next row, one compare-select per gather)
+template <int H, int CIN, int COUT, int WP = wgrad_wp(H)>
 struct ConvWgrad {
   static constexpr bool A_KCONTIG = false;
   static constexpr bool B_KCONTIG = false;
   static constexpr int KW = 25 * CIN;
-  static constexpr int WP = wgrad_wp(H), LWP = ilog2(WP);
-  // rows a thread's offset can add to the tile's first row (BK <= 32)
-  static_assert((H & (H - 1)) == 0 || 32 / WP - 1 < H, "one row wrap at most");
+  static_assert(WP >= H, "row width below the map width");
+  // tiles start at multiples of BK (16 or 32): a thread's column offset never carries into
+  // the next row when WP divides 16 or is a multiple of 32
+  static constexpr bool XWRAP = !(16 % WP == 0 || WP % 32 == 0);
+  // rows a thread's offset can add to the tile's first row, plus a column carry
+  static_assert((H & (H - 1)) == 0 || 32 / WP + 1 < H, "one row wrap at most");
   static constexpr int padded_k(int batch) { return batch * H * WP; }
   int M, N, K;                     // K = padded_k(batch)
   const float* __restrict__ x;     // [B,H,H,CIN]
@@ -240,12 +245,19 @@ struct ConvWgrad {
     bool ok;
   };
 
-  static DDL_DEV Pos pos(int kk) { return {kk >> LWP, kk & (WP - 1)}; }
-  // (b, y, x, valid) of a thread's element in the K tile at k0 (k0 % min(WP, BK) == 0)
+  static DDL_DEV Pos pos(int kk) { return {kk / WP, kk % WP}; }
+  // (b, y, x, valid) of a thread's element in the K tile at k0 (a multiple of BK); the
+  // divisions by the constants WP, H of the uniform k0 run on the scalar unit
   DDL_DEV void decode(int k0, const Pos& p, int& b, int& y, int& xx, bool& ok) const {
-    const int r0 = k0 >> LWP;  // tile-uniform: scalar unit
-    const int x0 = k0 & (WP - 1);
-    int yy = r0 % H + p.dr;
+    const int r0 = k0 / WP;
+    int dr = p.dr;
+    xx = k0 % WP + p.xk;
+    if constexpr (XWRAP) {
+      const bool cx = xx >= WP;
+      xx -= cx ? WP : 0;
+      dr += cx ? 1 : 0;
+    }
+    int yy = r0 % H + dr;
     b = r0 / H;
     if constexpr ((H & (H - 1)) == 0) {
       b += yy >> ilog2(H);
@@ -256,8 +268,7 @@ struct ConvWgrad {
       b += wrap ? 1 : 0;
     }
     y = yy;
-    xx = x0 + p.xk;
-    ok = xx < H && ((r0 + p.dr) << LWP) < K;
+    ok = xx < H && (r0 + dr) * WP < K;
   }
 
   DDL_DEV AInfo prepA(int m, int kk) const {
@@ -272,7 +283,7 @@ struct ConvWgrad {
     return a;
   }
   DDL_DEV float4 loadA(const AInfo& a, int k0) const {
-    const int nimg = (K >> LWP) / H;
+    const int nimg = K / (WP * H);
     const brsrc_t r = make_rsrc(x, (uint32_t)nimg * H * H * CIN * 4u);
     int b, y, xx;
     bool kin;
@@ -300,7 +311,7 @@ struct ConvWgrad {
   }
   DDL_DEV BInfo prepB(int n, int kk) const { return {n, pos(kk), n < N}; }
   DDL_DEV float4 loadB(const BInfo& bi, int k0) const {
-    const int nimg = (K >> LWP) / H;
+    const int nimg = K / (WP * H);
     const brsrc_t r = make_rsrc(dpre, (uint32_t)nimg * H * H * COUT * 4u);
     int b, y, xx;
     bool kin;
@@ -317,6 +328,13 @@ struct ConvWgrad {
     }
   }
 };
+
+// The four conv weight-gradient GEMMs (conv4 .. conv1) with their K row widths.
+constexpr int kWgradRowPad = 0;  // 1: pad rows to powers of two, 0: exact rows (H = 7, 14, 28)
+using WgradConv4 = ConvWgrad<4, 128, 256, 4>;
+using WgradConv3 = ConvWgrad<7, 64, 128, kWgradRowPad ? 8 : 7>;
+using WgradConv2 = ConvWgrad<14, 32, 64, kWgradRowPad ? 16 : 14>;
+using WgradConv1 = ConvWgrad<28, 1, 32, kWgradRowPad ? 32 : 28>;
 
 // ---------------------------------------------------------------------------------------------
 // fully connected forward (model.py:70 fc1: +b, ReLU, dropout; :79,82 fc2: +b, dropout)
