@@ -195,13 +195,13 @@ struct ConvDgrad {
 // ---------------------------------------------------------------------------------------------
 // conv weight gradient (Conv2DBackpropFilter + bias grad, B10/B8): dW_aug[25*CIN+1, COUT].
 // M = 25*CIN + 1 (row 25*CIN is a row of ones -> db), N = COUT.
-// K enumerates positions with each image row padded to WP = next power of two >= H columns:
-// k = ((b*H + y) << LWP) + x, K = B*H*WP (x >= H reads 0, so the padding adds zeros to the
-// sum).  A K tile then covers whole rows (WP <= BK) or an aligned part of one row, so the
-// row index (b, y) comes from the tile base on the scalar unit and a thread's column x from
-// its fixed offset in the tile: the per-element position decode (k / H, k % H, k / (H*H):
-// ~20 VALU per gather, 8.7 VALU per MFMA in the dual launches by PMC) drops to a few adds.
-// The price is WP/H more MFMA work on the H = 7, 14, 28 layers (8/7, 16/14, 32/28).
+// K enumerates positions row by row with a row width WP >= H: k = (b*H + y)*WP + x,
+// K = B*H*WP (columns x >= H read 0).  The row index of a K tile's first element comes from
+// the tile base (uniform: scalar unit) and a thread's (row, column) offset inside the tile is
+// fixed (prepA/prepB), so a gather needs a column carry and a row wrap (compare-selects)
+// instead of the per-element position decode k / H, k % H, k / (H*H) (~20 VALU per gather).
+// WP = H (exact rows) is the default; WP = next power of two (no carry, but WP/H more MFMA
+// work on the H = 7, 14, 28 layers) measured 2 us/step slower (kWgradRowPad).
 // A[m=(tap,ci)][k=(b,y,x)] = x[b, y+ky-2, x+kx-2, ci] (ci contiguous => MN-contiguous),
 // B[n=co][k] = dpre[((b*H + y)*H + x)*COUT + co] (MN-contiguous).
 // ---------------------------------------------------------------------------------------------
