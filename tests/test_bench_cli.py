@@ -1,0 +1,62 @@
+"""The bench.py driver contract on CPU (gloo): one JSON line from rank 0 with the metric /
+config fields BASELINE.json names, for a single process and for torchrun with 2 ranks (the
+driver's N > 1 launch line, minus the GPUs)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+        "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _json_lines(out):
+    recs = []
+    for line in out.splitlines():
+        line = line.strip()
+        if line.startswith("{"):
+            recs.append(json.loads(line))
+    return recs
+
+
+def _env():
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    env["HIP_VISIBLE_DEVICES"] = ""
+    return env
+
+
+@pytest.mark.slow
+def test_bench_single_process_json():
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--tta", "0"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=600, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1
+    rec = recs[0]
+    assert KEYS <= rec.keys()
+    assert rec["n_gpus"] == 1 and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["value"] > 0 and rec["higher_is_better"] is True and rec["scaling"] == "weak"
+    assert rec["config"]["global_batch"] == 100
+    assert rec["config"]["parallelism"] == "dp1-ps1-sync-flat"
+
+
+@pytest.mark.slow
+def test_bench_torchrun_two_ranks_json(port):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--tta", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout  # rank 0 only
+    rec = recs[0]
+    assert KEYS <= rec.keys()
+    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 200
+    assert rec["config"]["parallelism"] == "dp2-ps2-sync-flat"
+    # whole-job aggregate: images/s = W * batch * steps / max-over-ranks time
+    assert rec["value"] == pytest.approx(2 * 100 / (rec["ms_per_step"] / 1e3), rel=1e-3)
