@@ -34,6 +34,7 @@ def _canon(rec):
     (3, dict(shard="greedy")),                     # mnist_sync_sharding_greedy
     (2, dict(shard="none")),                       # mnist_sync (1 PS)
     (2, dict(shard="flat")),                       # RS/AG fast path
+    (4, dict(shard="flat", data_sharding="stride")),  # the bench configuration at W = 4
     (3, dict(shard="lpt")),
     (3, dict(shard="contiguous", num_ps=2)),       # fewer PS than workers
     (2, dict(shard="contiguous", num_ps=5)),       # several PS per process
