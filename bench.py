@@ -58,6 +58,9 @@ def main(argv=None):
                     help="after the throughput run, train one reference epoch (500 steps/worker, "
                          "full test-set eval every 10 steps, eval time included) and report the "
                          "wall time to this test accuracy; <= 0 skips it")
+    ap.add_argument("--tta-sync-eval", action="store_true",
+                    help="time-to-accuracy run with the eval in line on the training stream "
+                         "(default on GPU: side-stream eval from parameter snapshots)")
     a = ap.parse_args(argv)
 
     import torch
@@ -116,13 +119,15 @@ def main(argv=None):
         cfg2 = TrainConfig(mode=a.mode, shard=a.shard, batch_size=a.batch_size, eval_every=10,
                            engine=a.engine, graph=a.graph and not a.no_graph,
                            overlap=not a.no_overlap, quiet=True, target_acc=a.tta,
-                           data_sharding="stride", native_exchange=not a.no_native_exchange)
+                           data_sharding="stride", native_exchange=not a.no_native_exchange,
+                           eval_async=cuda and not a.tta_sync_eval)
         tr2 = Trainer(cfg2, env, dataset=data)
         s = tr2.train()
         tta = {"target_acc": a.tta, "time_to_target_s": s["time_to_target"],
                "final_acc": round(s["final_acc"], 4), "epoch_wall_s": round(s["wall_time"], 4),
                "steps_per_worker": s["steps"], "eval_every": 10,
-               "eval": "distributed over ranks" if world > 1 and a.mode == "sync" else "full"}
+               "eval": ("distributed over ranks" if world > 1 and a.mode == "sync" else "full")
+               + ("; side stream from parameter snapshots" if cfg2.eval_async else "; in line")}
 
     if env.rank == 0:
         base = BASELINE_IMG_PER_S_PER_GPU

@@ -39,6 +39,7 @@ class TrainConfig:
     native_exchange: bool = True    # sync step in the C++ SyncRunner (HIP engine on GPU)
     force_collectives: bool = False  # W = 1: native runner keeps RS/reduce units on a 1-rank comm
     dist_eval: bool = True          # sync, W > 1: each rank scores 1/W of the test set
+    eval_async: bool = False        # HIP engine: periodic eval on a side stream from a snapshot
     check_provenance: bool = False  # async: verify every applied push
     log_jsonl: Optional[str] = None
     checkpoint_dir: Optional[str] = None
@@ -82,6 +83,9 @@ def add_args(p: argparse.ArgumentParser, mode_default: str = "sync") -> argparse
                    help="async: checksum every push and verify order/provenance at the PS")
     p.add_argument("--no-dist-eval", action="store_true",
                    help="every worker scores the full test set (reference behaviour)")
+    p.add_argument("--eval-async", action="store_true",
+                   help="HIP engine: run the periodic test-set eval on a side stream from a "
+                        "parameter snapshot, overlapped with training (same accuracies)")
     p.add_argument("--no-native-exchange", action="store_true",
                    help="drive the sync exchange from Python instead of the C++ SyncRunner")
     p.add_argument("--no-overlap", action="store_true")
@@ -105,6 +109,7 @@ def from_args(a: argparse.Namespace) -> TrainConfig:
         eval_every=a.eval_every, data=a.data, data_sharding=a.data_sharding,
         grad_reduce=a.grad_reduce, ref_quirks=a.ref_quirks, seed=a.seed, engine=a.engine,
         graph=a.graph and not a.no_graph, native_exchange=not a.no_native_exchange,
-        dist_eval=not a.no_dist_eval, check_provenance=a.check_provenance, overlap=not a.no_overlap, log_jsonl=a.log_jsonl,
+        dist_eval=not a.no_dist_eval, eval_async=a.eval_async,
+        check_provenance=a.check_provenance, overlap=not a.no_overlap, log_jsonl=a.log_jsonl,
         checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
         resume=a.resume, target_acc=a.target_acc, quiet=a.quiet, watchdog_s=a.watchdog_s)

@@ -164,12 +164,18 @@ class HipEngine:
 
     # ---- eval ------------------------------------------------------------------------------------
     @torch.no_grad()
-    def correct(self, x: torch.Tensor, labels: torch.Tensor) -> int:
+    def correct_async(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        """Enqueue the correct-count eval on the current stream; returns the device int32
+        [1] counter (valid once the stream reaches this point; no host sync)."""
         self.eng.zero_correct()
         for i in range(0, x.shape[0], self.eval_chunk):
             self.eng.eval_count(x[i:i + self.eval_chunk].contiguous(),
                                 labels[i:i + self.eval_chunk].contiguous())
-        return int(self.eng.buffer("correct", 1).item())
+        return self.eng.buffer("correct", 1)
+
+    @torch.no_grad()
+    def correct(self, x: torch.Tensor, labels: torch.Tensor) -> int:
+        return int(self.correct_async(x, labels).item())
 
     def accuracy(self, x: torch.Tensor, labels: torch.Tensor) -> float:
         return self.correct(x, labels) / x.shape[0]

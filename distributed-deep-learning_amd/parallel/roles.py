@@ -14,6 +14,7 @@ final accuracy and ``Time``.
 """
 from __future__ import annotations
 
+import contextlib
 import time
 from typing import Dict, List, Optional
 
@@ -168,30 +169,56 @@ class Trainer:
         wd = Watchdog(cfg.watchdog_s, name=f"rank{env.rank}", on_timeout=self._on_hang)
         t_target = None
         train_wall = 0.0
-        for epoch in range(cfg.epochs):
-            for cnt in range(self.steps):
-                t0 = time.perf_counter()
-                self.train_step(cnt)
-                wd.kick()
-                if cfg.eval_every and cnt % cfg.eval_every == 0:
-                    if env.device.type == "cuda":
-                        torch.cuda.synchronize()
-                    train_wall += time.perf_counter() - t0
-                    acc = self.evaluate()
-                    if not cfg.quiet:
-                        line = (metrics.single_progress(epoch, cnt, acc) if single else
-                                metrics.worker_progress(env.rank, epoch, cnt, acc))
-                        metrics.emit(line)
-                    self.log.log(event="eval", epoch=epoch, batch=cnt, acc=acc,
-                                 wall=clock.wall(), step=self.global_step)
-                    self.history.append({"step": self.global_step, "acc": acc, "wall": clock.wall()})
-                    if cfg.target_acc is not None and t_target is None and acc >= cfg.target_acc:
-                        t_target = clock.wall()
-                else:
-                    train_wall += time.perf_counter() - t0
-                if cfg.checkpoint_dir and cfg.checkpoint_every and \
-                        self.global_step % cfg.checkpoint_every == 0:
-                    ckpt.save(self, cfg.checkpoint_dir)
+
+        def on_eval(meta, acc, wall):
+            nonlocal t_target
+            if not cfg.quiet:
+                line = (metrics.single_progress(meta["epoch"], meta["cnt"], acc) if single else
+                        metrics.worker_progress(env.rank, meta["epoch"], meta["cnt"], acc))
+                metrics.emit(line)
+            self.log.log(event="eval", epoch=meta["epoch"], batch=meta["cnt"], acc=acc,
+                         wall=wall, step=meta["step"])
+            self.history.append({"step": meta["step"], "acc": acc, "wall": wall})
+            if cfg.target_acc is not None and t_target is None and acc >= cfg.target_acc:
+                t_target = wall
+
+        aeval = None
+        if cfg.eval_async and cfg.eval_every and getattr(self.engine, "name", "") == "hip":
+            from .async_eval import AsyncEvaluator
+            aeval = AsyncEvaluator(self, on_result=on_eval)
+            torch.cuda.synchronize()
+            clock = metrics.Clock()
+        # with the side-stream eval, training runs on the evaluator's high-priority stream
+        train_ctx = (torch.cuda.stream(aeval.train_stream) if aeval is not None
+                     else contextlib.nullcontext())
+        with train_ctx:
+            if aeval is not None:
+                aeval.start()
+            for epoch in range(cfg.epochs):
+                for cnt in range(self.steps):
+                    t0 = time.perf_counter()
+                    self.train_step(cnt)
+                    wd.kick()
+                    if aeval is not None:
+                        if cnt % cfg.eval_every == 0:
+                            aeval.submit({"epoch": epoch, "cnt": cnt, "step": self.global_step})
+                        aeval.poll()
+                        train_wall += time.perf_counter() - t0
+                    elif cfg.eval_every and cnt % cfg.eval_every == 0:
+                        if env.device.type == "cuda":
+                            torch.cuda.synchronize()
+                        train_wall += time.perf_counter() - t0
+                        acc = self.evaluate()
+                        on_eval({"epoch": epoch, "cnt": cnt, "step": self.global_step}, acc,
+                                clock.wall())
+                    else:
+                        train_wall += time.perf_counter() - t0
+                    if cfg.checkpoint_dir and cfg.checkpoint_every and \
+                            self.global_step % cfg.checkpoint_every == 0:
+                        ckpt.save(self, cfg.checkpoint_dir)
+        if aeval is not None:
+            torch.cuda.current_stream().wait_stream(aeval.train_stream)
+            aeval.drain()
         if isinstance(self.exchange, AsyncExchange):
             self.exchange.join()
             if cfg.check_provenance:

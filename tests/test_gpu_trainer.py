@@ -76,3 +76,20 @@ def test_single_role_on_gpu_prints_reference_lines(capsys, data):
     assert "epoch: 0 batch: 0 accuracy:" in out
     assert "epoch: 0 batch: 10 accuracy:" in out
     assert "final accuracy:" in out and "Time:" in out
+
+
+def test_async_eval_reports_the_same_accuracies(data):
+    """Periodic eval on the side stream from parameter snapshots (parallel/async_eval.py)
+    scores exactly the parameters after each eval step: same accuracy sequence as the in-line
+    eval, reported in order, with a time to target."""
+    hist = []
+    for eval_async in (False, True):
+        tr = _trainer(data, shard="flat", steps=30, eval_every=5, eval_async=eval_async,
+                      target_acc=0.0, lr=1e-3)
+        s = tr.train()
+        hist.append([(h["step"], h["acc"]) for h in tr.history])
+        assert s["time_to_target"] is not None and s["time_to_target"] > 0
+        walls = [h["wall"] for h in tr.history]
+        assert walls == sorted(walls)
+    assert len(hist[0]) == 6
+    assert hist[0] == hist[1]
