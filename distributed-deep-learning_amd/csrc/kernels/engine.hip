@@ -234,8 +234,7 @@ void Engine::backward_segment(int s, const float* x, const int64_t* labels, int 
     case 1: run_dual_inst<OP_CONV4_DGRAD, OP_CONV4_WGRAD>(*this, x, B, seed, st); break;
     case 2: run_dual_inst<OP_CONV3_DGRAD, OP_CONV3_WGRAD>(*this, x, B, seed, st); break;
     case 3:
-      run_dual_inst<OP_CONV2_DGRAD, OP_CONV2_WGRAD>(*this, x, B, seed, st);
-      run_op(OP_CONV1_WGRAD, x, B, seed, true, st, 0);
+      run_dual_then_inst<OP_CONV2_DGRAD, OP_CONV2_WGRAD, OP_CONV1_WGRAD>(*this, x, B, seed, st);
       break;
     default: break;
   }

@@ -10,5 +10,7 @@ void run_op_inst(Engine& e, const float* x, int B, const uint32_t* seed, bool tr
                  hipStream_t st, int si);
 template <int OA, int OB>
 void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st);
+template <int OA, int OB, int ON>
+void run_dual_then_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st);
 
 }  // namespace ddl

@@ -132,4 +132,36 @@ void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipSt
   }
 }
 
+// Dual launch OA + OB, then op ON with OB's wide split-K reduce fused into ON's launch (both
+// need only what the dual wrote; saves one dependent boundary: conv2 dual -> [conv2 wgrad
+// reduce | conv1 wgrad GEMM]).  Instantiated for the tuned configs (OA: 32x32, OB: 32x32
+// BK 16 pipelined, ON: 32x32 split-K); any other schedule takes the unfused sequence.
+template <int OA, int OB, int ON>
+void run_dual_then_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
+  if (!e.dual || e.cfg[OA] != 3 || e.cfg[OB] != 5 || e.cfg[ON] != 3 || e.workers[ON] > 0) {
+    run_dual_inst<OA, OB>(e, x, B, seed, st);
+    run_op_inst<ON>(e, x, B, seed, true, st, 0);
+    return;
+  }
+  const auto pa = make_policy<OA>(e, B, x, seed, true);
+  const auto pb = make_policy<OB>(e, B, x, seed, true);
+  const auto pn = make_policy<ON>(e, B, x, seed, true);
+  using PA = std::decay_t<decltype(pa)>;
+  using PB = std::decay_t<decltype(pb)>;
+  using PN = std::decay_t<decltype(pn)>;
+  using CA = TileCfg<TILE_3>;
+  using CB = TileCfg<TILE_5>;
+  using CN = TileCfg<TILE_3>;
+  SubGrid gb;
+  launch_gemm_dual<CA, PA, CB, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb,
+                                   e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st,
+                                   e.tail, &gb);
+  e.tail = UpdTail();
+  if (!launch_reduce_with_gemm<CB, PB, CN, PN>(pb, gb, pn, e.splits[ON], e.workers[ON],
+                                               e.wide[ON], e.scratch[0], st)) {
+    launch_reduce<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, st);
+    run_op_inst<ON>(e, x, B, seed, true, st, 0);
+  }
+}
+
 }  // namespace ddl

@@ -11,5 +11,7 @@ template void run_op_inst<OP_CONV1_WGRAD>(Engine&, const float*, int, const uint
                                   int);
 template void run_dual_inst<OP_CONV2_DGRAD, OP_CONV2_WGRAD>(Engine&, const float*, int, const uint32_t*,
                                                   hipStream_t);
+template void run_dual_then_inst<OP_CONV2_DGRAD, OP_CONV2_WGRAD, OP_CONV1_WGRAD>(
+    Engine&, const float*, int, const uint32_t*, hipStream_t);
 
 }  // namespace ddl

@@ -691,12 +691,12 @@ gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, UpdTail ut) {
     run_sub<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, b - ga.nblocks, lds, flag);
 }
 
-// Wide split-K reduce (mode 2): RL lanes cooperate on one float4 output element.
+// Wide split-K reduce (mode 2): RL lanes cooperate on one float4 output element; `gid` is the
+// global thread index (any block size that is a multiple of RL).
 template <int BM, int BN, int WM, int WN, int RL, class P>
-__global__ void __launch_bounds__(256)
-splitk_wide_reduce(P p, const float4* __restrict__ slab, int S, int gx, int ntiles) {
+DDL_DEV void wide_reduce_body(const P& p, const float4* __restrict__ slab, int S, int gx,
+                              int ntiles, int gid) {
   using G = TileGeo<BM, BN, WM, WN>;
-  const int gid = blockIdx.x * 256 + threadIdx.x;
   const int elem = gid / RL;
   const int sub = gid % RL;
   const int nelem = ntiles * G::PART4;
@@ -729,6 +729,35 @@ splitk_wide_reduce(P p, const float4* __restrict__ slab, int S, int gx, int ntil
   const int m0 = bx * BM + wm * G::WTM + i * 32 + 8 * g + 4 * (lane >> 5);
   const int n = by * BN + wn * G::WTN + j * 32 + (lane & 31);
   if (n < p.N && m0 < p.M) p.epi(m0, n, f32x4{s.x, s.y, s.z, s.w});
+}
+
+template <int BM, int BN, int WM, int WN, int RL, class P>
+__global__ void __launch_bounds__(256)
+splitk_wide_reduce(P p, const float4* __restrict__ slab, int S, int gx, int ntiles) {
+  wide_reduce_body<BM, BN, WM, WN, RL, P>(p, slab, S, gx, ntiles, blockIdx.x * 256 + threadIdx.x);
+}
+
+// The wide reduce of one mode-2 split-K problem (R, tile geometry RBM x RBN / RWM x RWN) and
+// an independent one-wave GEMM problem G in ONE launch: G's blocks, then nrb reduce blocks
+// (64 threads each).  Saves a dependent kernel boundary at the end of the
+// backward, where conv2's weight-gradient reduce and conv1's weight-gradient GEMM are
+// independent (both need only what conv2's dual launch wrote).
+template <int RBM, int RBN, int RWM, int RWN, int RL, class PR, class CG, class PG>
+__global__ void __launch_bounds__(64)
+reduce_gemm_kernel(PR pr, const float4* __restrict__ rslab, int S, int rgx, int rntiles, int nrb,
+                   PG pg, SubGrid gg) {
+  static_assert(CG::NT == 64, "one-wave GEMM blocks");
+  using TG = GemmTile<CG::BM, CG::BN, CG::BK, CG::WM, CG::WN, PG>;
+  __shared__ float4 lds4[TG::LDS_F4 + 1];
+  // GEMM blocks first (the longer pole: dispatched first), the reduce fills in behind them
+  const int b = blockIdx.x;
+  if (b >= gg.nblocks) {
+    wide_reduce_body<RBM, RBN, RWM, RWN, RL, PR>(pr, rslab, S, rgx, rntiles,
+                                                 (b - gg.nblocks) * 64 + threadIdx.x);
+    return;
+  }
+  run_sub<CG::BM, CG::BN, CG::BK, CG::WM, CG::WN, PG>(pg, gg, b, reinterpret_cast<float*>(lds4),
+                                                      reinterpret_cast<int*>(lds4 + TG::LDS_F4));
 }
 
 template <int BK>
@@ -843,12 +872,39 @@ inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch
   launch_reduce<BM, BN, BK, WM, WN, P>(p, g, stream);
 }
 
+// Launch R's pending wide reduce (SubGrid gr of a mode-2 split-K launch, tile config CR) fused
+// with GEMM problem G (config CG, its own schedule/scratch); G's own mode-2 reduce follows.
+// Returns false (nothing launched) when R has no pending wide reduce or G is stream-K.
+template <class CR, class PR, class CG, class PG>
+inline bool launch_reduce_with_gemm(const PR& pr, const SubGrid& gr, const PG& pg, int sg, int wg,
+                                    int wide_g, const SplitScratch& scg, hipStream_t stream) {
+  if (gr.streamk || gr.mode != 2 || gr.nblocks == 0) return false;
+  const SubGrid gg = plan_gemm<CG::BM, CG::BN, CG::BK>(pg, sg, wg, wide_g, scg);
+  if (gg.streamk || gg.nblocks == 0) return false;
+  using G = TileGeo<CR::BM, CR::BN, CR::WM, CR::WN>;
+  const int ntiles = gr.gx * gr.gy, z = gr.gz;
+  const size_t nelem = (size_t)ntiles * G::PART4;
+  const float4* s4 = gr.slab;
+#define DDL_RG(RL)                                                                            \
+  {                                                                                         \
+    const int nrb = (int)((nelem * RL + 63) / 64);                                          \
+    hipLaunchKernelGGL((reduce_gemm_kernel<CR::BM, CR::BN, CR::WM, CR::WN, RL, PR, CG, PG>),  \
+                       dim3(nrb + gg.nblocks), dim3(64), 0, stream, pr, s4, z, gr.gx, ntiles, nrb, \
+                       pg, gg);                                                             \
+  }
+  if (z > 32) DDL_RG(64) else if (z > 4) DDL_RG(16) else DDL_RG(4)
+#undef DDL_RG
+  launch_reduce<CG::BM, CG::BN, CG::BK, CG::WM, CG::WN, PG>(pg, gg, stream);
+  return true;
+}
+
 // Problems A and B (one-wave tile configs CA / CB) in one launch, each with its own schedule
 // and its own scratch (slab + tickets); mode-2 reduces follow on the same stream.
 template <class CA, class PA, class CB, class PB>
 inline void launch_gemm_dual(const PA& pa, int sa, int wa, const SplitScratch& sca, int wide_a,
                              const PB& pb, int sb, int wb, const SplitScratch& scb, int wide_b,
-                             hipStream_t stream, const UpdTail& ut = UpdTail()) {
+                             hipStream_t stream, const UpdTail& ut = UpdTail(),
+                             SubGrid* defer_b = nullptr) {
   const SubGrid ga = plan_gemm<CA::BM, CA::BN, CA::BK>(pa, sa, wa, wide_a, sca);
   const SubGrid gb = plan_gemm<CB::BM, CB::BN, CB::BK>(pb, sb, wb, wide_b, scb);
   const int n = ut.nblocks + ga.nblocks + gb.nblocks;
@@ -856,7 +912,8 @@ inline void launch_gemm_dual(const PA& pa, int sa, int wa, const SplitScratch& s
     hipLaunchKernelGGL((gemm_dual_kernel<CA, PA, CB, PB>), dim3(n), dim3(64), 0, stream, pa, ga,
                        pb, gb, ut);
   launch_reduce<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, stream);
-  launch_reduce<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, stream);
+  if (defer_b) *defer_b = gb;  // the caller launches B's reduce (launch_reduce_with_gemm)
+  else launch_reduce<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, stream);
 }
 
 }  // namespace ddl
