@@ -193,3 +193,22 @@ def test_run_sh_launches_two_workers():
                        timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "Worker0 final accuracy:" in r.stdout and "Worker1 final accuracy:" in r.stdout
+
+
+def test_eval_async_without_hip_engine_falls_back_to_inline_eval():
+    """--eval-async needs the HIP engine; on the CPU torch engine the reference in-line eval
+    runs and gives the same history."""
+    import torch
+    from ddl_amd.config import TrainConfig
+    from ddl_amd.parallel.comm import DistEnv
+    from ddl_amd.parallel.roles import Trainer
+    from ddl_amd.utils.data import synthetic_mnist
+    data = synthetic_mnist(n_train=400, n_test=200, seed=3)
+    hist = []
+    for ea in (False, True):
+        cfg = TrainConfig(mode="single", shard="none", steps=4, batch_size=50, eval_every=2,
+                          engine="torch", quiet=True, eval_async=ea)
+        tr = Trainer(cfg, DistEnv(device=torch.device("cpu")), dataset=data)
+        tr.train()
+        hist.append([(h["step"], h["acc"]) for h in tr.history])
+    assert len(hist[0]) == 2 and hist[0] == hist[1]
