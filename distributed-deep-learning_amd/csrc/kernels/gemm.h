@@ -39,6 +39,11 @@
 //     and runs the epilogue.
 #pragma once
 #include "common.h"
+
+// s_setprio 1 around each K tile's MFMA cluster in the basic main loop (A/B knob)
+#ifndef DDL_MFMA_PRIO
+#define DDL_MFMA_PRIO 1
+#endif
 #include "scratch.h"
 #include "tail.h"
 
@@ -414,6 +419,9 @@ struct GemmTile {
       if (kt + 1 < nk) sstore(SOLO ? 0 : (cur ^ 1));
       if (kt + 2 < nk) gload(kb + (kt + 2) * BK);
       __builtin_amdgcn_sched_barrier(0);
+#if DDL_MFMA_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -429,6 +437,9 @@ struct GemmTile {
                 acc[i][j] = mfma32x32x2(av[r][i][s], bv[r][j][s], acc[i][j]);
           }
         }
+#if DDL_MFMA_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (!SOLO) __syncthreads();
     }
