@@ -52,10 +52,10 @@ void Engine::init_streams() {
 void Engine::op_shape(int op, int B, int* M, int* N, int* K) {
   int m = 0, n = 0, k = 0;
   switch (op) {
-    case OP_CONV1_FWD: m = B * 14 * 14 * 4; n = 32; k = 25; break;
-    case OP_CONV2_FWD: m = B * 7 * 7 * 4; n = 64; k = 800; break;
-    case OP_CONV3_FWD: m = B * 4 * 4 * 4; n = 128; k = 1600; break;
-    case OP_CONV4_FWD: m = B * 2 * 2 * 4; n = 256; k = 3200; break;
+    case OP_CONV1_FWD: m = ConvFwd<28, 1, 32>::rows(B); n = 32; k = 25; break;
+    case OP_CONV2_FWD: m = ConvFwd<14, 32, 64>::rows(B); n = 64; k = 800; break;
+    case OP_CONV3_FWD: m = ConvFwd<7, 64, 128>::rows(B); n = 128; k = 1600; break;
+    case OP_CONV4_FWD: m = ConvFwd<4, 128, 256>::rows(B); n = 256; k = 3200; break;
     case OP_FC1_FWD: m = B; n = 1024; k = 1024; break;
     case OP_FC2_FWD: m = B; n = 512; k = 1024; break;
     case OP_FC2_DGRAD: m = B; n = 1024; k = 512; break;

@@ -22,18 +22,27 @@ struct LinInfo {   // linear operand: element offset of (row, k = 0 + kk), valid
 
 // ---------------------------------------------------------------------------------------------
 // conv 5x5 SAME + bias + ReLU + max-pool 2x2/2 SAME, forward (model.py:28-31 etc.)
-// M enumerates conv output positions pool-window-major: m = ((b*HP+py)*HP+px)*4 + q,
-// q = dy*2+dx, so a lane's 4 consecutive C rows are one pool window.  N = COUT,
-// K = 25*CIN (k = tap*CIN + ci, tap = ky*5+kx).  Positions outside an odd-sized map
-// (SAME pool 7->4) are -inf for the max.  Epilogue writes the pooled output and a 1-byte
-// code: argmax q, or 0xFF when the max is <= 0 (ReLU inactive => no gradient).
+// M enumerates conv output positions pool-window-major, in groups of 4 rows: a lane's 4
+// consecutive C rows are one 2x2 pool window (q = dy*2+dx), so the epilogue pools in registers.
+// Even maps (28, 14, 4): m = ((b*HP+py)*HP+px)*4 + q.  Odd maps (7, SAME pool 7->4) in
+// compact order: the (HP-1)^2 full windows, then the 2(HP-1) edge windows (2 valid positions
+// each, two windows per 4-row group), then the corner window (1 valid row of 4) — 52 rows
+// per image instead of 64 (the padded enumeration computed 15 rows of the 64 that pool away).
+// N = COUT, K = 25*CIN (k = tap*CIN + ci, tap = ky*5+kx).  Epilogue writes the pooled output
+// and a 1-byte code: argmax q, or 0xFF when the max is <= 0 (ReLU inactive => no gradient).
 // ---------------------------------------------------------------------------------------------
 template <int H, int CIN, int COUT>
 struct ConvFwd {
   static constexpr int HP = (H + 1) / 2;
+  static constexpr bool ODD = (H % 2) == 1;
+  static constexpr int FULLW = ODD ? (HP - 1) * (HP - 1) : HP * HP;  // full 2x2 windows
+  static constexpr int EDGEW = ODD ? HP - 1 : 0;                       // per edge
+  static constexpr int GROUPS = ODD ? FULLW + EDGEW + 1 : FULLW;       // 4-row groups per image
+  static constexpr int RP = 4 * GROUPS;                                // GEMM rows per image
   static constexpr bool A_KCONTIG = true;
   static constexpr bool B_KCONTIG = false;
   static_assert(CIN == 1 || CIN % kBK == 0, "tap must be tile-uniform");
+  static constexpr int rows(int batch) { return batch * RP; }
   int M, N, K;
   const float* __restrict__ x;     // [B,H,H,CIN]
   const float* __restrict__ w;     // [25*CIN, COUT]
@@ -49,19 +58,30 @@ struct ConvFwd {
   };
   using BInfo = LinInfo;
 
-  DDL_DEV uint32_t x_bytes() const { return (uint32_t)((M / (HP * HP * 4)) * H * H * CIN) * 4u; }
+  // position (y, x) of row r (0..3) of 4-row group g of an image; false = no position
+  static DDL_DEV bool group_row(int g, int r, int& y, int& x) {
+    if (!ODD || g < FULLW) {
+      const int w = ODD ? HP - 1 : HP;
+      y = 2 * (g / w) + (r >> 1);
+      x = 2 * (g % w) + (r & 1);
+      return true;
+    }
+    if (g < FULLW + EDGEW) {
+      const int e = 2 * (g - FULLW) + (r >> 1), j = r & 1;
+      if (e < EDGEW) { y = H - 1; x = 2 * e + j; }              // bottom edge window
+      else { y = 2 * (e - EDGEW) + j; x = H - 1; }               // right edge window
+      return true;
+    }
+    y = x = H - 1;  // corner window: row 0 only
+    return r == 0;
+  }
+
+  DDL_DEV uint32_t x_bytes() const { return (uint32_t)((M / RP) * H * H * CIN) * 4u; }
 
   DDL_DEV AInfo prepA(int m, int kk) const {
     AInfo a;
-    const int q = m & 3;
-    int t = m >> 2;
-    const int px = t % HP;
-    t /= HP;
-    const int py = t % HP;
-    const int b = t / HP;
-    a.y = 2 * py + (q >> 1);
-    a.x = 2 * px + (q & 1);
-    a.ok = m < M && a.y < H && a.x < H;
+    const int b = m / RP, rem = m - b * RP;
+    a.ok = group_row(rem >> 2, rem & 3, a.y, a.x) && m < M && a.y < H && a.x < H;
     a.base = b * H * H * CIN;
     a.kk = kk;
     return a;
@@ -95,24 +115,52 @@ struct ConvFwd {
     const bool good = b.ok && k0 + b.kk < K;
     return bload4(r, good ? (b.off + k0 * COUT) * 4 : kOOB);
   }
-  DDL_DEV void epi(int m0, int n, f32x4 v) const {
-    const int t = m0 >> 2;
-    const int px = t % HP;
-    const int py = (t / HP) % HP;
-    const float bb = bias[n];
+  // max-pool + bias + ReLU of the rows [lo, hi) of the group as one window whose rows have
+  // pool codes q(r); writes pooled output (py, px)
+  DDL_DEV void pool_out(int b, int py, int px, int n, float bb, const float* v, const int* qs,
+                        int cnt) const {
     float best = -INFINITY;
     int arg = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int y = 2 * py + (q >> 1), xx = 2 * px + (q & 1);
-      if (y < H && xx < H) {
-        const float val = v[q] + bb;
-        if (val > best) { best = val; arg = q; }
-      }
+    for (int i = 0; i < cnt; ++i) {
+      const float val = v[i] + bb;
+      if (val > best) { best = val; arg = qs[i]; }
     }
-    const size_t o = (size_t)t * COUT + n;
+    const size_t o = ((size_t)(b * HP + py) * HP + px) * COUT + n;
     out[o] = best > 0.f ? best : 0.f;
     if (code) code[o] = best > 0.f ? (uint8_t)arg : (uint8_t)0xFF;
+  }
+  DDL_DEV void epi(int m0, int n, f32x4 v) const {
+    const float bb = bias[n];
+    const int b = m0 / RP, g = (m0 - b * RP) >> 2;
+    const float vv[4] = {v[0], v[1], v[2], v[3]};
+    if (!ODD || g < FULLW) {
+      const int w = ODD ? HP - 1 : HP;
+      const int py = g / w, px = g % w;
+      float best = -INFINITY;
+      int arg = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int y = 2 * py + (q >> 1), xx = 2 * px + (q & 1);
+        if (y < H && xx < H) {
+          const float val = vv[q] + bb;
+          if (val > best) { best = val; arg = q; }
+        }
+      }
+      const size_t o = ((size_t)(b * HP + py) * HP + px) * COUT + n;
+      out[o] = best > 0.f ? best : 0.f;
+      if (code) code[o] = best > 0.f ? (uint8_t)arg : (uint8_t)0xFF;
+    } else if (g < FULLW + EDGEW) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int e = 2 * (g - FULLW) + h;
+        const bool bottom = e < EDGEW;
+        const int qs[2] = {0, bottom ? 1 : 2};  // (dy, dx) = (0, j) bottom, (j, 0) right
+        pool_out(b, bottom ? HP - 1 : e - EDGEW, bottom ? e : HP - 1, n, bb, vv + 2 * h, qs, 2);
+      }
+    } else {
+      const int qs[1] = {0};
+      pool_out(b, HP - 1, HP - 1, n, bb, vv, qs, 1);
+    }
   }
 };
 
