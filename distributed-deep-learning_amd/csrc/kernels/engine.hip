@@ -30,9 +30,11 @@ Engine::Engine() {
   static const bool inl[OP_COUNT] = {0, 1, 1, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0};
   memcpy(cfg, defc, sizeof(defc));
   memcpy(eval_cfg, defc, sizeof(defc));
-  // eval forward at 10k-row chunks (scripts/eval_sweep.py): conv3 on 4-wave 64x64 blocks,
-  // full test-set eval 7.25 -> 7.16 ms (the others measured best on 32x32 one-wave blocks)
+  // eval forward at 10k-row chunks (scripts/eval_sweep.py, after the compact conv3 rows):
+  // conv2-4 on 4-wave 64x64 blocks, full test-set eval 6.76 -> 6.66 ms (106 TF)
+  eval_cfg[OP_CONV2_FWD] = 6;
   eval_cfg[OP_CONV3_FWD] = 6;
+  eval_cfg[OP_CONV4_FWD] = 6;
   memcpy(splits, defs, sizeof(defs));
   memcpy(workers, defw, sizeof(defw));
   for (int op = 0; op < OP_COUNT; ++op) wide[op] = inl[op] ? (1 << 20) : 1;
