@@ -22,9 +22,11 @@ Engine::Engine() {
   // (scripts/step_tune.py over the scripts/op_bench.py per-op sweep) on one MI355X, batch 100,
   // single-stream backward with dual dgrad+wgrad launches: fwd+bwd 367 us (was 449 us)
   static const int defc[OP_COUNT] = {3, 3, 3, 3, 3, 3, 3, 5, 3, 5, 3, 3, 3, 3, 3, 5, 3};
-  // (conv3 forward re-tuned after the compact 52-row enumeration: split 4 + in-launch reduce,
-  // 372.4 -> 369.5 us/step in scripts/sched_ab.py, vs stream-K 3072 workers before)
-  static const int defs[OP_COUNT] = {1, 2, 4, 8, 8, 16, 4, 1, 4, 1, 1, 8, 8, 16, 4, 32, 1024};
+  // (re-tuned in the real step with scripts/sched_ab.py after the compact 52-row conv3
+  // enumeration and the wgrad row decode: conv3 forward split 4 + in-launch reduce instead of
+  // stream-K 3072 workers, 372.4 -> 369.5 us; conv4 weight gradient split 4 instead of 8,
+  // 370.5 -> 368.0 us)
+  static const int defs[OP_COUNT] = {1, 2, 4, 8, 8, 16, 4, 1, 4, 1, 1, 4, 8, 16, 4, 32, 1024};
   static const int defw[OP_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2048, 0, 0, 0, 0, 0, 0};
   // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
   static const bool inl[OP_COUNT] = {0, 1, 1, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0};
