@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""Coordinate-descent schedule tune on the REAL training step (native runner, W = 1: dual
+launches, optimizer tail, fused end-of-backward launch) — unlike step_tune.py, which times the
+Python engine path.  Per op, candidates around the current schedule (split x0.5 / x2, in-launch
+vs separate reduce, stream-K worker counts, tile config 3 / 5); a candidate is kept only if it
+beats the incumbent by > --gain in a re-measured head-to-head.
+
+usage: python scripts/runner_tune.py [--passes 2] [--steps 250] [--json out.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from op_bench import OPS  # noqa: E402
+
+STREAMK_OK = {1, 2, 3, 10, 11, 12, 13, 14}  # conv GEMMs (big enough for stream-K)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--passes", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=250)
+    ap.add_argument("--gain", type=float, default=0.004)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    import torch
+    from ddl_amd.config import TrainConfig
+    from ddl_amd.parallel.comm import DistEnv
+    from ddl_amd.parallel.roles import Trainer
+    from ddl_amd.utils.data import synthetic_mnist
+
+    env = DistEnv(0, 1, 0, torch.device("cuda", 0))
+    cfg = TrainConfig(mode="sync", shard="flat", steps=10 ** 7, batch_size=100, eval_every=0,
+                      engine="hip", quiet=True, data_sharding="stride")
+    tr = Trainer(cfg, env, dataset=synthetic_mnist())
+    e = tr.engine.eng
+    W = 1 << 20
+    cur = {"cfg": e.get_cfg(), "splits": e.get_splits(), "workers": e.get_workers(),
+           "wide": e.get_wide()}
+    step = [0]
+
+    def apply(s):
+        e.set_cfg(s["cfg"])
+        e.set_splits(s["splits"])
+        e.set_workers(s["workers"])
+        e.set_wide(s["wide"])
+
+    def timed(s):
+        apply(s)
+        for _ in range(20):
+            tr.train_step(step[0])
+            step[0] += 1
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            tr.train_step(step[0])
+            step[0] += 1
+        torch.cuda.synchronize()
+        return 1e6 * (time.perf_counter() - t0) / a.steps
+
+    def cands(op):
+        c, s, w, wd = cur["cfg"][op], cur["splits"][op], cur["workers"][op], cur["wide"][op]
+        out = []
+
+        def mk(c2, s2, w2, wd2):
+            d = {k: list(v) for k, v in cur.items()}
+            d["cfg"][op], d["splits"][op], d["workers"][op], d["wide"][op] = c2, s2, w2, wd2
+            return d
+        for s2 in {max(1, s // 2), min(2048, s * 2)} - {s}:
+            out.append(mk(c, s2, 0, wd))
+        out.append(mk(c, s, w, 1 if wd > 1 else W))            # toggle the reduce mode
+        if op in STREAMK_OK:
+            for w2 in (1024, 2048, 3072):
+                if w2 != w:
+                    out.append(mk(c, 1, w2, wd))
+            if w:
+                out.append(mk(c, s if s > 1 else 4, 0, wd))
+        for c2 in (3, 5):
+            if c2 != c:
+                out.append(mk(c2, s, w, wd))
+        return out
+
+    base = timed(cur)
+    print(f"start {base:.1f} us/step", flush=True)
+    for p in range(a.passes):
+        for op, name in enumerate(OPS):
+            best, best_t = None, None
+            for cand in cands(op):
+                t = timed(cand)
+                if best_t is None or t < best_t:
+                    best, best_t = cand, t
+            # head-to-head re-measure of the incumbent vs the best candidate
+            t_inc = min(timed(cur), timed(cur))
+            t_new = min(timed(best), timed(best))
+            if t_new < t_inc * (1 - a.gain):
+                cur = best
+                print(f"pass {p} {name:12s} -> c{cur['cfg'][op]} s{cur['splits'][op]} "
+                      f"w{cur['workers'][op]} {'inl' if cur['wide'][op] > 1 else 'wide'}  "
+                      f"{t_inc:.1f} -> {t_new:.1f} us", flush=True)
+            else:
+                print(f"pass {p} {name:12s} keep ({t_inc:.1f} vs best cand {t_new:.1f})", flush=True)
+    final = min(timed(cur), timed(cur))
+    print(f"final {final:.1f} us/step (start {base:.1f})")
+    print("DEFAULT_CFG", ",".join(map(str, cur["cfg"])))
+    print("DEFAULT_SPLITS", ",".join(map(str, cur["splits"])))
+    print("DEFAULT_WORKERS", ",".join(map(str, cur["workers"])))
+    print("DEFAULT_INL", ",".join("1" if w > 1 else "0" for w in cur["wide"]))
+    if a.json:
+        json.dump(dict(cur, step_us=final, start_us=base), open(a.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
