@@ -27,6 +27,13 @@ void launch_scale(float* p, int64_t n, float a, hipStream_t st);
 // ---- classifier head (head.hip) --------------------------------------------------------------
 void launch_head_fwd(const float* h2, const float* w, const float* bias, const int64_t* labels,
                      int B, float* dlog, float* loss, int* correct, hipStream_t st);
+// fused head: logits, loss, dlogits and dh2 (with fc2's dropout backward) per sample; fc3's
+// weight gradient is left to launch_head_wgrad or the next dual launch (head.h)
+void launch_head_fused(const float* h2, const float* w, const float* bias, const int64_t* labels,
+                       int B, const uint32_t* seed, uint32_t seed_v, uint32_t thr24,
+                       float inv_keep, float* dlog, float* loss, float* dpre2, hipStream_t st);
+void launch_head_wgrad(const float* h2, const float* dlog, int B, float* gw, float* gb,
+                       hipStream_t st);
 void launch_head_bwd(const float* h2, const float* w, const float* dlog, int B,
                      const uint32_t* seed, uint32_t seed_v, uint32_t thr24, float inv_keep,
                      float* gw, float* gb, float* dpre2, hipStream_t st);
@@ -91,6 +98,8 @@ struct Engine {
   // optimizer tail (tail.h) for the next dual launch; consumed (and cleared) by it, or by
   // flush_tail() as a launch of its own when no dual launch takes it
   UpdTail tail;
+  // fc3 weight gradient still to compute (fused head kernel ran): taken by the fc2 dual launch
+  int head_wgrad_pending = 0;
 
   Engine();
   ~Engine();
@@ -114,6 +123,7 @@ struct Engine {
               int si = 0);
   // launch a pending optimizer tail on its own (no-op when none is pending)
   void flush_tail(hipStream_t st);
+  void flush_head_wgrad(int B, hipStream_t st);
 
  private:
   void fork(hipStream_t st);

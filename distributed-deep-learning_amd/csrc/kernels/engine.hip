@@ -175,6 +175,12 @@ void Engine::flush_tail(hipStream_t st) {
   tail = UpdTail();
 }
 
+void Engine::flush_head_wgrad(int B, hipStream_t st) {
+  if (!head_wgrad_pending) return;
+  launch_head_wgrad(h2, dlog, B, G[12], G[13], st);
+  head_wgrad_pending = 0;
+}
+
 void Engine::forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st) {
   for (int op = OP_CONV1_FWD; op <= OP_FC2_FWD; ++op) run_op(op, x, B, seed, train, st, 0);
 }
@@ -231,10 +237,12 @@ void Engine::backward_segment(int s, const float* x, const int64_t* labels, int 
   // single stream: each layer's dgrad + wgrad as one dual launch
   switch (s) {
     case 0:
-      launch_head_fwd(h2, P[12], P[13], labels, B, dlog, loss, nullptr, st);
-      launch_head_bwd(h2, P[12], dlog, B, seed, seed_value, thr24, inv_keep, G[12], G[13],
-                        dpre2fc, st);
+      // one head launch (per-sample fwd + dlogits + dh2); fc3's dW/db ride in the fc2 dual
+      launch_head_fused(h2, P[12], P[13], labels, B, seed, seed_value, thr24, inv_keep, dlog,
+                        loss, dpre2fc, st);
+      head_wgrad_pending = 1;
       run_dual_inst<OP_FC2_DGRAD, OP_FC2_WGRAD>(*this, x, B, seed, st);
+      flush_head_wgrad(B, st);
       run_dual_inst<OP_FC1_DGRAD, OP_FC1_WGRAD>(*this, x, B, seed, st);
       break;
     case 1: run_dual_inst<OP_CONV4_DGRAD, OP_CONV4_WGRAD>(*this, x, B, seed, st); break;

@@ -8,6 +8,7 @@
 
 #include "api.h"
 #include "layers.h"
+#include "head.h"
 #include "engine_decl.h"
 
 namespace ddl {
@@ -95,20 +96,46 @@ void run_op_inst(Engine& e, const float* x, int B, const uint32_t* seed, bool tr
 // dual launches are instantiated for these one-wave configs (others run back to back)
 inline bool one_wave_cfg(int c) { return c == 0 || c == 3 || c == 4 || c == 5; }
 
+// fc3's weight gradient as aux blocks (head.h), pending after the fused head kernel
+inline HeadWgradAux head_aux(Engine& e, int B) {
+  HeadWgradAux a;
+  if (e.head_wgrad_pending) {
+    a.h2 = e.h2;
+    a.dlog = e.dlog;
+    a.B = B;
+    a.gw = e.G[12];
+    a.gb = e.G[13];
+    a.nblk = HK + 1;
+  }
+  e.head_wgrad_pending = 0;
+  return a;
+}
+
 template <class CA, int OA, int OB, class PA, class PB>
-inline void dual_b(Engine& e, const PA& pa, const PB& pb, hipStream_t st) {
-#define DDL_DUAL_B(CB) \
+inline void dual_b(Engine& e, const PA& pa, const PB& pb, int B, hipStream_t st) {
+#define DDL_DUAL_B(CB, AUXV) \
   launch_gemm_dual<CA, PA, TileCfg<CB>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], \
                                             e.wide[OA], pb, e.splits[OB], e.workers[OB], \
-                                            e.scratch[1], e.wide[OB], st, e.tail)
-  switch (e.cfg[OB]) {
-    case 0: DDL_DUAL_B(TILE_0); break;
-    case 3: DDL_DUAL_B(TILE_3); break;
-    case 4: DDL_DUAL_B(TILE_4); break;
-    default: DDL_DUAL_B(TILE_5); break;
+                                            e.scratch[1], e.wide[OB], st, AUXV)
+  // the fc2 dual carries fc3's weight gradient; the others a pending optimizer tail
+#define DDL_DUAL_SW(AUXV)                      \
+  switch (e.cfg[OB]) {                         \
+    case 0: DDL_DUAL_B(TILE_0, AUXV); break;   \
+    case 3: DDL_DUAL_B(TILE_3, AUXV); break;   \
+    case 4: DDL_DUAL_B(TILE_4, AUXV); break;   \
+    default: DDL_DUAL_B(TILE_5, AUXV); break;  \
   }
+  if constexpr (OA == OP_FC2_DGRAD) {
+    e.flush_tail(st);
+    const HeadWgradAux aux = head_aux(e, B);
+    DDL_DUAL_SW(aux)
+  } else {
+    const TailAux aux(e.tail);
+    DDL_DUAL_SW(aux)
+    e.tail = UpdTail();
+  }
+#undef DDL_DUAL_SW
 #undef DDL_DUAL_B
-  e.tail = UpdTail();
 }
 
 // Ops OA and OB (independent) in one launch if both use one-wave tiles, else back to back.
@@ -116,6 +143,7 @@ template <int OA, int OB>
 void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
   if (!e.dual || !one_wave_cfg(e.cfg[OA]) || !one_wave_cfg(e.cfg[OB])) {
     e.flush_tail(st);
+    if constexpr (OA == OP_FC2_DGRAD) e.flush_head_wgrad(B, st);
     run_op_inst<OA>(e, x, B, seed, true, st, 0);
     run_op_inst<OB>(e, x, B, seed, true, st, 0);
     return;
@@ -125,10 +153,10 @@ void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipSt
   using PA = std::decay_t<decltype(pa)>;
   using PB = std::decay_t<decltype(pb)>;
   switch (e.cfg[OA]) {
-    case 0: dual_b<TileCfg<TILE_0>, OA, OB, PA, PB>(e, pa, pb, st); break;
-    case 3: dual_b<TileCfg<TILE_3>, OA, OB, PA, PB>(e, pa, pb, st); break;
-    case 4: dual_b<TileCfg<TILE_4>, OA, OB, PA, PB>(e, pa, pb, st); break;
-    default: dual_b<TileCfg<TILE_5>, OA, OB, PA, PB>(e, pa, pb, st); break;
+    case 0: dual_b<TileCfg<TILE_0>, OA, OB, PA, PB>(e, pa, pb, B, st); break;
+    case 3: dual_b<TileCfg<TILE_3>, OA, OB, PA, PB>(e, pa, pb, B, st); break;
+    case 4: dual_b<TileCfg<TILE_4>, OA, OB, PA, PB>(e, pa, pb, B, st); break;
+    default: dual_b<TileCfg<TILE_5>, OA, OB, PA, PB>(e, pa, pb, B, st); break;
   }
 }
 
@@ -155,7 +183,7 @@ void run_dual_then_inst(Engine& e, const float* x, int B, const uint32_t* seed, 
   SubGrid gb;
   launch_gemm_dual<CA, PA, CB, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb,
                                    e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st,
-                                   e.tail, &gb);
+                                   TailAux(e.tail), &gb);
   e.tail = UpdTail();
   if (!launch_reduce_with_gemm<CB, PB, CN, PN>(pb, gb, pn, e.splits[ON], e.workers[ON],
                                                e.wide[ON], e.scratch[0], st)) {

@@ -668,15 +668,27 @@ struct TileCfg {
   static constexpr int NT = WM * WN * 64;
 };
 
+// Auxiliary work riding in a dual launch: `nblk` extra one-wave blocks before (first_) or after
+// the GEMM blocks, each running aux.run(block index).  The optimizer tail (tail.h) is one;
+// head.h's fc3 weight gradient another.
+struct TailAux {
+  UpdTail t;
+  int nblk = 0;
+  int first_ = 0;
+  TailAux() = default;
+  explicit TailAux(const UpdTail& u) : t(u), nblk(u.nblocks), first_(u.first) {}
+  DDL_DEV void run(int b) const { tail_body(t, b); }
+};
+
 // Two independent GEMM problems in one launch: blocks [0, ga.nblocks) run problem A, the
 // rest problem B.  Both must use one-wave blocks.  An optional optimizer tail (tail.h) takes
 // ut.nblocks more blocks, after the GEMM blocks (ut.first = 0, measured faster: the update
 // fills CUs as GEMM blocks retire) or before them (a multiple of 8 so the GEMMs' XCD-major
 // numbering holds).  The tail path must stay under the GEMM paths' VGPR count: at 8 float4
 // per lane it raised the conv4 dual from 113 to 149 VGPRs (3 -> 2 waves/SIMD, +9 us).
-template <class CA, class PA, class CB, class PB>
+template <class CA, class PA, class CB, class PB, class AUX>
 __global__ void __launch_bounds__(64)
-gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, UpdTail ut) {
+gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut) {
   static_assert(CA::NT == 64 && CB::NT == 64, "dual launch needs one-wave blocks");
   using TA = GemmTile<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>;
   using TB = GemmTile<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>;
@@ -686,14 +698,14 @@ gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, UpdTail ut) {
   int* flag = reinterpret_cast<int*>(lds4 + L);
   const int gemm_blocks = ga.nblocks + gb.nblocks;
   int b = blockIdx.x;
-  if (ut.first) {
-    if (b < ut.nblocks) {
-      tail_body(ut, b);
+  if (ut.first_) {
+    if (b < ut.nblk) {
+      ut.run(b);
       return;
     }
-    b -= ut.nblocks;
+    b -= ut.nblk;
   } else if (b >= gemm_blocks) {
-    tail_body(ut, b - gemm_blocks);
+    ut.run(b - gemm_blocks);
     return;
   }
   if (b < ga.nblocks)
@@ -911,17 +923,17 @@ inline bool launch_reduce_with_gemm(const PR& pr, const SubGrid& gr, const PG& p
 
 // Problems A and B (one-wave tile configs CA / CB) in one launch, each with its own schedule
 // and its own scratch (slab + tickets); mode-2 reduces follow on the same stream.
-template <class CA, class PA, class CB, class PB>
+template <class CA, class PA, class CB, class PB, class AUX = TailAux>
 inline void launch_gemm_dual(const PA& pa, int sa, int wa, const SplitScratch& sca, int wide_a,
                              const PB& pb, int sb, int wb, const SplitScratch& scb, int wide_b,
-                             hipStream_t stream, const UpdTail& ut = UpdTail(),
+                             hipStream_t stream, const AUX& ut = AUX(),
                              SubGrid* defer_b = nullptr) {
   const SubGrid ga = plan_gemm<CA::BM, CA::BN, CA::BK>(pa, sa, wa, wide_a, sca);
   const SubGrid gb = plan_gemm<CB::BM, CB::BN, CB::BK>(pb, sb, wb, wide_b, scb);
-  const int n = ut.nblocks + ga.nblocks + gb.nblocks;
+  const int n = ut.nblk + ga.nblocks + gb.nblocks;
   if (n > 0)
-    hipLaunchKernelGGL((gemm_dual_kernel<CA, PA, CB, PB>), dim3(n), dim3(64), 0, stream, pa, ga,
-                       pb, gb, ut);
+    hipLaunchKernelGGL((gemm_dual_kernel<CA, PA, CB, PB, AUX>), dim3(n), dim3(64), 0, stream, pa,
+                       ga, pb, gb, ut);
   launch_reduce<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, stream);
   if (defer_b) *defer_b = gb;  // the caller launches B's reduce (launch_reduce_with_gemm)
   else launch_reduce<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, stream);

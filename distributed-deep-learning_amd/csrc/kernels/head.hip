@@ -6,13 +6,13 @@
 //              or in eval mode the correct-prediction count (F22).
 //   head_bwd : dW3_aug[513,10] = [h2;1]^T dlogits and dh2 = dlogits W3^T, with the fc2
 //              dropout backward fused (mask regenerated from the seed, nothing stored).
+//   head_fused: head_fwd + the dh2 part of head_bwd per sample (one launch in training; the
+//              fc3 weight gradient then rides in the next dual launch, head.h HeadWgradAux).
 #include "common.h"
 #include "api.h"
+#include "head.h"
 
 namespace ddl {
-
-constexpr int HK = 512;  // fc3 input width
-constexpr int HC = 10;   // classes
 
 __global__ void __launch_bounds__(256)
 head_fwd_kernel(const float* __restrict__ h2, const float* __restrict__ w,
@@ -74,35 +74,8 @@ head_bwd_kernel(const float* __restrict__ h2, const float* __restrict__ w,
                 uint32_t thr24, float inv_keep, float* __restrict__ gw, float* __restrict__ gb,
                 float* __restrict__ dpre2) {
   if ((int)blockIdx.x < wblocks) {
-    // dW_aug row i (i == HK: bias row of ones): one wave per row, lanes stride the batch,
-    // 10 class partials reduced across the wave.
-    const int lane = threadIdx.x & 63;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (i > HK) return;
-    float acc[HC];
-#pragma unroll
-    for (int c = 0; c < HC; ++c) acc[c] = 0.f;
-    for (int b = lane; b < B; b += 64) {
-      const float hv = i < HK ? h2[(size_t)b * HK + i] : 1.f;
-      const float* dl = dlog + (size_t)b * HC;
-#pragma unroll
-      for (int c = 0; c < HC; ++c) acc[c] = fmaf(hv, dl[c], acc[c]);
-    }
-#pragma unroll
-    for (int c = 0; c < HC; ++c) {
-      float v = acc[c];
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-      acc[c] = v;
-    }
-    if (lane < HC) {
-      float v = 0.f;
-#pragma unroll
-      for (int c = 0; c < HC; ++c)
-        if (c == lane) v = acc[c];
-      if (i < HK) gw[i * HC + lane] = v;
-      else gb[lane] = v;
-    }
+    if (i <= HK) head_wgrad_row(h2, dlog, B, i, gw, gb);
     return;
   }
   const int idx = (blockIdx.x - wblocks) * 256 + threadIdx.x;
@@ -116,6 +89,84 @@ head_bwd_kernel(const float* __restrict__ h2, const float* __restrict__ w,
     g = ddl_keep(key, (uint32_t)idx, thr24) ? g * inv_keep : 0.f;
   }
   dpre2[idx] = g;
+}
+
+__global__ void __launch_bounds__(256)
+head_fused_kernel(const float* __restrict__ h2, const float* __restrict__ w,
+                  const float* __restrict__ bias, const int64_t* __restrict__ labels, int B,
+                  float inv_batch, const uint32_t* __restrict__ seed, uint32_t seed_v,
+                  uint32_t thr24, float inv_keep, float* __restrict__ dlog,
+                  float* __restrict__ loss, float* __restrict__ dpre2) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  float acc[HC];
+#pragma unroll
+  for (int c = 0; c < HC; ++c) acc[c] = 0.f;
+  const float* hr = h2 + (size_t)row * HK;
+#pragma unroll 4
+  for (int k = lane; k < HK; k += 64) {
+    const float hv = hr[k];
+    const float* wr = w + k * HC;
+#pragma unroll
+    for (int c = 0; c < HC; ++c) acc[c] = fmaf(hv, wr[c], acc[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < HC; ++c) {
+    float v = acc[c];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    acc[c] = v + bias[c];
+  }
+  float mx = acc[0];
+#pragma unroll
+  for (int c = 1; c < HC; ++c) mx = acc[c] > mx ? acc[c] : mx;
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < HC; ++c) se += __expf(acc[c] - mx);
+  const int lab = (int)labels[row];
+  // dlogits of this sample in every lane (same arithmetic as head_fwd_kernel's per-lane form)
+  float dl[HC];
+#pragma unroll
+  for (int c = 0; c < HC; ++c) dl[c] = (__expf(acc[c] - mx) / se - (c == lab ? 1.f : 0.f)) * inv_batch;
+  if (lane == 0) {
+    float ll = 0.f;
+#pragma unroll
+    for (int c = 0; c < HC; ++c)
+      if (c == lab) ll = acc[c];
+    loss[row] = (mx + __logf(se)) - ll;
+  }
+  if (lane < HC) {
+    float v = 0.f;
+#pragma unroll
+    for (int c = 0; c < HC; ++c)
+      if (c == lane) v = dl[c];
+    dlog[(size_t)row * HC + lane] = v;
+  }
+  // dh2 = dlogits W3^T with fc2's dropout backward (mask regenerated from the seed)
+  const uint32_t key = thr24 ? ddl_mix32((seed ? *seed : seed_v) + 2u * 0x9E3779B9u) : 0u;
+  for (int i = lane; i < HK; i += 64) {
+    float g = 0.f;
+#pragma unroll
+    for (int c = 0; c < HC; ++c) g = fmaf(dl[c], w[i * HC + c], g);
+    const int idx = row * HK + i;
+    if (thr24) g = ddl_keep(key, (uint32_t)idx, thr24) ? g * inv_keep : 0.f;
+    dpre2[idx] = g;
+  }
+}
+
+void launch_head_fused(const float* h2, const float* w, const float* bias, const int64_t* labels,
+                       int B, const uint32_t* seed, uint32_t seed_v, uint32_t thr24,
+                       float inv_keep, float* dlog, float* loss, float* dpre2, hipStream_t st) {
+  hipLaunchKernelGGL(head_fused_kernel, dim3((B + 3) / 4), dim3(256), 0, st, h2, w, bias, labels,
+                     B, 1.f / (float)B, seed, seed_v, thr24, inv_keep, dlog, loss, dpre2);
+}
+
+void launch_head_wgrad(const float* h2, const float* dlog, int B, float* gw, float* gb,
+                       hipStream_t st) {
+  const int wblocks = (HK + 1 + 3) / 4;
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(wblocks), dim3(256), 0, st, h2, nullptr, dlog, B,
+                     wblocks, nullptr, 0u, 0u, 1.f, gw, gb, nullptr);
 }
 
 void launch_head_fwd(const float* h2, const float* w, const float* bias, const int64_t* labels,
