@@ -82,6 +82,11 @@ struct Engine {
   // gains; dgrad/wgrad concurrency comes from fused dual-problem launches instead.
   bool concurrent = false;
   bool dual = true;          // single stream: dgrad + wgrad of a layer in one launch
+  // bit op: that dual launch dispatches its second problem first.  conv2's (weight gradient
+  // split 32 ways, the longer pole) measured 0.3663 -> 0.3650 ms/step; conv4's / conv3's worse
+  // (their data gradients are the longer poles; conv4's stream-K loses its XCD-major numbering).
+  // DDL_DUAL_BFIRST overrides (scripts/ab_env.sh).
+  int dual_bfirst = 1 << OP_CONV2_DGRAD;
 
   // workspace carve-out
   float *p1 = nullptr, *p2 = nullptr, *p3 = nullptr, *p4 = nullptr, *h1 = nullptr, *h2 = nullptr;

@@ -7,6 +7,7 @@
 // next segment computes (SURVEY.md §5.8 bucket plan); inside a segment the weight-gradient
 // GEMM runs on a second stream concurrently with the data-gradient GEMM that feeds the
 // next segment (fork/join events, captured as parallel graph branches).
+#include <stdlib.h>
 #include <string.h>
 
 #include <type_traits>
@@ -30,6 +31,7 @@ Engine::Engine() {
   static const int defw[OP_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2048, 0, 0, 0, 0, 0, 0};
   // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
   static const bool inl[OP_COUNT] = {0, 1, 1, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0};
+  if (const char* s = getenv("DDL_DUAL_BFIRST")) dual_bfirst = (int)strtol(s, nullptr, 0);
   memcpy(cfg, defc, sizeof(defc));
   memcpy(eval_cfg, defc, sizeof(defc));
   // eval forward at 10k-row chunks (scripts/eval_sweep.py, after the compact conv3 rows):

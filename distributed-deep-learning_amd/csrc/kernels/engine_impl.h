@@ -116,7 +116,8 @@ inline void dual_b(Engine& e, const PA& pa, const PB& pb, int B, hipStream_t st)
 #define DDL_DUAL_B(CB, AUXV) \
   launch_gemm_dual<CA, PA, TileCfg<CB>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], \
                                             e.wide[OA], pb, e.splits[OB], e.workers[OB], \
-                                            e.scratch[1], e.wide[OB], st, AUXV)
+                                            e.scratch[1], e.wide[OB], st, AUXV, nullptr, \
+                                            (e.dual_bfirst >> OA) & 1)
   // the fc2 dual carries fc3's weight gradient; the others a pending optimizer tail
 #define DDL_DUAL_SW(AUXV)                      \
   switch (e.cfg[OB]) {                         \
@@ -183,7 +184,7 @@ void run_dual_then_inst(Engine& e, const float* x, int B, const uint32_t* seed, 
   SubGrid gb;
   launch_gemm_dual<CA, PA, CB, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb,
                                    e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st,
-                                   TailAux(e.tail), &gb);
+                                   TailAux(e.tail), &gb, (e.dual_bfirst >> OA) & 1);
   e.tail = UpdTail();
   if (!launch_reduce_with_gemm<CB, PB, CN, PN>(pb, gb, pn, e.splits[ON], e.workers[ON],
                                                e.wide[ON], e.scratch[0], st)) {

@@ -688,7 +688,7 @@ struct TailAux {
 // per lane it raised the conv4 dual from 113 to 149 VGPRs (3 -> 2 waves/SIMD, +9 us).
 template <class CA, class PA, class CB, class PB, class AUX>
 __global__ void __launch_bounds__(64)
-gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut) {
+gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut, int bfirst) {
   static_assert(CA::NT == 64 && CB::NT == 64, "dual launch needs one-wave blocks");
   using TA = GemmTile<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>;
   using TB = GemmTile<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>;
@@ -708,10 +708,15 @@ gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut) {
     ut.run(b - gemm_blocks);
     return;
   }
-  if (b < ga.nblocks)
-    run_sub<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, b, lds, flag);
+  // bfirst: problem B's blocks are dispatched first (longest-first ordering shortens the
+  // launch's tail when B's blocks run longer)
+  const bool is_a = bfirst ? (b >= gb.nblocks) : (b < ga.nblocks);
+  if (is_a)
+    run_sub<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, bfirst ? b - gb.nblocks : b, lds,
+                                                        flag);
   else
-    run_sub<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, b - ga.nblocks, lds, flag);
+    run_sub<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, bfirst ? b : b - ga.nblocks, lds,
+                                                        flag);
 }
 
 // Wide split-K reduce (mode 2): RL lanes cooperate on one float4 output element; `gid` is the
@@ -927,13 +932,13 @@ template <class CA, class PA, class CB, class PB, class AUX = TailAux>
 inline void launch_gemm_dual(const PA& pa, int sa, int wa, const SplitScratch& sca, int wide_a,
                              const PB& pb, int sb, int wb, const SplitScratch& scb, int wide_b,
                              hipStream_t stream, const AUX& ut = AUX(),
-                             SubGrid* defer_b = nullptr) {
+                             SubGrid* defer_b = nullptr, int bfirst = 0) {
   const SubGrid ga = plan_gemm<CA::BM, CA::BN, CA::BK>(pa, sa, wa, wide_a, sca);
   const SubGrid gb = plan_gemm<CB::BM, CB::BN, CB::BK>(pb, sb, wb, wide_b, scb);
   const int n = ut.nblk + ga.nblocks + gb.nblocks;
   if (n > 0)
     hipLaunchKernelGGL((gemm_dual_kernel<CA, PA, CB, PB, AUX>), dim3(n), dim3(64), 0, stream, pa,
-                       ga, pb, gb, ut);
+                       ga, pb, gb, ut, bfirst);
   launch_reduce<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, stream);
   if (defer_b) *defer_b = gb;  // the caller launches B's reduce (launch_reduce_with_gemm)
   else launch_reduce<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, stream);
