@@ -53,6 +53,10 @@ def main(argv=None):
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-native-exchange", action="store_true",
                     help="Python-driven exchange instead of the C++ SyncRunner")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="W = 1 rehearsal of the multi-GPU step: keep the reduce-scatter / "
+                         "all-gather units on a 1-rank RCCL communicator (comm stream, events, "
+                         "RCCL launches) instead of the local update")
     ap.add_argument("--splits", default=None, help="comma-separated split-K factors per op")
     ap.add_argument("--tta", type=float, default=0.95,
                     help="after the throughput run, train one reference epoch (500 steps/worker, "
@@ -80,7 +84,8 @@ def main(argv=None):
     cfg = TrainConfig(mode=a.mode, shard=a.shard, steps=total_steps, batch_size=a.batch_size,
                       eval_every=0, engine=a.engine, graph=a.graph and not a.no_graph,
                       overlap=not a.no_overlap, quiet=True, data_sharding="stride",
-                      native_exchange=not a.no_native_exchange)
+                      native_exchange=not a.no_native_exchange,
+                      force_collectives=a.force_collectives)
     data = synthetic_mnist()
     tr = Trainer(cfg, env, dataset=data)
     if a.splits and hasattr(tr.engine, "set_splits"):
@@ -155,6 +160,7 @@ def main(argv=None):
                 "hip_graph": bool(a.graph and not a.no_graph),
                 "overlap": not a.no_overlap,
                 "exchange": "native" if getattr(tr.exchange, "native", False) else "python",
+                "forced_1rank_collectives": bool(a.force_collectives),
                 "optimizer": "adam(1e-4) on PS shards",
             },
             "test_acc_after_run": round(acc, 4),

@@ -289,6 +289,7 @@ class PyRunner {
   }
   void set_scale(double grad_scale, double coef) { r_->set_scale((float)grad_scale, (float)coef); }
   void set_local_on_main(bool on) { r_->set_local_on_main(on); }
+  void set_last_on_main(bool on) { r_->set_last_on_main(on); }
   void set_use_tail(bool on) { r_->set_use_tail(on); }
   void set_tail_cfg(int64_t first, int64_t f4) { r_->set_tail_cfg((int)first, (int)f4); }
   void step(at::Tensor x, at::Tensor labels, int64_t seed, std::vector<double> lr_t) {
@@ -381,6 +382,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_optimizer", &PyRunner::set_optimizer)
       .def("set_scale", &PyRunner::set_scale)
       .def("set_local_on_main", &PyRunner::set_local_on_main)
+      .def("set_last_on_main", &PyRunner::set_last_on_main)
       .def("set_use_tail", &PyRunner::set_use_tail)
       .def("set_tail_cfg", &PyRunner::set_tail_cfg)
       .def("step", &PyRunner::step)

@@ -173,6 +173,9 @@ class SyncRunner {
             hipStream_t st);
   bool selftest(std::string* why);
   void set_local_on_main(bool on) { local_on_main_ = on; }
+  // collective units of the LAST backward segment on the compute stream (no event hop on the
+  // step's critical path; RCCL still orders them after the comm stream's earlier units)
+  void set_last_on_main(bool on) { last_on_main_ = on; }
   std::string async_error();  // "" while the communicator is healthy
   void abort();               // ncclCommAbort: unblocks this rank's pending collectives
   hipStream_t comm_stream() const { return cs_; }
@@ -198,6 +201,7 @@ class SyncRunner {
   float lr_ = 1e-4f, b1_ = 0.9f, b2_ = 0.999f, eps_ = 1e-8f, mu_ = 0.9f;
   float grad_scale_ = 1.f, coef_ = 1.f;
   bool local_on_main_ = true;
+  bool last_on_main_ = true;
   struct Piece {
     RunnerRange r;
     int ps;

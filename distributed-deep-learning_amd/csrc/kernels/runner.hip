@@ -313,11 +313,16 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
              p.r.hi - p.r.lo, lr_t[p.ps], st);
     return;
   }
+  // The last segment's gradients complete with the backward, so nothing is left to overlap
+  // its exchange with: its collectives go in order on the compute stream (no event record /
+  // stream wait between the final backward launch, the exchange and the next forward).
   bool comm_used = false;
   std::vector<const RunnerUnit*> reduces;
   for (int s = 0; s < kSegments; ++s) {
     eng_->backward_segment(s, x, labels, B, seed, st);
-    bool waited = false;
+    const bool on_main = last_on_main_ && s == kSegments - 1;
+    hipStream_t xs = on_main ? st : cs_;
+    bool waited = on_main;
     reduces.clear();
     for (const auto& u : units_) {
       if (u.seg != s) continue;
@@ -330,11 +335,11 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
         HIP_CHECK(hipStreamWaitEvent(cs_, seg_ev_[s], 0));
         waited = true;
       }
-      comm_used = true;
+      comm_used |= !on_main;
       if (u.kind == RunnerUnit::REDUCE) reduces.push_back(&u);
-      else issue(u, lr_t, cs_);
+      else issue(u, lr_t, xs);
     }
-    if (!reduces.empty()) issue_reduce_group(reduces, lr_t, cs_);
+    if (!reduces.empty()) issue_reduce_group(reduces, lr_t, xs);
   }
   if (comm_used) {
     // the next step's forward reads the updated parameters

@@ -17,6 +17,7 @@ checkpointing and inspection are unchanged.
 """
 from __future__ import annotations
 
+import os
 import sys
 from typing import Dict, Sequence
 
@@ -84,6 +85,9 @@ class NativeSyncExchange(SyncExchange):
         self.runner.set_optimizer(0 if optimizer == "adam" else 1, h.lr, h.beta1, h.beta2, h.eps,
                                   momentum)
         self.runner.set_scale(self.grad_scale, self.coef)
+        # A/B knob: DDL_LAST_ON_MAIN=0 puts the last segment's collectives back on the comm
+        # stream (one event hop more on the critical path of every W > 1 step)
+        self.runner.set_last_on_main(os.environ.get("DDL_LAST_ON_MAIN", "1") != "0")
         self._lr = [0.0] * max(plan.num_ps, env.world)
         self._n = 0
 

@@ -88,6 +88,21 @@ def test_forced_collectives_on_one_rank_match_local(data, kw):
         assert torch.equal(s_loc[p][2], s_col[p][2])
 
 
+@pytest.mark.parametrize("shard", ["flat", "contiguous"])
+def test_last_segment_exchange_stream_placement(data, shard, monkeypatch):
+    """The last backward segment's collectives on the compute stream (default) or on the comm
+    stream behind an event (DDL_LAST_ON_MAIN=0): same kernels in the same RCCL order, so the
+    results are bit-identical."""
+    monkeypatch.setenv("DDL_LAST_ON_MAIN", "1")
+    p_main, s_main = _run(data, True, force_collectives=True, shard=shard)
+    monkeypatch.setenv("DDL_LAST_ON_MAIN", "0")
+    p_comm, s_comm = _run(data, True, force_collectives=True, shard=shard)
+    assert torch.equal(p_main, p_comm)
+    for p in s_main:
+        assert torch.equal(s_main[p][1], s_comm[p][1])
+        assert torch.equal(s_main[p][2], s_comm[p][2])
+
+
 def test_rccl_probe_resolves_torch_librccl():
     from ddl_amd.ops import native
     assert native.ops().SyncRunner.probe() == ""
