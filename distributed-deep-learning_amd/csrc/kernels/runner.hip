@@ -22,6 +22,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -99,9 +100,16 @@ SyncRunner::SyncRunner(Engine* eng, float* params, float* grads, int world, int 
   HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   // collectives + optimizer on a high-priority stream so they are not starved by the GEMMs
   HIP_CHECK(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, hi));
+  // The events only order the two streams of this device (RCCL's kernels read the gradients
+  // locally), so a device-scope release suffices; the default system-scope fence at every
+  // record showed as a ~7 us gap on the compute stream per backward segment (forced 1-rank
+  // timeline).  DDL_EVENT_SYSFENCE=1 restores it (A/B).
+  const char* sf = getenv("DDL_EVENT_SYSFENCE");
+  const unsigned ev_flags =
+      hipEventDisableTiming | ((sf && sf[0] == '1') ? 0u : (unsigned)hipEventDisableSystemFence);
   for (int s = 0; s < kSegments; ++s)
-    HIP_CHECK(hipEventCreateWithFlags(&seg_ev_[s], hipEventDisableTiming));
-  HIP_CHECK(hipEventCreateWithFlags(&done_ev_, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&seg_ev_[s], ev_flags));
+  HIP_CHECK(hipEventCreateWithFlags(&done_ev_, ev_flags));
 }
 
 SyncRunner::~SyncRunner() {

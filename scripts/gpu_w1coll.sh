@@ -11,9 +11,9 @@ timeout -k 10 300 python -u -m pytest ${TESTS:-tests/test_native_runner.py} -x -
 tail -2 gpurun_out/w1c_tests.log
 for i in 1 2; do
   for v in ${VALS:-1 0}; do
-    DDL_LAST_ON_MAIN=$v timeout -k 10 120 python bench.py --steps 400 --warmup 40 --tta 0 \
+    env ${VAR:-DDL_LAST_ON_MAIN}=$v timeout -k 10 120 python bench.py --steps 400 --warmup 40 --tta 0 \
       --force-collectives ${EXTRA:-} > gpurun_out/w1c_$v.log 2>&1 || { tail -5 gpurun_out/w1c_$v.log; exit 1; }
-    python -c "import sys,json; d=json.loads(open('gpurun_out/w1c_$v.log').readlines()[-1]); print('forced last_on_main=$v', d['ms_per_step'], d['config']['exchange'])"
+    python -c "import sys,json; d=json.loads(open('gpurun_out/w1c_$v.log').readlines()[-1]); print('forced ${VAR:-DDL_LAST_ON_MAIN}=$v', d['ms_per_step'], d['config']['exchange'])"
   done
 done
 timeout -k 10 120 python bench.py --steps 400 --warmup 40 --tta 0 > gpurun_out/w1c_default.log 2>&1 || exit 1
