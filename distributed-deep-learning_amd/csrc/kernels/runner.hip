@@ -100,16 +100,18 @@ SyncRunner::SyncRunner(Engine* eng, float* params, float* grads, int world, int 
   HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   // collectives + optimizer on a high-priority stream so they are not starved by the GEMMs
   HIP_CHECK(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, hi));
-  // The events only order the two streams of this device (RCCL's kernels read the gradients
-  // locally), so a device-scope release suffices; the default system-scope fence at every
+  // The segment events only hand gradients written by this device's GEMMs to RCCL kernels on
+  // this device, so a device-scope release suffices; the default system-scope fence at every
   // record showed as a ~7 us gap on the compute stream per backward segment (forced 1-rank
-  // timeline).  DDL_EVENT_SYSFENCE=1 restores it (A/B).
+  // timeline).  DDL_EVENT_SYSFENCE=1 restores it (A/B).  The end-of-exchange event keeps the
+  // system scope: it orders the next forward after collectives that received peer data, and
+  // it is recorded on the comm stream, off the compute stream's critical path.
   const char* sf = getenv("DDL_EVENT_SYSFENCE");
   const unsigned ev_flags =
       hipEventDisableTiming | ((sf && sf[0] == '1') ? 0u : (unsigned)hipEventDisableSystemFence);
   for (int s = 0; s < kSegments; ++s)
     HIP_CHECK(hipEventCreateWithFlags(&seg_ev_[s], ev_flags));
-  HIP_CHECK(hipEventCreateWithFlags(&done_ev_, ev_flags));
+  HIP_CHECK(hipEventCreateWithFlags(&done_ev_, hipEventDisableTiming));
 }
 
 SyncRunner::~SyncRunner() {
