@@ -105,7 +105,7 @@ def test_gradients_match_autograd(setup, B):
     eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, seed)
     torch.cuda.synchronize()
     loss = check_grads(grads, flat, x, y, 0.5, seed)
-    assert abs(float(eng.eng.buffer("loss", B).mean()) - float(loss)) < 1e-5
+    assert abs(float(eng.eng.buffer("loss", B).mean()) - float(loss.detach())) < 1e-5
 
 
 def test_gradients_no_dropout(setup):
