@@ -227,7 +227,7 @@ class PyEngine {
 class PyRunner {
  public:
   PyRunner(PyEngine& eng, at::Tensor params, at::Tensor grads, int64_t world, int64_t rank)
-      : eng_(eng), params_(params), grads_(grads) {
+      : eng_(eng), params_(params), grads_(grads), world_(world) {
     check_f32_cuda(params, "params");
     check_f32_cuda(grads, "grads");
     TORCH_CHECK(params.numel() == grads.numel(), "params/grads size mismatch");
@@ -268,18 +268,26 @@ class PyRunner {
         keep_.push_back(x);
         return x.data_ptr<float>();
       };
-      int64_t need_state = 0;
+      int64_t need_state = 0, need_shard = 0;
       for (auto r : t[4].cast<py::list>()) {
         auto rr = r.cast<py::tuple>();
         ddl::RunnerRange range{rr[0].cast<int64_t>(), rr[1].cast<int64_t>(), rr[2].cast<int64_t>()};
         TORCH_CHECK(0 <= range.lo && range.lo <= range.hi && range.hi <= n, "range out of bounds");
-        const int64_t len = u.kind == ddl::RunnerUnit::RS ? 0 : range.hi - range.lo;
+        int64_t len = range.hi - range.lo;
+        if (u.kind == ddl::RunnerUnit::RS) {
+          // reduce-scatter: this rank updates (and needs state / a shard buffer for) 1/W of it;
+          // a remainder would silently get no exchange and no update
+          TORCH_CHECK(len % world_ == 0, "RS unit range [", range.lo, ", ", range.hi,
+                      ") is not divisible by the world size ", world_);
+          len /= world_;
+          need_shard = std::max(need_shard, len);
+        }
         need_state = std::max(need_state, range.state_off + len);
         u.ranges.push_back(range);
       }
       u.m = opt_ptr(t[5], need_state, "m");
       u.v = opt_ptr(t[6], need_state, "v");
-      u.shard = opt_ptr(t[7], 0, "shard");
+      u.shard = opt_ptr(t[7], need_shard, "shard");
       out.push_back(std::move(u));
     }
     r_->set_units(out);
@@ -319,6 +327,7 @@ class PyRunner {
   std::vector<at::Tensor> keep_;
   std::vector<float> lr_;
   std::unique_ptr<ddl::SyncRunner> r_;
+  int64_t world_;
 };
 
 }  // namespace

@@ -100,15 +100,18 @@ SyncRunner::SyncRunner(Engine* eng, float* params, float* grads, int world, int 
   HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   // collectives + optimizer on a high-priority stream so they are not starved by the GEMMs
   HIP_CHECK(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, hi));
-  // The segment events only hand gradients written by this device's GEMMs to RCCL kernels on
-  // this device, so a device-scope release suffices; the default system-scope fence at every
-  // record showed as a ~7 us gap on the compute stream per backward segment (forced 1-rank
-  // timeline).  DDL_EVENT_SYSFENCE=1 restores it (A/B).  The end-of-exchange event keeps the
-  // system scope: it orders the next forward after collectives that received peer data, and
-  // it is recorded on the comm stream, off the compute stream's critical path.
+  // The segment events hand gradients written by this device's GEMMs to RCCL kernels on this
+  // device.  On the 1-rank rehearsal (W = 1, every collective a local copy) a device-scope
+  // release suffices and removed a ~7 us gap per backward segment (forced 1-rank timeline).
+  // With W > 1, RCCL's P2P transports may read these buffers from a peer GPU, and the relaxed
+  // fence has not been validated there, so W > 1 keeps the system-scope fence unless
+  // DDL_EVENT_SYSFENCE=0 asks for the device scope explicitly (A/B).  The end-of-exchange
+  // event keeps the system scope: it orders the next forward after collectives that received
+  // peer data, and it is recorded on the comm stream, off the compute stream's critical path.
   const char* sf = getenv("DDL_EVENT_SYSFENCE");
+  const bool sysfence = sf ? sf[0] == '1' : world_ > 1;
   const unsigned ev_flags =
-      hipEventDisableTiming | ((sf && sf[0] == '1') ? 0u : (unsigned)hipEventDisableSystemFence);
+      hipEventDisableTiming | (sysfence ? 0u : (unsigned)hipEventDisableSystemFence);
   for (int s = 0; s < kSegments; ++s)
     HIP_CHECK(hipEventCreateWithFlags(&seg_ev_[s], ev_flags));
   HIP_CHECK(hipEventCreateWithFlags(&done_ev_, hipEventDisableTiming));
@@ -154,6 +157,8 @@ void SyncRunner::set_units(const std::vector<RunnerUnit>& units) {
       throw std::invalid_argument("collective unit without an RCCL communicator");
     if (u.kind == RunnerUnit::RS && (u.ranges.size() != 1 || !u.shard))
       throw std::invalid_argument("RS unit needs exactly one range and a shard buffer");
+    if (u.kind == RunnerUnit::RS && (u.ranges[0].hi - u.ranges[0].lo) % world_ != 0)
+      throw std::invalid_argument("RS unit range not divisible by the world size");
   }
   units_ = units;
   // W = 1 (every unit LOCAL): one stream.  Ranges adjacent in both the parameter buffer and

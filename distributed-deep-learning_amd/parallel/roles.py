@@ -46,6 +46,8 @@ def resolve_num_ps(cfg: TrainConfig, world: int) -> int:
 class Trainer:
     """One process = one GPU = one worker (+ the PS shards it hosts)."""
 
+    ABORT_GRACE_S = 5.0  # watchdog: longest wait for ncclCommAbort before os._exit
+
     def __init__(self, cfg: TrainConfig, env: Optional[DistEnv] = None,
                  dataset: Optional[Dataset] = None):
         self.cfg = cfg
@@ -149,12 +151,22 @@ class Trainer:
         job down."""
         import os
         import sys
+        import threading
         ab = getattr(self.exchange, "abort", None)
         if ab is not None:
-            try:
-                ab()
-            except Exception as e:  # best effort: we are exiting anyway
-                sys.stderr.write(f"[watchdog] comm abort failed: {e}\n")
+            # ncclCommAbort can itself block (proxy threads, kernels stuck on a dead peer):
+            # run it on a daemon thread and exit unconditionally after a bounded join
+            def _abort():
+                try:
+                    ab()
+                except Exception as e:  # best effort: we are exiting anyway
+                    sys.stderr.write(f"[watchdog] comm abort failed: {e}\n")
+            t = threading.Thread(target=_abort, name="ddl-comm-abort", daemon=True)
+            t.start()
+            t.join(timeout=self.ABORT_GRACE_S)
+            if t.is_alive():
+                sys.stderr.write("[watchdog] comm abort still blocked; exiting anyway\n")
+                sys.stderr.flush()
         os._exit(124)
 
     # ---- reference main loop -----------------------------------------------------------------------

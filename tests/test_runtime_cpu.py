@@ -90,6 +90,30 @@ def test_watchdog_fires_and_kick_prevents():
     wd.stop()
 
 
+_BLOCKED_ABORT = r"""
+import sys, threading, time
+sys.path.insert(0, sys.argv[1])
+from ddl_amd.parallel.roles import Trainer
+class Ex:  # a communicator abort that never returns (e.g. stuck on a dead peer)
+    def abort(self):
+        threading.Event().wait()
+t = Trainer.__new__(Trainer)
+t.exchange = Ex()
+Trainer.ABORT_GRACE_S = 0.5
+t0 = time.monotonic()
+t._on_hang()
+"""
+
+
+def test_watchdog_exits_even_if_comm_abort_blocks():
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", _BLOCKED_ABORT, ROOT], capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 124, r.stderr
+    assert "still blocked" in r.stderr
+    assert time.monotonic() - t0 < 30
+
+
 def test_synthetic_data_shapes_and_learnability():
     d = synthetic_mnist(2000, 500, seed=3)
     assert d.x_train.shape == (2000, 784) and d.y_train.shape == (2000,)
