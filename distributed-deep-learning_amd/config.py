@@ -38,6 +38,10 @@ class TrainConfig:
     overlap: bool = True            # bucketed grad push overlapped with backward
     native_exchange: bool = True    # sync step in the C++ SyncRunner (HIP engine on GPU)
     force_collectives: bool = False  # W = 1: native runner keeps RS/reduce units on a 1-rank comm
+    # W > 1 data plane of the native sync runner: rccl (reduce-scatter / all-gather or reduce /
+    # broadcast) or xgmi (flat plan: one fused push / owner-Adam / pull kernel per bucket over
+    # IPC-mapped peer memory, csrc/kernels/xgmi.hip); auto = rccl
+    exchange_backend: str = "auto"
     dist_eval: bool = True          # sync, W > 1: each rank scores 1/W of the test set
     eval_async: bool = False        # HIP engine: periodic eval on a side stream from a snapshot
     check_provenance: bool = False  # async: verify every applied push
@@ -89,6 +93,10 @@ def add_args(p: argparse.ArgumentParser, mode_default: str = "sync") -> argparse
     p.add_argument("--no-native-exchange", action="store_true",
                    help="drive the sync exchange from Python instead of the C++ SyncRunner")
     p.add_argument("--no-overlap", action="store_true")
+    p.add_argument("--exchange", dest="exchange_backend", default=d.exchange_backend,
+                   choices=["auto", "rccl", "xgmi"],
+                   help="W > 1 sync data plane of the native runner: RCCL collectives or the "
+                        "fused xGMI peer-memory exchange (flat plan)")
     p.add_argument("--log-jsonl", default=None)
     p.add_argument("--checkpoint-dir", default=None)
     p.add_argument("--checkpoint-every", type=int, default=0)
@@ -111,5 +119,6 @@ def from_args(a: argparse.Namespace) -> TrainConfig:
         graph=a.graph and not a.no_graph, native_exchange=not a.no_native_exchange,
         dist_eval=not a.no_dist_eval, eval_async=a.eval_async,
         check_provenance=a.check_provenance, overlap=not a.no_overlap, log_jsonl=a.log_jsonl,
+        exchange_backend=a.exchange_backend,
         checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
         resume=a.resume, target_acc=a.target_acc, quiet=a.quiet, watchdog_s=a.watchdog_s)

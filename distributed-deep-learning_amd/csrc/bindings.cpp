@@ -224,6 +224,46 @@ class PyEngine {
 };
 
 // Python-facing wrapper of ddl::SyncRunner (native sync step: engine + exchange + update).
+// xGMI peer exchange (kernels/xgmi.hip): IPC handles out, every rank's handles in.
+class PyPeer {
+ public:
+  PyPeer(at::Tensor params, at::Tensor grads, int64_t world, int64_t rank, py::list buckets,
+         int64_t max_slices)
+      : params_(params), grads_(grads) {
+    check_f32_cuda(params, "params");
+    check_f32_cuda(grads, "grads");
+    TORCH_CHECK(params.numel() == grads.numel(), "params/grads size mismatch");
+    std::vector<std::pair<int64_t, int64_t>> bk;
+    for (auto b : buckets) {
+      auto t = b.cast<py::tuple>();
+      bk.emplace_back(t[0].cast<int64_t>(), t[1].cast<int64_t>());
+    }
+    c10::hip::HIPGuard guard(params.device().index());
+    p_ = std::make_unique<ddl::PeerExchange>(params.data_ptr<float>(), grads.data_ptr<float>(),
+                                             params.numel(), (int)world, (int)rank, bk,
+                                             (int)max_slices);
+  }
+  py::bytes handle() const {
+    c10::hip::HIPGuard guard(params_.device().index());
+    return py::bytes(p_->handle());
+  }
+  void open(std::vector<std::string> handles) {
+    c10::hip::HIPGuard guard(params_.device().index());
+    p_->open(handles);
+  }
+  int error() const { return p_->error(); }
+  std::vector<int64_t> nslices() const {
+    std::vector<int64_t> v;
+    for (int b = 0; b < p_->num_buckets(); ++b) v.push_back(p_->nslices(b));
+    return v;
+  }
+  ddl::PeerExchange* raw() { return p_.get(); }
+
+ private:
+  at::Tensor params_, grads_;
+  std::unique_ptr<ddl::PeerExchange> p_;
+};
+
 class PyRunner {
  public:
   PyRunner(PyEngine& eng, at::Tensor params, at::Tensor grads, int64_t world, int64_t rank)
@@ -247,14 +287,25 @@ class PyRunner {
     r_->init_comm(s.data(), force);
   }
   bool has_comm() const { return r_->has_comm(); }
-  // units: list of (seg, kind, host, ps, [(lo, hi, state_off)], m|None, v|None, shard|None)
+  void set_peer(PyPeer& p) {
+    peer_keep_ = &p;
+    r_->set_peer(p.raw());
+  }
+  // all buckets with w := sum over ranks of g (the xGMI self-test; blocks until done)
+  void peer_selftest_step() {
+    py::gil_scoped_release nogil;
+    r_->peer_selftest_step(cur_stream());
+    (void)hipStreamSynchronize(cur_stream());
+  }
+  // units: list of (seg, kind, host, ps, [(lo, hi, state_off)], m|None, v|None, shard|None
+  //                 [, bucket])
   void set_units(py::list units) {
     std::vector<ddl::RunnerUnit> out;
     keep_.clear();
     const int64_t n = params_.numel();
     for (auto item : units) {
       auto t = item.cast<py::tuple>();
-      TORCH_CHECK(t.size() == 8, "unit tuple must have 8 fields");
+      TORCH_CHECK(t.size() == 8 || t.size() == 9, "unit tuple must have 8 or 9 fields");
       ddl::RunnerUnit u;
       u.seg = t[0].cast<int>();
       u.kind = t[1].cast<int>();
@@ -274,13 +325,13 @@ class PyRunner {
         ddl::RunnerRange range{rr[0].cast<int64_t>(), rr[1].cast<int64_t>(), rr[2].cast<int64_t>()};
         TORCH_CHECK(0 <= range.lo && range.lo <= range.hi && range.hi <= n, "range out of bounds");
         int64_t len = range.hi - range.lo;
-        if (u.kind == ddl::RunnerUnit::RS) {
+        if (u.kind == ddl::RunnerUnit::RS || u.kind == ddl::RunnerUnit::XGMI) {
           // reduce-scatter: this rank updates (and needs state / a shard buffer for) 1/W of it;
           // a remainder would silently get no exchange and no update
           TORCH_CHECK(len % world_ == 0, "RS unit range [", range.lo, ", ", range.hi,
                       ") is not divisible by the world size ", world_);
           len /= world_;
-          need_shard = std::max(need_shard, len);
+          if (u.kind == ddl::RunnerUnit::RS) need_shard = std::max(need_shard, len);
         }
         need_state = std::max(need_state, range.state_off + len);
         u.ranges.push_back(range);
@@ -288,6 +339,7 @@ class PyRunner {
       u.m = opt_ptr(t[5], need_state, "m");
       u.v = opt_ptr(t[6], need_state, "v");
       u.shard = opt_ptr(t[7], need_shard, "shard");
+      if (t.size() == 9) u.bucket = t[8].cast<int>();
       out.push_back(std::move(u));
     }
     r_->set_units(out);
@@ -328,6 +380,7 @@ class PyRunner {
   std::vector<float> lr_;
   std::unique_ptr<ddl::SyncRunner> r_;
   int64_t world_;
+  PyPeer* peer_keep_ = nullptr;
 };
 
 }  // namespace
@@ -396,8 +449,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_tail_cfg", &PyRunner::set_tail_cfg)
       .def("step", &PyRunner::step)
       .def("selftest", &PyRunner::selftest)
+      .def("set_peer", &PyRunner::set_peer, py::keep_alive<1, 2>())
+      .def("peer_selftest_step", &PyRunner::peer_selftest_step)
       .def("async_error", &PyRunner::async_error)
       .def("abort", &PyRunner::abort);
+
+  py::class_<PyPeer>(m, "PeerExchange")
+      .def(py::init<at::Tensor, at::Tensor, int64_t, int64_t, py::list, int64_t>(),
+           py::arg("params"), py::arg("grads"), py::arg("world"), py::arg("rank"),
+           py::arg("buckets"), py::arg("max_slices") = 128)
+      .def("handle", &PyPeer::handle)
+      .def("open", &PyPeer::open)
+      .def("error", &PyPeer::error)
+      .def("nslices", &PyPeer::nslices);
 
   py::class_<ddl::ShmMailbox>(m, "ShmMailbox")
       .def(py::init<const std::string&, int64_t, bool>(), py::arg("name"), py::arg("capacity"),

@@ -142,7 +142,7 @@ struct RunnerRange {
   int64_t state_off;    // offset of the range's optimizer state in the unit's m / v
 };
 struct RunnerUnit {
-  enum Kind { LOCAL = 0, RS = 1, REDUCE = 2 };
+  enum Kind { LOCAL = 0, RS = 1, REDUCE = 2, XGMI = 3 };
   int seg = 0;          // backward segment after which the unit's gradients are complete
   int kind = LOCAL;
   int host = 0;         // REDUCE: rank that owns the PS
@@ -151,6 +151,71 @@ struct RunnerUnit {
   float* m = nullptr;   // optimizer state base of the owning PS (null where not hosted)
   float* v = nullptr;
   float* shard = nullptr;  // RS: 1/W chunk buffer
+  int bucket = -1;         // XGMI: bucket index of the runner's PeerExchange
+};
+
+// ---- parameter-server exchange over xGMI peer memory (xgmi.hip) ------------------------------
+constexpr int kXgmiMaxPeers = 16;
+constexpr int kXgmiMaxBuckets = 8;
+constexpr int kXgmiMaxSlices = 128;
+struct XgmiTable {               // every rank's IPC-mapped buffers, indexed by rank
+  float* params[kXgmiMaxPeers];
+  float* inbox[kXgmiMaxPeers];
+  uint32_t* flags[kXgmiMaxPeers];
+};
+struct XgmiLaunch {              // one bucket's kernel arguments
+  int world, rank, bucket, nbuckets, final_wait, opt;
+  uint32_t epoch;
+  int64_t lo, c, inbox_off, slice;
+  int nslices[kXgmiMaxBuckets];
+  const float* grads;
+  float* m;
+  float* v;
+  float lr_t, c1, c2, eps, lr, mu, scale, coef;
+  int* err;
+  long long timeout_ticks;
+};
+struct XgmiUpdate {              // owner-side update of one bucket chunk
+  int opt = 0;                   // 0 Adam (TF1), 1 momentum, 2 self-test (w := summed g)
+  float* m = nullptr;            // optimizer state of this rank's chunk of the bucket
+  float* v = nullptr;
+  float lr_t = 0.f, c1 = 0.1f, c2 = 0.001f, eps = 1e-8f, lr = 0.f, mu = 0.9f;
+  float scale = 1.f, coef = 1.f;
+};
+
+class PeerExchange {
+ public:
+  // buckets: [lo, hi) ranges of the flat plan buffer, each divisible by 4 * world; rank r owns
+  // chunk r of every bucket.  Allocates the inbox (one slot per source rank) and the flags.
+  PeerExchange(float* params, const float* grads, int64_t total, int world, int rank,
+               const std::vector<std::pair<int64_t, int64_t>>& buckets, int max_slices);
+  ~PeerExchange();
+  std::string handle() const;                         // this rank's IPC handles, as bytes
+  void open(const std::vector<std::string>& handles);  // every rank's, in rank order
+  // the fused push / owner update / pull of one bucket at step `epoch` (same on all ranks)
+  void launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool final_wait, hipStream_t st);
+  int error() const;             // nonzero once a wait timed out (1 arrive, 2 done)
+  int num_buckets() const { return (int)bk_.size(); }
+  int nslices(int b) const { return bk_[b].nslice; }
+  int64_t chunk(int b) const { return bk_[b].c; }
+  int world() const { return world_; }
+
+ private:
+  struct Bucket { int64_t lo, c, inbox_off, slice; int nslice; };
+  float* params_;
+  const float* grads_;
+  int64_t total_;
+  int world_, rank_;
+  std::vector<Bucket> bk_;
+  float* inbox_ = nullptr;
+  int64_t inbox_elems_ = 0;
+  uint32_t* flags_ = nullptr;
+  size_t flag_bytes_ = 0;
+  int* err_ = nullptr;
+  double timeout_s_ = 60.0;
+  XgmiTable table_{};
+  void* opened_[kXgmiMaxPeers][3] = {};
+  bool opened_ok_ = false;
 };
 
 class SyncRunner {
@@ -176,7 +241,12 @@ class SyncRunner {
   // collective units of the LAST backward segment on the compute stream (no event hop on the
   // step's critical path; RCCL still orders them after the comm stream's earlier units)
   void set_last_on_main(bool on) { last_on_main_ = on; }
-  std::string async_error();  // "" while the communicator is healthy
+  std::string async_error();  // "" while the communicator is healthy (RCCL and xGMI)
+  // XGMI units exchange through this (owned by the caller; outlives the runner's use)
+  void set_peer(PeerExchange* p) { peer_ = p; }
+  // one full exchange of every bucket with w := sum over ranks of g (no optimizer) at the
+  // next epoch; the caller fills g, checks w
+  void peer_selftest_step(hipStream_t st);
   void abort();               // ncclCommAbort: unblocks this rank's pending collectives
   hipStream_t comm_stream() const { return cs_; }
 
@@ -188,11 +258,15 @@ class SyncRunner {
                           hipStream_t st);
   void update(float* w, const float* g, float* m, float* v, int64_t n, float lr_t,
               hipStream_t st);
+  void issue_xgmi(const RunnerUnit& u, const float* lr_t, bool final_wait, hipStream_t st);
+  int last_xgmi_ = -1;     // index of the step's last XGMI unit (carries the final wait)
   Engine* eng_;
   float* w_;
   float* g_;
   int world_, rank_;
   void* comm_ = nullptr;  // ncclComm_t
+  PeerExchange* peer_ = nullptr;
+  uint32_t epoch_ = 0;     // xGMI flag epoch: one per step, identical on every rank
   hipStream_t cs_ = nullptr;
   hipEvent_t seg_ev_[kSegments] = {};
   hipEvent_t done_ev_ = nullptr;

@@ -153,14 +153,26 @@ void SyncRunner::init_comm(const char id_bytes[128], bool force) {
 void SyncRunner::set_units(const std::vector<RunnerUnit>& units) {
   for (const auto& u : units) {
     if (u.seg < 0 || u.seg >= kSegments) throw std::invalid_argument("unit segment out of range");
-    if (u.kind != RunnerUnit::LOCAL && !comm_)
+    if (u.kind != RunnerUnit::LOCAL && u.kind != RunnerUnit::XGMI && !comm_)
       throw std::invalid_argument("collective unit without an RCCL communicator");
     if (u.kind == RunnerUnit::RS && (u.ranges.size() != 1 || !u.shard))
       throw std::invalid_argument("RS unit needs exactly one range and a shard buffer");
     if (u.kind == RunnerUnit::RS && (u.ranges[0].hi - u.ranges[0].lo) % world_ != 0)
       throw std::invalid_argument("RS unit range not divisible by the world size");
+    if (u.kind == RunnerUnit::XGMI) {
+      if (!peer_) throw std::invalid_argument("xGMI unit without a PeerExchange");
+      if (u.bucket < 0 || u.bucket >= peer_->num_buckets())
+        throw std::invalid_argument("xGMI unit bucket out of range");
+      if (opt_ == 0 && !u.v) throw std::invalid_argument("xGMI unit without Adam state");
+    }
   }
   units_ = units;
+  // the step's last xGMI unit also waits until every owner's parameters have landed here
+  last_xgmi_ = -1;
+  for (size_t i = 0; i < units_.size(); ++i)
+    if (units_[i].kind == RunnerUnit::XGMI &&
+        (last_xgmi_ < 0 || units_[i].seg >= units_[last_xgmi_].seg))
+      last_xgmi_ = (int)i;
   // W = 1 (every unit LOCAL): one stream.  Ranges adjacent in both the parameter buffer and
   // the PS state merge; per segment they become the optimizer tail of the next segment's dual
   // launch (tail.h), else all of them one coalesced launch at the end of the step.  Same
@@ -332,6 +344,12 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
   // its exchange with: its collectives go in order on the compute stream (no event record /
   // stream wait between the final backward launch, the exchange and the next forward).
   bool comm_used = false;
+  if (last_xgmi_ >= 0) {
+    if (const int e = peer_->error())
+      throw std::runtime_error("xGMI exchange timed out waiting for a peer (code " +
+                               std::to_string(e) + ")");
+    ++epoch_;
+  }
   std::vector<const RunnerUnit*> reduces;
   for (int s = 0; s < kSegments; ++s) {
     eng_->backward_segment(s, x, labels, B, seed, st);
@@ -339,7 +357,8 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
     hipStream_t xs = on_main ? st : cs_;
     bool waited = on_main;
     reduces.clear();
-    for (const auto& u : units_) {
+    for (size_t i = 0; i < units_.size(); ++i) {
+      const auto& u = units_[i];
       if (u.seg != s) continue;
       if (u.kind == RunnerUnit::LOCAL && local_on_main_) {
         issue(u, lr_t, st);
@@ -349,6 +368,14 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
         HIP_CHECK(hipEventRecord(seg_ev_[s], st));
         HIP_CHECK(hipStreamWaitEvent(cs_, seg_ev_[s], 0));
         waited = true;
+      }
+      if (u.kind == RunnerUnit::XGMI) {
+        // the final wait orders the next forward after every owner's pushes; only if it runs
+        // on the comm stream does the compute stream need the end-of-exchange event
+        const bool fin = (int)i == last_xgmi_;
+        comm_used |= fin && !on_main;
+        issue_xgmi(u, lr_t, fin, xs);
+        continue;
       }
       comm_used |= !on_main;
       if (u.kind == RunnerUnit::REDUCE) reduces.push_back(&u);
@@ -363,10 +390,40 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
   }
 }
 
+void SyncRunner::issue_xgmi(const RunnerUnit& u, const float* lr_t, bool final_wait,
+                            hipStream_t st) {
+  XgmiUpdate up;
+  const auto& r = u.ranges[0];
+  up.opt = opt_;
+  up.m = u.m ? u.m + r.state_off : nullptr;
+  up.v = u.v ? u.v + r.state_off : nullptr;
+  up.lr_t = lr_t[u.ps];
+  up.c1 = 1.f - b1_;
+  up.c2 = 1.f - b2_;
+  up.eps = eps_;
+  up.lr = lr_;
+  up.mu = mu_;
+  up.scale = grad_scale_;
+  up.coef = coef_;
+  peer_->launch(u.bucket, epoch_, up, final_wait, st);
+}
+
+void SyncRunner::peer_selftest_step(hipStream_t st) {
+  if (!peer_) throw std::runtime_error("no PeerExchange");
+  ++epoch_;
+  XgmiUpdate up;
+  up.opt = 2;
+  const int nb = peer_->num_buckets();
+  for (int b = 0; b < nb; ++b) peer_->launch(b, epoch_, up, b == nb - 1, st);
+}
+
 // Failure detection: RCCL reports remote-peer / network failures
 // asynchronously; the trainer polls this between steps and the watchdog aborts the comm (so
 // blocked collectives on this rank return and the job can be torn down) on a hang.
 std::string SyncRunner::async_error() {
+  if (peer_ && peer_->error())
+    return "xGMI exchange timed out waiting for a peer (code " + std::to_string(peer_->error()) +
+           ")";
   if (!comm_) return std::string();
   ncclResult_t st = ncclSuccess;
   RCCL_CHECK(rccl().CommGetAsyncError(as_comm(comm_), &st));

@@ -1,0 +1,334 @@
+// Parameter-server exchange over xGMI peer memory: one kernel per gradient bucket does the
+// whole synchronous PS round trip of SURVEY.md §2.7 for the byte-equal flat plan — push the
+// gradient chunks to their owners, sum at the owner, Adam on the owner's shard, push the new
+// parameters back to every worker — with remote stores into IPC-mapped peer buffers instead
+// of RCCL's reduce-scatter + all-gather (two collective launches, a ring pass each).
+//
+// Reference behaviour being replaced: every worker Sends each gradient tensor to the owning
+// PS, the PS sums the W arrivals with NumPy and runs ApplyAdam, then Sends the parameters back
+// (mnist_sync_sharding/worker.py:30-37,88-94; parameter_server.py:76-82,108-126).
+//
+// Why a kernel of our own (MI355X): the 8 GPUs of a node are a full xGMI mesh (7 links per GPU),
+// so the owner of chunk r can receive its W-1 gradient pieces on W-1 different links at once,
+// and a store to a peer's HBM is posted (no round trip).  One launch per bucket with a few dozen
+// workgroups leaves the CUs to the backward GEMMs it overlaps with; all traffic is writes.
+//
+// Protocol (per bucket b, step epoch e; workgroup j owns slice j of every rank's chunk):
+//   phase 1  for every owner r != me: store grads[b][chunk r][slice j] -> inbox_r[b][me][slice j]
+//            (write-through, system scope), drain, then ARRIVE_r[b][me][j] = e
+//   phase 2  wait ARRIVE_me[b][q][j] >= e for every peer q; sum the W contributions in rank order
+//            (deterministic), optimizer update of my chunk's slice, store the new parameters to
+//            EVERY rank's parameter buffer (self included, write-through), drain, DONE_q[b][me][j] = e
+//   final    (the step's last bucket, on the compute stream) wait DONE_me[b'][q][*] >= e for every
+//            bucket and rank: when the kernel ends, every parameter of this step has landed and the
+//            next forward (a later kernel: L2 invalidated at its start) reads them.
+// Buffer reuse is safe by construction: a rank overwrites an inbox slot (step e+1 backward) only
+// after its step e+1 forward, i.e. after the final wait saw every owner's DONE of step e, which
+// each owner sets after reading that slot; an owner writes a peer's parameters of bucket b only
+// after that peer's ARRIVE for b, i.e. after its backward segment b, the last reader of them.
+// Flags live in uncached device memory and are only touched by system-scope atomics; payload
+// stores carry sc0|sc1 (system write-through) and every storing wave drains (vmcnt(0)) before
+// the workgroup barrier that precedes the flag store.  Every wait is bounded: on timeout the
+// kernel records an error word in host memory and runs to completion (no GPU hang); the host
+// raises at the next step.
+#include <stdlib.h>
+#include <string.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "api.h"
+#include "common.h"
+
+namespace ddl {
+
+namespace {
+
+constexpr unsigned kSys = 1u | 16u;  // buffer-op cache policy: sc0 | sc1 = system coherent
+
+DDL_DEV void st4_sys(brsrc_t r, int byte_off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(
+      __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), r, byte_off, 0,
+      kSys);
+}
+DDL_DEV float4 ld4_sys(brsrc_t r, int byte_off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kSys);
+  return *reinterpret_cast<float4*>(&v);
+}
+DDL_DEV void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+DDL_DEV uint32_t flag_load(const uint32_t* f) {
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+DDL_DEV void flag_store(uint32_t* f, uint32_t v) {
+  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+DDL_DEV int arrive_idx(int b, int src, int j) { return (b * kXgmiMaxPeers + src) * kXgmiMaxSlices + j; }
+DDL_DEV int done_idx(int b, int src, int j) {
+  return kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices + arrive_idx(b, src, j);
+}
+
+// Bounded wait until *f >= epoch (wrap-safe).  false on timeout or when another workgroup
+// already reported an error (then the caller just runs to the end).
+DDL_DEV bool wait_ge(const uint32_t* f, uint32_t epoch, long long deadline, int* err, int code) {
+  while ((int32_t)(flag_load(f) - epoch) < 0) {
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return false;
+    if (wall_clock64() > deadline) {
+      __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return true;
+}
+
+__global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a) {
+  const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int W = a.world, me = a.rank, b = a.bucket;
+  const long long deadline = wall_clock64() + a.timeout_ticks;
+  const int64_t s0 = (int64_t)j * a.slice;
+  const int64_t s1 = s0 + a.slice < a.c ? s0 + a.slice : a.c;
+  const int n4 = s0 < s1 ? (int)((s1 - s0) >> 2) : 0;
+  uint32_t* myflags = T.flags[me];
+
+  // ---- phase 1: push my gradient pieces to their owners (start at a different owner per
+  // workgroup so the W-1 links carry traffic at once)
+  for (int k = 0; k < W - 1; ++k) {
+    const int r = (me + 1 + (k + j) % (W - 1)) % W;
+    const float4* src = reinterpret_cast<const float4*>(a.grads + a.lo + r * a.c + s0);
+    const brsrc_t dst = make_rsrc(T.inbox[r] + a.inbox_off + (int64_t)me * a.c + s0,
+                                  (uint32_t)n4 * 16u);
+    for (int i = tid; i < n4; i += 256) {
+      float4 x = src[i];
+      if (a.coef != 1.f) { x.x *= a.coef; x.y *= a.coef; x.z *= a.coef; x.w *= a.coef; }
+      st4_sys(dst, i * 16, x);
+    }
+  }
+  drain_vm();
+  __syncthreads();
+  if (tid == 0)
+    for (int r = 0; r < W; ++r)
+      if (r != me) flag_store(T.flags[r] + arrive_idx(b, me, j), a.epoch);
+
+  // ---- phase 2: every peer's piece of my slice has arrived
+  if (tid < 64) {
+    bool ok = true;
+    if (lane < W && lane != me) ok = wait_ge(myflags + arrive_idx(b, lane, j), a.epoch, deadline,
+                                             a.err, 1);
+    (void)ok;
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // keep the loads below the poll
+
+  const float4* own = reinterpret_cast<const float4*>(a.grads + a.lo + me * a.c + s0);
+  const brsrc_t inbox = make_rsrc(T.inbox[me] + a.inbox_off, (uint32_t)(W * a.c * 4));
+  float4* m4 = reinterpret_cast<float4*>(a.m + s0);
+  float4* v4 = a.v ? reinterpret_cast<float4*>(a.v + s0) : nullptr;
+  float4* w4 = reinterpret_cast<float4*>(T.params[me] + a.lo + me * a.c + s0);
+  for (int i = tid; i < n4; i += 256) {
+    float4 g = f4zero();
+    for (int q = 0; q < W; ++q) {  // rank order: the same sum on every run
+      float4 x;
+      if (q == me) {
+        x = own[i];
+        if (a.coef != 1.f) { x.x *= a.coef; x.y *= a.coef; x.z *= a.coef; x.w *= a.coef; }
+      } else {
+        x = ld4_sys(inbox, (int)(((int64_t)q * a.c + s0) * 4) + i * 16);
+      }
+      g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
+    }
+    float4 w = w4[i];
+    if (a.opt == 0) {  // TF1 Adam (optim.hip form)
+      float4 M = m4[i], V = v4[i];
+      adam1(w.x, g.x * a.scale, M.x, V.x, a.lr_t, a.c1, a.c2, a.eps);
+      adam1(w.y, g.y * a.scale, M.y, V.y, a.lr_t, a.c1, a.c2, a.eps);
+      adam1(w.z, g.z * a.scale, M.z, V.z, a.lr_t, a.c1, a.c2, a.eps);
+      adam1(w.w, g.w * a.scale, M.w, V.w, a.lr_t, a.c1, a.c2, a.eps);
+      m4[i] = M; v4[i] = V;
+    } else if (a.opt == 1) {  // momentum SGD (optim.hip momentum_kernel form)
+      float4 M = m4[i];
+      M.x = M.x * a.mu + g.x * a.scale; w.x -= a.lr * M.x;
+      M.y = M.y * a.mu + g.y * a.scale; w.y -= a.lr * M.y;
+      M.z = M.z * a.mu + g.z * a.scale; w.z -= a.lr * M.z;
+      M.w = M.w * a.mu + g.w * a.scale; w.w -= a.lr * M.w;
+      m4[i] = M;
+    } else {  // self-test: parameters := the summed gradient
+      w = g;
+    }
+    // every rank's copy, this one included: write-through, so a later kernel of any rank
+    // (other XCD, other GPU) reads it from memory even while this kernel is still running
+    for (int k = 0; k < W; ++k) {
+      const int q = (me + k + j) % W;
+      const brsrc_t dst = make_rsrc(T.params[q] + a.lo + me * a.c + s0, (uint32_t)n4 * 16u);
+      st4_sys(dst, i * 16, w);
+    }
+  }
+  drain_vm();
+  __syncthreads();
+  if (tid == 0)
+    for (int q = 0; q < W; ++q) flag_store(T.flags[q] + done_idx(b, me, j), a.epoch);
+
+  // ---- final wait: every bucket's new parameters from every owner have landed here
+  if (a.final_wait && tid < 64) {
+    for (int bb = 0; bb < a.nbuckets; ++bb)
+      for (int jj = j; jj < a.nslices[bb]; jj += gridDim.x)
+        if (lane < W) wait_ge(myflags + done_idx(bb, lane, jj), a.epoch, deadline, a.err, 2);
+  }
+}
+
+#define X_CHECK(x)                                                                        \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess)                                                                 \
+      throw std::runtime_error(std::string("xgmi: ") + #x + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct HandleBlob {  // what one rank publishes (exchanged as bytes over the default group)
+  hipIpcMemHandle_t params, inbox, flags;
+  int64_t params_off;
+  int32_t world, rank;
+};
+
+}  // namespace
+
+PeerExchange::PeerExchange(float* params, const float* grads, int64_t total, int world, int rank,
+                           const std::vector<std::pair<int64_t, int64_t>>& buckets, int max_slices)
+    : params_(params), grads_(grads), total_(total), world_(world), rank_(rank) {
+  if (world < 1 || world > kXgmiMaxPeers) throw std::invalid_argument("xgmi: world out of range");
+  if (rank < 0 || rank >= world) throw std::invalid_argument("xgmi: rank out of range");
+  if (buckets.empty() || (int)buckets.size() > kXgmiMaxBuckets)
+    throw std::invalid_argument("xgmi: 1..8 buckets");
+  if (max_slices < 1 || max_slices > kXgmiMaxSlices)
+    throw std::invalid_argument("xgmi: max_slices out of range");
+  if (reinterpret_cast<uintptr_t>(params) % 16 || reinterpret_cast<uintptr_t>(grads) % 16)
+    throw std::invalid_argument("xgmi: buffers must be 16-B aligned");
+  int64_t inbox = 0;
+  for (const auto& bk : buckets) {
+    const int64_t lo = bk.first, hi = bk.second;
+    if (lo < 0 || hi > total || hi <= lo) throw std::invalid_argument("xgmi: bucket out of range");
+    if ((hi - lo) % (4 * world)) throw std::invalid_argument("xgmi: bucket not divisible by 4W");
+    Bucket B;
+    B.lo = lo;
+    B.c = (hi - lo) / world;
+    B.inbox_off = inbox;
+    // >= 1024 elements (4 KB) per workgroup slice, at most max_slices workgroups
+    int64_t ns = (B.c + 1023) / 1024;
+    if (ns > max_slices) ns = max_slices;
+    if (ns < 1) ns = 1;
+    B.slice = ((B.c + ns - 1) / ns + 3) & ~(int64_t)3;
+    B.nslice = (int)((B.c + B.slice - 1) / B.slice);
+    if (B.c * 4 * world > 0x7fffffffLL) throw std::invalid_argument("xgmi: bucket too large");
+    inbox += B.c * world;
+    bk_.push_back(B);
+  }
+  inbox_elems_ = inbox;
+  X_CHECK(hipMalloc(&inbox_, inbox_elems_ * sizeof(float)));
+  X_CHECK(hipMemset(inbox_, 0, inbox_elems_ * sizeof(float)));
+  flag_bytes_ = 2ull * kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices * sizeof(uint32_t);
+  X_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes_,
+                                hipDeviceMallocUncached));
+  X_CHECK(hipMemset(flags_, 0, flag_bytes_));
+  X_CHECK(hipHostMalloc(reinterpret_cast<void**>(&err_), 64, hipHostMallocDefault));
+  memset(err_, 0, 64);
+  X_CHECK(hipDeviceSynchronize());
+  const char* t = getenv("DDL_XGMI_TIMEOUT_S");
+  timeout_s_ = t ? atof(t) : 60.0;
+}
+
+PeerExchange::~PeerExchange() {
+  for (int q = 0; q < world_; ++q) {
+    if (q == rank_) continue;
+    for (void* p : opened_[q])
+      if (p) (void)hipIpcCloseMemHandle(p);
+  }
+  if (inbox_) (void)hipFree(inbox_);
+  if (flags_) (void)hipFree(flags_);
+  if (err_) (void)hipHostFree(err_);
+}
+
+std::string PeerExchange::handle() const {
+  HandleBlob h;
+  memset(&h, 0, sizeof(h));
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  X_CHECK(hipMemGetAddressRange(&base, &size, const_cast<float*>(params_)));
+  X_CHECK(hipIpcGetMemHandle(&h.params, base));
+  h.params_off = reinterpret_cast<const char*>(params_) - reinterpret_cast<const char*>(base);
+  X_CHECK(hipIpcGetMemHandle(&h.inbox, inbox_));
+  X_CHECK(hipIpcGetMemHandle(&h.flags, flags_));
+  h.world = world_;
+  h.rank = rank_;
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void PeerExchange::open(const std::vector<std::string>& handles) {
+  if ((int)handles.size() != world_) throw std::invalid_argument("xgmi: need one handle per rank");
+  for (int q = 0; q < world_; ++q) {
+    if (handles[q].size() != sizeof(HandleBlob)) throw std::invalid_argument("xgmi: bad handle");
+    HandleBlob h;
+    memcpy(&h, handles[q].data(), sizeof(h));
+    if (h.world != world_ || h.rank != q) throw std::invalid_argument("xgmi: handle rank mismatch");
+    if (q == rank_) {
+      table_.params[q] = params_;
+      table_.inbox[q] = inbox_;
+      table_.flags[q] = flags_;
+      continue;
+    }
+    void *p = nullptr, *ib = nullptr, *fl = nullptr;
+    X_CHECK(hipIpcOpenMemHandle(&p, h.params, hipIpcMemLazyEnablePeerAccess));
+    opened_[q][0] = p;
+    X_CHECK(hipIpcOpenMemHandle(&ib, h.inbox, hipIpcMemLazyEnablePeerAccess));
+    opened_[q][1] = ib;
+    X_CHECK(hipIpcOpenMemHandle(&fl, h.flags, hipIpcMemLazyEnablePeerAccess));
+    opened_[q][2] = fl;
+    table_.params[q] = reinterpret_cast<float*>(reinterpret_cast<char*>(p) + h.params_off);
+    table_.inbox[q] = reinterpret_cast<float*>(ib);
+    table_.flags[q] = reinterpret_cast<uint32_t*>(fl);
+  }
+  opened_ok_ = true;
+}
+
+void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool final_wait,
+                          hipStream_t st) {
+  if (!opened_ok_) throw std::runtime_error("xgmi: open() the peer handles first");
+  if (bucket < 0 || bucket >= (int)bk_.size()) throw std::invalid_argument("xgmi: bucket index");
+  const Bucket& B = bk_[bucket];
+  if (u.opt != 2 && !u.m) throw std::invalid_argument("xgmi: optimizer state missing");
+  if (u.opt == 0 && !u.v) throw std::invalid_argument("xgmi: Adam needs v");
+  XgmiLaunch a;
+  memset(&a, 0, sizeof(a));
+  a.world = world_;
+  a.rank = rank_;
+  a.bucket = bucket;
+  a.nbuckets = (int)bk_.size();
+  a.final_wait = final_wait ? 1 : 0;
+  a.epoch = epoch;
+  a.lo = B.lo;
+  a.c = B.c;
+  a.inbox_off = B.inbox_off;
+  a.slice = B.slice;
+  for (size_t i = 0; i < bk_.size(); ++i) a.nslices[i] = bk_[i].nslice;
+  a.grads = grads_;
+  a.m = u.m;
+  a.v = u.v;
+  a.opt = u.opt;
+  a.lr_t = u.lr_t;
+  a.c1 = u.c1;
+  a.c2 = u.c2;
+  a.eps = u.eps;
+  a.lr = u.lr;
+  a.mu = u.mu;
+  a.scale = u.scale;
+  a.coef = u.coef;
+  a.err = err_;
+  a.timeout_ticks = (long long)(timeout_s_ * 1e8);  // wall_clock64: 100 MHz
+  hipLaunchKernelGGL(xgmi_ps_kernel, dim3(B.nslice), dim3(256), 0, st, table_, a);
+  DDL_CHECK_LAUNCH();
+}
+
+int PeerExchange::error() const {
+  return __atomic_load_n(err_, __ATOMIC_ACQUIRE);
+}
+
+}  // namespace ddl

@@ -53,22 +53,29 @@ class DistEnv:
 
 def init_distributed(device: str = "auto") -> DistEnv:
     """One process per GPU.  Reads RANK/WORLD_SIZE/LOCAL_RANK (torchrun); backend
-    ``nccl`` (= RCCL on ROCm) on GPU, ``gloo`` on CPU."""
+    ``nccl`` (= RCCL on ROCm) on GPU, ``gloo`` on CPU.
+
+    ``DDL_DIST_BACKEND`` overrides the default process group's backend, and with more ranks
+    than GPUs rank ``l`` uses GPU ``l % count``: ``DDL_DIST_BACKEND=gloo`` with several ranks on
+    ONE GPU is the multi-process rehearsal of a W > 1 job on a one-GPU box (RCCL refuses two
+    ranks on one device; the xGMI exchange and everything above it run unchanged)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = (device == "cuda") or (device == "auto" and torch.cuda.is_available())
     if use_gpu:
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
+        ndev = torch.cuda.device_count()
+        local_dev = local % ndev if ndev > 0 else local
+        torch.cuda.set_device(local_dev)
+        dev = torch.device("cuda", local_dev)
     else:
         dev = torch.device("cpu")
     backend = None
     if world > 1:
-        backend = "nccl" if use_gpu else "gloo"
+        backend = os.environ.get("DDL_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         if not dist.is_initialized():
             kw = {}
-            if use_gpu:
+            if use_gpu and backend == "nccl":
                 kw["device_id"] = dev
             dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     return DistEnv(rank, world, local, dev, backend)
@@ -90,6 +97,7 @@ class Unit:
     host: int = 0
     state_offs: List[int] = field(default_factory=list)
     shard_buf: Optional[torch.Tensor] = None
+    bucket: int = -1                # flat plan: index into plan.bucket_ranges
 
 
 def quirk_coefficient(plan: ShardPlan, rank: int, world: int, ref_quirks: bool) -> float:
@@ -151,7 +159,7 @@ class SyncExchange:
             for bi, (lo, hi) in enumerate(plan.bucket_ranges):
                 ts = tensors_in(lo, hi)
                 if self.collective and plan.num_ps == W:
-                    u = Unit("rs", ts, [(lo, hi)])
+                    u = Unit("rs", ts, [(lo, hi)], bucket=bi)
                     c = (hi - lo) // W
                     u.shard_buf = torch.empty(c, dtype=torch.float32, device=self.params.device)
                     if self.env.rank in self.servers:

@@ -14,6 +14,13 @@ multi-GPU job, a collective self-test (reduce-scatter/all-gather and reduce/broa
 known pattern) runs on every rank and the decision to use it is agreed by all ranks.
 PS state (``m``/``v``/step counter ``t``) stays in the Python ``ParameterServer`` objects, so
 checkpointing and inspection are unchanged.
+
+``backend="xgmi"`` (flat plan, one PS per GPU): instead of RCCL, each bucket is ONE fused kernel
+over IPC-mapped peer memory (``csrc/kernels/xgmi.hip``): push gradient chunks to their owners,
+owner sum + Adam, push the parameters back.  Set up collectively (IPC handles all-gathered over
+the default group) and verified by a self-test on a known pattern whose result all ranks vote
+on; it needs no RCCL communicator, so it also runs with several ranks on ONE GPU (gloo default
+group) — the multi-process rehearsal of the W > 1 step on a one-GPU box.
 """
 from __future__ import annotations
 
@@ -30,7 +37,7 @@ from .comm import DistEnv, SyncExchange
 from .ps import ParameterServer
 from .sharding import ShardPlan
 
-_KIND = {"local": 0, "rs": 1, "reduce": 2}
+_KIND = {"local": 0, "rs": 1, "reduce": 2, "xgmi": 3}
 
 
 class NativeUnavailable(RuntimeError):
@@ -44,7 +51,7 @@ class NativeSyncExchange(SyncExchange):
                  segments: Sequence[Sequence[int]], servers: Dict[int, ParameterServer], engine,
                  grad_reduce: str = "sum", ref_quirks: bool = False, overlap: bool = True,
                  optimizer: str = "adam", hyper=None, momentum: float = 0.9,
-                 force_collectives: bool = False):
+                 force_collectives: bool = False, backend: str = "rccl"):
         if optimizer not in ("adam", "momentum"):
             raise NativeUnavailable(f"native runner has no '{optimizer}' update")
         if not params.is_cuda or getattr(engine, "name", "") != "hip":
@@ -57,7 +64,13 @@ class NativeSyncExchange(SyncExchange):
         self.optimizer = optimizer
         ops = native.ops()
         self.runner = ops.SyncRunner(engine.eng, params, grads, env.world, env.rank)
-        if env.world > 1:
+        self.backend = "local" if env.world == 1 and not force_collectives else backend
+        self.peer = None
+        if env.world > 1 and backend == "xgmi":
+            if plan.bucket_ranges is None or plan.num_ps != env.world:
+                raise NativeUnavailable("xgmi exchange needs the flat plan with one PS per GPU")
+            self._init_peer_collectively(ops, env, plan, params, grads)
+        elif env.world > 1:
             self._init_comm_collectively(ops, env)
         elif force_collectives:
             self.runner.init_comm(ops.SyncRunner.unique_id(), True)
@@ -77,9 +90,11 @@ class NativeSyncExchange(SyncExchange):
             srv = servers.get(ps)
             offs = u.state_offs or [0] * len(u.ranges)
             ranges = [(int(lo), int(hi), int(off)) for (lo, hi), off in zip(u.ranges, offs)]
-            units.append((seg_of(u.tensors), _KIND[u.kind], int(u.host), int(ps), ranges,
+            kind = "xgmi" if (self.peer is not None and u.kind == "rs") else u.kind
+            units.append((seg_of(u.tensors), _KIND[kind], int(u.host), int(ps), ranges,
                           srv.m if srv is not None else None,
-                          srv.v if srv is not None else None, u.shard_buf))
+                          srv.v if srv is not None else None,
+                          None if kind == "xgmi" else u.shard_buf, int(u.bucket)))
         self.runner.set_units(units)
         h = hyper if hyper is not None else next(iter(servers.values())).h
         self.runner.set_optimizer(0 if optimizer == "adam" else 1, h.lr, h.beta1, h.beta2, h.eps,
@@ -117,6 +132,59 @@ class NativeSyncExchange(SyncExchange):
         ok, why = self.runner.selftest()
         agree(ok, why, "RCCL self-test")
 
+    def _init_peer_collectively(self, ops, env: DistEnv, plan: ShardPlan, params: torch.Tensor,
+                                grads: torch.Tensor) -> None:
+        """IPC handles out and in, then a self-test: every rank fills its gradients with
+        (rank + 1) * (i % 13 + 1), one exchange with w := sum of g must give
+        W (W + 1) / 2 * (i % 13 + 1) everywhere (exact in fp32).  Every stage is voted on, so
+        a failure anywhere makes all ranks fall back together."""
+        def agree(ok: bool, why: str, what: str) -> None:
+            votes = [None] * env.world
+            dist.all_gather_object(votes, (bool(ok), why))
+            bad = [(r, w) for r, (o, w) in enumerate(votes) if not o]
+            if bad:
+                raise NativeUnavailable(f"{what} failed on ranks {bad}")
+
+        peer, why = None, ""
+        try:
+            peer = ops.PeerExchange(params, grads, env.world, env.rank,
+                                    [tuple(map(int, b)) for b in plan.bucket_ranges])
+            mine = peer.handle()
+        except RuntimeError as e:
+            mine, why = None, str(e)
+        agree(mine is not None, why, "xGMI buffer export")
+        handles = [None] * env.world
+        dist.all_gather_object(handles, mine)
+        try:
+            peer.open(handles)
+            why = ""
+        except RuntimeError as e:
+            why = str(e)
+        agree(not why, why, "xGMI peer mapping")
+        self.runner.set_peer(peer)
+        self.peer = peer
+        saved = params.clone()
+        n = params.numel()
+        i = torch.arange(n, device=params.device)
+        pat = (i % 13 + 1).to(torch.float32)
+        grads.copy_(pat * float(env.rank + 1))
+        torch.cuda.synchronize(params.device)
+        self.runner.peer_selftest_step()
+        want = pat * float(env.world * (env.world + 1) // 2)
+        ok, why = True, ""
+        if peer.error():
+            ok, why = False, f"timed out (code {peer.error()})"
+        else:
+            for lo, hi in plan.bucket_ranges:
+                if not torch.equal(params[lo:hi], want[lo:hi]):
+                    bad = int((params[lo:hi] != want[lo:hi]).nonzero()[0]) + lo
+                    ok, why = False, f"mismatch at {bad}: {float(params[bad])} != {float(want[bad])}"
+                    break
+        params.copy_(saved)
+        grads.zero_()
+        torch.cuda.synchronize(params.device)
+        agree(ok, why, "xGMI self-test")
+
     def step(self, x: torch.Tensor, labels: torch.Tensor, keep_prob: float, seed: int) -> None:
         """One synchronous global step: every hosted PS advances its step counter (one
         ``apply_gradients`` per global step, like the reference PS) and the runner enqueues
@@ -148,10 +216,11 @@ def make_sync_exchange(plan, env, params, grads, segments, servers, engine, cfg,
     exchange.  On a multi-GPU job the choice is collective (self-test votes)."""
     if cfg.native_exchange:
         try:
+            backend = cfg.exchange_backend if cfg.exchange_backend != "auto" else "rccl"
             return NativeSyncExchange(plan, env, params, grads, segments, servers, engine,
                                       cfg.grad_reduce, cfg.ref_quirks, cfg.overlap,
                                       cfg.optimizer, hyper, cfg.momentum,
-                                      force_collectives=cfg.force_collectives)
+                                      force_collectives=cfg.force_collectives, backend=backend)
         except NativeUnavailable as e:
             if env.rank == 0 and getattr(engine, "name", "") == "hip":
                 print(f"[ddl_amd] native sync runner unavailable ({e}); using the Python "
