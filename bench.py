@@ -57,6 +57,14 @@ def main(argv=None):
                     help="W = 1 rehearsal of the multi-GPU step: keep the reduce-scatter / "
                          "all-gather units on a 1-rank RCCL communicator (comm stream, events, "
                          "RCCL launches) instead of the local update")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "rccl", "xgmi"],
+                    help="W > 1 data plane of the native sync runner: RCCL reduce-scatter / "
+                         "all-gather, or the fused xGMI peer-memory exchange (one push / "
+                         "owner-Adam / pull kernel per bucket).  auto: both are set up and "
+                         "timed on a short A/B before the warmup, the faster one is benchmarked "
+                         "(both timings are reported)")
+    ap.add_argument("--ab-steps", type=int, default=30,
+                    help="timed steps per candidate of the --exchange auto A/B")
     ap.add_argument("--splits", default=None, help="comma-separated split-K factors per op")
     ap.add_argument("--tta", type=float, default=0.95,
                     help="after the throughput run, train one reference epoch (500 steps/worker, "
@@ -81,22 +89,94 @@ def main(argv=None):
         if env.rank == 0:
             print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     total_steps = a.warmup + a.steps
-    cfg = TrainConfig(mode=a.mode, shard=a.shard, steps=total_steps, batch_size=a.batch_size,
-                      eval_every=0, engine=a.engine, graph=a.graph and not a.no_graph,
-                      overlap=not a.no_overlap, quiet=True, data_sharding="stride",
-                      native_exchange=not a.no_native_exchange,
-                      force_collectives=a.force_collectives)
-    data = synthetic_mnist()
-    tr = Trainer(cfg, env, dataset=data)
-    if a.splits and hasattr(tr.engine, "set_splits"):
-        tr.engine.set_splits([int(s) for s in a.splits.split(",")])
     cuda = env.device.type == "cuda"
+    data = synthetic_mnist()
+
+    def make_trainer(backend):
+        cfg = TrainConfig(mode=a.mode, shard=a.shard, steps=total_steps, batch_size=a.batch_size,
+                          eval_every=0, engine=a.engine, graph=a.graph and not a.no_graph,
+                          overlap=not a.no_overlap, quiet=True, data_sharding="stride",
+                          native_exchange=not a.no_native_exchange,
+                          force_collectives=a.force_collectives, exchange_backend=backend)
+        t = Trainer(cfg, env, dataset=data)
+        if a.splits and hasattr(t.engine, "set_splits"):
+            t.engine.set_splits([int(s) for s in a.splits.split(",")])
+        return t
 
     def sync():
         if cuda:
             torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=env.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def backend_of(t) -> str:
+        ex = t.exchange
+        if not getattr(ex, "native", False):
+            return "python"
+        return "native-" + getattr(ex, "backend", "rccl")
+
+    # W > 1, sync, flat plan: the xGMI exchange is a candidate next to RCCL.  With several ranks
+    # on one GPU (DDL_DIST_BACKEND=gloo rehearsal) RCCL cannot run, so xgmi is the only one.
+    shared_gpu = os.environ.get("DDL_DIST_BACKEND", "") == "gloo" and cuda
+    candidates = [a.exchange]
+    if a.exchange == "auto":
+        candidates = ["rccl"]
+        if world > 1 and a.mode == "sync" and a.shard == "flat" and cuda:
+            candidates = ["xgmi"] if shared_gpu else ["rccl", "xgmi"]
+    ab = {}
+    tr = None
+    if len(candidates) > 1:
+        # short A/B before the benchmark proper (a wait that times out in the xGMI path raises
+        # at the next step on that rank; every rank votes, so a failed candidate is dropped
+        # by all ranks together)
+        best = None
+        for c in candidates:
+            try:
+                t = make_trainer(c)
+            except Exception as e:  # noqa: BLE001 - reported, not fatal for the other candidate
+                ab[c] = {"error": str(e)[:200]}
+                t = None
+            ok, ms = t is not None, None
+            if ok:
+                try:
+                    for i in range(5):
+                        t.train_step(i)
+                    sync()
+                    t0 = time.perf_counter()
+                    for i in range(5, 5 + a.ab_steps):
+                        t.train_step(i)
+                    sync()
+                    ms = 1e3 * (time.perf_counter() - t0) / a.ab_steps
+                    if hasattr(t.exchange, "check"):
+                        t.exchange.check()
+                except RuntimeError as e:
+                    ok = False
+                    ab[c] = {"error": str(e)[:200]}
+            votes = [None] * world
+            dist.all_gather_object(votes, bool(ok))
+            if not all(votes):
+                ab.setdefault(c, {"error": "failed on some rank"})
+                continue
+            ms = max_over_ranks(ms)
+            ab[c] = {"ms_per_step": round(ms, 4), "exchange": backend_of(t)}
+            if best is None or ms < best[0]:
+                best = (ms, c, t)
+        if best is None:
+            raise RuntimeError(f"no exchange candidate worked: {ab}")
+        chosen, tr = best[1], best[2]
+        # a fresh trainer for the benchmark proper: identical initial state for every choice
+        tr = make_trainer(chosen)
+    else:
+        chosen = candidates[0]
+        tr = make_trainer(chosen)
+    cfg = tr.cfg
 
     if a.mode == "async":
         tr.exchange.steps = total_steps
@@ -110,11 +190,7 @@ def main(argv=None):
     if a.mode == "async":
         tr.exchange.join()
     sync()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=env.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0)
     ms = 1e3 * elapsed / a.steps
     imgs = world * a.batch_size * a.steps / elapsed
     acc = tr.evaluate()
@@ -125,7 +201,7 @@ def main(argv=None):
                            engine=a.engine, graph=a.graph and not a.no_graph,
                            overlap=not a.no_overlap, quiet=True, target_acc=a.tta,
                            data_sharding="stride", native_exchange=not a.no_native_exchange,
-                           eval_async=cuda and not a.tta_sync_eval)
+                           eval_async=cuda and not a.tta_sync_eval, exchange_backend=chosen)
         tr2 = Trainer(cfg2, env, dataset=data)
         s = tr2.train()
         tta = {"target_acc": a.tta, "time_to_target_s": s["time_to_target"],
@@ -159,12 +235,17 @@ def main(argv=None):
                 "engine": engine_name,
                 "hip_graph": bool(a.graph and not a.no_graph),
                 "overlap": not a.no_overlap,
-                "exchange": "native" if getattr(tr.exchange, "native", False) else "python",
+                "exchange": backend_of(tr),
                 "forced_1rank_collectives": bool(a.force_collectives),
                 "optimizer": "adam(1e-4) on PS shards",
             },
             "test_acc_after_run": round(acc, 4),
         }
+        if ab:
+            rec["exchange_ab"] = ab
+        if shared_gpu and world > 1:
+            rec["note"] = (f"{world} ranks share ONE GPU (DDL_DIST_BACKEND=gloo rehearsal): "
+                           "functional check of the W > 1 path, not a multi-GPU measurement")
         if tta is not None:
             rec["time_to_acc"] = tta
         print(json.dumps(rec), flush=True)
