@@ -18,10 +18,10 @@
 //            (write-through, system scope), drain, then ARRIVE_r[b][me][j] = e
 //   phase 2  wait ARRIVE_me[b][q][j] >= e for every peer q; sum the W contributions in rank order
 //            (deterministic), optimizer update of my chunk's slice, store the new parameters to
-//            EVERY rank's parameter buffer (self included, write-through), drain, DONE_q[b][me][j] = e
-//   final    (the step's last bucket, on the compute stream) wait DONE_me[b'][q][*] >= e for every
-//            bucket and rank: when the kernel ends, every parameter of this step has landed and the
-//            next forward (a later kernel: L2 invalidated at its start) reads them.
+//            EVERY rank's parameter buffer (self included, write-through), drain, DONE_q[b][me] += 1
+//   final    (the step's last bucket, on the compute stream) wait DONE_me[b'][q] >= e * nslices[b']
+//            for every bucket and rank: when the kernel ends, every parameter of this step has
+//            landed and the next forward (a later kernel: L2 invalidated at its start) reads them.
 // Buffer reuse is safe by construction: a rank overwrites an inbox slot (step e+1 backward) only
 // after its step e+1 forward, i.e. after the final wait saw every owner's DONE of step e, which
 // each owner sets after reading that slot; an owner writes a peer's parameters of bucket b only
@@ -65,14 +65,17 @@ DDL_DEV void flag_store(uint32_t* f, uint32_t v) {
 }
 
 DDL_DEV int arrive_idx(int b, int src, int j) { return (b * kXgmiMaxPeers + src) * kXgmiMaxSlices + j; }
-DDL_DEV int done_idx(int b, int src, int j) {
-  return kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices + arrive_idx(b, src, j);
+// one completion counter per (bucket, owner): every workgroup of the owner's kernel adds 1, so
+// at step e it reaches e * nslices[b]; the final wait is then ONE parallel poll of buckets x W
+// words instead of a poll per slice
+DDL_DEV int done_idx(int b, int src) {
+  return kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices + b * kXgmiMaxPeers + src;
 }
 
-// Bounded wait until *f >= epoch (wrap-safe).  false on timeout or when another workgroup
+// Bounded wait until *f >= target (wrap-safe).  false on timeout or when another workgroup
 // already reported an error (then the caller just runs to the end).
-DDL_DEV bool wait_ge(const uint32_t* f, uint32_t epoch, long long deadline, int* err, int code) {
-  while ((int32_t)(flag_load(f) - epoch) < 0) {
+DDL_DEV bool wait_ge(const uint32_t* f, uint32_t target, long long deadline, int* err, int code) {
+  while ((int32_t)(flag_load(f) - target) < 0) {
     if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return false;
     if (wall_clock64() > deadline) {
       __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -83,41 +86,53 @@ DDL_DEV bool wait_ge(const uint32_t* f, uint32_t epoch, long long deadline, int*
   return true;
 }
 
+DDL_DEV float4 scale4(float4 x, float a) {
+  x.x *= a; x.y *= a; x.z *= a; x.w *= a;
+  return x;
+}
+
+// WT = world size when instantiated for it (loops over ranks fully unrolled: all of an
+// element's remote loads / stores are in flight together), 0 = any world size.
+template <int WT>
 __global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a) {
-  const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-  const int W = a.world, me = a.rank, b = a.bucket;
+  constexpr int NQ = WT ? WT : kXgmiMaxPeers;
+  const int j = blockIdx.x, tid = threadIdx.x;
+  const int W = WT ? WT : a.world, me = a.rank, b = a.bucket;
   const long long deadline = wall_clock64() + a.timeout_ticks;
   const int64_t s0 = (int64_t)j * a.slice;
   const int64_t s1 = s0 + a.slice < a.c ? s0 + a.slice : a.c;
   const int n4 = s0 < s1 ? (int)((s1 - s0) >> 2) : 0;
   uint32_t* myflags = T.flags[me];
 
-  // ---- phase 1: push my gradient pieces to their owners (start at a different owner per
-  // workgroup so the W-1 links carry traffic at once)
-  for (int k = 0; k < W - 1; ++k) {
-    const int r = (me + 1 + (k + j) % (W - 1)) % W;
-    const float4* src = reinterpret_cast<const float4*>(a.grads + a.lo + r * a.c + s0);
-    const brsrc_t dst = make_rsrc(T.inbox[r] + a.inbox_off + (int64_t)me * a.c + s0,
-                                  (uint32_t)n4 * 16u);
-    for (int i = tid; i < n4; i += 256) {
-      float4 x = src[i];
-      if (a.coef != 1.f) { x.x *= a.coef; x.y *= a.coef; x.z *= a.coef; x.w *= a.coef; }
-      st4_sys(dst, i * 16, x);
+  // ---- phase 1: push my gradient pieces to their owners.  Per element index every owner's
+  // load is issued before the first store; workgroup j starts at a different owner so the
+  // W-1 links carry traffic at once.
+  for (int i = tid; i < n4; i += 256) {
+    float4 x[NQ - 1];
+#pragma unroll
+    for (int k = 0; k < NQ - 1; ++k) {
+      if (k < W - 1) {
+        const int r = (me + 1 + (k + j) % (W - 1)) % W;
+        x[k] = reinterpret_cast<const float4*>(a.grads + a.lo + r * a.c + s0)[i];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NQ - 1; ++k) {
+      if (k < W - 1) {
+        const int r = (me + 1 + (k + j) % (W - 1)) % W;
+        const brsrc_t dst = make_rsrc(T.inbox[r] + a.inbox_off + (int64_t)me * a.c + s0,
+                                      (uint32_t)n4 * 16u);
+        st4_sys(dst, i * 16, a.coef != 1.f ? scale4(x[k], a.coef) : x[k]);
+      }
     }
   }
   drain_vm();
   __syncthreads();
-  if (tid == 0)
-    for (int r = 0; r < W; ++r)
-      if (r != me) flag_store(T.flags[r] + arrive_idx(b, me, j), a.epoch);
+  if (tid < W && tid != me) flag_store(T.flags[tid] + arrive_idx(b, me, j), a.epoch);
 
-  // ---- phase 2: every peer's piece of my slice has arrived
-  if (tid < 64) {
-    bool ok = true;
-    if (lane < W && lane != me) ok = wait_ge(myflags + arrive_idx(b, lane, j), a.epoch, deadline,
-                                             a.err, 1);
-    (void)ok;
-  }
+  // ---- phase 2: every peer's piece of my slice has arrived (one parallel poll)
+  if (tid < W && tid != me)
+    wait_ge(myflags + arrive_idx(b, tid, j), a.epoch, deadline, a.err, 1);
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // keep the loads below the poll
 
@@ -127,27 +142,27 @@ __global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a)
   float4* v4 = a.v ? reinterpret_cast<float4*>(a.v + s0) : nullptr;
   float4* w4 = reinterpret_cast<float4*>(T.params[me] + a.lo + me * a.c + s0);
   for (int i = tid; i < n4; i += 256) {
-    float4 g = f4zero();
-    for (int q = 0; q < W; ++q) {  // rank order: the same sum on every run
-      float4 x;
-      if (q == me) {
-        x = own[i];
-        if (a.coef != 1.f) { x.x *= a.coef; x.y *= a.coef; x.z *= a.coef; x.w *= a.coef; }
-      } else {
-        x = ld4_sys(inbox, (int)(((int64_t)q * a.c + s0) * 4) + i * 16);
-      }
-      g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
-    }
+    float4 x[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      if (q < W)
+        x[q] = q == me ? (a.coef != 1.f ? scale4(own[i], a.coef) : own[i])
+                       : ld4_sys(inbox, (int)(((int64_t)q * a.c + s0) * 4) + i * 16);
     float4 w = w4[i];
+    float4 M = f4zero(), V = f4zero();
+    if (a.opt == 0) { M = m4[i]; V = v4[i]; }
+    else if (a.opt == 1) M = m4[i];
+    float4 g = f4zero();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)  // rank order: the same sum on every run and every rank count
+      if (q < W) { g.x += x[q].x; g.y += x[q].y; g.z += x[q].z; g.w += x[q].w; }
     if (a.opt == 0) {  // TF1 Adam (optim.hip form)
-      float4 M = m4[i], V = v4[i];
       adam1(w.x, g.x * a.scale, M.x, V.x, a.lr_t, a.c1, a.c2, a.eps);
       adam1(w.y, g.y * a.scale, M.y, V.y, a.lr_t, a.c1, a.c2, a.eps);
       adam1(w.z, g.z * a.scale, M.z, V.z, a.lr_t, a.c1, a.c2, a.eps);
       adam1(w.w, g.w * a.scale, M.w, V.w, a.lr_t, a.c1, a.c2, a.eps);
       m4[i] = M; v4[i] = V;
     } else if (a.opt == 1) {  // momentum SGD (optim.hip momentum_kernel form)
-      float4 M = m4[i];
       M.x = M.x * a.mu + g.x * a.scale; w.x -= a.lr * M.x;
       M.y = M.y * a.mu + g.y * a.scale; w.y -= a.lr * M.y;
       M.z = M.z * a.mu + g.z * a.scale; w.z -= a.lr * M.z;
@@ -158,22 +173,26 @@ __global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a)
     }
     // every rank's copy, this one included: write-through, so a later kernel of any rank
     // (other XCD, other GPU) reads it from memory even while this kernel is still running
-    for (int k = 0; k < W; ++k) {
-      const int q = (me + k + j) % W;
-      const brsrc_t dst = make_rsrc(T.params[q] + a.lo + me * a.c + s0, (uint32_t)n4 * 16u);
-      st4_sys(dst, i * 16, w);
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      if (k < W) {
+        const int q = (me + k + j) % W;
+        const brsrc_t dst = make_rsrc(T.params[q] + a.lo + me * a.c + s0, (uint32_t)n4 * 16u);
+        st4_sys(dst, i * 16, w);
+      }
     }
   }
   drain_vm();
   __syncthreads();
-  if (tid == 0)
-    for (int q = 0; q < W; ++q) flag_store(T.flags[q] + done_idx(b, me, j), a.epoch);
+  if (tid < W)
+    __hip_atomic_fetch_add(T.flags[tid] + done_idx(b, me), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 
   // ---- final wait: every bucket's new parameters from every owner have landed here
-  if (a.final_wait && tid < 64) {
-    for (int bb = 0; bb < a.nbuckets; ++bb)
-      for (int jj = j; jj < a.nslices[bb]; jj += gridDim.x)
-        if (lane < W) wait_ge(myflags + done_idx(bb, lane, jj), a.epoch, deadline, a.err, 2);
+  // (one lane per (bucket, owner) counter, all polled at once)
+  if (a.final_wait && tid < a.nbuckets * W) {
+    const int bb = tid / W, q = tid - bb * W;
+    wait_ge(myflags + done_idx(bb, q), a.epoch * (uint32_t)a.nslices[bb], deadline, a.err, 2);
   }
 }
 
@@ -225,7 +244,8 @@ PeerExchange::PeerExchange(float* params, const float* grads, int64_t total, int
   inbox_elems_ = inbox;
   X_CHECK(hipMalloc(&inbox_, inbox_elems_ * sizeof(float)));
   X_CHECK(hipMemset(inbox_, 0, inbox_elems_ * sizeof(float)));
-  flag_bytes_ = 2ull * kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices * sizeof(uint32_t);
+  flag_bytes_ = (size_t)(kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices +
+                         kXgmiMaxBuckets * kXgmiMaxPeers) * sizeof(uint32_t);
   X_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes_,
                                 hipDeviceMallocUncached));
   X_CHECK(hipMemset(flags_, 0, flag_bytes_));
@@ -323,7 +343,13 @@ void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool 
   a.coef = u.coef;
   a.err = err_;
   a.timeout_ticks = (long long)(timeout_s_ * 1e8);  // wall_clock64: 100 MHz
-  hipLaunchKernelGGL(xgmi_ps_kernel, dim3(B.nslice), dim3(256), 0, st, table_, a);
+  switch (world_) {
+#define X_CASE(N) \
+  case N: hipLaunchKernelGGL(xgmi_ps_kernel<N>, dim3(B.nslice), dim3(256), 0, st, table_, a); break;
+    X_CASE(2) X_CASE(3) X_CASE(4) X_CASE(5) X_CASE(6) X_CASE(7) X_CASE(8)
+#undef X_CASE
+    default: hipLaunchKernelGGL(xgmi_ps_kernel<0>, dim3(B.nslice), dim3(256), 0, st, table_, a);
+  }
   DDL_CHECK_LAUNCH();
 }
 

@@ -100,6 +100,7 @@ def _simulate(world, kw):
     (2, {}),
     (3, dict(grad_reduce="mean")),
     (4, dict(overlap=False)),
+    (8, {}),  # the 8-GPU node's size (eight processes time-share the one card here)
 ])
 def test_xgmi_exchange_matches_simulation(tmp_path, world, kw):
     import torch.multiprocessing as mp
