@@ -85,7 +85,10 @@ class PyEngine {
   void set_eval_cfg(std::vector<int64_t> c) {
     TORCH_CHECK((int)c.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " tile configs");
     for (int i = 0; i < ddl::OP_COUNT; ++i) {
-      TORCH_CHECK(c[i] >= 0 && c[i] < ddl::NUM_TILE_CFGS, "tile config out of range");
+      // the eval-only large tiles exist for the conv2-4 forward ops only
+      const bool big = i == ddl::OP_CONV2_FWD || i == ddl::OP_CONV3_FWD || i == ddl::OP_CONV4_FWD;
+      TORCH_CHECK(c[i] >= 0 && c[i] < (big ? ddl::NUM_EVAL_TILE_CFGS : ddl::NUM_TILE_CFGS),
+                  "tile config out of range");
       e_.eval_cfg[i] = (int)c[i];
     }
   }

@@ -61,6 +61,10 @@ enum Op {
 // multi-wave blocks share each staged operand tile between waves (half the L1/L2 bytes per
 // MFMA of one-wave 32x32 blocks at 64x64), at one barrier per K tile.
 constexpr int NUM_TILE_CFGS = 9;
+// Eval-only large-M configs (conv forward ops at 10k-row test-set chunks; no split-K, so only
+// instantiated for those ops): 9 = 128x128 (2x2 waves of 64x64), 10 = 128x64 (2x2 waves of
+// 64x32), 11 = 256x64 (4x1 waves of 64x64), 12 = 128x128 (4x1 waves of 32x128).
+constexpr int NUM_EVAL_TILE_CFGS = 13;
 
 struct Engine {
   const float* P[14] = {};   // parameter tensors v0..v13 (any flat layout)

@@ -36,9 +36,12 @@ Engine::Engine() {
   memcpy(cfg, defc, sizeof(defc));
   memcpy(eval_cfg, defc, sizeof(defc));
   // eval forward at 10k-row chunks (scripts/eval_sweep.py, after the compact conv3 rows):
-  // conv2-4 on 4-wave 64x64 blocks, full test-set eval 6.76 -> 6.66 ms (106 TF)
+  // conv2-4 on 4-wave 64x64 blocks, full test-set eval 6.76 -> 6.66 ms (106 TF); round 2:
+  // conv3 on the eval-only 128x128 block (2x2 waves of 64x64), 6.62 -> 6.53 ms (108 TF) —
+  // the larger eval tiles (9-12) gain at most 1.4 %, so the eval is bound by the main loop,
+  // not by tile shape (profiles/r2_eval_sweep_big_tiles.log)
   eval_cfg[OP_CONV2_FWD] = 6;
-  eval_cfg[OP_CONV3_FWD] = 6;
+  eval_cfg[OP_CONV3_FWD] = 9;
   eval_cfg[OP_CONV4_FWD] = 6;
   memcpy(splits, defs, sizeof(defs));
   memcpy(workers, defw, sizeof(defw));

@@ -22,6 +22,11 @@ namespace ddl {
 #define TILE_6 64, 64, 32, 2, 2   // 4 waves of 32x32 sharing one LDS-staged 64x64 block tile
 #define TILE_7 64, 32, 32, 2, 1   // 2 waves of 32x32 along M
 #define TILE_8 32, 64, 32, 1, 2   // 2 waves of 32x32 along N
+// eval-only (conv forward, large M)
+#define TILE_9 128, 128, 32, 2, 2
+#define TILE_10 128, 64, 32, 2, 2
+#define TILE_11 256, 64, 32, 4, 1
+#define TILE_12 128, 128, 32, 4, 1
 
 template <class P>
 inline void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const SplitScratch& sc,
@@ -87,6 +92,17 @@ template <int OP>
 void run_op_inst(Engine& e, const float* x, int B, const uint32_t* seed, bool train,
                      hipStream_t st, int si) {
   const auto p = make_policy<OP>(e, B, x, seed, train);
+  if constexpr (OP == OP_CONV2_FWD || OP == OP_CONV3_FWD || OP == OP_CONV4_FWD) {
+    if (!train && e.eval_cfg[OP] >= NUM_TILE_CFGS) {  // eval-only large tiles, no split
+      switch (e.eval_cfg[OP]) {
+        case 9: launch_gemm<TILE_9>(p, 1, 1, e.scratch[si], st, 0); break;
+        case 10: launch_gemm<TILE_10>(p, 1, 1, e.scratch[si], st, 0); break;
+        case 11: launch_gemm<TILE_11>(p, 1, 1, e.scratch[si], st, 0); break;
+        default: launch_gemm<TILE_12>(p, 1, 1, e.scratch[si], st, 0); break;
+      }
+      return;
+    }
+  }
   launch_cfg(train ? e.cfg[OP] : e.eval_cfg[OP], p, train ? e.splits[OP] : 1,
              train ? e.workers[OP] : 0, e.wide[OP],
              e.scratch[si], st);

@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--chunks", default="2000,5000,10000")
-    ap.add_argument("--cfgs", default="0,1,2,3,4,6,7,8")
+    ap.add_argument("--cfgs", default="0,1,2,3,4,6,7,8,9,10,11,12")
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
     from ddl_amd.models.layout import CANON_OFFSETS, TOTAL_NUMEL
@@ -59,8 +59,12 @@ def main():
             keep, best_t = ec[op], cur
             for c in cfgs:
                 ec[op] = c
-                eng.eng.set_eval_cfg(ec)
+                try:
+                    eng.eng.set_eval_cfg(ec)
+                except RuntimeError:  # eval-only large tiles: conv2-4 forward only
+                    continue
                 t = t_eval()
+                print(f"    op {op} c{c}: {t:.3f} ms", flush=True)
                 if t < best_t * 0.99:
                     keep, best_t = c, t
             ec[op] = keep
