@@ -236,3 +236,20 @@ def test_eval_async_without_hip_engine_falls_back_to_inline_eval():
         tr.train()
         hist.append([(h["step"], h["acc"]) for h in tr.history])
     assert len(hist[0]) == 2 and hist[0] == hist[1]
+
+
+def test_exchange_flag_and_cpu_fallback():
+    """--exchange reaches the config; on a CPU (no HIP engine) the native runner is not
+    available, so the sync exchange falls back to the Python one whatever the flag says."""
+    import argparse
+    from ddl_amd.config import add_args, from_args, TrainConfig
+    from ddl_amd.parallel.comm import DistEnv, SyncExchange
+    from ddl_amd.parallel.roles import Trainer
+    a = add_args(argparse.ArgumentParser()).parse_args(["--exchange", "xgmi", "--shard", "flat"])
+    cfg = from_args(a)
+    assert cfg.exchange_backend == "xgmi"
+    cfg = TrainConfig(mode="sync", shard="flat", steps=1, batch_size=20, eval_every=0,
+                      quiet=True, engine="torch", exchange_backend="xgmi")
+    tr = Trainer(cfg, DistEnv(), dataset=synthetic_mnist(200, 50, seed=1))
+    assert type(tr.exchange) is SyncExchange and not getattr(tr.exchange, "native", False)
+    tr.train_step(0)
