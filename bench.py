@@ -129,10 +129,8 @@ def main(argv=None):
     # on one GPU (DDL_DIST_BACKEND=gloo rehearsal) RCCL cannot run, so xgmi is the only one.
     shared_gpu = os.environ.get("DDL_DIST_BACKEND", "") == "gloo" and cuda
     candidates = [a.exchange]
-    if a.exchange == "auto":
-        candidates = ["rccl"]
-        if world > 1 and a.mode == "sync" and a.shard == "flat" and cuda:
-            candidates = ["xgmi"] if shared_gpu else ["rccl", "xgmi"]
+    if a.exchange == "auto" and world > 1 and a.mode == "sync" and a.shard == "flat" and cuda:
+        candidates = ["xgmi"] if shared_gpu else ["rccl", "xgmi"]
     ab = {}
     tr = None
     if len(candidates) > 1:

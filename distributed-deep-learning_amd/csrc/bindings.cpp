@@ -267,6 +267,65 @@ class PyPeer {
   std::unique_ptr<ddl::PeerExchange> p_;
 };
 
+// asynchronous PS over xGMI peer memory (kernels/xgmi_async.hip); kernels on the current stream
+class PyAsyncPeer {
+ public:
+  PyAsyncPeer(at::Tensor params, at::Tensor grads, int64_t world, int64_t rank, py::list ranges,
+              std::vector<int64_t> hosts, int64_t max_slices)
+      : params_(params), grads_(grads) {
+    check_f32_cuda(params, "params");
+    check_f32_cuda(grads, "grads");
+    TORCH_CHECK(params.numel() == grads.numel(), "params/grads size mismatch");
+    std::vector<std::pair<int64_t, int64_t>> rg;
+    for (auto r : ranges) {
+      auto t = r.cast<py::tuple>();
+      rg.emplace_back(t[0].cast<int64_t>(), t[1].cast<int64_t>());
+    }
+    std::vector<int> h(hosts.begin(), hosts.end());
+    c10::hip::HIPGuard guard(params.device().index());
+    p_ = std::make_unique<ddl::AsyncPeer>(params.data_ptr<float>(), grads.data_ptr<float>(),
+                                          params.numel(), (int)world, (int)rank, rg, h,
+                                          (int)max_slices);
+  }
+  py::bytes handle() const {
+    c10::hip::HIPGuard guard(params_.device().index());
+    return py::bytes(p_->handle());
+  }
+  void open(std::vector<std::string> handles) {
+    c10::hip::HIPGuard guard(params_.device().index());
+    p_->open(handles);
+  }
+  void push_all(double coef) { p_->push_all((float)coef, cur_stream()); }
+  void attach_done(std::string name, bool create) { p_->attach_done(name, create); }
+  bool wait_done(int64_t epoch, double timeout_s) {
+    py::gil_scoped_release nogil;
+    return p_->wait_done((uint32_t)epoch, timeout_s);
+  }
+  // opt: 0 Adam (lr_t, b1, b2, eps), 1 momentum (lr, mu), 2 self-test
+  void apply(int64_t ps, int64_t worker, int64_t epoch, int64_t opt, at::Tensor ps_params,
+             c10::optional<at::Tensor> m, c10::optional<at::Tensor> v, double lr_t, double b1,
+             double b2, double eps, double lr, double mu, double scale) {
+    check_f32_cuda(ps_params, "ps_params");
+    ddl::XgmiUpdate u;
+    u.opt = (int)opt;
+    if (m) { check_f32_cuda(*m, "m"); u.m = m->data_ptr<float>(); }
+    if (v) { check_f32_cuda(*v, "v"); u.v = v->data_ptr<float>(); }
+    u.lr_t = (float)lr_t;
+    u.c1 = 1.f - (float)b1;
+    u.c2 = 1.f - (float)b2;
+    u.eps = (float)eps;
+    u.lr = (float)lr;
+    u.mu = (float)mu;
+    u.scale = (float)scale;
+    p_->apply((int)ps, (int)worker, (uint32_t)epoch, u, ps_params.data_ptr<float>(), cur_stream());
+  }
+  int error() const { return p_->error(); }
+
+ private:
+  at::Tensor params_, grads_;
+  std::unique_ptr<ddl::AsyncPeer> p_;
+};
+
 class PyRunner {
  public:
   PyRunner(PyEngine& eng, at::Tensor params, at::Tensor grads, int64_t world, int64_t rank)
@@ -456,6 +515,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("peer_selftest_step", &PyRunner::peer_selftest_step)
       .def("async_error", &PyRunner::async_error)
       .def("abort", &PyRunner::abort);
+
+  py::class_<PyAsyncPeer>(m, "AsyncPeer")
+      .def(py::init<at::Tensor, at::Tensor, int64_t, int64_t, py::list, std::vector<int64_t>,
+                    int64_t>(),
+           py::arg("params"), py::arg("grads"), py::arg("world"), py::arg("rank"),
+           py::arg("ranges"), py::arg("hosts"), py::arg("max_slices") = 64)
+      .def("handle", &PyAsyncPeer::handle)
+      .def("open", &PyAsyncPeer::open)
+      .def("push_all", &PyAsyncPeer::push_all)
+      .def("attach_done", &PyAsyncPeer::attach_done)
+      .def("wait_done", &PyAsyncPeer::wait_done)
+      .def("apply", &PyAsyncPeer::apply)
+      .def("error", &PyAsyncPeer::error);
 
   py::class_<PyPeer>(m, "PeerExchange")
       .def(py::init<at::Tensor, at::Tensor, int64_t, int64_t, py::list, int64_t>(),

@@ -222,6 +222,61 @@ class PeerExchange {
   bool opened_ok_ = false;
 };
 
+// ---- asynchronous PS over xGMI peer memory (xgmi_async.hip) ----------------------------------
+constexpr int kAsyncMaxPs = 64;
+struct AsyncShard {              // one PS's contiguous range of the flat buffer
+  int64_t lo, n, slice, inbox_off;
+  int host, nslice;
+};
+struct AsyncTable {
+  float* params[kXgmiMaxPeers];  // every rank's worker parameter buffer (IPC-mapped)
+  float* inbox[kXgmiMaxPeers];
+  uint32_t* flags[kXgmiMaxPeers];
+  uint32_t* done;                // DONE[worker][ps] in host memory shared by all ranks
+  AsyncShard shard[kAsyncMaxPs];
+};
+
+class AsyncPeer {
+ public:
+  AsyncPeer(float* params, const float* grads, int64_t total, int world, int rank,
+            const std::vector<std::pair<int64_t, int64_t>>& ps_ranges,
+            const std::vector<int>& ps_host, int max_slices);
+  ~AsyncPeer();
+  std::string handle() const;
+  void open(const std::vector<std::string>& handles);
+  // worker: every PS shard of the gradient (x coef) into its host's inbox slot
+  void push_all(float coef, hipStream_t st);
+  // the DONE counters: a POSIX shm segment (created by one rank, attached by the others)
+  // registered with HIP, so every GPU bumps them and every host polls them directly
+  void attach_done(const std::string& name, bool create);
+  // worker host: wait until every PS has stored round `epoch`'s parameters here (false on
+  // timeout or a recorded kernel error)
+  bool wait_done(uint32_t epoch, double timeout_s);
+  // PS host: apply worker `worker`'s round-`epoch` push to PS `ps` (private copy ps_params,
+  // optimizer state in u) and store the new shard into that worker's parameter buffer
+  void apply(int ps, int worker, uint32_t epoch, const XgmiUpdate& u, float* ps_params,
+             hipStream_t st);
+  int error() const;
+  int num_ps() const { return nps_; }
+
+ private:
+  float* params_;
+  const float* grads_;
+  int world_, rank_, nps_ = 0;
+  AsyncTable table_;
+  float* inbox_ = nullptr;
+  int64_t inbox_elems_ = 0;
+  uint32_t* flags_ = nullptr;
+  int* err_ = nullptr;
+  double timeout_s_ = 60.0;
+  void* opened_[kXgmiMaxPeers][3] = {};
+  bool opened_ok_ = false;
+  uint32_t* done_host_ = nullptr;
+  size_t done_bytes_ = 0;
+  std::string done_name_;
+  bool done_owner_ = false;
+};
+
 class SyncRunner {
  public:
   static constexpr int kSegments = 4;

@@ -1,0 +1,390 @@
+// Asynchronous parameter server over xGMI peer memory (SURVEY.md §2.3 async PS, §7.3 hard
+// part 1).
+//
+// Reference behaviour (mnist_async_sharding/worker.py:30-37,88-94; parameter_server.py:94-111):
+// every worker Sends each gradient tensor to its PS and blocks in Recv for the parameters; the
+// PS Recvs from ANY_SOURCE, applies Adam per arrival (its own step counter) and Sends the
+// parameters back to whoever sent.  Staleness is at most one step per worker.
+//
+// A worker round:
+//   push_all  (worker stream)  one kernel: every PS shard of the gradient -> that PS host's
+//             inbox slot [ps][worker] (system write-through stores), ARRIVE[ps][worker] += 1
+//             per workgroup at the host
+//   post      (worker host, after the push kernel completed) (worker, ps) tokens into each PS
+//             host's arrival mailbox
+//   apply     (PS host, its PS stream, issued by the host's service thread in arrival order)
+//             Adam on the PS's private parameter copy (one step of its counter t per arrival,
+//             atomic per shard: the reference's per-tag mixing race Q3 cannot happen), store
+//             the new shard into the WORKER's parameter buffer, then DONE[worker][ps] += 1 per
+//             workgroup in host memory shared by all ranks (POSIX shm registered with HIP)
+//   wait      (worker host) polls DONE[me][*] >= e * nslices, then enqueues the next forward
+// NO kernel of this protocol waits for another kernel.  HIP multiplexes streams onto a few
+// hardware queues (GPU_MAX_HW_QUEUES), so a spinning kernel can sit in front of the very kernel
+// it waits for; with applies of many workers interleaving on every PS stream such a cycle is
+// reachable.  Here the apply is issued only after the push it reads has completed (the token is
+// posted after the push kernel's completion), and the worker's wait is on the host, so every
+// GPU queue only ever holds kernels that can run to completion.  The apply still checks the
+// arrival counter (bounded) as a guard, and records an error word instead of hanging.
+#include <fcntl.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <stdexcept>
+#include <string>
+#include <thread>
+
+#include "api.h"
+#include "common.h"
+
+namespace ddl {
+
+namespace {
+
+constexpr unsigned kSys = 1u | 16u;  // sc0 | sc1: system-coherent buffer op
+
+DDL_DEV void st4_sys(brsrc_t r, int byte_off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(
+      __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), r, byte_off, 0,
+      kSys);
+}
+DDL_DEV float4 ld4_sys(brsrc_t r, int byte_off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kSys);
+  return *reinterpret_cast<float4*>(&v);
+}
+DDL_DEV void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+DDL_DEV bool wait_ge(const uint32_t* f, uint32_t target, long long deadline, int* err, int code) {
+  while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) <
+         0) {
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return false;
+    if (wall_clock64() > deadline) {
+      __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return true;
+}
+DDL_DEV void bump(uint32_t* f) {
+  __hip_atomic_fetch_add(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// arrival words of one rank: ARRIVE[ps][src]
+DDL_DEV int arrive_idx(int p, int src) { return p * kXgmiMaxPeers + src; }
+
+struct PushArgs {
+  int world, rank, nps;
+  int first_blk[kAsyncMaxPs + 1];  // block range of PS p: [first_blk[p], first_blk[p+1])
+  const float* grads;
+  float coef;
+};
+
+__global__ void __launch_bounds__(256) async_push_kernel(AsyncTable T, PushArgs a) {
+  const int blk = blockIdx.x, tid = threadIdx.x;
+  int p = 0;
+  while (p + 1 < a.nps && blk >= a.first_blk[p + 1]) ++p;
+  const AsyncShard& S = T.shard[p];
+  const int j = blk - a.first_blk[p];
+  const int64_t s0 = (int64_t)j * S.slice;
+  const int64_t s1 = s0 + S.slice < S.n ? s0 + S.slice : S.n;
+  const int n4 = s0 < s1 ? (int)((s1 - s0) >> 2) : 0;
+  const float4* src = reinterpret_cast<const float4*>(a.grads + S.lo + s0);
+  const brsrc_t dst = make_rsrc(T.inbox[S.host] + S.inbox_off + (int64_t)a.rank * S.n + s0,
+                                (uint32_t)n4 * 16u);
+  for (int i = tid; i < n4; i += 256) {
+    float4 x = src[i];
+    if (a.coef != 1.f) { x.x *= a.coef; x.y *= a.coef; x.z *= a.coef; x.w *= a.coef; }
+    st4_sys(dst, i * 16, x);
+  }
+  drain_vm();
+  __syncthreads();
+  if (tid == 0) bump(T.flags[S.host] + arrive_idx(p, a.rank));
+}
+
+struct ApplyArgs {
+  int me, ps, worker;
+  uint32_t epoch;
+  float* ps_params;  // the PS's private parameter copy of its shard [n]
+  float* m;
+  float* v;
+  int opt;
+  float lr_t, c1, c2, eps, lr, mu, scale;
+  int* err;
+  long long timeout_ticks;
+};
+
+__global__ void __launch_bounds__(256) async_apply_kernel(AsyncTable T, ApplyArgs a) {
+  const long long deadline = wall_clock64() + a.timeout_ticks;
+  const AsyncShard& S = T.shard[a.ps];
+  const int j = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0)
+    wait_ge(T.flags[a.me] + arrive_idx(a.ps, a.worker), a.epoch * (uint32_t)S.nslice, deadline,
+            a.err, 1);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // keep the loads below the poll
+  const int64_t s0 = (int64_t)j * S.slice;
+  const int64_t s1 = s0 + S.slice < S.n ? s0 + S.slice : S.n;
+  const int n4 = s0 < s1 ? (int)((s1 - s0) >> 2) : 0;
+  const brsrc_t in = make_rsrc(T.inbox[a.me] + S.inbox_off + (int64_t)a.worker * S.n + s0,
+                               (uint32_t)n4 * 16u);
+  const brsrc_t out = make_rsrc(T.params[a.worker] + S.lo + s0, (uint32_t)n4 * 16u);
+  float4* w4 = reinterpret_cast<float4*>(a.ps_params + s0);
+  float4* m4 = reinterpret_cast<float4*>(a.m + s0);
+  float4* v4 = a.v ? reinterpret_cast<float4*>(a.v + s0) : nullptr;
+  for (int i = tid; i < n4; i += 256) {
+    const float4 g = ld4_sys(in, i * 16);
+    float4 w = w4[i];
+    if (a.opt == 0) {
+      float4 M = m4[i], V = v4[i];
+      adam1(w.x, g.x * a.scale, M.x, V.x, a.lr_t, a.c1, a.c2, a.eps);
+      adam1(w.y, g.y * a.scale, M.y, V.y, a.lr_t, a.c1, a.c2, a.eps);
+      adam1(w.z, g.z * a.scale, M.z, V.z, a.lr_t, a.c1, a.c2, a.eps);
+      adam1(w.w, g.w * a.scale, M.w, V.w, a.lr_t, a.c1, a.c2, a.eps);
+      m4[i] = M; v4[i] = V;
+    } else if (a.opt == 1) {
+      float4 M = m4[i];
+      M.x = M.x * a.mu + g.x * a.scale; w.x -= a.lr * M.x;
+      M.y = M.y * a.mu + g.y * a.scale; w.y -= a.lr * M.y;
+      M.z = M.z * a.mu + g.z * a.scale; w.z -= a.lr * M.z;
+      M.w = M.w * a.mu + g.w * a.scale; w.w -= a.lr * M.w;
+      m4[i] = M;
+    } else {  // self-test: the PS shard := the pushed gradient
+      w = g;
+    }
+    w4[i] = w;
+    st4_sys(out, i * 16, w);
+  }
+  drain_vm();
+  __syncthreads();
+  if (tid == 0) bump(T.done + a.worker * kAsyncMaxPs + a.ps);
+}
+
+#define X_CHECK(x)                                                                        \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess)                                                                 \
+      throw std::runtime_error(std::string("xgmi-async: ") + #x + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct HandleBlob {
+  hipIpcMemHandle_t params, inbox, flags;
+  int64_t params_off;
+  int32_t world, rank;
+};
+
+}  // namespace
+
+AsyncPeer::AsyncPeer(float* params, const float* grads, int64_t total, int world, int rank,
+                     const std::vector<std::pair<int64_t, int64_t>>& ps_ranges,
+                     const std::vector<int>& ps_host, int max_slices)
+    : params_(params), grads_(grads), world_(world), rank_(rank) {
+  if (world < 1 || world > kXgmiMaxPeers) throw std::invalid_argument("async xgmi: world");
+  if (rank < 0 || rank >= world) throw std::invalid_argument("async xgmi: rank");
+  if (ps_ranges.empty() || (int)ps_ranges.size() > kAsyncMaxPs ||
+      ps_ranges.size() != ps_host.size())
+    throw std::invalid_argument("async xgmi: 1..64 PS, one host each");
+  if (max_slices < 1) throw std::invalid_argument("async xgmi: max_slices");
+  if (reinterpret_cast<uintptr_t>(params) % 16 || reinterpret_cast<uintptr_t>(grads) % 16)
+    throw std::invalid_argument("async xgmi: buffers must be 16-B aligned");
+  memset(&table_, 0, sizeof(table_));
+  nps_ = (int)ps_ranges.size();
+  int64_t inbox = 0;
+  for (int p = 0; p < nps_; ++p) {
+    AsyncShard& S = table_.shard[p];
+    S.lo = ps_ranges[p].first;
+    S.n = ps_ranges[p].second - ps_ranges[p].first;
+    S.host = ps_host[p];
+    if (S.lo < 0 || S.n <= 0 || S.lo + S.n > total || S.n % 4 || S.lo % 4)
+      throw std::invalid_argument("async xgmi: PS range must be a 4-aligned slice of the buffer");
+    if (S.host < 0 || S.host >= world) throw std::invalid_argument("async xgmi: PS host");
+    int64_t ns = (S.n + 1023) / 1024;
+    if (ns > max_slices) ns = max_slices;
+    S.slice = ((S.n + ns - 1) / ns + 3) & ~(int64_t)3;
+    S.nslice = (int)((S.n + S.slice - 1) / S.slice);
+    if (S.n * 4 * world > 0x7fffffffLL) throw std::invalid_argument("async xgmi: shard too large");
+  }
+  // inbox of a host: one [W][n] slot block per hosted PS, in PS order (every rank computes
+  // every host's layout identically, so pushes know where to write)
+  std::vector<int64_t> off(world, 0);
+  for (int p = 0; p < nps_; ++p) {
+    AsyncShard& S = table_.shard[p];
+    S.inbox_off = off[S.host];
+    off[S.host] += S.n * world;
+  }
+  inbox = off[rank];
+  inbox_elems_ = inbox > 0 ? inbox : 4;
+  X_CHECK(hipMalloc(&inbox_, inbox_elems_ * sizeof(float)));
+  X_CHECK(hipMemset(inbox_, 0, inbox_elems_ * sizeof(float)));
+  const size_t flag_bytes = (size_t)(kAsyncMaxPs * kXgmiMaxPeers) * sizeof(uint32_t);
+  X_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes,
+                                hipDeviceMallocUncached));
+  X_CHECK(hipMemset(flags_, 0, flag_bytes));
+  X_CHECK(hipHostMalloc(reinterpret_cast<void**>(&err_), 64, hipHostMallocDefault));
+  memset(err_, 0, 64);
+  X_CHECK(hipDeviceSynchronize());
+  const char* t = getenv("DDL_XGMI_TIMEOUT_S");
+  timeout_s_ = t ? atof(t) : 60.0;
+}
+
+AsyncPeer::~AsyncPeer() {
+  for (int q = 0; q < world_; ++q) {
+    if (q == rank_) continue;
+    for (void* p : opened_[q])
+      if (p) (void)hipIpcCloseMemHandle(p);
+  }
+  if (inbox_) (void)hipFree(inbox_);
+  if (flags_) (void)hipFree(flags_);
+  if (err_) (void)hipHostFree(err_);
+  if (done_host_) {
+    (void)hipHostUnregister(done_host_);
+    munmap(done_host_, done_bytes_);
+    if (done_owner_) shm_unlink(done_name_.c_str());
+  }
+}
+
+std::string AsyncPeer::handle() const {
+  HandleBlob h;
+  memset(&h, 0, sizeof(h));
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  X_CHECK(hipMemGetAddressRange(&base, &size, const_cast<float*>(params_)));
+  X_CHECK(hipIpcGetMemHandle(&h.params, base));
+  h.params_off = reinterpret_cast<const char*>(params_) - reinterpret_cast<const char*>(base);
+  X_CHECK(hipIpcGetMemHandle(&h.inbox, inbox_));
+  X_CHECK(hipIpcGetMemHandle(&h.flags, flags_));
+  h.world = world_;
+  h.rank = rank_;
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void AsyncPeer::open(const std::vector<std::string>& handles) {
+  if ((int)handles.size() != world_) throw std::invalid_argument("async xgmi: one handle per rank");
+  for (int q = 0; q < world_; ++q) {
+    if (handles[q].size() != sizeof(HandleBlob)) throw std::invalid_argument("async xgmi: handle");
+    HandleBlob h;
+    memcpy(&h, handles[q].data(), sizeof(h));
+    if (h.world != world_ || h.rank != q) throw std::invalid_argument("async xgmi: handle rank");
+    if (q == rank_) {
+      table_.params[q] = params_;
+      table_.inbox[q] = inbox_;
+      table_.flags[q] = flags_;
+      continue;
+    }
+    void *p = nullptr, *ib = nullptr, *fl = nullptr;
+    X_CHECK(hipIpcOpenMemHandle(&p, h.params, hipIpcMemLazyEnablePeerAccess));
+    opened_[q][0] = p;
+    X_CHECK(hipIpcOpenMemHandle(&ib, h.inbox, hipIpcMemLazyEnablePeerAccess));
+    opened_[q][1] = ib;
+    X_CHECK(hipIpcOpenMemHandle(&fl, h.flags, hipIpcMemLazyEnablePeerAccess));
+    opened_[q][2] = fl;
+    table_.params[q] = reinterpret_cast<float*>(reinterpret_cast<char*>(p) + h.params_off);
+    table_.inbox[q] = reinterpret_cast<float*>(ib);
+    table_.flags[q] = reinterpret_cast<uint32_t*>(fl);
+  }
+  opened_ok_ = true;
+}
+
+void AsyncPeer::push_all(float coef, hipStream_t st) {
+  if (!opened_ok_) throw std::runtime_error("async xgmi: open() first");
+  PushArgs a;
+  memset(&a, 0, sizeof(a));
+  a.world = world_;
+  a.rank = rank_;
+  a.nps = nps_;
+  int blk = 0;
+  for (int p = 0; p < nps_; ++p) {
+    a.first_blk[p] = blk;
+    blk += table_.shard[p].nslice;
+  }
+  a.first_blk[nps_] = blk;
+  a.grads = grads_;
+  a.coef = coef;
+  hipLaunchKernelGGL(async_push_kernel, dim3(blk), dim3(256), 0, st, table_, a);
+  DDL_CHECK_LAUNCH();
+}
+
+void AsyncPeer::attach_done(const std::string& name, bool create) {
+  const size_t bytes = (size_t)world_ * kAsyncMaxPs * sizeof(uint32_t);
+  int fd = -1;
+  if (create) {
+    shm_unlink(name.c_str());  // stale segment of a crashed job
+    fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd >= 0 && ftruncate(fd, (off_t)bytes) != 0) {
+      close(fd);
+      fd = -1;
+    }
+  } else {
+    fd = shm_open(name.c_str(), O_RDWR, 0600);
+  }
+  if (fd < 0) throw std::runtime_error("async xgmi: shm_open failed: " + name);
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) throw std::runtime_error("async xgmi: mmap failed: " + name);
+  if (create) memset(p, 0, bytes);
+  X_CHECK(hipHostRegister(p, bytes, hipHostRegisterMapped));
+  void* dp = nullptr;
+  X_CHECK(hipHostGetDevicePointer(&dp, p, 0));
+  done_host_ = reinterpret_cast<uint32_t*>(p);
+  done_bytes_ = bytes;
+  done_name_ = name;
+  done_owner_ = create;
+  table_.done = reinterpret_cast<uint32_t*>(dp);
+}
+
+bool AsyncPeer::wait_done(uint32_t epoch, double timeout_s) {
+  if (!done_host_) throw std::runtime_error("async xgmi: attach_done() first");
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int spins = 0;; ++spins) {
+    bool all = true;
+    for (int p = 0; p < nps_ && all; ++p) {
+      const uint32_t v = __atomic_load_n(done_host_ + rank_ * kAsyncMaxPs + p, __ATOMIC_ACQUIRE);
+      all = (int32_t)(v - epoch * (uint32_t)table_.shard[p].nslice) >= 0;
+    }
+    if (all) return true;
+    if (error()) return false;
+    if (spins > 256) {
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+        return false;
+      std::this_thread::sleep_for(std::chrono::microseconds(spins > 4096 ? 100 : 2));
+    }
+  }
+}
+
+void AsyncPeer::apply(int ps, int worker, uint32_t epoch, const XgmiUpdate& u, float* ps_params,
+                      hipStream_t st) {
+  if (!opened_ok_ || !table_.done) throw std::runtime_error("async xgmi: open(), attach_done() first");
+  if (ps < 0 || ps >= nps_ || table_.shard[ps].host != rank_)
+    throw std::invalid_argument("async xgmi: apply on a PS this rank does not host");
+  if (worker < 0 || worker >= world_) throw std::invalid_argument("async xgmi: worker");
+  if (u.opt != 2 && !u.m) throw std::invalid_argument("async xgmi: optimizer state missing");
+  if (u.opt == 0 && !u.v) throw std::invalid_argument("async xgmi: Adam needs v");
+  ApplyArgs a;
+  memset(&a, 0, sizeof(a));
+  a.me = rank_;
+  a.ps = ps;
+  a.worker = worker;
+  a.epoch = epoch;
+  a.ps_params = ps_params;
+  a.m = u.m;
+  a.v = u.v;
+  a.opt = u.opt;
+  a.lr_t = u.lr_t;
+  a.c1 = u.c1;
+  a.c2 = u.c2;
+  a.eps = u.eps;
+  a.lr = u.lr;
+  a.mu = u.mu;
+  a.scale = u.scale;
+  a.err = err_;
+  a.timeout_ticks = (long long)(timeout_s_ * 1e8);
+  hipLaunchKernelGGL(async_apply_kernel, dim3(table_.shard[ps].nslice), dim3(256), 0, st, table_,
+                     a);
+  DDL_CHECK_LAUNCH();
+}
+
+int AsyncPeer::error() const { return __atomic_load_n(err_, __ATOMIC_ACQUIRE); }
+
+}  // namespace ddl

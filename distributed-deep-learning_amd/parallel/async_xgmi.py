@@ -1,0 +1,253 @@
+"""Asynchronous parameter server over xGMI peer memory (``csrc/kernels/xgmi_async.hip``).
+
+Reference (``mnist_async_sharding/worker.py:30-37,88-94``,
+``parameter_server.py:94-111``): each worker Sends its gradient tensors to their PS and
+blocks in Recv for the parameters; each PS serves whichever push arrives (``ANY_SOURCE``),
+applies Adam with its own step counter and Sends the parameters back to that worker.
+
+MI355X design (no host staging, no RCCL pair communicators):
+
+* worker step: one ``push_all`` kernel stores every PS shard of the gradient into the PS
+  host's inbox slot for this worker (remote stores over xGMI); once it has completed the host
+  posts ``(worker, ps)`` tokens into each PS host's arrival mailbox (the ``ANY_SOURCE`` order,
+  ``parallel/mailbox.py``) and waits — like the reference's blocking Recv — until every PS
+  has stored the new parameters back (completion counters in host memory shared by all ranks);
+* PS host: a service thread pops tokens in arrival order and enqueues, on its PS stream, an
+  ``apply`` kernel: Adam on the PS's private copy (one step of its counter per arrival, atomic
+  per shard — fixing the reference's per-tag mixing race Q3), store the shard into the
+  worker's parameter buffer, bump the worker's completion counter.  The host never touches
+  the data.
+
+No kernel waits for another kernel (the kernel file says why that matters: HIP multiplexes
+streams onto a few hardware queues), so no interleaving of workers and PS streams can
+deadlock.  Staleness is one round per worker, as in the reference.
+
+Works with several processes on ONE GPU (IPC does, RCCL does not), so the async W > 1 path is
+tested on a one-GPU box (``tests/test_xgmi_gpu.py``).
+"""
+from __future__ import annotations
+
+import threading
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..ops import native
+from ..ops.adam import adam_coeffs
+from . import mailbox as mbox
+from .comm import DistEnv
+from .ps import ParameterServer
+from .sharding import ShardPlan
+
+
+class AsyncPeerUnavailable(RuntimeError):
+    pass
+
+
+class AsyncPeerExchange:
+    backend = "xgmi"
+
+    def __init__(self, plan: ShardPlan, env: DistEnv, params: torch.Tensor, grads: torch.Tensor,
+                 servers: Dict[int, ParameterServer], steps_per_worker: int,
+                 grad_reduce: str = "sum", mailbox_kind: str = "auto", job_id: str = "ddl",
+                 check_provenance: bool = False, optimizer: str = "adam"):
+        if not params.is_cuda or not native.available():
+            raise AsyncPeerUnavailable("async xGMI exchange needs the extension and a GPU")
+        if optimizer not in ("adam", "momentum"):
+            raise AsyncPeerUnavailable(f"async xGMI exchange has no '{optimizer}' update")
+        P, W, r = plan.num_ps, env.world, env.rank
+        for p in range(P):
+            if len(plan.ps_segments(p)) != 1:
+                raise AsyncPeerUnavailable("async mode needs one contiguous range per PS")
+        self.plan, self.env, self.params, self.grads = plan, env, params, grads
+        self.servers = servers
+        self.steps = steps_per_worker
+        self.grad_scale = 1.0  # the async PS applies each worker's gradient as-is
+        self.opt = 0 if optimizer == "adam" else 1
+        self.ranges: List[Tuple[int, int]] = [plan.ps_segments(p)[0] for p in range(P)]
+        self.hosts = [plan.host_rank(p, W) for p in range(P)]
+        ops = native.ops()
+
+        def agree(ok: bool, why: str, what: str) -> None:
+            if W == 1:
+                if not ok:
+                    raise AsyncPeerUnavailable(f"{what} failed: {why}")
+                return
+            votes = [None] * W
+            dist.all_gather_object(votes, (bool(ok), why))
+            bad = [(q, w) for q, (o, w) in enumerate(votes) if not o]
+            if bad:
+                raise AsyncPeerUnavailable(f"{what} failed on ranks {bad}")
+
+        peer, mine, why = None, None, ""
+        try:
+            peer = ops.AsyncPeer(params, grads, W, r, [tuple(map(int, x)) for x in self.ranges],
+                                 [int(h) for h in self.hosts])
+            mine = peer.handle()
+        except RuntimeError as e:
+            why = str(e)
+        agree(mine is not None, why, "async xGMI buffer export")
+        handles = [mine]
+        if W > 1:
+            handles = [None] * W
+            dist.all_gather_object(handles, mine)
+        why = ""
+        try:
+            peer.open(handles)
+        except RuntimeError as e:
+            why = str(e)
+        agree(not why, why, "async xGMI peer mapping")
+        done_name = f"/{job_id}_xdone"
+        why = ""
+        try:
+            if r == 0:
+                peer.attach_done(done_name, True)
+        except RuntimeError as e:
+            why = str(e)
+        agree(not why, why, "async xGMI completion counters (create)")
+        try:
+            if r != 0:
+                peer.attach_done(done_name, False)
+        except RuntimeError as e:
+            why = str(e)
+        agree(not why, why, "async xGMI completion counters (attach)")
+        self.peer = peer
+        self._selftest(agree)
+
+        store = dist.distributed_c10d._get_default_store() if W > 1 else None
+        kind = mailbox_kind if W > 1 else "shm"
+        hosted = [p for p in range(P) if self.hosts[p] == r]
+        self.mailbox = (mbox.make_mailbox(kind, store, f"{job_id}_xmbox_{r}", owner=True)
+                        if hosted else None)
+        if W > 1:
+            dist.barrier()
+        self.boxes = {}
+        for h in set(self.hosts):
+            self.boxes[h] = self.mailbox if h == r else \
+                mbox.make_mailbox(kind, store, f"{job_id}_xmbox_{h}", owner=False)
+        self.coef = 1.0
+        self.timeout_s = 600.0
+        self._thread: Optional[threading.Thread] = None
+        self._error: Optional[BaseException] = None
+        self.served = 0
+        self.check_provenance = check_provenance
+        self.provenance: List[Tuple[int, int, int, int]] = []
+
+    # -- set-up check ------------------------------------------------------------------------------
+    def _selftest(self, agree) -> None:
+        """Round 1 with the self-test update (PS shard := pushed gradient): every worker must
+        get back exactly what it pushed, from every PS."""
+        W, r = self.env.world, self.env.rank
+        dev = self.params.device
+        saved = self.params.clone()
+        n = self.params.numel()
+        pat = (torch.arange(n, device=dev) % 13 + 1).to(torch.float32) * float(r + 1)
+        self.grads.copy_(pat)
+        self.params.zero_()
+        torch.cuda.synchronize(dev)
+        self.peer.push_all(1.0)
+        torch.cuda.synchronize(dev)
+        if W > 1:
+            dist.barrier()  # every push has completed before any apply is issued
+        for p, (lo, hi) in enumerate(self.ranges):
+            if self.hosts[p] != r:
+                continue
+            tmp = torch.empty(hi - lo, device=dev)
+            for w in range(W):
+                self.peer.apply(p, w, 1, 2, tmp, None, None, 0.0, 0.9, 0.999, 1e-8, 0.0, 0.0, 1.0)
+        ok = self.peer.wait_done(1, 60.0)
+        torch.cuda.synchronize(dev)
+        why = f"timed out (code {self.peer.error()})"
+        ok = ok and self.peer.error() == 0
+        if ok:
+            for lo, hi in self.ranges:
+                if not torch.equal(self.params[lo:hi], pat[lo:hi]):
+                    bad = int((self.params[lo:hi] != pat[lo:hi]).nonzero()[0]) + lo
+                    ok, why = False, f"mismatch at {bad}"
+                    break
+        self.params.copy_(saved)
+        self.grads.zero_()
+        torch.cuda.synchronize(dev)
+        agree(ok, why, "async xGMI self-test")
+        self.epoch = 1                                   # worker rounds done
+        self.count = {(w, p): 1 for w in range(W) for p in range(len(self.ranges))}
+
+    # -- PS service thread -------------------------------------------------------------------------
+    def _expected(self) -> int:
+        W, r = self.env.world, self.env.rank
+        return sum(1 for h in self.hosts if h == r) * W * self.steps
+
+    def start(self) -> None:
+        if self._expected() == 0:
+            return
+        self._thread = threading.Thread(target=self._serve, name="ps-xgmi-service", daemon=True)
+        self._thread.start()
+
+    def _serve(self) -> None:
+        try:
+            dev = self.params.device
+            torch.cuda.set_device(dev)
+            for _ in range(self._expected()):
+                v = self.mailbox.pop(600.0)
+                if v is None:
+                    raise TimeoutError("async PS: no arrival within 600 s")
+                w, p = mbox.decode(v)
+                e = self.count[(w, p)] + 1
+                self.count[(w, p)] = e
+                ps = self.servers[p]
+                ps.begin()
+                lr_t = adam_coeffs(ps.h, ps.t) if self.opt == 0 else 0.0
+                with torch.cuda.stream(ps.stream):
+                    self.peer.apply(p, w, e, self.opt, ps.params, ps.m, ps.v, lr_t, ps.h.beta1,
+                                    ps.h.beta2, ps.h.eps, ps.h.lr, ps.momentum, self.grad_scale)
+                if self.check_provenance:
+                    self.provenance.append((w, p, e - 2, ps.t))
+                self.served += 1
+                if self.peer.error():
+                    raise RuntimeError(f"async xGMI wait timed out (code {self.peer.error()})")
+            for p, ps in self.servers.items():
+                ps.stream.synchronize()
+        except BaseException as e:  # surfaced by join()
+            self._error = e
+
+    def join(self) -> None:
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+        if self._error is not None:
+            raise RuntimeError("async xGMI PS service failed") from self._error
+        if self.peer.error():
+            raise RuntimeError(f"async xGMI wait timed out (code {self.peer.error()})")
+
+    def verify_provenance(self) -> None:
+        """Every hosted PS applied exactly `steps` pushes of every worker, in step order, and
+        its step counter advanced once per push."""
+        for p in self.servers:
+            for w in range(self.env.world):
+                steps = [s for (ww, pp, s, _) in self.provenance if ww == w and pp == p]
+                if steps != list(range(self.steps)):
+                    raise RuntimeError(f"provenance: PS {p} / worker {w} steps {steps[:5]}...")
+            ts = [t for (_, pp, _, t) in self.provenance if pp == p]
+            if ts != sorted(ts) or len(set(ts)) != len(ts):
+                raise RuntimeError(f"provenance: PS {p} step counter not strictly increasing")
+
+    # -- worker side --------------------------------------------------------------------------------
+    def push_pull(self) -> None:
+        """Push round e, post it once the push has completed, wait until every PS stored the
+        parameters back (host-side: the reference's blocking pull)."""
+        r = self.env.rank
+        self.peer.push_all(self.coef)
+        ev = torch.cuda.Event()
+        ev.record()
+        ev.synchronize()
+        self.epoch += 1
+        for p in range(len(self.ranges)):
+            self.boxes[self.hosts[p]].push(mbox.encode(r, p))
+        if not self.peer.wait_done(self.epoch, self.timeout_s):
+            raise RuntimeError(f"async xGMI: round {self.epoch} did not come back "
+                               f"(kernel error code {self.peer.error()})")
+
+    def close(self) -> None:
+        if self.mailbox is not None:
+            self.mailbox.close()

@@ -298,6 +298,10 @@ class AsyncExchange:
             if len(plan.ps_segments(p)) != 1:
                 raise ValueError("async mode needs one contiguous range per PS "
                                  "(use a tensor-granular plan or an unbucketed flat plan)")
+        if env.world > 1 and params.is_cuda and env.backend != "nccl":
+            # gloo has no GPU send/recv: the RCCL pair path needs the nccl (RCCL) backend
+            raise RuntimeError("async RCCL-pair exchange needs the nccl backend for GPU tensors "
+                               "(with several ranks on one GPU use --exchange xgmi)")
         self.plan, self.env = plan, env
         self.params, self.grads = params, grads
         self.servers = servers

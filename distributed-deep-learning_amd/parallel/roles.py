@@ -89,16 +89,38 @@ class Trainer:
         self.data = self.data.to(dev)
         self.steps = cfg.steps or (self.data.total_batch // cfg.batch_size)
         if asyncm:
-            self.exchange = AsyncExchange(self.plan, env, self.params, self.grads, self.servers,
-                                          steps_per_worker=self.steps * cfg.epochs,
-                                          grad_reduce=cfg.grad_reduce,
-                                          check_provenance=cfg.check_provenance)
+            self.exchange = self._make_async_exchange(cfg, env)
         else:
             self.exchange = make_sync_exchange(self.plan, env, self.params, self.grads, segs,
                                                self.servers, self.engine, cfg, hyper)
         self.log = metrics.JsonlLogger(cfg.log_jsonl, r)
         self.global_step = 0
         self.history: List[dict] = []
+
+    def _make_async_exchange(self, cfg: TrainConfig, env: DistEnv):
+        """xGMI peer-memory async PS (``async_xgmi.py``) when asked for, or by default at W > 1
+        with the HIP engine; otherwise (or if its collective set-up fails on any rank) the
+        RCCL pair-communicator one (``comm.AsyncExchange``)."""
+        steps = self.steps * cfg.epochs
+        want = cfg.exchange_backend == "xgmi" or (
+            cfg.exchange_backend == "auto" and env.world > 1 and self.engine.name == "hip")
+        if want and env.device.type == "cuda":
+            from .async_xgmi import AsyncPeerExchange, AsyncPeerUnavailable
+            import os
+            try:
+                return AsyncPeerExchange(self.plan, env, self.params, self.grads, self.servers,
+                                         steps_per_worker=steps, grad_reduce=cfg.grad_reduce,
+                                         check_provenance=cfg.check_provenance,
+                                         optimizer=cfg.optimizer,
+                                         job_id=f"ddl{os.environ.get('MASTER_PORT', '')}")
+            except AsyncPeerUnavailable as e:
+                if env.rank == 0:
+                    import sys
+                    print(f"[ddl_amd] async xGMI exchange unavailable ({e}); using RCCL pairs",
+                          file=sys.stderr)
+        return AsyncExchange(self.plan, env, self.params, self.grads, self.servers,
+                             steps_per_worker=steps, grad_reduce=cfg.grad_reduce,
+                             check_provenance=cfg.check_provenance)
 
     # ---- one worker step (reference SyncWorker.work + pull + assign) -----------------------------
     def batch(self, step: int):
@@ -176,7 +198,8 @@ class Trainer:
         single = cfg.mode == "single"
         if cfg.resume and cfg.checkpoint_dir:
             ckpt.load(self, cfg.checkpoint_dir)
-        if isinstance(self.exchange, AsyncExchange):
+        asyncx = cfg.mode == "async"
+        if asyncx:
             self.exchange.start()
         wd = Watchdog(cfg.watchdog_s, name=f"rank{env.rank}", on_timeout=self._on_hang)
         t_target = None
@@ -231,7 +254,7 @@ class Trainer:
         if aeval is not None:
             torch.cuda.current_stream().wait_stream(aeval.train_stream)
             aeval.drain()
-        if isinstance(self.exchange, AsyncExchange):
+        if asyncx:
             self.exchange.join()
             if cfg.check_provenance:
                 self.exchange.verify_provenance()
@@ -254,7 +277,7 @@ class Trainer:
                        images=imgs, images_per_s=imgs / max(train_wall, 1e-9),
                        time_to_target=t_target, steps=self.global_step, plan=self.plan.describe())
         self.log.log(event="final", **summary)
-        if isinstance(self.exchange, AsyncExchange):
+        if asyncx:
             self.exchange.close()
         return summary
 

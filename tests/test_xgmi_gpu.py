@@ -114,3 +114,66 @@ def test_xgmi_exchange_matches_simulation(tmp_path, world, kw):
     got = recs[0]["params"]
     diff = float((got - ref).abs().max())
     assert torch.equal(got, ref), f"max |diff| {diff}"
+
+
+ASYNC_STEPS = 6
+
+
+def _async_rank(rank, world, port, outdir, kw):
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DDL_DIST_BACKEND="gloo",
+                      DDL_XGMI_TIMEOUT_S="20")
+    try:
+        import torch.distributed as dist
+        from ddl_amd.config import TrainConfig
+        from ddl_amd.parallel.async_xgmi import AsyncPeerExchange
+        from ddl_amd.parallel.comm import init_distributed
+        from ddl_amd.parallel.roles import Trainer
+        from ddl_amd.utils.data import synthetic_mnist
+        env = init_distributed()
+        cfg = TrainConfig(mode="async", steps=ASYNC_STEPS, batch_size=100, eval_every=0,
+                          engine="hip", quiet=True, data_sharding="stride",
+                          exchange_backend="xgmi", check_provenance=True, watchdog_s=120.0,
+                          **kw)
+        tr = Trainer(cfg, env, dataset=synthetic_mnist(2000, 500, seed=5))
+        assert isinstance(tr.exchange, AsyncPeerExchange), type(tr.exchange)
+        s = tr.train()  # verify_provenance runs inside (check_provenance=True)
+        torch.cuda.synchronize()
+        torch.save({"params": tr.params.cpu(), "served": tr.exchange.served,
+                    "ps": {p: (sv.t, sv.params.cpu()) for p, sv in tr.servers.items()},
+                    "ranges": {p: tr.plan.ps_segments(p)[0] for p in tr.servers},
+                    "acc": s["final_acc"]},
+                   os.path.join(outdir, f"rank{rank}.pt"))
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
+@pytest.mark.parametrize("world,kw", [
+    (1, dict(shard="none")),                     # one worker, its own PS through the mailbox
+    (2, dict(shard="contiguous")),               # mnist_async_sharding
+    (4, dict(shard="greedy", num_ps=4)),         # mnist_async_sharding_greedy
+    (3, dict(shard="contiguous", num_ps=5)),     # several PS per host
+])
+def test_async_xgmi_serves_every_push(tmp_path, world, kw):
+    import torch.multiprocessing as mp
+    mp.spawn(_async_rank, args=(world, free_port(), str(tmp_path), kw), nprocs=world, join=True)
+    recs = [torch.load(os.path.join(tmp_path, f"rank{r}.pt")) for r in range(world)]
+    n_ps = sum(len(rec["ps"]) for rec in recs)
+    assert n_ps == kw.get("num_ps", 1 if kw["shard"] == "none" else world)
+    for rec in recs:
+        # every hosted PS applied exactly one update per push of every worker
+        for p, (t, _) in rec["ps"].items():
+            assert t == world * ASYNC_STEPS, (p, t)
+        assert rec["served"] == len(rec["ps"]) * world * ASYNC_STEPS
+        assert torch.isfinite(rec["params"]).all()
+    # the last worker a PS served holds exactly that PS's final parameters
+    for rec in recs:
+        for p, (_, ps_params) in rec["ps"].items():
+            lo, hi = rec["ranges"][p]
+            assert any(torch.equal(o["params"][lo:hi], ps_params) for o in recs), p
