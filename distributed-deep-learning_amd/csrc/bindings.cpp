@@ -1,6 +1,7 @@
 // Python bindings of the native extension ``_C`` (kernels launch on torch's current HIP
 // stream so they compose with RCCL collectives and hipGraph capture).
 #include <torch/extension.h>
+#include <pybind11/stl.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/hip/HIPGuard.h>
 
@@ -63,10 +64,6 @@ class PyEngine {
     e_.max_batch = (int)std::max(max_batch, train_batch);
     e_.train_batch = (int)train_batch;
     set_keep_prob(keep_prob);
-    {
-      c10::hip::HIPGuard guard(device_.index());
-      e_.init_streams();
-    }
     realloc();
   }
 
@@ -95,7 +92,15 @@ class PyEngine {
   std::vector<int64_t> get_eval_cfg() const {
     return std::vector<int64_t>(e_.eval_cfg, e_.eval_cfg + ddl::OP_COUNT);
   }
-  void set_concurrent(bool on) { e_.concurrent = on; }
+  // the side stream exists only in the (slower, A/B) two-stream mode: every extra HIP stream
+  // competes for the GPU_MAX_HW_QUEUES hardware queues
+  void set_concurrent(bool on) {
+    if (on) {
+      c10::hip::HIPGuard guard(device_.index());
+      e_.init_streams();
+    }
+    e_.concurrent = on;
+  }
   void set_dual(bool on) { e_.dual = on; }
   void set_wide_thr(int64_t t) {
     e_.wide_thr = (int)std::max<int64_t>(1, t);
@@ -295,7 +300,7 @@ class PyAsyncPeer {
     c10::hip::HIPGuard guard(params_.device().index());
     p_->open(handles);
   }
-  void push_all(double coef) { p_->push_all((float)coef, cur_stream()); }
+  void push_all(int64_t epoch, double coef) { p_->push_all((uint32_t)epoch, (float)coef, cur_stream()); }
   void attach_done(std::string name, bool create) { p_->attach_done(name, create); }
   bool wait_done(int64_t epoch, double timeout_s) {
     py::gil_scoped_release nogil;
@@ -320,10 +325,60 @@ class PyAsyncPeer {
     p_->apply((int)ps, (int)worker, (uint32_t)epoch, u, ps_params.data_ptr<float>(), cur_stream());
   }
   int error() const { return p_->error(); }
+  ddl::AsyncPeer* raw() { return p_.get(); }
+  int device() const { return params_.device().index(); }
 
  private:
   at::Tensor params_, grads_;
   std::unique_ptr<ddl::AsyncPeer> p_;
+};
+
+// native PS service thread of the async xGMI exchange
+class PyAsyncService {
+ public:
+  // ps: list of (ps id, params, m, v | None, t)
+  PyAsyncService(PyAsyncPeer& peer, std::string mbox, int64_t world, py::list ps, int64_t opt,
+                 double lr, double b1, double b2, double eps, double mu, double scale,
+                 int64_t epoch0, bool provenance) {
+    std::vector<ddl::AsyncPsState> st;
+    for (auto item : ps) {
+      auto t = item.cast<py::tuple>();
+      ddl::AsyncPsState s;
+      s.ps = t[0].cast<int>();
+      at::Tensor w = t[1].cast<at::Tensor>(), m = t[2].cast<at::Tensor>();
+      check_f32_cuda(w, "ps params");
+      check_f32_cuda(m, "m");
+      keep_.push_back(w);
+      keep_.push_back(m);
+      s.params = w.data_ptr<float>();
+      s.m = m.data_ptr<float>();
+      s.v = nullptr;
+      if (!t[3].is_none()) {
+        at::Tensor v = t[3].cast<at::Tensor>();
+        check_f32_cuda(v, "v");
+        keep_.push_back(v);
+        s.v = v.data_ptr<float>();
+      }
+      s.t = t[4].cast<int64_t>();
+      st.push_back(s);
+    }
+    svc_ = std::make_unique<ddl::AsyncService>(peer.raw(), mbox, (int)world, peer.device(), st,
+                                               (int)opt, (float)lr, (float)b1, (float)b2,
+                                               (float)eps, (float)mu, (float)scale,
+                                               (uint32_t)epoch0, provenance);
+  }
+  void start(int64_t expected) { svc_->start(expected); }
+  void join() {
+    py::gil_scoped_release nogil;
+    svc_->join();
+  }
+  int64_t t(int64_t ps) const { return svc_->t((int)ps); }
+  int64_t served() const { return svc_->served(); }
+  std::vector<std::array<int64_t, 4>> provenance() const { return svc_->provenance(); }
+
+ private:
+  std::vector<at::Tensor> keep_;
+  std::unique_ptr<ddl::AsyncService> svc_;
 };
 
 class PyRunner {
@@ -528,6 +583,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("wait_done", &PyAsyncPeer::wait_done)
       .def("apply", &PyAsyncPeer::apply)
       .def("error", &PyAsyncPeer::error);
+
+  py::class_<PyAsyncService>(m, "AsyncService")
+      .def(py::init<PyAsyncPeer&, std::string, int64_t, py::list, int64_t, double, double, double,
+                    double, double, double, int64_t, bool>(),
+           py::keep_alive<1, 2>())
+      .def("start", &PyAsyncService::start)
+      .def("join", &PyAsyncService::join)
+      .def("t", &PyAsyncService::t)
+      .def("served", &PyAsyncService::served)
+      .def("provenance", &PyAsyncService::provenance);
 
   py::class_<PyPeer>(m, "PeerExchange")
       .def(py::init<at::Tensor, at::Tensor, int64_t, int64_t, py::list, int64_t>(),

@@ -6,7 +6,10 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "scratch.h"
@@ -224,6 +227,7 @@ class PeerExchange {
 
 // ---- asynchronous PS over xGMI peer memory (xgmi_async.hip) ----------------------------------
 constexpr int kAsyncMaxPs = 64;
+constexpr int kAsyncMaxSlices = 64;
 struct AsyncShard {              // one PS's contiguous range of the flat buffer
   int64_t lo, n, slice, inbox_off;
   int host, nslice;
@@ -244,8 +248,8 @@ class AsyncPeer {
   ~AsyncPeer();
   std::string handle() const;
   void open(const std::vector<std::string>& handles);
-  // worker: every PS shard of the gradient (x coef) into its host's inbox slot
-  void push_all(float coef, hipStream_t st);
+  // worker: every PS shard of the gradient (x coef) into its host's inbox slot, round `epoch`
+  void push_all(uint32_t epoch, float coef, hipStream_t st);
   // the DONE counters: a POSIX shm segment (created by one rank, attached by the others)
   // registered with HIP, so every GPU bumps them and every host polls them directly
   void attach_done(const std::string& name, bool create);
@@ -275,6 +279,45 @@ class AsyncPeer {
   size_t done_bytes_ = 0;
   std::string done_name_;
   bool done_owner_ = false;
+};
+
+struct AsyncPsState {            // one hosted PS as the service thread sees it
+  int ps;
+  float* params;                 // the PS's private parameter copy
+  float* m;
+  float* v;
+  int64_t t;                     // its step counter (advanced once per arrival)
+};
+
+class AsyncService {
+ public:
+  AsyncService(AsyncPeer* peer, const std::string& mbox_name, int world, int device,
+               const std::vector<AsyncPsState>& ps, int opt, float lr, float b1, float b2,
+               float eps, float mu, float scale, uint32_t epoch0, bool provenance);
+  ~AsyncService();
+  void start(int64_t expected);  // serve `expected` tokens on a native thread
+  void join();                   // rethrows the thread's error, if any
+  int64_t t(int ps) const;
+  int64_t served() const { return served_.load(); }
+  // (worker, ps, worker round, PS step) per apply, in service order
+  const std::vector<std::array<int64_t, 4>>& provenance() const { return prov_; }
+
+ private:
+  void run();
+  AsyncPeer* peer_;
+  std::string mbox_name_;
+  int world_, device_;
+  std::vector<AsyncPsState> ps_;
+  int opt_;
+  float lr_, b1_, b2_, eps_, mu_, scale_;
+  bool keep_prov_;
+  std::vector<uint32_t> epoch_;
+  std::vector<std::array<int64_t, 4>> prov_;
+  std::atomic<int64_t> served_{0};
+  int64_t expected_ = 0;
+  hipStream_t stream_ = nullptr;
+  std::thread th_;
+  std::string error_;
 };
 
 class SyncRunner {

@@ -18,15 +18,16 @@
 //            (write-through, system scope), drain, then ARRIVE_r[b][me][j] = e
 //   phase 2  wait ARRIVE_me[b][q][j] >= e for every peer q; sum the W contributions in rank order
 //            (deterministic), optimizer update of my chunk's slice, store the new parameters to
-//            EVERY rank's parameter buffer (self included, write-through), drain, DONE_q[b][me] += 1
-//   final    (the step's last bucket, on the compute stream) wait DONE_me[b'][q] >= e * nslices[b']
-//            for every bucket and rank: when the kernel ends, every parameter of this step has
+//            EVERY rank's parameter buffer (self included, write-through), drain, DONE_q[b][me][j] = e
+//   final    (the step's last bucket, on the compute stream) wait DONE_me[b'][q][*] >= e for every
+//            bucket, rank and slice: when the kernel ends, every parameter of this step has
 //            landed and the next forward (a later kernel: L2 invalidated at its start) reads them.
 // Buffer reuse is safe by construction: a rank overwrites an inbox slot (step e+1 backward) only
 // after its step e+1 forward, i.e. after the final wait saw every owner's DONE of step e, which
 // each owner sets after reading that slot; an owner writes a peer's parameters of bucket b only
 // after that peer's ARRIVE for b, i.e. after its backward segment b, the last reader of them.
-// Flags live in uncached device memory and are only touched by system-scope atomics; payload
+// Flags live in uncached device memory, each has ONE writer and is only stored (never
+// read-modify-written) and polled, all with system-scope atomic loads/stores; payload
 // stores carry sc0|sc1 (system write-through) and every storing wave drains (vmcnt(0)) before
 // the workgroup barrier that precedes the flag store.  Every wait is bounded: on timeout the
 // kernel records an error word in host memory and runs to completion (no GPU hang); the host
@@ -65,11 +66,12 @@ DDL_DEV void flag_store(uint32_t* f, uint32_t v) {
 }
 
 DDL_DEV int arrive_idx(int b, int src, int j) { return (b * kXgmiMaxPeers + src) * kXgmiMaxSlices + j; }
-// one completion counter per (bucket, owner): every workgroup of the owner's kernel adds 1, so
-// at step e it reaches e * nslices[b]; the final wait is then ONE parallel poll of buckets x W
-// words instead of a poll per slice
-DDL_DEV int done_idx(int b, int src) {
-  return kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices + b * kXgmiMaxPeers + src;
+// one completion word per (bucket, owner, slice), written only by that owner's workgroup: every
+// flag has a single writer and is only ever stored (no read-modify-write: atomics through an
+// IPC mapping are performed in whichever XCD L2 the writer's mapping caches them in, so counters
+// bumped by several writers can lose updates); the final wait polls them all in parallel
+DDL_DEV int done_idx(int b, int src, int j) {
+  return kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices + arrive_idx(b, src, j);
 }
 
 // Bounded wait until *f >= target (wrap-safe).  false on timeout or when another workgroup
@@ -184,15 +186,19 @@ __global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a)
   }
   drain_vm();
   __syncthreads();
-  if (tid < W)
-    __hip_atomic_fetch_add(T.flags[tid] + done_idx(b, me), 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < W) flag_store(T.flags[tid] + done_idx(b, me, j), a.epoch);
 
-  // ---- final wait: every bucket's new parameters from every owner have landed here
-  // (one lane per (bucket, owner) counter, all polled at once)
-  if (a.final_wait && tid < a.nbuckets * W) {
-    const int bb = tid / W, q = tid - bb * W;
-    wait_ge(myflags + done_idx(bb, q), a.epoch * (uint32_t)a.nslices[bb], deadline, a.err, 2);
+  // ---- final wait: every bucket's new parameters from every owner have landed here; the
+  // (bucket, owner, slice) words are spread over all threads of the launch and polled at once
+  if (a.final_wait) {
+    int total = 0;
+    for (int bb = 0; bb < a.nbuckets; ++bb) total += W * a.nslices[bb];
+    for (int k = j * 256 + tid; k < total; k += gridDim.x * 256) {
+      int bb = 0, x = k;
+      while (x >= W * a.nslices[bb]) x -= W * a.nslices[bb++];
+      const int q = x / a.nslices[bb], jj = x - q * a.nslices[bb];
+      wait_ge(myflags + done_idx(bb, q, jj), a.epoch, deadline, a.err, 2);
+    }
   }
 }
 
@@ -244,8 +250,7 @@ PeerExchange::PeerExchange(float* params, const float* grads, int64_t total, int
   inbox_elems_ = inbox;
   X_CHECK(hipMalloc(&inbox_, inbox_elems_ * sizeof(float)));
   X_CHECK(hipMemset(inbox_, 0, inbox_elems_ * sizeof(float)));
-  flag_bytes_ = (size_t)(kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices +
-                         kXgmiMaxBuckets * kXgmiMaxPeers) * sizeof(uint32_t);
+  flag_bytes_ = 2ull * kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices * sizeof(uint32_t);
   X_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes_,
                                 hipDeviceMallocUncached));
   X_CHECK(hipMemset(flags_, 0, flag_bytes_));

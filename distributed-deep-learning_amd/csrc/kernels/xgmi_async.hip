@@ -8,16 +8,16 @@
 //
 // A worker round:
 //   push_all  (worker stream)  one kernel: every PS shard of the gradient -> that PS host's
-//             inbox slot [ps][worker] (system write-through stores), ARRIVE[ps][worker] += 1
+//             inbox slot [ps][worker] (system write-through stores), ARRIVE[ps][worker][slice] = e
 //             per workgroup at the host
 //   post      (worker host, after the push kernel completed) (worker, ps) tokens into each PS
 //             host's arrival mailbox
 //   apply     (PS host, its PS stream, issued by the host's service thread in arrival order)
 //             Adam on the PS's private parameter copy (one step of its counter t per arrival,
 //             atomic per shard: the reference's per-tag mixing race Q3 cannot happen), store
-//             the new shard into the WORKER's parameter buffer, then DONE[worker][ps] += 1 per
-//             workgroup in host memory shared by all ranks (POSIX shm registered with HIP)
-//   wait      (worker host) polls DONE[me][*] >= e * nslices, then enqueues the next forward
+//             the new shard into the WORKER's parameter buffer, then DONE[worker][ps][slice] = e
+//             per workgroup in host memory shared by all ranks (POSIX shm registered with HIP)
+//   wait      (worker host) polls DONE[me][*][*] >= e, then enqueues the next forward
 // NO kernel of this protocol waits for another kernel.  HIP multiplexes streams onto a few
 // hardware queues (GPU_MAX_HW_QUEUES), so a spinning kernel can sit in front of the very kernel
 // it waits for; with applies of many workers interleaving on every PS stream such a cycle is
@@ -36,8 +36,11 @@
 #include <string>
 #include <thread>
 
+#include <cmath>
+
 #include "api.h"
 #include "common.h"
+#include "runtime/mailbox.h"
 
 namespace ddl {
 
@@ -68,15 +71,21 @@ DDL_DEV bool wait_ge(const uint32_t* f, uint32_t target, long long deadline, int
   }
   return true;
 }
-DDL_DEV void bump(uint32_t* f) {
-  __hip_atomic_fetch_add(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+DDL_DEV void flag_store(uint32_t* f, uint32_t v) {
+  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// arrival words of one rank: ARRIVE[ps][src]
-DDL_DEV int arrive_idx(int p, int src) { return p * kXgmiMaxPeers + src; }
+// arrival words of one rank: ARRIVE[ps][src][slice]; completion words DONE[worker][ps][slice]
+// in the shared host segment.  Every word has ONE writer and is only stored, never
+// read-modify-written (atomics through IPC / host mappings are not safe to combine)
+DDL_DEV int arrive_idx(int p, int src, int j) {
+  return (p * kXgmiMaxPeers + src) * kAsyncMaxSlices + j;
+}
+DDL_DEV int done_word(int w, int p, int j) { return (w * kAsyncMaxPs + p) * kAsyncMaxSlices + j; }
 
 struct PushArgs {
   int world, rank, nps;
+  uint32_t epoch;
   int first_blk[kAsyncMaxPs + 1];  // block range of PS p: [first_blk[p], first_blk[p+1])
   const float* grads;
   float coef;
@@ -101,7 +110,7 @@ __global__ void __launch_bounds__(256) async_push_kernel(AsyncTable T, PushArgs 
   }
   drain_vm();
   __syncthreads();
-  if (tid == 0) bump(T.flags[S.host] + arrive_idx(p, a.rank));
+  if (tid == 0) flag_store(T.flags[S.host] + arrive_idx(p, a.rank, j), a.epoch);
 }
 
 struct ApplyArgs {
@@ -121,8 +130,7 @@ __global__ void __launch_bounds__(256) async_apply_kernel(AsyncTable T, ApplyArg
   const AsyncShard& S = T.shard[a.ps];
   const int j = blockIdx.x, tid = threadIdx.x;
   if (tid == 0)
-    wait_ge(T.flags[a.me] + arrive_idx(a.ps, a.worker), a.epoch * (uint32_t)S.nslice, deadline,
-            a.err, 1);
+    wait_ge(T.flags[a.me] + arrive_idx(a.ps, a.worker, j), a.epoch, deadline, a.err, 1);
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // keep the loads below the poll
   const int64_t s0 = (int64_t)j * S.slice;
@@ -159,7 +167,7 @@ __global__ void __launch_bounds__(256) async_apply_kernel(AsyncTable T, ApplyArg
   }
   drain_vm();
   __syncthreads();
-  if (tid == 0) bump(T.done + a.worker * kAsyncMaxPs + a.ps);
+  if (tid == 0) flag_store(T.done + done_word(a.worker, a.ps, j), a.epoch);
 }
 
 #define X_CHECK(x)                                                                        \
@@ -186,7 +194,8 @@ AsyncPeer::AsyncPeer(float* params, const float* grads, int64_t total, int world
   if (ps_ranges.empty() || (int)ps_ranges.size() > kAsyncMaxPs ||
       ps_ranges.size() != ps_host.size())
     throw std::invalid_argument("async xgmi: 1..64 PS, one host each");
-  if (max_slices < 1) throw std::invalid_argument("async xgmi: max_slices");
+  if (max_slices < 1 || max_slices > kAsyncMaxSlices)
+    throw std::invalid_argument("async xgmi: max_slices");
   if (reinterpret_cast<uintptr_t>(params) % 16 || reinterpret_cast<uintptr_t>(grads) % 16)
     throw std::invalid_argument("async xgmi: buffers must be 16-B aligned");
   memset(&table_, 0, sizeof(table_));
@@ -218,7 +227,7 @@ AsyncPeer::AsyncPeer(float* params, const float* grads, int64_t total, int world
   inbox_elems_ = inbox > 0 ? inbox : 4;
   X_CHECK(hipMalloc(&inbox_, inbox_elems_ * sizeof(float)));
   X_CHECK(hipMemset(inbox_, 0, inbox_elems_ * sizeof(float)));
-  const size_t flag_bytes = (size_t)(kAsyncMaxPs * kXgmiMaxPeers) * sizeof(uint32_t);
+  const size_t flag_bytes = (size_t)kAsyncMaxPs * kXgmiMaxPeers * kAsyncMaxSlices * sizeof(uint32_t);
   X_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes,
                                 hipDeviceMallocUncached));
   X_CHECK(hipMemset(flags_, 0, flag_bytes));
@@ -287,13 +296,14 @@ void AsyncPeer::open(const std::vector<std::string>& handles) {
   opened_ok_ = true;
 }
 
-void AsyncPeer::push_all(float coef, hipStream_t st) {
+void AsyncPeer::push_all(uint32_t epoch, float coef, hipStream_t st) {
   if (!opened_ok_) throw std::runtime_error("async xgmi: open() first");
   PushArgs a;
   memset(&a, 0, sizeof(a));
   a.world = world_;
   a.rank = rank_;
   a.nps = nps_;
+  a.epoch = epoch;
   int blk = 0;
   for (int p = 0; p < nps_; ++p) {
     a.first_blk[p] = blk;
@@ -307,7 +317,7 @@ void AsyncPeer::push_all(float coef, hipStream_t st) {
 }
 
 void AsyncPeer::attach_done(const std::string& name, bool create) {
-  const size_t bytes = (size_t)world_ * kAsyncMaxPs * sizeof(uint32_t);
+  const size_t bytes = (size_t)world_ * kAsyncMaxPs * kAsyncMaxSlices * sizeof(uint32_t);
   int fd = -1;
   if (create) {
     shm_unlink(name.c_str());  // stale segment of a crashed job
@@ -339,10 +349,12 @@ bool AsyncPeer::wait_done(uint32_t epoch, double timeout_s) {
   const auto t0 = std::chrono::steady_clock::now();
   for (int spins = 0;; ++spins) {
     bool all = true;
-    for (int p = 0; p < nps_ && all; ++p) {
-      const uint32_t v = __atomic_load_n(done_host_ + rank_ * kAsyncMaxPs + p, __ATOMIC_ACQUIRE);
-      all = (int32_t)(v - epoch * (uint32_t)table_.shard[p].nslice) >= 0;
-    }
+    for (int p = 0; p < nps_ && all; ++p)
+      for (int j = 0; j < table_.shard[p].nslice && all; ++j) {
+        const uint32_t v = __atomic_load_n(
+            done_host_ + ((size_t)rank_ * kAsyncMaxPs + p) * kAsyncMaxSlices + j, __ATOMIC_ACQUIRE);
+        all = (int32_t)(v - epoch) >= 0;
+      }
     if (all) return true;
     if (error()) return false;
     if (spins > 256) {
@@ -387,4 +399,85 @@ void AsyncPeer::apply(int ps, int worker, uint32_t epoch, const XgmiUpdate& u, f
 
 int AsyncPeer::error() const { return __atomic_load_n(err_, __ATOMIC_ACQUIRE); }
 
+// ---- the PS service loop in C++ -------------------------------------------------------------------
+// Pops (worker, ps) tokens from this host's arrival mailbox in order and enqueues one apply per
+// token on one PS stream; no Python, no GIL on the critical path of every remote worker's round.
+AsyncService::AsyncService(AsyncPeer* peer, const std::string& mbox_name, int world, int device,
+                           const std::vector<AsyncPsState>& ps, int opt, float lr, float b1,
+                           float b2, float eps, float mu, float scale, uint32_t epoch0,
+                           bool provenance)
+    : peer_(peer), mbox_name_(mbox_name), world_(world), device_(device), ps_(ps), opt_(opt),
+      lr_(lr), b1_(b1), b2_(b2), eps_(eps), mu_(mu), scale_(scale), keep_prov_(provenance) {
+  if (world < 1 || world > kXgmiMaxPeers) throw std::invalid_argument("async service: world");
+  for (const auto& s : ps)
+    if (s.ps < 0 || s.ps >= kAsyncMaxPs || !s.params || !s.m || (opt == 0 && !s.v))
+      throw std::invalid_argument("async service: PS state");
+  epoch_.assign((size_t)world * kAsyncMaxPs, epoch0);
+}
+
+AsyncService::~AsyncService() {
+  if (th_.joinable()) th_.join();
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void AsyncService::start(int64_t expected) {
+  if (th_.joinable()) throw std::runtime_error("async service already running");
+  X_CHECK(hipSetDevice(device_));
+  if (!stream_) X_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  expected_ = expected;
+  th_ = std::thread([this] { run(); });
+}
+
+void AsyncService::run() {
+  try {
+    X_CHECK(hipSetDevice(device_));
+    ShmMailbox box(mbox_name_, 2, false);
+    for (int64_t k = 0; k < expected_; ++k) {
+      const int64_t v = box.pop(600.0);
+      if (v < 0) throw std::runtime_error("async PS: no arrival within 600 s");
+      const int w = (int)(v >> 20), p = (int)(v & ((1 << 20) - 1));
+      AsyncPsState* st = nullptr;
+      for (auto& s : ps_)
+        if (s.ps == p) st = &s;
+      if (!st || w < 0 || w >= world_) throw std::runtime_error("async PS: bad token");
+      const uint32_t e = ++epoch_[(size_t)w * kAsyncMaxPs + p];
+      const int64_t t = ++st->t;  // one apply_gradients of this PS per arrival
+      XgmiUpdate u;
+      u.opt = opt_;
+      u.m = st->m;
+      u.v = st->v;
+      // TF1 Adam: lr_t = lr * sqrt(1 - beta2^t) / (1 - beta1^t) (ops/adam.py adam_coeffs)
+      u.lr_t = (float)((double)lr_ * std::sqrt(1.0 - std::pow((double)b2_, (double)t)) /
+                       (1.0 - std::pow((double)b1_, (double)t)));
+      u.c1 = 1.f - b1_;
+      u.c2 = 1.f - b2_;
+      u.eps = eps_;
+      u.lr = lr_;
+      u.mu = mu_;
+      u.scale = scale_;
+      peer_->apply(p, w, e, u, st->params, stream_);
+      if (keep_prov_) prov_.push_back({(int64_t)w, (int64_t)p, (int64_t)e, t});
+      served_.fetch_add(1);
+      if (const int err = peer_->error())
+        throw std::runtime_error("async PS: kernel wait timed out (code " + std::to_string(err) +
+                                 ")");
+    }
+    X_CHECK(hipStreamSynchronize(stream_));
+  } catch (const std::exception& ex) {
+    error_ = ex.what();
+  }
+}
+
+void AsyncService::join() {
+  if (th_.joinable()) th_.join();
+  if (!error_.empty()) throw std::runtime_error(error_);
+}
+
+int64_t AsyncService::t(int ps) const {
+  for (const auto& s : ps_)
+    if (s.ps == ps) return s.t;
+  throw std::invalid_argument("async service: PS not hosted here");
+}
+
 }  // namespace ddl
+

@@ -129,6 +129,7 @@ class AsyncPeerExchange:
         self.coef = 1.0
         self.timeout_s = 600.0
         self._thread: Optional[threading.Thread] = None
+        self._svc = None
         self._error: Optional[BaseException] = None
         self.served = 0
         self.check_provenance = check_provenance
@@ -146,7 +147,7 @@ class AsyncPeerExchange:
         self.grads.copy_(pat)
         self.params.zero_()
         torch.cuda.synchronize(dev)
-        self.peer.push_all(1.0)
+        self.peer.push_all(1, 1.0)
         torch.cuda.synchronize(dev)
         if W > 1:
             dist.barrier()  # every push has completed before any apply is issued
@@ -179,7 +180,19 @@ class AsyncPeerExchange:
         return sum(1 for h in self.hosts if h == r) * W * self.steps
 
     def start(self) -> None:
-        if self._expected() == 0:
+        n = self._expected()
+        if n == 0:
+            return
+        if isinstance(self.mailbox, mbox.ShmMailbox):
+            # the service loop in C++ (xgmi_async.hip AsyncService): no Python and no GIL
+            # between a remote worker's token and its apply kernel
+            ps_list = [(p, ps.params, ps.m, ps.v, ps.t) for p, ps in self.servers.items()]
+            h = next(iter(self.servers.values())).h
+            mom = next(iter(self.servers.values())).momentum
+            self._svc = native.ops().AsyncService(
+                self.peer, self.mailbox.name, self.env.world, ps_list, self.opt, h.lr, h.beta1,
+                h.beta2, h.eps, mom, self.grad_scale, 1, self.check_provenance)
+            self._svc.start(n)
             return
         self._thread = threading.Thread(target=self._serve, name="ps-xgmi-service", daemon=True)
         self._thread.start()
@@ -212,6 +225,18 @@ class AsyncPeerExchange:
             self._error = e
 
     def join(self) -> None:
+        if self._svc is not None:
+            svc, self._svc = self._svc, None
+            try:
+                svc.join()
+            finally:
+                for p, ps in self.servers.items():
+                    n = svc.t(p) - ps.t
+                    ps.t += n
+                    ps.updates += n
+                self.served = svc.served()
+                if self.check_provenance:
+                    self.provenance = [(w, p, e - 2, t) for (w, p, e, t) in svc.provenance()]
         if self._thread is not None:
             self._thread.join()
             self._thread = None
@@ -237,11 +262,11 @@ class AsyncPeerExchange:
         """Push round e, post it once the push has completed, wait until every PS stored the
         parameters back (host-side: the reference's blocking pull)."""
         r = self.env.rank
-        self.peer.push_all(self.coef)
+        self.epoch += 1
+        self.peer.push_all(self.epoch, self.coef)
         ev = torch.cuda.Event()
         ev.record()
         ev.synchronize()
-        self.epoch += 1
         for p in range(len(self.ranges)):
             self.boxes[self.hosts[p]].push(mbox.encode(r, p))
         if not self.peer.wait_done(self.epoch, self.timeout_s):

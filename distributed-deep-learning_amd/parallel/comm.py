@@ -114,6 +114,8 @@ def quirk_coefficient(plan: ShardPlan, rank: int, world: int, ref_quirks: bool) 
 
 
 class SyncExchange:
+    uses_side = True
+
     def __init__(self, plan: ShardPlan, env: DistEnv, params: torch.Tensor,
                  grads: torch.Tensor, segments: Sequence[Sequence[int]],
                  servers: Dict[int, ParameterServer], grad_reduce: str = "sum",
@@ -136,7 +138,8 @@ class SyncExchange:
         self.segments = [set(s) for s in segments] if overlap else [set().union(*map(set, segments))]
         self.units = self._build_units()
         cuda = params.is_cuda
-        self.side = torch.cuda.Stream(device=params.device) if cuda else None
+        # the Python exchange's comm stream (the native runner has its own)
+        self.side = torch.cuda.Stream(device=params.device) if cuda and self.uses_side else None
         self._pending: List = []
         self._issued: Set[int] = set()
         self._ready: Set[int] = set()

@@ -75,6 +75,7 @@ class ShmMailbox:
     def __init__(self, name: str, owner: bool, capacity: int = 4096):
         self.mb = native.ops().ShmMailbox(name, capacity, owner)
         self.owner = owner
+        self.name = name
 
     def push(self, value: int) -> None:
         if not self.mb.push(value, 600.0):

@@ -46,6 +46,7 @@ class NativeUnavailable(RuntimeError):
 
 class NativeSyncExchange(SyncExchange):
     native = True
+    uses_side = False  # collectives go on the C++ runner's own comm stream
 
     def __init__(self, plan: ShardPlan, env: DistEnv, params: torch.Tensor, grads: torch.Tensor,
                  segments: Sequence[Sequence[int]], servers: Dict[int, ParameterServer], engine,

@@ -52,8 +52,16 @@ class ParameterServer:
         if own_params is not None:
             self.params = torch.cat([own_params[lo:hi] for lo, hi in self.segments]).to(self.device)
         self.gbuf = None                 # receive buffer for remote gradients (async)
-        # async: all updates of this PS are serialised on one stream under `lock`
-        self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        # async: all updates of this PS are serialised on one stream under `lock` (created on
+        # first use: sync runs never need it, and every HIP stream competes for the few
+        # hardware queues)
+        self._stream = None
+
+    @property
+    def stream(self):
+        if self._stream is None and self.device.type == "cuda":
+            self._stream = torch.cuda.Stream(device=self.device)
+        return self._stream
 
     @contextlib.contextmanager
     def exclusive(self):
