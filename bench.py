@@ -59,7 +59,8 @@ def main(argv=None):
     ap.add_argument("--force-collectives", action="store_true",
                     help="W = 1 rehearsal of the multi-GPU step: keep the reduce-scatter / "
                          "all-gather units on a 1-rank RCCL communicator (comm stream, events, "
-                         "RCCL launches) instead of the local update")
+                         "RCCL launches) instead of the local update; with --exchange xgmi the "
+                         "fused xGMI bucket kernels (every push to itself) instead")
     ap.add_argument("--exchange", default="auto", choices=["auto", "rccl", "xgmi"],
                     help="W > 1 data plane of the native sync runner: RCCL reduce-scatter / "
                          "all-gather, or the fused xGMI peer-memory exchange (one push / "

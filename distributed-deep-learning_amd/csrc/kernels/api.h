@@ -371,6 +371,8 @@ class SyncRunner {
   uint32_t epoch_ = 0;     // xGMI flag epoch: one per step, identical on every rank
   hipStream_t cs_ = nullptr;
   hipEvent_t seg_ev_[kSegments] = {};
+  hipEvent_t seg_ev_dev_[kSegments] = {};  // device-scope release (xGMI-only segments)
+  bool seg_xgmi_only_[kSegments] = {};
   hipEvent_t done_ev_ = nullptr;
   std::vector<RunnerUnit> units_;
   int opt_ = 0;

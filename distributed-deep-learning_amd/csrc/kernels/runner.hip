@@ -112,8 +112,14 @@ SyncRunner::SyncRunner(Engine* eng, float* params, float* grads, int world, int 
   const bool sysfence = sf ? sf[0] == '1' : world_ > 1;
   const unsigned ev_flags =
       hipEventDisableTiming | (sysfence ? 0u : (unsigned)hipEventDisableSystemFence);
-  for (int s = 0; s < kSegments; ++s)
+  for (int s = 0; s < kSegments; ++s) {
     HIP_CHECK(hipEventCreateWithFlags(&seg_ev_[s], ev_flags));
+    // xGMI units: the consumer of the segment's gradients is our own kernel on this device
+    // (peers never read them: the exchange pushes), so a device-scope release is exact at
+    // any world size
+    HIP_CHECK(hipEventCreateWithFlags(&seg_ev_dev_[s],
+                                      hipEventDisableTiming | hipEventDisableSystemFence));
+  }
   HIP_CHECK(hipEventCreateWithFlags(&done_ev_, hipEventDisableTiming));
 }
 
@@ -121,6 +127,8 @@ SyncRunner::~SyncRunner() {
   if (comm_) (void)rccl().CommDestroy(as_comm(comm_));
   for (int s = 0; s < kSegments; ++s)
     if (seg_ev_[s]) (void)hipEventDestroy(seg_ev_[s]);
+  for (int s = 0; s < kSegments; ++s)
+    if (seg_ev_dev_[s]) (void)hipEventDestroy(seg_ev_dev_[s]);
   if (done_ev_) (void)hipEventDestroy(done_ev_);
   if (cs_) (void)hipStreamDestroy(cs_);
 }
@@ -167,6 +175,16 @@ void SyncRunner::set_units(const std::vector<RunnerUnit>& units) {
     }
   }
   units_ = units;
+  // segments whose off-stream units are all xGMI take the device-scope event
+  for (int sg = 0; sg < kSegments; ++sg) {
+    bool any = false, only = true;
+    for (const auto& u : units_)
+      if (u.seg == sg && !(u.kind == RunnerUnit::LOCAL && local_on_main_)) {
+        any = true;
+        only &= u.kind == RunnerUnit::XGMI;
+      }
+    seg_xgmi_only_[sg] = any && only;
+  }
   // the step's last xGMI unit also waits until every owner's parameters have landed here
   last_xgmi_ = -1;
   for (size_t i = 0; i < units_.size(); ++i)
@@ -365,8 +383,9 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
         continue;
       }
       if (!waited) {
-        HIP_CHECK(hipEventRecord(seg_ev_[s], st));
-        HIP_CHECK(hipStreamWaitEvent(cs_, seg_ev_[s], 0));
+        hipEvent_t ev = seg_xgmi_only_[s] ? seg_ev_dev_[s] : seg_ev_[s];
+        HIP_CHECK(hipEventRecord(ev, st));
+        HIP_CHECK(hipStreamWaitEvent(cs_, ev, 0));
         waited = true;
       }
       if (u.kind == RunnerUnit::XGMI) {

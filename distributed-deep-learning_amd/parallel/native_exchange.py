@@ -67,7 +67,9 @@ class NativeSyncExchange(SyncExchange):
         self.runner = ops.SyncRunner(engine.eng, params, grads, env.world, env.rank)
         self.backend = "local" if env.world == 1 and not force_collectives else backend
         self.peer = None
-        if env.world > 1 and backend == "xgmi":
+        if backend == "xgmi" and (env.world > 1 or force_collectives):
+            # (W = 1 with force_collectives: the whole W > 1 step structure — comm stream,
+            # events, fused bucket kernels, final wait — on one GPU, every push to itself)
             if plan.bucket_ranges is None or plan.num_ps != env.world:
                 raise NativeUnavailable("xgmi exchange needs the flat plan with one PS per GPU")
             self._init_peer_collectively(ops, env, plan, params, grads)
@@ -140,6 +142,10 @@ class NativeSyncExchange(SyncExchange):
         W (W + 1) / 2 * (i % 13 + 1) everywhere (exact in fp32).  Every stage is voted on, so
         a failure anywhere makes all ranks fall back together."""
         def agree(ok: bool, why: str, what: str) -> None:
+            if env.world == 1:
+                if not ok:
+                    raise NativeUnavailable(f"{what} failed: {why}")
+                return
             votes = [None] * env.world
             dist.all_gather_object(votes, (bool(ok), why))
             bad = [(r, w) for r, (o, w) in enumerate(votes) if not o]
@@ -154,8 +160,10 @@ class NativeSyncExchange(SyncExchange):
         except RuntimeError as e:
             mine, why = None, str(e)
         agree(mine is not None, why, "xGMI buffer export")
-        handles = [None] * env.world
-        dist.all_gather_object(handles, mine)
+        handles = [mine]
+        if env.world > 1:
+            handles = [None] * env.world
+            dist.all_gather_object(handles, mine)
         try:
             peer.open(handles)
             why = ""

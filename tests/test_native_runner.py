@@ -28,7 +28,10 @@ def _run(data, native, steps=6, **kw):
     tr = Trainer(cfg, env, dataset=data)
     assert getattr(tr.exchange, "native", False) == native
     if kw.get("force_collectives"):
-        assert tr.exchange.runner.has_comm()
+        if kw.get("exchange_backend") == "xgmi":
+            assert tr.exchange.peer is not None
+        else:
+            assert tr.exchange.runner.has_comm()
         assert any(u.kind != "local" for u in tr.exchange.units)
     for i in range(steps):
         tr.train_step(i)
@@ -73,6 +76,8 @@ def test_native_runner_trains(data):
     dict(shard="contiguous"),                 # REDUCE units -> grouped ncclReduce/Broadcast
     dict(shard="greedy", num_ps=3),           # several PS hosts, several ranges per unit
     dict(shard="contiguous", num_ps=2, overlap=False),
+    dict(shard="flat", exchange_backend="xgmi"),  # fused xGMI bucket kernels, push to self
+    dict(shard="flat", exchange_backend="xgmi", overlap=False),
 ])
 def test_forced_collectives_on_one_rank_match_local(data, kw):
     """The multi-GPU exchange path on one GPU: torch's librccl resolved by dlsym, a 1-rank
