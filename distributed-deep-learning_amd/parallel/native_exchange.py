@@ -81,11 +81,27 @@ class NativeSyncExchange(SyncExchange):
             if not ok:
                 raise RuntimeError(f"RCCL 1-rank self-test failed: {why}")
         seg_sets = [set(s) for s in segments]
+        # DDL_SEG_ISSUE="a,b,c,d": the backward segment after which each segment's units are
+        # issued.  Every issue point costs an event record on the compute stream (~4.5 us gap,
+        # forced-rehearsal timeline), so the RCCL path issues the fc bucket together with conv4's
+        # after segment 1 (still overlapped by the conv3 + conv2 backward): forced 1-rank
+        # rehearsal 0.405 -> 0.3965 ms/step.  The xGMI kernels are one launch per bucket with no
+        # ring passes, and measured 0.402 (own point) vs 0.404 (merged): each bucket right after
+        # its own segment.
+        issue_after = list(range(len(seg_sets)))
+        if self.backend == "rccl" and len(seg_sets) == 4:
+            issue_after = [1, 1, 2, 3]
+        env_map = os.environ.get("DDL_SEG_ISSUE")
+        if env_map:
+            m = [int(v) for v in env_map.split(",")]
+            if len(m) == len(seg_sets) and all(i <= j < len(seg_sets) for i, j in enumerate(m)):
+                issue_after = m
 
         def seg_of(tensors):
             if not overlap:
                 return len(seg_sets) - 1
-            return max(next(i for i, s in enumerate(seg_sets) if t in s) for t in tensors)
+            return issue_after[max(next(i for i, s in enumerate(seg_sets) if t in s)
+                                   for t in tensors)]
 
         units = []
         for u in self.units:
