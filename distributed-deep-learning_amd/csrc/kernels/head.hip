@@ -1,7 +1,7 @@
 // Classifier head: fc3 (512->10) + softmax cross-entropy (model.py:85-92) and its backward.
 //
 // fc3 is too skinny (N = 10) for MFMA tiles to pay, so it is two small VALU kernels:
-//   head_fwd : one wave64 per sample: logits, loss, dlogits = (softmax - onehot)/B
+//   head_fwd : one 4-wave workgroup per sample: logits, loss, dlogits = (softmax - onehot)/B
 //              (SoftmaxCrossEntropyWithLogits + Mean fwd/bwd),
 //              or in eval mode the correct-prediction count (F22).
 //   head_bwd : dW3_aug[513,10] = [h2;1]^T dlogits and dh2 = dlogits W3^T, with the fc2
@@ -14,20 +14,20 @@
 
 namespace ddl {
 
-__global__ void __launch_bounds__(256)
-head_fwd_kernel(const float* __restrict__ h2, const float* __restrict__ w,
-                const float* __restrict__ bias, const int64_t* __restrict__ labels, int B,
-                float inv_batch, float* __restrict__ dlog, float* __restrict__ loss,
-                int* __restrict__ correct) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= B) return;
-  float acc[HC];
+// Logits of sample `row` by a whole 256-thread workgroup: wave v sums columns [128v, 128v+128)
+// (2 per lane), a shuffle tree per wave, then the four wave partials through LDS in a fixed order.
+// Four waves per sample instead of one: at batch 100 the head is latency-bound (100 waves on a
+// 256-CU chip), so shorter per-wave chains beat fewer launches.  Every thread returns all HC
+// logits.  Shared by head_fwd and head_fused so their arithmetic is identical (bitwise).
+DDL_DEV void head_logits(const float* __restrict__ hr, const float* __restrict__ w,
+                         const float* __restrict__ bias, float (&part)[4][HC],
+                         float (&acc)[HC]) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
   for (int c = 0; c < HC; ++c) acc[c] = 0.f;
-  const float* hr = h2 + (size_t)row * HK;
-#pragma unroll 4
-  for (int k = lane; k < HK; k += 64) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int k = wave * 128 + t * 64 + lane;
     const float hv = hr[k];
     const float* wr = w + k * HC;
 #pragma unroll
@@ -38,8 +38,24 @@ head_fwd_kernel(const float* __restrict__ h2, const float* __restrict__ w,
     float v = acc[c];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    acc[c] = v + bias[c];
+    if (lane == 0) part[wave][c] = v;
   }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < HC; ++c)
+    acc[c] = ((part[0][c] + part[1][c]) + (part[2][c] + part[3][c])) + bias[c];
+}
+
+__global__ void __launch_bounds__(256)
+head_fwd_kernel(const float* __restrict__ h2, const float* __restrict__ w,
+                const float* __restrict__ bias, const int64_t* __restrict__ labels, int B,
+                float inv_batch, float* __restrict__ dlog, float* __restrict__ loss,
+                int* __restrict__ correct) {
+  __shared__ float part[4][HC];
+  const int row = blockIdx.x;
+  if (row >= B) return;
+  float acc[HC];
+  head_logits(h2 + (size_t)row * HK, w, bias, part, acc);
   float mx = acc[0];
   int arg = 0;
 #pragma unroll
@@ -49,7 +65,7 @@ head_fwd_kernel(const float* __restrict__ h2, const float* __restrict__ w,
 #pragma unroll
   for (int c = 0; c < HC; ++c) se += __expf(acc[c] - mx);
   const int lab = (int)labels[row];
-  if (lane == 0) {
+  if (threadIdx.x == 0) {
     float ll = 0.f;
 #pragma unroll
     for (int c = 0; c < HC; ++c)
@@ -57,13 +73,13 @@ head_fwd_kernel(const float* __restrict__ h2, const float* __restrict__ w,
     if (loss) loss[row] = (mx + __logf(se)) - ll;
     if (correct && arg == lab) atomicAdd(correct, 1);
   }
-  if (dlog && lane < HC) {
+  if (dlog && threadIdx.x < HC) {
     float lc = 0.f;
 #pragma unroll
     for (int c = 0; c < HC; ++c)
-      if (c == lane) lc = acc[c];
+      if (c == (int)threadIdx.x) lc = acc[c];
     const float p = __expf(lc - mx) / se;
-    dlog[(size_t)row * HC + lane] = (p - (lane == lab ? 1.f : 0.f)) * inv_batch;
+    dlog[(size_t)row * HC + threadIdx.x] = (p - ((int)threadIdx.x == lab ? 1.f : 0.f)) * inv_batch;
   }
 }
 
@@ -97,27 +113,11 @@ head_fused_kernel(const float* __restrict__ h2, const float* __restrict__ w,
                   float inv_batch, const uint32_t* __restrict__ seed, uint32_t seed_v,
                   uint32_t thr24, float inv_keep, float* __restrict__ dlog,
                   float* __restrict__ loss, float* __restrict__ dpre2) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ float part[4][HC];
+  const int row = blockIdx.x;
   if (row >= B) return;
   float acc[HC];
-#pragma unroll
-  for (int c = 0; c < HC; ++c) acc[c] = 0.f;
-  const float* hr = h2 + (size_t)row * HK;
-#pragma unroll 4
-  for (int k = lane; k < HK; k += 64) {
-    const float hv = hr[k];
-    const float* wr = w + k * HC;
-#pragma unroll
-    for (int c = 0; c < HC; ++c) acc[c] = fmaf(hv, wr[c], acc[c]);
-  }
-#pragma unroll
-  for (int c = 0; c < HC; ++c) {
-    float v = acc[c];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    acc[c] = v + bias[c];
-  }
+  head_logits(h2 + (size_t)row * HK, w, bias, part, acc);
   float mx = acc[0];
 #pragma unroll
   for (int c = 1; c < HC; ++c) mx = acc[c] > mx ? acc[c] : mx;
@@ -125,27 +125,28 @@ head_fused_kernel(const float* __restrict__ h2, const float* __restrict__ w,
 #pragma unroll
   for (int c = 0; c < HC; ++c) se += __expf(acc[c] - mx);
   const int lab = (int)labels[row];
-  // dlogits of this sample in every lane (same arithmetic as head_fwd_kernel's per-lane form)
+  // dlogits of this sample in every thread (same arithmetic as head_fwd_kernel's per-lane form)
   float dl[HC];
 #pragma unroll
   for (int c = 0; c < HC; ++c) dl[c] = (__expf(acc[c] - mx) / se - (c == lab ? 1.f : 0.f)) * inv_batch;
-  if (lane == 0) {
+  if (threadIdx.x == 0) {
     float ll = 0.f;
 #pragma unroll
     for (int c = 0; c < HC; ++c)
       if (c == lab) ll = acc[c];
     loss[row] = (mx + __logf(se)) - ll;
   }
-  if (lane < HC) {
+  if (threadIdx.x < HC) {
     float v = 0.f;
 #pragma unroll
     for (int c = 0; c < HC; ++c)
-      if (c == lane) v = dl[c];
-    dlog[(size_t)row * HC + lane] = v;
+      if (c == (int)threadIdx.x) v = dl[c];
+    dlog[(size_t)row * HC + threadIdx.x] = v;
   }
-  // dh2 = dlogits W3^T with fc2's dropout backward (mask regenerated from the seed)
+  // dh2 = dlogits W3^T with fc2's dropout backward (mask regenerated from the seed), 2 columns
+  // per thread
   const uint32_t key = thr24 ? ddl_mix32((seed ? *seed : seed_v) + 2u * 0x9E3779B9u) : 0u;
-  for (int i = lane; i < HK; i += 64) {
+  for (int i = threadIdx.x; i < HK; i += 256) {
     float g = 0.f;
 #pragma unroll
     for (int c = 0; c < HC; ++c) g = fmaf(dl[c], w[i * HC + c], g);
@@ -158,7 +159,7 @@ head_fused_kernel(const float* __restrict__ h2, const float* __restrict__ w,
 void launch_head_fused(const float* h2, const float* w, const float* bias, const int64_t* labels,
                        int B, const uint32_t* seed, uint32_t seed_v, uint32_t thr24,
                        float inv_keep, float* dlog, float* loss, float* dpre2, hipStream_t st) {
-  hipLaunchKernelGGL(head_fused_kernel, dim3((B + 3) / 4), dim3(256), 0, st, h2, w, bias, labels,
+  hipLaunchKernelGGL(head_fused_kernel, dim3(B), dim3(256), 0, st, h2, w, bias, labels,
                      B, 1.f / (float)B, seed, seed_v, thr24, inv_keep, dlog, loss, dpre2);
 }
 
@@ -171,7 +172,7 @@ void launch_head_wgrad(const float* h2, const float* dlog, int B, float* gw, flo
 
 void launch_head_fwd(const float* h2, const float* w, const float* bias, const int64_t* labels,
                      int B, float* dlog, float* loss, int* correct, hipStream_t st) {
-  hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, st, h2, w, bias, labels, B,
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(B), dim3(256), 0, st, h2, w, bias, labels, B,
                      1.f / (float)B, dlog, loss, correct);
 }
 
