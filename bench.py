@@ -134,6 +134,10 @@ def main(argv=None):
         candidates = ["xgmi"] if shared_gpu else ["rccl", "xgmi"]
     ab = {}
     tr = None
+    # every trainer built here stays referenced until the process ends: a garbage-collected
+    # runner would destroy its RCCL communicator / IPC mappings at a different moment on each
+    # rank
+    keep = []
     if len(candidates) > 1:
         # short A/B before the benchmark proper (a wait that times out in the xGMI path raises
         # at the next step on that rank; every rank votes, so a failed candidate is dropped
@@ -142,6 +146,7 @@ def main(argv=None):
         for c in candidates:
             try:
                 t = make_trainer(c)
+                keep.append(t)
             except Exception as e:  # noqa: BLE001 - reported, not fatal for the other candidate
                 ab[c] = {"error": str(e)[:200]}
                 t = None
@@ -172,12 +177,13 @@ def main(argv=None):
                 best = (ms, c, t)
         if best is None:
             raise RuntimeError(f"no exchange candidate worked: {ab}")
-        chosen, tr = best[1], best[2]
+        chosen = best[1]
         # a fresh trainer for the benchmark proper: identical initial state for every choice
         tr = make_trainer(chosen)
     else:
         chosen = candidates[0]
         tr = make_trainer(chosen)
+    keep.append(tr)
     cfg = tr.cfg
 
     if a.mode == "async":
@@ -205,6 +211,7 @@ def main(argv=None):
                            data_sharding="stride", native_exchange=not a.no_native_exchange,
                            eval_async=cuda and not a.tta_sync_eval, exchange_backend=chosen)
         tr2 = Trainer(cfg2, env, dataset=data)
+        keep.append(tr2)
         s = tr2.train()
         tta = {"target_acc": a.tta, "time_to_target_s": s["time_to_target"],
                "final_acc": round(s["final_acc"], 4), "epoch_wall_s": round(s["wall_time"], 4),
