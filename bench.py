@@ -259,7 +259,8 @@ def main(argv=None):
             rec["time_to_acc"] = tta
         print(json.dumps(rec), flush=True)
     if world > 1:
-        dist.barrier()
+        from ddl_amd.parallel.roles import close_trainers
+        close_trainers(keep, env)
         dist.destroy_process_group()
 
 

@@ -480,6 +480,10 @@ class PyRunner {
   }
   std::string async_error() { return r_->async_error(); }
   void abort() { r_->abort(); }
+  void close() {
+    py::gil_scoped_release nogil;
+    r_->close();
+  }
   py::tuple selftest() {
     std::string why;
     bool ok;
@@ -569,7 +573,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_peer", &PyRunner::set_peer, py::keep_alive<1, 2>())
       .def("peer_selftest_step", &PyRunner::peer_selftest_step)
       .def("async_error", &PyRunner::async_error)
-      .def("abort", &PyRunner::abort);
+      .def("abort", &PyRunner::abort)
+      .def("close", &PyRunner::close);
 
   py::class_<PyAsyncPeer>(m, "AsyncPeer")
       .def(py::init<at::Tensor, at::Tensor, int64_t, int64_t, py::list, std::vector<int64_t>,

@@ -350,6 +350,7 @@ class SyncRunner {
   // next epoch; the caller fills g, checks w
   void peer_selftest_step(hipStream_t st);
   void abort();               // ncclCommAbort: unblocks this rank's pending collectives
+  void close();               // orderly ncclCommDestroy (call on every rank at the same point)
   hipStream_t comm_stream() const { return cs_; }
 
  private:

@@ -450,6 +450,16 @@ std::string SyncRunner::async_error() {
   return rccl().GetErrorString(st);
 }
 
+// Orderly teardown: every rank calls this at the same point of its program (after a barrier),
+// so a communicator finalisation that synchronises with the peers cannot hang on a rank that
+// has not reached it yet; afterwards the destructor has nothing collective left to do.
+void SyncRunner::close() {
+  if (!comm_) return;
+  HIP_CHECK(hipStreamSynchronize(cs_));
+  (void)rccl().CommDestroy(as_comm(comm_));
+  comm_ = nullptr;
+}
+
 void SyncRunner::abort() {
   if (!comm_) return;
   (void)rccl().CommAbort(as_comm(comm_));

@@ -35,6 +35,8 @@ def main(argv=None, mode_default: str = "sync") -> dict:
             json.dump(summary, f, indent=1)
     if env.world > 1:
         import torch.distributed as dist
+        from .roles import close_trainers
+        close_trainers([tr], env)
         dist.destroy_process_group()
     return summary
 

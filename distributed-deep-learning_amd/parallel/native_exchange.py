@@ -235,6 +235,10 @@ class NativeSyncExchange(SyncExchange):
         """Watchdog hook: abort the communicator so blocked collectives return."""
         self.runner.abort()
 
+    def close(self) -> None:
+        """Orderly teardown of the runner's communicator (every rank, same program point)."""
+        self.runner.close()
+
 
 def make_sync_exchange(plan, env, params, grads, segments, servers, engine, cfg, hyper):
     """Native runner when it applies (HIP engine, sync, adam/momentum), else the Python

@@ -282,6 +282,22 @@ class Trainer:
         return summary
 
 
+def close_trainers(trainers, env: DistEnv) -> None:
+    """Tear down the native communicators of these trainers on every rank in the same order,
+    between barriers (a finalisation that synchronises with the peers must not wait on a rank
+    still computing, and garbage collection would destroy them at rank-dependent moments)."""
+    if env.world > 1:
+        if env.device.type == "cuda":
+            torch.cuda.synchronize()
+        dist.barrier()
+    for t in trainers:
+        close = getattr(t.exchange, "close", None)
+        if close is not None and getattr(t.exchange, "native", False):
+            close()
+    if env.world > 1:
+        dist.barrier()
+
+
 class Single(Trainer):
     """``Single(epoch, batch_size).train()`` — reference ``mnist_sync/single.py:3-21``."""
 
