@@ -61,7 +61,20 @@ DDL_DEV void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 DDL_DEV uint32_t flag_load(const uint32_t* f) {
   return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// The flag that publishes a workgroup's payload: a system-scope RELEASE store.  The payload was
+// stored write-through and drained (vmcnt(0)) by every wave before the barrier, which is the
+// whole release on one device; across GPUs the payload and the flag can travel different fabric
+// paths (and, in the async protocol, the flag goes to host memory while the payload goes to a
+// peer GPU), so the release fence (L2 writeback + wait) is what orders the payload before the
+// flag for every observer.  One wave executes it per workgroup and phase.  The release is one
+// asm statement (system-scope L2 write-back, then the wait for it): the compiler's own release
+// store omits the wait when the scoreboard is already drained (MI355X guide, compiler hazard),
+// and a separate asm wait gets scheduled above the fence's write-back.
+#ifndef DDL_XGMI_RELEASE
+#define DDL_XGMI_RELEASE 1
+#endif
 DDL_DEV void flag_store(uint32_t* f, uint32_t v) {
+  if (DDL_XGMI_RELEASE) asm volatile("buffer_wbl2 sc0 sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
