@@ -173,9 +173,23 @@ class PyEngine {
     auto f = at::TensorOptions().dtype(at::kFloat).device(device_);
     auto u8 = at::TensorOptions().dtype(at::kByte).device(device_);
     auto i32 = at::TensorOptions().dtype(at::kInt).device(device_);
-    if (name == "p1") return torch::from_blob(e_.p1, {B, 14, 14, 32}, f);
-    if (name == "p2") return torch::from_blob(e_.p2, {B, 7, 7, 64}, f);
-    if (name == "p3") return torch::from_blob(e_.p3, {B, 4, 4, 128}, f);
+    // maps stored with the 2-pixel zero halo (layers.h kHalo): the interior view
+    // ("p1+halo" etc.: the whole stored map, border included)
+    const bool whole = name.size() > 5 && name.compare(name.size() - 5, 5, "+halo") == 0;
+    const std::string base_name = whole ? name.substr(0, name.size() - 5) : name;
+    auto halo = [&](float* p, int64_t h, int64_t c) {
+      auto t = torch::from_blob(p, {B, h + 4, h + 4, c}, f);
+      return whole ? t : t.narrow(1, 2, h).narrow(2, 2, h);
+    };
+    if (whole && base_name == "p1") return halo(e_.p1, 14, 32);
+    if (whole && base_name == "p2") return halo(e_.p2, 7, 64);
+    if (whole && base_name == "p3") return halo(e_.p3, 4, 128);
+    if (whole && base_name == "d4") return halo(e_.d4, 4, 256);
+    if (whole && base_name == "d3") return halo(e_.d3, 7, 128);
+    if (whole && base_name == "d2") return halo(e_.d2, 14, 64);
+    if (name == "p1") return halo(e_.p1, 14, 32);
+    if (name == "p2") return halo(e_.p2, 7, 64);
+    if (name == "p3") return halo(e_.p3, 4, 128);
     if (name == "p4") return torch::from_blob(e_.p4, {B, 1024}, f);
     if (name == "h1") return torch::from_blob(e_.h1, {B, 1024}, f);
     if (name == "h2") return torch::from_blob(e_.h2, {B, 512}, f);
@@ -183,9 +197,9 @@ class PyEngine {
     if (name == "loss") return torch::from_blob(e_.loss, {B}, f);
     if (name == "dpre2fc") return torch::from_blob(e_.dpre2fc, {B, 512}, f);
     if (name == "dpre1fc") return torch::from_blob(e_.dpre1fc, {B, 1024}, f);
-    if (name == "d4") return torch::from_blob(e_.d4, {B, 4, 4, 256}, f);
-    if (name == "d3") return torch::from_blob(e_.d3, {B, 7, 7, 128}, f);
-    if (name == "d2") return torch::from_blob(e_.d2, {B, 14, 14, 64}, f);
+    if (name == "d4") return halo(e_.d4, 4, 256);
+    if (name == "d3") return halo(e_.d3, 7, 128);
+    if (name == "d2") return halo(e_.d2, 14, 64);
     if (name == "d1") return torch::from_blob(e_.d1, {B, 28, 28, 32}, f);
     if (name == "c1") return torch::from_blob(e_.c1, {B, 14, 14, 32}, u8);
     if (name == "c2") return torch::from_blob(e_.c2, {B, 7, 7, 64}, u8);

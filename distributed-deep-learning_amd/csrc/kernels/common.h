@@ -59,6 +59,12 @@ DDL_DEV float4 bload4(brsrc_t r, int byte_off) {
   auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
   return *reinterpret_cast<float4*>(&v);
 }
+// per-lane offset + wave-uniform (SGPR) offset: the gather's per-K-tile part rides in the
+// instruction's soffset field, no VALU add.  Only for offsets known to be in range.
+DDL_DEV float4 bload4_so(brsrc_t r, int voff_bytes, int soff_bytes) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff_bytes, soff_bytes, 0);
+  return *reinterpret_cast<float4*>(&v);
+}
 DDL_DEV float bload1(brsrc_t r, int byte_off) {
   auto v = __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0);
   return __builtin_bit_cast(float, v);

@@ -123,8 +123,9 @@ size_t Engine::slab_floats_needed(int B) const {
 
 static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-static const size_t kActPer[] = {6272, 3136, 2048, 1024, 1024, 512, 16, 1,
-                                 512, 1024, 4096, 6272, 12544, 25088};
+// floats per image: p1..p3 and d4..d2 with the 2-pixel zero halo (layers.h kHalo)
+static const size_t kActPer[] = {18 * 18 * 32, 11 * 11 * 64, 8 * 8 * 128, 1024, 1024, 512, 16, 1,
+                                 512, 1024, 8 * 8 * 256, 11 * 11 * 128, 18 * 18 * 64, 25088};
 static const size_t kCodePer[] = {6272, 3136, 2048, 1024};
 
 size_t Engine::workspace_bytes() const {

@@ -14,6 +14,22 @@ namespace ddl {
 
 constexpr int kBK = 32;
 
+// SAME-conv halo.  The 5x5 convolutions' inputs (p1..p3) and the pre-pool gradient maps their
+// data gradients read (d2..d4) are stored with a 2-pixel zero border, [B, H+4, H+4, C]: the
+// workspace is zeroed once at allocation and no kernel ever writes a border element, so an
+// im2col gather is one buffer load at (per-lane voffset fixed for the whole K loop, per-K-tile
+// tap offset in the instruction's SGPR soffset) — no range checks, no per-load VALU, and the
+// per-row (b, y, x, valid) state collapses into one VGPR.  The image (conv1 input), d1 (read
+// only by conv1's weight gradient) and p4 (fc1's input) stay unpadded.
+constexpr int kHalo = 2;
+constexpr int halo_w(int h) { return h + 2 * kHalo; }
+// element offset of (b, y, x, c) in a [B, H, H, C] map, with or without the halo
+template <int H, int C, bool PAD>
+DDL_DEV int map_off(int b, int y, int x, int c) {
+  if constexpr (PAD) return ((b * halo_w(H) + y + kHalo) * halo_w(H) + x + kHalo) * C + c;
+  else return ((b * H + y) * H + x) * C + c;
+}
+
 struct LinInfo {   // linear operand: element offset of (row, k = 0 + kk), validity
   int off;
   int kk;
@@ -42,12 +58,17 @@ struct ConvFwd {
   static constexpr bool A_KCONTIG = true;
   static constexpr bool B_KCONTIG = false;
   static_assert(CIN == 1 || CIN % kBK == 0, "tap must be tile-uniform");
+  static_assert(COUT % kBK == 0, "weight columns need no range check");
+  // input with halo (conv2-4; conv1 reads the image); output with halo when a conv reads it
+  static constexpr bool PADIN = CIN % kBK == 0;
+  static constexpr bool PADOUT = H > 4;
+  static constexpr int HI = halo_w(H);
   static constexpr int rows(int batch) { return batch * RP; }
   int M, N, K;
-  const float* __restrict__ x;     // [B,H,H,CIN]
+  const float* __restrict__ x;     // [B,H,H,CIN] (+ halo when PADIN)
   const float* __restrict__ w;     // [25*CIN, COUT]
   const float* __restrict__ bias;  // [COUT]
-  float* __restrict__ out;         // [B,HP,HP,COUT]
+  float* __restrict__ out;         // [B,HP,HP,COUT] (+ halo when PADOUT)
   uint8_t* __restrict__ code;      // [B,HP,HP,COUT] or nullptr
 
   struct AInfo {
@@ -55,6 +76,7 @@ struct ConvFwd {
     int y, x;
     int kk;
     bool ok;
+    int voff;   // PADIN: byte offset of tap (0, 0) of the row (row without a position: image 0)
   };
   using BInfo = LinInfo;
 
@@ -76,7 +98,9 @@ struct ConvFwd {
     return r == 0;
   }
 
-  DDL_DEV uint32_t x_bytes() const { return (uint32_t)((M / RP) * H * H * CIN) * 4u; }
+  DDL_DEV uint32_t x_bytes() const {
+    return (uint32_t)((M / RP) * (PADIN ? HI * HI : H * H) * CIN) * 4u;
+  }
 
   DDL_DEV AInfo prepA(int m, int kk) const {
     AInfo a;
@@ -84,17 +108,17 @@ struct ConvFwd {
     a.ok = group_row(rem >> 2, rem & 3, a.y, a.x) && m < M && a.y < H && a.x < H;
     a.base = b * H * H * CIN;
     a.kk = kk;
+    // halo coordinates of input pixel (y + ky - 2, x + kx - 2) are (y + ky, x + kx); a row
+    // without a position gathers image 0 (its MFMA row is never stored)
+    a.voff = (a.ok ? (b * HI + a.y) * HI * CIN + a.x * CIN + kk : kk) * 4;
     return a;
   }
   DDL_DEV float4 loadA(const AInfo& a, int k0) const {
     const brsrc_t r = make_rsrc(x, x_bytes());
-    if constexpr (CIN % kBK == 0) {
+    if constexpr (PADIN) {
       const int tap = k0 / CIN, cib = k0 - tap * CIN;
       const int ky = tap / 5, kx = tap - ky * 5;
-      const int iy = a.y + ky - 2, ix = a.x + kx - 2;
-      const bool good = a.ok && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)H;
-      const int off = a.base + (iy * H + ix) * CIN + cib + a.kk;
-      return bload4(r, good ? off * 4 : kOOB);
+      return bload4_so(r, a.voff, ((ky * HI + kx) * CIN + cib) * 4);
     } else {  // CIN == 1: k = tap, 4 taps per float4
       float v[4];
 #pragma unroll
@@ -112,8 +136,18 @@ struct ConvFwd {
   DDL_DEV BInfo prepB(int n, int kk) const { return {kk * COUT + n, kk, n < N}; }
   DDL_DEV float4 loadB(const BInfo& b, int k0) const {
     const brsrc_t r = make_rsrc(w, 25u * CIN * COUT * 4u);
-    const bool good = b.ok && k0 + b.kk < K;
-    return bload4(r, good ? (b.off + k0 * COUT) * 4 : kOOB);
+    if constexpr (PADIN) {  // K = 25*CIN is a whole number of tiles (loop-invariant guard)
+      return bload4_so(r, b.ok ? b.off * 4 : kOOB, k0 * COUT * 4);
+    } else {
+      const bool good = b.ok && k0 + b.kk < K;
+      return bload4(r, good ? (b.off + k0 * COUT) * 4 : kOOB);
+    }
+  }
+  // pooled output (halo layout when a conv reads it) and its pool code (no halo)
+  DDL_DEV void store_pooled(int b, int py, int px, int n, float best, int arg) const {
+    out[map_off<HP, COUT, PADOUT>(b, py, px, n)] = best > 0.f ? best : 0.f;
+    if (code)
+      code[((size_t)(b * HP + py) * HP + px) * COUT + n] = best > 0.f ? (uint8_t)arg : (uint8_t)0xFF;
   }
   // max-pool + bias + ReLU of the rows [lo, hi) of the group as one window whose rows have
   // pool codes q(r); writes pooled output (py, px)
@@ -125,9 +159,7 @@ struct ConvFwd {
       const float val = v[i] + bb;
       if (val > best) { best = val; arg = qs[i]; }
     }
-    const size_t o = ((size_t)(b * HP + py) * HP + px) * COUT + n;
-    out[o] = best > 0.f ? best : 0.f;
-    if (code) code[o] = best > 0.f ? (uint8_t)arg : (uint8_t)0xFF;
+    store_pooled(b, py, px, n, best, arg);
   }
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
     const float bb = bias[n];
@@ -146,9 +178,7 @@ struct ConvFwd {
           if (val > best) { best = val; arg = q; }
         }
       }
-      const size_t o = ((size_t)(b * HP + py) * HP + px) * COUT + n;
-      out[o] = best > 0.f ? best : 0.f;
-      if (code) code[o] = best > 0.f ? (uint8_t)arg : (uint8_t)0xFF;
+      store_pooled(b, py, px, n, best, arg);
     } else if (g < FULLW + EDGEW) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -166,6 +196,7 @@ struct ConvFwd {
 
 // Scatter one pooled-output gradient g into the 2x2 window of the pre-pool gradient:
 // dpre[b, 2y+dy, 2x+dx, c] = (code == dy*2+dx) ? g : 0  (ReLU folded in via code 0xFF).
+// dpre has the halo layout when a data gradient reads it (HPREV < 28: d2..d4).
 template <int HPREV, int C>
 DDL_DEV void pool_bwd_scatter(float* __restrict__ dpre, int b, int y, int x, int c, uint8_t code,
                               float g) {
@@ -173,7 +204,7 @@ DDL_DEV void pool_bwd_scatter(float* __restrict__ dpre, int b, int y, int x, int
   for (int q = 0; q < 4; ++q) {
     const int yy = 2 * y + (q >> 1), xx = 2 * x + (q & 1);
     if (yy < HPREV && xx < HPREV)
-      dpre[((size_t)(b * HPREV + yy) * HPREV + xx) * C + c] = (code == q) ? g : 0.f;
+      dpre[map_off<HPREV, C, (HPREV < 28)>(b, yy, xx, c)] = (code == q) ? g : 0.f;
   }
 }
 
@@ -188,44 +219,37 @@ struct ConvDgrad {
   static constexpr bool A_KCONTIG = true;
   static constexpr bool B_KCONTIG = true;
   static_assert(COUT % kBK == 0, "tap must be tile-uniform");
+  static constexpr int HI = halo_w(H);
   int M, N, K;
-  const float* __restrict__ dpre;        // [B,H,H,COUT]
+  const float* __restrict__ dpre;        // [B,H+4,H+4,COUT] (halo)
   const float* __restrict__ w;           // [25*CIN, COUT]
   const uint8_t* __restrict__ code_prev; // [B,H,H,CIN]
-  float* __restrict__ dpre_prev;         // [B,HPREV,HPREV,CIN]
+  float* __restrict__ dpre_prev;         // [B,HPREV,HPREV,CIN] (+ halo if HPREV < 28)
 
   struct AInfo {
-    int base;
-    int y, x;
-    int kk;
-    bool ok;
+    int voff;  // byte offset of halo pixel (y, x) + kk (row m >= M: image 0's)
   };
   using BInfo = LinInfo;
 
   DDL_DEV AInfo prepA(int m, int kk) const {
-    AInfo a;
-    a.ok = m < M;
-    const int mm = a.ok ? m : 0;
-    a.x = mm % H;
-    const int t = mm / H;
-    a.y = t % H;
-    a.base = (t / H) * H * H * COUT;
-    a.kk = kk;
-    return a;
+    const bool ok = m < M;
+    const int mm = ok ? m : 0;
+    const int x = mm % H, t = mm / H;
+    const int y = t % H, b = t / H;
+    return {(((b * HI + y) * HI + x) * COUT + kk) * 4};
   }
+  // output gradient at (y - ky + 2, x - kx + 2) = halo pixel (y + 4 - ky, x + 4 - kx)
   DDL_DEV float4 loadA(const AInfo& a, int k0) const {
-    const brsrc_t r = make_rsrc(dpre, (uint32_t)M * COUT * 4u);
+    const brsrc_t r = make_rsrc(dpre, (uint32_t)(M / (H * H)) * HI * HI * COUT * 4u);
     const int tap = k0 / COUT, cob = k0 - tap * COUT;
     const int ky = tap / 5, kx = tap - ky * 5;
-    const int oy = a.y - ky + 2, ox = a.x - kx + 2;
-    const bool good = a.ok && (unsigned)oy < (unsigned)H && (unsigned)ox < (unsigned)H;
-    return bload4(r, good ? (a.base + (oy * H + ox) * COUT + cob + a.kk) * 4 : kOOB);
+    return bload4_so(r, a.voff, (((2 * kHalo - ky) * HI + (2 * kHalo - kx)) * COUT + cob) * 4);
   }
   DDL_DEV BInfo prepB(int n, int kk) const { return {n * COUT + kk, kk, n < N}; }
   DDL_DEV float4 loadB(const BInfo& b, int k0) const {
     const brsrc_t r = make_rsrc(w, 25u * CIN * COUT * 4u);
     const int tap = k0 / COUT, cob = k0 - tap * COUT;
-    return bload4(r, b.ok ? (b.off + tap * CIN * COUT + cob) * 4 : kOOB);
+    return bload4_so(r, b.ok ? b.off * 4 : kOOB, (tap * CIN * COUT + cob) * 4);
   }
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
 #pragma unroll
@@ -263,6 +287,10 @@ struct ConvWgrad {
   static constexpr bool A_KCONTIG = false;
   static constexpr bool B_KCONTIG = false;
   static constexpr int KW = 25 * CIN;
+  // x = p1..p3 and dpre = d2..d4 carry the halo; conv1's image and d1 do not
+  static constexpr bool PADX = CIN >= kBK;
+  static constexpr bool PADD = H < 28;
+  static constexpr int HI = halo_w(H);
   static_assert(WP >= H, "row width below the map width");
   // tiles start at multiples of BK (16 or 32): a thread's column offset never carries into
   // the next row when WP divides 16 or is a multiple of 32
@@ -332,7 +360,7 @@ struct ConvWgrad {
   }
   DDL_DEV float4 loadA(const AInfo& a, int k0) const {
     const int nimg = K / (WP * H);
-    const brsrc_t r = make_rsrc(x, (uint32_t)nimg * H * H * CIN * 4u);
+    const brsrc_t r = make_rsrc(x, (uint32_t)nimg * (PADX ? HI * HI : H * H) * CIN * 4u);
     int b, y, xx;
     bool kin;
     decode(k0, a.p, b, y, xx, kin);
@@ -340,8 +368,9 @@ struct ConvWgrad {
       // KW = 25*CIN is a multiple of 4, so a 4-row group is either all weight rows (one
       // 16-B gather) or starts at row >= KW: the ones row (db) then zeros.  Branch-free.
       const int iy = y + a.dy, ix = xx + a.dx;
-      const bool good = a.vec && kin && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)H;
-      float4 v = bload4(r, good ? (((b * H + iy) * H + ix) * CIN + a.ci) * 4 : kOOB);
+      bool good = a.vec && kin;
+      if constexpr (!PADX) good = good && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)H;
+      float4 v = bload4(r, good ? map_off<H, CIN, PADX>(b, iy, ix, a.ci) * 4 : kOOB);
       if (a.m == KW) v.x = kin ? 1.f : 0.f;
       return v;
     }
@@ -360,12 +389,12 @@ struct ConvWgrad {
   DDL_DEV BInfo prepB(int n, int kk) const { return {n, pos(kk), n < N}; }
   DDL_DEV float4 loadB(const BInfo& bi, int k0) const {
     const int nimg = K / (WP * H);
-    const brsrc_t r = make_rsrc(dpre, (uint32_t)nimg * H * H * COUT * 4u);
+    const brsrc_t r = make_rsrc(dpre, (uint32_t)nimg * (PADD ? HI * HI : H * H) * COUT * 4u);
     int b, y, xx;
     bool kin;
     decode(k0, bi.p, b, y, xx, kin);
     const bool good = bi.ok && kin;
-    return bload4(r, good ? (((b * H + y) * H + xx) * COUT + bi.n) * 4 : kOOB);
+    return bload4(r, good ? map_off<H, COUT, PADD>(b, y, xx, bi.n) * 4 : kOOB);
   }
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
 #pragma unroll
@@ -476,7 +505,7 @@ template <int HP, int C>
 struct FcDgradPool : FcDgradBase {
   static constexpr int HPREV = 2 * HP;
   const uint8_t* __restrict__ code;    // [B,HP,HP,C] == [B,N]
-  float* __restrict__ dpre_prev;       // [B,HPREV,HPREV,C]
+  float* __restrict__ dpre_prev;       // [B,HPREV,HPREV,C] + halo
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
     const int c = n % C;
     const int t = n / C;

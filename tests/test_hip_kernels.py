@@ -77,6 +77,24 @@ def test_forward_activations(setup):
     assert torch.equal(eng.eng.buffer("h1", B).cpu() > 0, h1 > 0)
 
 
+def test_halo_borders_stay_zero(setup):
+    """Conv inputs and conv data-gradient inputs are stored with a 2-pixel zero halo that no
+    kernel writes (csrc/kernels/layers.h kHalo): after training steps and a full-batch eval
+    every border element is still exactly 0 and the interior is not."""
+    eng, flat, params, grads, x, y = setup
+    for i in range(3):
+        eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 100 + i)
+    eng.correct(x.to(DEV), y.to(DEV))
+    torch.cuda.synchronize()
+    B = eng.eng.max_batch()
+    for name in ["p1", "p2", "p3", "d4", "d3", "d2"]:
+        whole = eng.eng.buffer(name + "+halo", B).cpu()
+        inner = whole[:, 2:-2, 2:-2, :].clone()
+        whole[:, 2:-2, 2:-2, :] = 0
+        assert torch.count_nonzero(whole) == 0, name
+        assert torch.count_nonzero(inner[: x.shape[0]]) > 0, name
+
+
 def ref_grads(flat, x, y, keep, seed, dtype):
     pv = [v.detach().to(dtype).clone().requires_grad_(True) for v in param_views(flat, CANON_OFFSETS)]
     loss = xent_loss(torch_forward(pv, x.to(dtype), keep, seed), y)
