@@ -75,11 +75,11 @@ void Engine::op_shape(int op, int B, int* M, int* N, int* K) {
     case OP_FC1_DGRAD: m = B; n = 1024; k = 1024; break;
     case OP_FC1_WGRAD: m = 1025; n = 1024; k = B; break;
     case OP_CONV4_DGRAD: m = B * 16; n = 128; k = 6400; break;
-    case OP_CONV4_WGRAD: m = 3201; n = 256; k = WgradConv4::padded_k(B); break;
+    case OP_CONV4_WGRAD: m = 3201; n = 256; k = WgradConv4::k_of(B); break;
     case OP_CONV3_DGRAD: m = B * 49; n = 64; k = 3200; break;
-    case OP_CONV3_WGRAD: m = 1601; n = 128; k = WgradConv3::padded_k(B); break;
+    case OP_CONV3_WGRAD: m = 1601; n = 128; k = WgradConv3::k_of(B); break;
     case OP_CONV2_DGRAD: m = B * 196; n = 32; k = 1600; break;
-    case OP_CONV2_WGRAD: m = 801; n = 64; k = WgradConv2::padded_k(B); break;
+    case OP_CONV2_WGRAD: m = 801; n = 64; k = WgradConv2::k_of(B); break;
     case OP_CONV1_WGRAD: m = 26; n = 32; k = WgradConv1::padded_k(B); break;
     default: break;
   }

@@ -4,6 +4,7 @@
 // product of its two ops' one-wave configs, so the templates live here and are explicitly
 // instantiated in several translation units (engine_ops_*.hip) that compile in parallel.
 #pragma once
+#include <stdexcept>
 #include <type_traits>
 
 #include "api.h"
@@ -44,6 +45,15 @@ inline void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const Spli
   }
 }
 
+template <class W>
+inline W wgrad_bm(int M, int N, int K, const float* x, const float* dpre, float* gw, float* gb,
+                  int B) {
+  const int nb = W::nb(B);
+  if ((uint64_t)K * (uint64_t)nb >= (1ull << 32))  // W::magic's exactness bound
+    throw std::runtime_error("weight-gradient batch too large for the batch-minor enumeration");
+  return W{M, N, K, x, dpre, gw, gb, B, nb, W::magic(nb)};
+}
+
 // Problem policy of op OP (layers.h) bound to this engine's buffers, at batch B.
 template <int OP>
 inline auto make_policy(const Engine& e, int B, const float* x, const uint32_t* seed,
@@ -75,15 +85,15 @@ inline auto make_policy(const Engine& e, int B, const float* x, const uint32_t* 
   else if constexpr (OP == OP_CONV4_DGRAD)
     return ConvDgrad<4, 128, 256, 7>{M, N, K, e.d4, P[6], e.c3, e.d3};
   else if constexpr (OP == OP_CONV4_WGRAD)
-    return WgradConv4{M, N, K, e.p3, e.d4, G[6], G[7]};
+    return wgrad_bm<WgradConv4>(M, N, K, e.p3, e.d4, G[6], G[7], B);
   else if constexpr (OP == OP_CONV3_DGRAD)
     return ConvDgrad<7, 64, 128, 14>{M, N, K, e.d3, P[4], e.c2, e.d2};
   else if constexpr (OP == OP_CONV3_WGRAD)
-    return WgradConv3{M, N, K, e.p2, e.d3, G[4], G[5]};
+    return wgrad_bm<WgradConv3>(M, N, K, e.p2, e.d3, G[4], G[5], B);
   else if constexpr (OP == OP_CONV2_DGRAD)
     return ConvDgrad<14, 32, 64, 28>{M, N, K, e.d2, P[2], e.c1, e.d1};
   else if constexpr (OP == OP_CONV2_WGRAD)
-    return WgradConv2{M, N, K, e.p1, e.d2, G[2], G[3]};
+    return wgrad_bm<WgradConv2>(M, N, K, e.p1, e.d2, G[2], G[3], B);
   else
     return WgradConv1{M, N, K, x, e.d1, G[0], G[1]};
 }

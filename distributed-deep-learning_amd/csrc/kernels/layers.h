@@ -406,12 +406,109 @@ struct ConvWgrad {
   }
 };
 
-// The four conv weight-gradient GEMMs (conv4 .. conv1) with their K row widths.
-constexpr int kWgradRowPad = 0;  // 1: pad rows to powers of two, 0: exact rows (H = 7, 14, 28)
-using WgradConv4 = ConvWgrad<4, 128, 256, 4>;
-using WgradConv3 = ConvWgrad<7, 64, 128, kWgradRowPad ? 8 : 7>;
-using WgradConv2 = ConvWgrad<14, 32, 64, kWgradRowPad ? 16 : 14>;
-using WgradConv1 = ConvWgrad<28, 1, 32, kWgradRowPad ? 32 : 28>;
+// ---------------------------------------------------------------------------------------------
+// conv weight gradient of conv2-4 (inputs and output gradients in the halo layout), K
+// enumerated batch-minor: k = pos * NB + b, pos = y*H + x, NB = max(B, 32) images per position
+// (b >= B reads 0).  A K tile (<= 32 deep) then spans at most two positions, so a slot's image
+// and pixel are the tile's scalar (b0, pos0) plus one per-lane carry, and its pixel offset is
+// one of two scalars: a gather costs an add, a compare, three selects and a multiply-add, shared
+// between the A and B slots of the same k, instead of a per-load (b, y, x) decode with column,
+// row and image carries (~17 VALU per load in the row-major enumeration of ConvWgrad).
+// A[m=(tap,ci)][k] = x[b, y+ky-2, x+kx-2, ci] = halo x[b, y+ky, x+kx, ci],
+// B[n=co][k] = halo dpre[b, y+2, x+2, co]; both MN-contiguous (ci / co innermost).
+// ---------------------------------------------------------------------------------------------
+template <int H, int CIN, int COUT>
+struct ConvWgradBM {
+  static constexpr bool A_KCONTIG = false;
+  static constexpr bool B_KCONTIG = false;
+  static constexpr int KW = 25 * CIN;
+  static constexpr int HI = halo_w(H);
+  static_assert(CIN % kBK == 0 && COUT % 4 == 0, "halo-layout conv layers only");
+  static constexpr int nb(int batch) { return batch < kBK ? kBK : batch; }
+  static constexpr int k_of(int batch) { return H * H * nb(batch); }
+  // floor(2^32 / NB) + 1: k0 / NB == umulhi(k0, mag) exactly while k0 * NB < 2^32
+  static uint32_t magic(int nbv) { return (uint32_t)((1ull << 32) / (uint64_t)nbv) + 1u; }
+  int M, N, K;                     // K = k_of(B)
+  const float* __restrict__ x;     // [B,H+4,H+4,CIN]
+  const float* __restrict__ dpre;  // [B,H+4,H+4,COUT]
+  float* __restrict__ gw;          // [25*CIN, COUT]
+  float* __restrict__ gb;          // [COUT]
+  int nimg;                        // B
+  int NB;                          // nb(B)
+  uint32_t mag;                    // magic(NB)
+
+  struct AInfo {
+    int m;       // first of the 4 rows
+    int tapoff;  // (ky*HI + kx)*CIN + ci of row m
+    int kk;
+    bool vec;    // all 4 rows are weight rows of one tap
+  };
+  struct BInfo {
+    int n;
+    int kk;
+    bool ok;
+  };
+  // image b and position carry w of slot k0 + kk; kin = inside [0, K) and b < B.  Bitwise
+  // logic only: a short-circuit && becomes an exec-mask branch per load.
+  DDL_DEV void slot(int k0, int kk, int& b, bool& w, bool& kin) const {
+    const int pos0 = (int)__umulhi((uint32_t)k0, mag);
+    const bool c0 = pos0 < H * H, c1 = pos0 + 1 < H * H;  // scalar
+    const int t = k0 - pos0 * NB + kk;
+    w = t >= NB;
+    b = t - (w ? NB : 0);
+    kin = (w ? c1 : c0) & (b < nimg);
+  }
+  DDL_DEV AInfo prepA(int m, int kk) const {
+    const int tap = m / CIN, ci = m - tap * CIN;
+    const int ky = tap / 5, kx = tap - ky * 5;
+    return {m, (ky * HI + kx) * CIN + ci, kk, m + 3 < KW};
+  }
+  DDL_DEV float4 loadA(const AInfo& a, int k0) const {
+    const brsrc_t r = make_rsrc(x, (uint32_t)nimg * HI * HI * CIN * 4u);
+    const int pos0 = (int)__umulhi((uint32_t)k0, mag);
+    const int y0 = pos0 / H, x0 = pos0 - y0 * H;
+    const int y1 = (pos0 + 1) / H, x1 = (pos0 + 1) - y1 * H;
+    const int p0 = (y0 * HI + x0) * CIN, p1 = (y1 * HI + x1) * CIN;  // scalar
+    int b;
+    bool w, kin;
+    slot(k0, a.kk, b, w, kin);
+    // the offset is computed unconditionally and pushed out of range by an add (a select of
+    // the whole address lets hipcc branch around its computation per load)
+    const int off = ((int)__umul24(b, HI * HI * CIN) + (w ? p1 : p0) + a.tapoff) * 4;
+    float4 v = bload4(r, off + ((a.vec & kin) ? 0 : kOOB));
+    if (a.m == KW) v.x = kin ? 1.f : 0.f;  // ones row: bias gradient
+    return v;
+  }
+  DDL_DEV BInfo prepB(int n, int kk) const { return {n, kk, n < N}; }
+  DDL_DEV float4 loadB(const BInfo& bi, int k0) const {
+    const brsrc_t r = make_rsrc(dpre, (uint32_t)nimg * HI * HI * COUT * 4u);
+    const int pos0 = (int)__umulhi((uint32_t)k0, mag);
+    const int y0 = pos0 / H, x0 = pos0 - y0 * H;
+    const int y1 = (pos0 + 1) / H, x1 = (pos0 + 1) - y1 * H;
+    const int q0 = ((y0 + kHalo) * HI + x0 + kHalo) * COUT;
+    const int q1 = ((y1 + kHalo) * HI + x1 + kHalo) * COUT;
+    int b;
+    bool w, kin;
+    slot(k0, bi.kk, b, w, kin);
+    const int off = ((int)__umul24(b, HI * HI * COUT) + (w ? q1 : q0) + bi.n) * 4;
+    return bload4(r, off + ((bi.ok & kin) ? 0 : kOOB));
+  }
+  DDL_DEV void epi(int m0, int n, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + r;
+      if (m < KW) gw[(size_t)m * COUT + n] = v[r];
+      else if (m == KW) gb[n] = v[r];
+    }
+  }
+};
+
+// The four conv weight-gradient GEMMs (conv4 .. conv1); conv1 (image input, d1 without halo)
+// keeps the row-major enumeration with exact rows.
+using WgradConv4 = ConvWgradBM<4, 128, 256>;
+using WgradConv3 = ConvWgradBM<7, 64, 128>;
+using WgradConv2 = ConvWgradBM<14, 32, 64>;
+using WgradConv1 = ConvWgrad<28, 1, 32, 28>;
 
 // ---------------------------------------------------------------------------------------------
 // fully connected forward (model.py:70 fc1: +b, ReLU, dropout; :79,82 fc2: +b, dropout)

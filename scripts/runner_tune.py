@@ -79,7 +79,7 @@ def main():
                     out.append(mk(c, 1, w2, wd))
             if w:
                 out.append(mk(c, s if s > 1 else 4, 0, wd))
-        for c2 in (3, 5):
+        for c2 in (0, 3, 4, 5):  # the one-wave configs (dual launches instantiate these)
             if c2 != c:
                 out.append(mk(c2, s, w, wd))
         return out
