@@ -22,7 +22,10 @@ Engine::Engine() {
   // {tile config, split-K, stream-K workers} per op: whole-step coordinate-descent tune
   // (scripts/step_tune.py over the scripts/op_bench.py per-op sweep) on one MI355X, batch 100,
   // single-stream backward with dual dgrad+wgrad launches: fwd+bwd 367 us (was 449 us)
-  static const int defc[OP_COUNT] = {3, 3, 3, 3, 3, 3, 3, 5, 3, 5, 3, 3, 3, 3, 3, 5, 3};
+  // (round 2, after the halo layout and the batch-minor weight-gradient enumeration: conv2
+  // weight gradient on the basic BK 32 loop instead of the pipelined BK 16 one, 342.8 ->
+  // 336.5 us, profiles/r2_runner_tune_halo.log)
+  static const int defc[OP_COUNT] = {3, 3, 3, 3, 3, 3, 3, 5, 3, 5, 3, 3, 3, 3, 3, 3, 3};
   // (re-tuned in the real step with scripts/sched_ab.py after the compact 52-row conv3
   // enumeration and the wgrad row decode: conv3 forward split 4 + in-launch reduce instead of
   // stream-K 3072 workers, 372.4 -> 369.5 us; conv4 weight gradient split 4 instead of 8,

@@ -191,13 +191,8 @@ void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipSt
 // need only what the dual wrote; saves one dependent boundary: conv2 dual -> [conv2 wgrad
 // reduce | conv1 wgrad GEMM]).  Instantiated for the tuned configs (OA: 32x32, OB: 32x32
 // BK 16 pipelined, ON: 32x32 split-K); any other schedule takes the unfused sequence.
-template <int OA, int OB, int ON>
-void run_dual_then_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
-  if (!e.dual || e.cfg[OA] != 3 || e.cfg[OB] != 5 || e.cfg[ON] != 3 || e.workers[ON] > 0) {
-    run_dual_inst<OA, OB>(e, x, B, seed, st);
-    run_op_inst<ON>(e, x, B, seed, true, st, 0);
-    return;
-  }
+template <int OA, int OB, int ON, class CB>
+void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
   const auto pa = make_policy<OA>(e, B, x, seed, true);
   const auto pb = make_policy<OB>(e, B, x, seed, true);
   const auto pn = make_policy<ON>(e, B, x, seed, true);
@@ -205,7 +200,6 @@ void run_dual_then_inst(Engine& e, const float* x, int B, const uint32_t* seed, 
   using PB = std::decay_t<decltype(pb)>;
   using PN = std::decay_t<decltype(pn)>;
   using CA = TileCfg<TILE_3>;
-  using CB = TileCfg<TILE_5>;
   using CN = TileCfg<TILE_3>;
   SubGrid gb;
   launch_gemm_dual<CA, PA, CB, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb,
@@ -217,6 +211,20 @@ void run_dual_then_inst(Engine& e, const float* x, int B, const uint32_t* seed, 
     launch_reduce<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, st);
     run_op_inst<ON>(e, x, B, seed, true, st, 0);
   }
+}
+
+// Instantiated for OA on 32x32 tiles, OB on 32x32 (BK 32 or pipelined BK 16), ON on 32x32
+// split-K; any other schedule takes the unfused sequence.
+template <int OA, int OB, int ON>
+void run_dual_then_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
+  const int cb = e.cfg[OB];
+  if (!e.dual || e.cfg[OA] != 3 || (cb != 3 && cb != 5) || e.cfg[ON] != 3 || e.workers[ON] > 0) {
+    run_dual_inst<OA, OB>(e, x, B, seed, st);
+    run_op_inst<ON>(e, x, B, seed, true, st, 0);
+    return;
+  }
+  if (cb == 3) dual_then_b<OA, OB, ON, TileCfg<TILE_3>>(e, x, B, seed, st);
+  else dual_then_b<OA, OB, ON, TileCfg<TILE_5>>(e, x, B, seed, st);
 }
 
 }  // namespace ddl
