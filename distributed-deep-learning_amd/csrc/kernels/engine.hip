@@ -31,8 +31,11 @@ Engine::Engine() {
   // stream-K 3072 workers, 372.4 -> 369.5 us; conv4 weight gradient split 4 instead of 8,
   // 370.5 -> 368.0 us; conv4 data gradient 2560 stream-K workers and conv3 weight gradient
   // split 12, 365.2 -> 362.3 us)
-  static const int defs[OP_COUNT] = {1, 2, 4, 8, 8, 16, 4, 1, 4, 1, 1, 4, 8, 12, 4, 32, 1024};
-  static const int defw[OP_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2560, 0, 0, 0, 0, 0, 0};
+  // (round 2, with the tap-skipping K maps of conv3/conv4: conv4 data gradient split-K 4 with
+  // a separate reduce instead of stream-K over the full K, 322.2 -> 313.3 us,
+  // profiles/r2_runner_tune_kmap.log)
+  static const int defs[OP_COUNT] = {1, 2, 4, 8, 8, 16, 4, 1, 4, 1, 4, 4, 8, 12, 4, 32, 1024};
+  static const int defw[OP_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
   static const bool inl[OP_COUNT] = {0, 1, 1, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0};
   if (const char* s = getenv("DDL_DUAL_BFIRST")) dual_bfirst = (int)strtol(s, nullptr, 0);

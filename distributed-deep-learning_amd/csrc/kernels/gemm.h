@@ -38,6 +38,8 @@
 //   mode 2: partials only; splitk_wide_reduce sums them with RL lanes per output element
 //     and runs the epilogue.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 // s_setprio 1 around each K tile's MFMA cluster in the basic main loop (A/B knob)
@@ -101,6 +103,25 @@ struct TileGeo {
   static constexpr int PART4 = NW * FRAGS * 4 * 64;
 };
 
+// ---- K maps: skipping K tiles that only multiply zeros ---------------------------------------
+// A policy with `static constexpr bool KMAP = true` enumerates, per block tile, only part of
+// its K range: `KWin kwin(m_lo, m_hi)` describes the rows' useful K sub-space (for a SAME
+// conv: the 5x5 taps that land inside the image for some row of the tile), `kvlen(win)` is its
+// length and the loaders take a *virtual* k (0 .. kvlen) plus the window: loadA(info, kv, win).
+// Split-K divides each tile's virtual length (balanced per tile); stream-K (uniform K per
+// tile) uses `kfull()`, the identity window.  Anything a window keeps beyond the useful set
+// reads zeros (halo layout), so a window only has to be a superset.
+template <class P, class = void>
+struct KMapOf {
+  static constexpr bool value = false;
+  struct Win {};
+};
+template <class P>
+struct KMapOf<P, std::void_t<decltype(P::KMAP)>> {
+  static constexpr bool value = P::KMAP;
+  using Win = typename P::KWin;
+};
+
 // ---- per-tile building blocks shared by the split-K and stream-K drivers ---------------------
 template <int BM, int BN, int BK, int WM, int WN, class P>
 struct GemmTile {
@@ -130,16 +151,27 @@ struct GemmTile {
   // end) so consecutive MFMAs are independent.
   static constexpr int NCH = (TM * TN == 1) ? 2 : 1;
   static constexpr int WPART = TM * TN * 4 * 64;  // float4 of one wave's partial fragments
+  static constexpr bool KM = KMapOf<P>::value;
+  using Win = typename KMapOf<P>::Win;
+  static DDL_DEV float4 ldA(const P& p, const typename P::AInfo& a, int k, const Win& w) {
+    if constexpr (KM) return p.loadA(a, k, w);
+    else return p.loadA(a, k);
+  }
+  static DDL_DEV float4 ldB(const P& p, const typename P::BInfo& b, int k, const Win& w) {
+    if constexpr (KM) return p.loadB(b, k, w);
+    else return p.loadB(b, k);
+  }
 
   // acc = sum over k in [kb, ke) of the (m_blk, n_blk) block tile; kb is a multiple of BK.
   // One-wave single-fragment tiles with BK = 16 take the software-pipelined loop (its double
   // register sets fit at 3 waves/SIMD only with the 16-deep K step: at BK = 32 it needed
   // 256 VGPRs + 64 AGPRs, one wave per SIMD, and lost to the basic loop); others the basic loop.
   static constexpr bool PIPE = SOLO && TM * TN == 1 && BK == 16;
+  // [kb, ke) is virtual (window w) for K-map policies
   static DDL_DEV void mainloop(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
-                               f32x16 (&acc)[TM][TN]) {
-    if constexpr (PIPE) mainloop_pipe(p, m_blk, n_blk, kb, ke, lds, acc);
-    else mainloop_basic(p, m_blk, n_blk, kb, ke, lds, acc);
+                               f32x16 (&acc)[TM][TN], const Win& w = Win()) {
+    if constexpr (PIPE) mainloop_pipe(p, m_blk, n_blk, kb, ke, lds, acc, w);
+    else mainloop_basic(p, m_blk, n_blk, kb, ke, lds, acc, w);
   }
 
   // Software-pipelined main loop (one wave, one 32x32 fragment, single LDS buffer).
@@ -151,7 +183,7 @@ struct GemmTile {
   // the stores.  PMC on the unpipelined loop: MFMA pipe ~40 % busy with waves stalled on
   // LDS-read latency and on global loads issued only one tile ahead.
   static DDL_DEV void mainloop_pipe(const P& p, int m_blk, int n_blk, int kb, int ke,
-                                    float* lds, f32x16 (&acc)[TM][TN]) {
+                                    float* lds, f32x16 (&acc)[TM][TN], const Win& w) {
     float* const As = lds;
     float* const Bs = lds + A_ELEMS;
     const int tid = threadIdx.x;
@@ -190,9 +222,9 @@ struct GemmTile {
     float f0a[R][4], f0b[R][4], f1a[R][4], f1b[R][4];  // fragments F[0], F[1]
     auto gload = [&](int k0, float4 (&ra)[FA], float4 (&rb)[FB]) {
 #pragma unroll
-      for (int it = 0; it < FA; ++it) ra[it] = p.loadA(ai[it], k0);
+      for (int it = 0; it < FA; ++it) ra[it] = ldA(p, ai[it], k0, w);
 #pragma unroll
-      for (int it = 0; it < FB; ++it) rb[it] = p.loadB(bi[it], k0);
+      for (int it = 0; it < FB; ++it) rb[it] = ldB(p, bi[it], k0, w);
     };
     auto sstore = [&](const float4 (&ra)[FA], const float4 (&rb)[FB]) {
 #pragma unroll
@@ -301,7 +333,7 @@ struct GemmTile {
   }
 
   static DDL_DEV void mainloop_basic(const P& p, int m_blk, int n_blk, int kb, int ke,
-                                     float* lds, f32x16 (&acc)[TM][TN]) {
+                                     float* lds, f32x16 (&acc)[TM][TN], const Win& w) {
     float* const As0 = lds;
     float* const Bs0 = lds + NBUF * A_ELEMS;
     const int tid = threadIdx.x;
@@ -348,9 +380,9 @@ struct GemmTile {
     float4 ra[FA], rb[FB];
     auto gload = [&](int k0) {
 #pragma unroll
-      for (int it = 0; it < FA; ++it) ra[it] = p.loadA(ai[it], k0);
+      for (int it = 0; it < FA; ++it) ra[it] = ldA(p, ai[it], k0, w);
 #pragma unroll
-      for (int it = 0; it < FB; ++it) rb[it] = p.loadB(bi[it], k0);
+      for (int it = 0; it < FB; ++it) rb[it] = ldB(p, bi[it], k0, w);
     };
     auto sstore = [&](int buf) {
       float* As = As0 + buf * A_ELEMS;
@@ -549,10 +581,19 @@ DDL_DEV void splitk_body(const P& p, int kchunk, int mode, float4* __restrict__ 
   using G = typename T::G;
   const int m_blk = bx * BM;
   const int n_blk = by * BN;
-  const int kb = bz * kchunk;
-  const int ke = min(p.K, kb + kchunk);
   f32x16 acc[T::TM][T::TN];
-  T::mainloop(p, m_blk, n_blk, kb, ke, lds, acc);
+  if constexpr (T::KM) {
+    // this tile's useful K sub-space, divided over the gz splits (whole BK tiles)
+    const typename T::Win w = p.kwin(m_blk, min(p.M, m_blk + BM));
+    const int kv = p.kvlen(w);
+    const int kc = gz > 1 ? ((kv + gz - 1) / gz + BK - 1) / BK * BK : kv;
+    const int kb = bz * kc;
+    T::mainloop(p, m_blk, n_blk, kb, min(kv, kb + kc), lds, acc, w);
+  } else {
+    const int kb = bz * kchunk;
+    const int ke = min(p.K, kb + kchunk);
+    T::mainloop(p, m_blk, n_blk, kb, ke, lds, acc);
+  }
   if (mode != 0) {
     const int tile = by * gx + bx;
     const int ntiles = gx * gy;
@@ -590,12 +631,14 @@ DDL_DEV void streamk_body(const P& p, int KI, int gx, long long I, float4* __res
   const long long end = first_iter(w + 1);
   const int start_tile = (int)(it / KI);
   f32x16 acc[T::TM][T::TN];
+  typename T::Win win{};
+  if constexpr (T::KM) win = p.kfull();  // stream-K needs the same K per tile
   while (it < end) {
     const int tile = (int)(it / KI);
     const int klo = (int)(it - (long long)tile * KI);
     const int khi = (int)min((long long)KI, (long long)klo + (end - it));
     const int m_blk = (tile % gx) * BM, n_blk = (tile / gx) * BN;
-    T::mainloop(p, m_blk, n_blk, klo * BK, min(p.K, khi * BK), lds, acc);
+    T::mainloop(p, m_blk, n_blk, klo * BK, min(p.K, khi * BK), lds, acc, win);
     it += khi - klo;
     if (klo == 0 && khi == KI) {
       T::epilogue(p, m_blk, n_blk, acc);

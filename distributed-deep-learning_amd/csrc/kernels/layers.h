@@ -30,6 +30,23 @@ DDL_DEV int map_off(int b, int y, int x, int c) {
   else return ((b * H + y) * H + x) * C + c;
 }
 
+// Tap skipping (gemm.h K maps).  On the 4x4 / 7x7 / 14x14 maps 51 / 31 / 16 % of the 5x5 taps of
+// a SAME conv land in the zero halo.  With M enumerated position-major (all images of one pixel /
+// pool window adjacent) a 32-row tile covers one or two positions, so its useful taps are a
+// rectangle [ty0, ty0+nty) x [tx0, tx0+ntx) of the 5x5 grid and its K loop runs only over those
+// (virtual tap t -> (ty0 + t / ntx, tx0 + t % ntx); rx = ceil(2^16 / ntx) divides exactly for t < 25).
+struct TapWin {
+  int ty0, nty, tx0, ntx, rx;
+};
+DDL_DEV TapWin tap_win(int ty0, int ty1, int tx0, int tx1) {  // inclusive bounds
+  const int nx = tx1 - tx0 + 1;
+  return {ty0, ty1 - ty0 + 1, tx0, nx, (65536 + nx - 1) / nx};
+}
+DDL_DEV int tap_of(const TapWin& w, int t) {
+  const int ty = (t * w.rx) >> 16;
+  return (w.ty0 + ty) * 5 + w.tx0 + (t - ty * w.ntx);
+}
+
 struct LinInfo {   // linear operand: element offset of (row, k = 0 + kk), validity
   int off;
   int kk;
@@ -64,6 +81,13 @@ struct ConvFwd {
   static constexpr bool PADOUT = H > 4;
   static constexpr int HI = halo_w(H);
   static constexpr int rows(int batch) { return batch * RP; }
+  // conv3-4: M group-major, m = (g*B + b)*4 + q (every image's pool window g adjacent), and a
+  // K map over the taps that reach the image from the tile's pixels.  conv1 (K = 25: one
+  // tile) and conv2 (14x14: only 16 % of the taps fall in the halo, while the group-major
+  // order spreads a tile's gathers over 32 images: 26.1 -> 26.6 us) keep the image-major
+  // order m = b*RP + 4g + q.
+  static constexpr bool KMAP = PADIN && H <= 7;
+  using KWin = TapWin;
   int M, N, K;
   const float* __restrict__ x;     // [B,H,H,CIN] (+ halo when PADIN)
   const float* __restrict__ w;     // [25*CIN, COUT]
@@ -101,11 +125,44 @@ struct ConvFwd {
   DDL_DEV uint32_t x_bytes() const {
     return (uint32_t)((M / RP) * (PADIN ? HI * HI : H * H) * CIN) * 4u;
   }
+  // image b and 4-row group g of row m
+  DDL_DEV void row_bg(int m, int& b, int& g) const {
+    if constexpr (KMAP) {
+      const int nimg = M / RP, gb = m >> 2;
+      g = gb / nimg;
+      b = gb - g * nimg;
+    } else {
+      b = m / RP;
+      g = (m - b * RP) >> 2;
+    }
+  }
+  DDL_DEV KWin kfull() const { return tap_win(0, 4, 0, 4); }
+  // input row y + ky - 2 is inside the image for ky in [2 - y, H + 1 - y]
+  DDL_DEV KWin kwin(int m_lo, int m_hi) const {
+    const int nimg = M / RP;
+    const int g0 = (m_lo >> 2) / nimg, g1 = ((m_hi - 1) >> 2) / nimg;
+    int ylo = H, yhi = 0, xlo = H, xhi = 0;
+    for (int g = g0; g <= g1; ++g)
+      for (int q = 0; q < 4; ++q) {
+        int y, xx;
+        if (group_row(g, q, y, xx) && y < H && xx < H) {
+          ylo = min(ylo, y); yhi = max(yhi, y);
+          xlo = min(xlo, xx); xhi = max(xhi, xx);
+        }
+      }
+    return tap_win(max(0, 2 - yhi), min(4, H + 1 - ylo), max(0, 2 - xhi), min(4, H + 1 - xlo));
+  }
+  DDL_DEV int kvlen(const KWin& w) const { return w.nty * w.ntx * CIN; }
+  DDL_DEV int kreal(const KWin& w, int kv) const {
+    const int t = kv / CIN;
+    return tap_of(w, t) * CIN + (kv - t * CIN);
+  }
 
   DDL_DEV AInfo prepA(int m, int kk) const {
     AInfo a;
-    const int b = m / RP, rem = m - b * RP;
-    a.ok = group_row(rem >> 2, rem & 3, a.y, a.x) && m < M && a.y < H && a.x < H;
+    int b, g;
+    row_bg(m, b, g);
+    a.ok = group_row(g, m & 3, a.y, a.x) && m < M && a.y < H && a.x < H;
     a.base = b * H * H * CIN;
     a.kk = kk;
     // halo coordinates of input pixel (y + ky - 2, x + kx - 2) are (y + ky, x + kx); a row
@@ -133,7 +190,13 @@ struct ConvFwd {
       return make_float4(v[0], v[1], v[2], v[3]);
     }
   }
+  DDL_DEV float4 loadA(const AInfo& a, int kv, const KWin& win) const {
+    return loadA(a, kreal(win, kv));
+  }
   DDL_DEV BInfo prepB(int n, int kk) const { return {kk * COUT + n, kk, n < N}; }
+  DDL_DEV float4 loadB(const BInfo& b, int kv, const KWin& win) const {
+    return loadB(b, kreal(win, kv));
+  }
   DDL_DEV float4 loadB(const BInfo& b, int k0) const {
     const brsrc_t r = make_rsrc(w, 25u * CIN * COUT * 4u);
     if constexpr (PADIN) {  // K = 25*CIN is a whole number of tiles (loop-invariant guard)
@@ -163,7 +226,8 @@ struct ConvFwd {
   }
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
     const float bb = bias[n];
-    const int b = m0 / RP, g = (m0 - b * RP) >> 2;
+    int b, g;
+    row_bg(m0, b, g);
     const float vv[4] = {v[0], v[1], v[2], v[3]};
     if (!ODD || g < FULLW) {
       const int w = ODD ? HP - 1 : HP;
@@ -220,6 +284,12 @@ struct ConvDgrad {
   static constexpr bool B_KCONTIG = true;
   static_assert(COUT % kBK == 0, "tap must be tile-uniform");
   static constexpr int HI = halo_w(H);
+  // conv3-4 (H <= 7): M pixel-major, m = (y*H + x)*B + b, and a K map over the taps whose
+  // output-gradient pixel (y - ky + 2, x - kx + 2) is inside the map for some row of the tile.
+  // conv2 (14x14, 16 % of the taps in the halo) keeps m = (b*H + y)*H + x: the pixel-major
+  // order made its dual launch 50.6 -> 58.4 us (gathers spread over 32 images per tile).
+  static constexpr bool KMAP = H <= 7;
+  using KWin = TapWin;
   int M, N, K;
   const float* __restrict__ dpre;        // [B,H+4,H+4,COUT] (halo)
   const float* __restrict__ w;           // [25*CIN, COUT]
@@ -231,11 +301,38 @@ struct ConvDgrad {
   };
   using BInfo = LinInfo;
 
+  // image and pixel of row m
+  DDL_DEV void row_pix(int m, int& b, int& y, int& x) const {
+    if constexpr (KMAP) {
+      const int nimg = M / (H * H);
+      const int pos = m / nimg;
+      b = m - pos * nimg;
+      y = pos / H;
+      x = pos - y * H;
+    } else {
+      x = m % H;
+      const int t = m / H;
+      y = t % H;
+      b = t / H;
+    }
+  }
+  DDL_DEV KWin kfull() const { return tap_win(0, 4, 0, 4); }
+  // oy = y - ky + 2 in [0, H) for ky in [y + 3 - H, y + 2]
+  DDL_DEV KWin kwin(int m_lo, int m_hi) const {
+    const int nimg = M / (H * H);
+    const int p0 = m_lo / nimg, p1 = (m_hi - 1) / nimg;
+    const int ylo = p0 / H, yhi = p1 / H;
+    const int xlo = ylo == yhi ? p0 - ylo * H : 0, xhi = ylo == yhi ? p1 - yhi * H : H - 1;
+    return tap_win(max(0, ylo + 3 - H), min(4, yhi + 2), max(0, xlo + 3 - H), min(4, xhi + 2));
+  }
+  DDL_DEV int kvlen(const KWin& w) const { return w.nty * w.ntx * COUT; }
+  DDL_DEV int kreal(const KWin& w, int kv) const {
+    const int t = kv / COUT;
+    return tap_of(w, t) * COUT + (kv - t * COUT);
+  }
   DDL_DEV AInfo prepA(int m, int kk) const {
-    const bool ok = m < M;
-    const int mm = ok ? m : 0;
-    const int x = mm % H, t = mm / H;
-    const int y = t % H, b = t / H;
+    int b, y, x;
+    row_pix(m < M ? m : 0, b, y, x);
     return {(((b * HI + y) * HI + x) * COUT + kk) * 4};
   }
   // output gradient at (y - ky + 2, x - kx + 2) = halo pixel (y + 4 - ky, x + 4 - kx)
@@ -251,15 +348,21 @@ struct ConvDgrad {
     const int tap = k0 / COUT, cob = k0 - tap * COUT;
     return bload4_so(r, b.ok ? b.off * 4 : kOOB, (tap * CIN * COUT + cob) * 4);
   }
+  DDL_DEV float4 loadA(const AInfo& a, int kv, const KWin& win) const {
+    return loadA(a, kreal(win, kv));
+  }
+  DDL_DEV float4 loadB(const BInfo& b, int kv, const KWin& win) const {
+    return loadB(b, kreal(win, kv));
+  }
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = m0 + r;
       if (m >= M) break;
-      const int xx = m % H;
-      const int t = m / H;
-      const int y = t % H, b = t / H;
-      pool_bwd_scatter<HPREV, CIN>(dpre_prev, b, y, xx, n, code_prev[(size_t)m * CIN + n], v[r]);
+      int b, y, xx;
+      row_pix(m, b, y, xx);
+      const size_t px = (size_t)(b * H + y) * H + xx;
+      pool_bwd_scatter<HPREV, CIN>(dpre_prev, b, y, xx, n, code_prev[px * CIN + n], v[r]);
     }
   }
 };
@@ -428,6 +531,14 @@ struct ConvWgradBM {
   static constexpr int k_of(int batch) { return H * H * nb(batch); }
   // floor(2^32 / NB) + 1: k0 / NB == umulhi(k0, mag) exactly while k0 * NB < 2^32
   static uint32_t magic(int nbv) { return (uint32_t)((1ull << 32) / (uint64_t)nbv) + 1u; }
+  // K map: a tile's rows are (one or two) taps; only the output positions whose input pixel
+  // (y + ky - 2, x + kx - 2) is inside the image contribute.  The window is a rectangle of
+  // positions [y0, y0+ny) x [x0, x0+nx); virtual position v -> (y0 + v / nx, x0 + v % nx)
+  // (rx = ceil(2^16 / nx): exact for v <= 196).
+  static constexpr bool KMAP = true;
+  struct KWin {
+    int y0, ny, x0, nx, rx;
+  };
   int M, N, K;                     // K = k_of(B)
   const float* __restrict__ x;     // [B,H+4,H+4,CIN]
   const float* __restrict__ dpre;  // [B,H+4,H+4,COUT]
@@ -448,11 +559,31 @@ struct ConvWgradBM {
     int kk;
     bool ok;
   };
-  // image b and position carry w of slot k0 + kk; kin = inside [0, K) and b < B.  Bitwise
-  // logic only: a short-circuit && becomes an exec-mask branch per load.
-  DDL_DEV void slot(int k0, int kk, int& b, bool& w, bool& kin) const {
+  static DDL_DEV KWin pos_win(int y0, int y1, int x0, int x1) {  // inclusive bounds
+    const int nx = x1 - x0 + 1;
+    return {y0, y1 - y0 + 1, x0, nx, (65536 + nx - 1) / nx};
+  }
+  DDL_DEV KWin kfull() const { return pos_win(0, H - 1, 0, H - 1); }
+  DDL_DEV KWin kwin(int m_lo, int m_hi) const {
+    if (m_hi > KW) return kfull();  // the ones row (bias gradient) sums every position
+    const int t0 = m_lo / CIN, t1 = (m_hi - 1) / CIN;
+    const int kylo = t0 / 5, kyhi = t1 / 5;
+    const int kxlo = kylo == kyhi ? t0 - kylo * 5 : 0, kxhi = kylo == kyhi ? t1 - kyhi * 5 : 4;
+    // input row y + ky - 2 is inside the image for y in [2 - ky, H + 1 - ky]
+    return pos_win(max(0, 2 - kyhi), min(H - 1, H + 1 - kylo), max(0, 2 - kxhi),
+                   min(H - 1, H + 1 - kxlo));
+  }
+  DDL_DEV int kvlen(const KWin& w) const { return w.ny * w.nx * NB; }
+  static DDL_DEV void vpos(const KWin& w, int v, int& y, int& xx) {
+    const int r = (v * w.rx) >> 16;
+    y = w.y0 + r;
+    xx = w.x0 + v - r * w.nx;
+  }
+  // image b and position carry w of virtual slot k0 + kk; kin = inside the window's K range
+  // and b < B.  Bitwise logic only: a short-circuit && becomes an exec-mask branch per load.
+  DDL_DEV void slot(int k0, int kk, int nvp, int& b, bool& w, bool& kin) const {
     const int pos0 = (int)__umulhi((uint32_t)k0, mag);
-    const bool c0 = pos0 < H * H, c1 = pos0 + 1 < H * H;  // scalar
+    const bool c0 = pos0 < nvp, c1 = pos0 + 1 < nvp;  // scalar
     const int t = k0 - pos0 * NB + kk;
     w = t >= NB;
     b = t - (w ? NB : 0);
@@ -463,15 +594,16 @@ struct ConvWgradBM {
     const int ky = tap / 5, kx = tap - ky * 5;
     return {m, (ky * HI + kx) * CIN + ci, kk, m + 3 < KW};
   }
-  DDL_DEV float4 loadA(const AInfo& a, int k0) const {
+  DDL_DEV float4 loadA(const AInfo& a, int k0, const KWin& win) const {
     const brsrc_t r = make_rsrc(x, (uint32_t)nimg * HI * HI * CIN * 4u);
     const int pos0 = (int)__umulhi((uint32_t)k0, mag);
-    const int y0 = pos0 / H, x0 = pos0 - y0 * H;
-    const int y1 = (pos0 + 1) / H, x1 = (pos0 + 1) - y1 * H;
+    int y0, x0, y1, x1;
+    vpos(win, pos0, y0, x0);
+    vpos(win, pos0 + 1, y1, x1);
     const int p0 = (y0 * HI + x0) * CIN, p1 = (y1 * HI + x1) * CIN;  // scalar
     int b;
     bool w, kin;
-    slot(k0, a.kk, b, w, kin);
+    slot(k0, a.kk, win.ny * win.nx, b, w, kin);
     // the offset is computed unconditionally and pushed out of range by an add (a select of
     // the whole address lets hipcc branch around its computation per load)
     const int off = ((int)__umul24(b, HI * HI * CIN) + (w ? p1 : p0) + a.tapoff) * 4;
@@ -480,16 +612,17 @@ struct ConvWgradBM {
     return v;
   }
   DDL_DEV BInfo prepB(int n, int kk) const { return {n, kk, n < N}; }
-  DDL_DEV float4 loadB(const BInfo& bi, int k0) const {
+  DDL_DEV float4 loadB(const BInfo& bi, int k0, const KWin& win) const {
     const brsrc_t r = make_rsrc(dpre, (uint32_t)nimg * HI * HI * COUT * 4u);
     const int pos0 = (int)__umulhi((uint32_t)k0, mag);
-    const int y0 = pos0 / H, x0 = pos0 - y0 * H;
-    const int y1 = (pos0 + 1) / H, x1 = (pos0 + 1) - y1 * H;
+    int y0, x0, y1, x1;
+    vpos(win, pos0, y0, x0);
+    vpos(win, pos0 + 1, y1, x1);
     const int q0 = ((y0 + kHalo) * HI + x0 + kHalo) * COUT;
     const int q1 = ((y1 + kHalo) * HI + x1 + kHalo) * COUT;
     int b;
     bool w, kin;
-    slot(k0, bi.kk, b, w, kin);
+    slot(k0, bi.kk, win.ny * win.nx, b, w, kin);
     const int off = ((int)__umul24(b, HI * HI * COUT) + (w ? q1 : q0) + bi.n) * 4;
     return bload4(r, off + ((bi.ok & kin) ? 0 : kOOB));
   }
