@@ -38,6 +38,8 @@
 //   mode 2: partials only; splitk_wide_reduce sums them with RL lanes per output element
 //     and runs the epilogue.
 #pragma once
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "common.h"
@@ -666,9 +668,19 @@ struct SubGrid {
   int kchunk = 0, mode = 0;  // split-K
   int KI = 0;                // stream-K
   long long I = 0;
+  int xcd = 0;               // split-K: XCD-contiguous block numbering (xcd_remap)
   float4* slab = nullptr;
   int* tickets = nullptr;
 };
+
+// The hardware dispatches block b to XCD b % 8 (each XCD has its own L2).  This bijection gives
+// XCD x a contiguous range of virtual ids instead, so the m-fastest neighbours that share a
+// weight panel (same n tile and K split) run behind one L2 (guide T1; any block count n).
+DDL_DEV int xcd_remap(int b, int n) {
+  const int q = n >> 3, r = n & 7;
+  const int x = b & 7, i = b >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
 
 template <int BM, int BN, int BK, int WM, int WN, class P>
 DDL_DEV void run_sub(const P& p, const SubGrid& g, int vb, float* lds, int* flag) {
@@ -676,6 +688,7 @@ DDL_DEV void run_sub(const P& p, const SubGrid& g, int vb, float* lds, int* flag
     streamk_body<BM, BN, BK, WM, WN, P>(p, g.KI, g.gx, g.I, g.slab, g.tickets, vb, g.nblocks,
                                         lds, flag);
   } else {
+    if (g.xcd) vb = xcd_remap(vb, g.nblocks);
     const int bx = vb % g.gx, t = vb / g.gx;
     splitk_body<BM, BN, BK, WM, WN, P>(p, g.kchunk, g.mode, g.slab, g.tickets, bx, t % g.gy,
                                        t / g.gy, g.gx, g.gy, g.gz, lds, flag);
@@ -684,13 +697,21 @@ DDL_DEV void run_sub(const P& p, const SubGrid& g, int vb, float* lds, int* flag
 
 template <int BM, int BN, int BK, int WM, int WN, class P>
 __global__ void __launch_bounds__(WM * WN * 64)
-gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets) {
+gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets,
+                int xcd) {
   using T = GemmTile<BM, BN, BK, WM, WN, P>;
   __shared__ float4 lds4[T::LDS_F4 + 1];  // staging images + last-arriver flag (one array:
                                           // guide §5 trap 4a)
-  splitk_body<BM, BN, BK, WM, WN, P>(p, kchunk, mode, slab, tickets, blockIdx.x, blockIdx.y,
-                                     blockIdx.z, gridDim.x, gridDim.y, gridDim.z,
-                                     reinterpret_cast<float*>(lds4),
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (xcd) {  // linear id (x fastest, the dispatch order) -> XCD-contiguous virtual id
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int v = xcd_remap(bx + gx * (by + gy * bz), gx * gy * gridDim.z);
+    bx = v % gx;
+    by = (v / gx) % gy;
+    bz = v / (gx * gy);
+  }
+  splitk_body<BM, BN, BK, WM, WN, P>(p, kchunk, mode, slab, tickets, bx, by, bz, gridDim.x,
+                                     gridDim.y, gridDim.z, reinterpret_cast<float*>(lds4),
                                      reinterpret_cast<int*>(lds4 + T::LDS_F4));
 }
 
@@ -877,6 +898,15 @@ inline size_t gemm_slab_f4(int M, int N, int K, int splits, int workers) {
   return sk > sp ? sk : sp;
 }
 
+// XCD-contiguous split-K numbering: DDL_XCD_REMAP=0/1 (A/B knob, read once)
+inline int xcd_remap_default() {
+  static const int v = [] {
+    const char* e = getenv("DDL_XCD_REMAP");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 // Schedule of one launch: stream-K when workers > 0 (and the tile count fits the tickets),
 // else split-K with `splits`: z > wide_thr uses mode 2 (separate wide reduce), else mode 1
 // (last arriver).
@@ -899,6 +929,7 @@ inline SubGrid plan_gemm(const P& p, int splits, int workers, int wide_thr,
   }
   g.gz = splitk_z<BK>(p.K, splits);
   g.kchunk = g.gz > 1 ? splitk_kchunk<BK>(p.K, splits) : p.K;
+  g.xcd = xcd_remap_default();
   g.mode = g.gz == 1 ? 0 : (g.gz > wide_thr ? 2 : 1);
   if (g.mode == 1 && (long long)g.gx * g.gy > sc.max_tiles) g.mode = 2;  // ticket capacity
   g.nblocks = g.gx * g.gy * g.gz;
@@ -939,7 +970,7 @@ inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch
     return;
   }
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, WM, WN, P>), dim3(g.gx, g.gy, g.gz),
-                     dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets);
+                     dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets, g.xcd);
   launch_reduce<BM, BN, BK, WM, WN, P>(p, g, stream);
 }
 
