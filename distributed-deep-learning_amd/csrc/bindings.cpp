@@ -70,7 +70,8 @@ class PyEngine {
   void set_cfg(std::vector<int64_t> c) {
     TORCH_CHECK((int)c.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " tile configs");
     for (int i = 0; i < ddl::OP_COUNT; ++i) {
-      TORCH_CHECK(c[i] >= 0 && c[i] < ddl::NUM_TILE_CFGS, "tile config out of range");
+      TORCH_CHECK((c[i] >= 0 && c[i] < ddl::NUM_TILE_CFGS) || c[i] == ddl::CFG_KWAVE,
+                  "tile config out of range");
       e_.cfg[i] = (int)c[i];
     }
     realloc();

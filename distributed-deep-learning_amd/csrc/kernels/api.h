@@ -68,6 +68,9 @@ constexpr int NUM_TILE_CFGS = 9;
 // instantiated for those ops): 9 = 128x128 (2x2 waves of 64x64), 10 = 128x64 (2x2 waves of
 // 64x32), 11 = 256x64 (4x1 waves of 64x64), 12 = 128x128 (4x1 waves of 32x128).
 constexpr int NUM_EVAL_TILE_CFGS = 13;
+// training-only: 32x32 one-wave tiles with the K range split over the waves of ONE workgroup
+// (gemm.h gemm_kwave_kernel; `splits` picks 4 / 8 / 16 waves); fc layers only
+constexpr int CFG_KWAVE = 13;
 
 struct Engine {
   const float* P[14] = {};   // parameter tensors v0..v13 (any flat layout)

@@ -25,7 +25,9 @@ Engine::Engine() {
   // (round 2, after the halo layout and the batch-minor weight-gradient enumeration: conv2
   // weight gradient on the basic BK 32 loop instead of the pipelined BK 16 one, 342.8 ->
   // 336.5 us, profiles/r2_runner_tune_halo.log)
-  static const int defc[OP_COUNT] = {3, 3, 3, 3, 3, 3, 3, 5, 3, 5, 3, 3, 3, 3, 3, 3, 3};
+  // fc1 forward on the K-wave launch (8 waves per workgroup, LDS reduction, no reduce launch):
+  // 313.4 -> 310.6 us (profiles/r2_runner_tune_kwave.log)
+  static const int defc[OP_COUNT] = {3, 3, 3, 3, CFG_KWAVE, 3, 3, 5, 3, 5, 3, 3, 3, 3, 3, 3, 3};
   // (re-tuned in the real step with scripts/sched_ab.py after the compact 52-row conv3
   // enumeration and the wgrad row decode: conv3 forward split 4 + in-launch reduce instead of
   // stream-K 3072 workers, 372.4 -> 369.5 us; conv4 weight gradient split 4 instead of 8,
@@ -104,6 +106,9 @@ void Engine::op_shape(int op, int B, int* M, int* N, int* K) {
 
 static size_t slab_need(int c, int M, int N, int K, int s, int w) {
   switch (c) {
+    // reduces in LDS; an op without a K-wave instantiation falls back to the 32x32 split-K
+    // launch with the same split factor (engine_impl.h launch_cfg), so size for that
+    case CFG_KWAVE: return gemm_slab_f4<TILE_3>(M, N, K, s, w);
     case 0: return gemm_slab_f4<TILE_0>(M, N, K, s, w);
     case 1: return gemm_slab_f4<TILE_1>(M, N, K, s, w);
     case 2: return gemm_slab_f4<TILE_2>(M, N, K, s, w);

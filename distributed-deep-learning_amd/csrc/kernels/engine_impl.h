@@ -32,6 +32,13 @@ namespace ddl {
 template <class P>
 inline void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const SplitScratch& sc,
                        hipStream_t st) {
+  if (c == CFG_KWAVE) {
+    if constexpr (KWaveOK<P>::value) {
+      launch_gemm_kwave<32>(p, s, st);
+      return;
+    }
+    c = 3;  // not instantiated for this op: the one-wave 32x32 tile
+  }
   switch (c) {
     case 0: launch_gemm<TILE_0>(p, s, wide_thr, sc, st, w); break;
     case 1: launch_gemm<TILE_1>(p, s, wide_thr, sc, st, w); break;

@@ -188,7 +188,7 @@ struct GemmTile {
                                     float* lds, f32x16 (&acc)[TM][TN], const Win& w) {
     float* const As = lds;
     float* const Bs = lds + A_ELEMS;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x & (NT - 1);  // a one-wave tile may be one wave of a larger block
     const int lane = tid & 63;
     const int nk = (ke - kb + BK - 1) / BK;
     typename P::AInfo ai[FA];
@@ -338,7 +338,7 @@ struct GemmTile {
                                      float* lds, f32x16 (&acc)[TM][TN], const Win& w) {
     float* const As0 = lds;
     float* const Bs0 = lds + NBUF * A_ELEMS;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x & (NT - 1);  // a one-wave tile may be one wave of a larger block
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
@@ -724,6 +724,64 @@ gemm_streamk_kernel(P p, int KI, int gx, long long I, float4* __restrict__ slab,
   streamk_body<BM, BN, BK, WM, WN, P>(p, KI, gx, I, slab, tickets, blockIdx.x, gridDim.x,
                                       reinterpret_cast<float*>(lds4),
                                       reinterpret_cast<int*>(lds4 + T::LDS_F4));
+}
+
+// K split inside ONE workgroup, for the skinny GEMMs (the fc layers at M = batch): KW waves each
+// run the one-wave 32x32 tile over 1/KW of the K range (own LDS staging image, no barriers),
+// then the KW accumulators are summed through LDS in wave order (deterministic) and the fused
+// epilogue runs in the same launch — no partial slab in HBM and no reduce launch, where the
+// split-K form of the same tile needs a partial round trip plus a dependent kernel boundary.
+template <int BK, int KW, class P>
+__global__ void __launch_bounds__(KW * 64) gemm_kwave_kernel(P p) {
+  using T = GemmTile<32, 32, BK, 1, 1, P>;
+  static_assert(KW == 4 || KW == 8 || KW == 16, "4, 8 or 16 waves");
+  static_assert(T::LDS_F4 * 16 >= 16 * 64 * 4, "a wave's reduction image fits its staging area");
+  __shared__ float4 lds4[KW * T::LDS_F4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int m_blk = blockIdx.x * 32, n_blk = blockIdx.y * 32;
+  float* mine = reinterpret_cast<float*>(lds4 + wave * T::LDS_F4);
+  f32x16 acc[1][1];
+  if constexpr (T::KM) {
+    const typename T::Win w = p.kwin(m_blk, min(p.M, m_blk + 32));
+    const int kv = p.kvlen(w);
+    const int kc = ((kv + KW - 1) / KW + BK - 1) / BK * BK;
+    const int kb = wave * kc;
+    T::mainloop(p, m_blk, n_blk, kb, min(kv, kb + kc), mine, acc, w);
+  } else {
+    const int kc = ((p.K + KW - 1) / KW + BK - 1) / BK * BK;
+    const int kb = wave * kc;
+    T::mainloop(p, m_blk, n_blk, kb, min(p.K, kb + kc), mine, acc);
+  }
+  __syncthreads();  // every wave is past its staging reads: the images become the sum buffer
+  float* red = reinterpret_cast<float*>(lds4);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) red[(wave * 16 + q) * 64 + lane] = acc[0][0][q];
+  __syncthreads();
+  if (wave < 4) {  // wave g finishes row group g (accumulator registers 4g..4g+3) of every lane
+    const int g = wave;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int ww = 0; ww < KW; ++ww)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] += red[(ww * 16 + 4 * g + j) * 64 + lane];
+    const int n = n_blk + (lane & 31);
+    const int m0 = m_blk + 8 * g + 4 * (lane >> 5);
+    if (n < p.N && m0 < p.M) p.epi(m0, n, f32x4{v[0], v[1], v[2], v[3]});
+  }
+}
+
+// waves per workgroup of the K-wave launch for a requested split factor
+inline int kwave_waves(int splits) { return splits <= 4 ? 4 : (splits <= 8 ? 8 : 16); }
+
+template <int BK, class P>
+inline void launch_gemm_kwave(const P& p, int splits, hipStream_t stream) {
+  if (p.M <= 0 || p.N <= 0) return;
+  const dim3 grid((p.M + 31) / 32, (p.N + 31) / 32);
+  switch (kwave_waves(splits)) {
+    case 4: hipLaunchKernelGGL((gemm_kwave_kernel<BK, 4, P>), grid, dim3(256), 0, stream, p); break;
+    case 8: hipLaunchKernelGGL((gemm_kwave_kernel<BK, 8, P>), grid, dim3(512), 0, stream, p); break;
+    default:
+      hipLaunchKernelGGL((gemm_kwave_kernel<BK, 16, P>), grid, dim3(1024), 0, stream, p);
+  }
 }
 
 template <int BM_, int BN_, int BK_, int WM_, int WN_>

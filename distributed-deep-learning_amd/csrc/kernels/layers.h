@@ -797,4 +797,14 @@ struct FcWgrad {
   }
 };
 
+// ops the K-wave launch (gemm.h gemm_kwave_kernel, CFG_KWAVE) is instantiated for
+template <class P>
+struct KWaveOK : std::false_type {};
+template <bool R>
+struct KWaveOK<FcFwd<R>> : std::true_type {};
+template <>
+struct KWaveOK<FcDgradAct> : std::true_type {};
+template <int HP, int C>
+struct KWaveOK<FcDgradPool<HP, C>> : std::true_type {};
+
 }  // namespace ddl

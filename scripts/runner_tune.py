@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from op_bench import OPS  # noqa: E402
 
 STREAMK_OK = {1, 2, 3, 10, 11, 12, 13, 14}  # conv GEMMs (big enough for stream-K)
+KWAVE_OK = {4, 5, 6, 8}  # fc forward / data-gradient GEMMs (csrc/kernels/layers.h KWaveOK)
 
 
 def main():
@@ -82,6 +83,10 @@ def main():
         for c2 in (0, 3, 4, 5):  # the one-wave configs (dual launches instantiate these)
             if c2 != c:
                 out.append(mk(c2, s, w, wd))
+        if op in KWAVE_OK:  # K split over the waves of one workgroup (4 / 8 / 16 waves)
+            for s2 in (4, 8, 16):
+                if (c, s) != (13, s2):
+                    out.append(mk(13, s2, 0, wd))
         return out
 
     base = timed(cur)

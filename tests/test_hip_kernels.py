@@ -230,6 +230,35 @@ def test_inlaunch_splitk_reduce_matches_reference(setup, cfg, wide):
         eng.set_wide(base_wide)
 
 
+@pytest.mark.parametrize("waves", [4, 8, 16])
+def test_kwave_config_matches_reference(setup, waves):
+    """The fc GEMMs on the K-wave launch (CFG_KWAVE = 13: K split over the waves of one
+    workgroup, LDS reduction, fused epilogue): fp64-reference activations-path gradients,
+    bit-deterministic across runs; other ops ignore the config value 13 (one-wave 32x32)."""
+    eng, flat, params, grads, x, y = setup
+    base_cfg, base_s, base_w = eng.get_cfg(), eng.get_splits(), eng.get_workers()
+    _, r64 = ref_grads(flat, x, y, 0.5, 55, torch.float64)
+    try:
+        eng.set_cfg([13] * len(base_cfg))
+        eng.set_splits([waves] * len(base_s))
+        eng.set_workers([0] * len(base_w))
+        outs = []
+        for _ in range(2):
+            grads.zero_()
+            eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 55)
+            torch.cuda.synchronize()
+            outs.append(grads.clone())
+        assert torch.equal(outs[0], outs[1])
+        for t in TENSORS:
+            o = CANON_OFFSETS[t.index]
+            tol = 5e-5 if t.index > 7 else 5e-3
+            assert rel_err(outs[0][o:o + t.numel], r64[t.index].reshape(-1)) < tol, t.name
+    finally:
+        eng.set_cfg(base_cfg)
+        eng.set_splits(base_s)
+        eng.set_workers(base_w)
+
+
 @pytest.mark.parametrize("conc,dual", [(False, True), (False, False), (True, False)])
 def test_backward_modes_match(setup, conc, dual):
     """Single-stream dual launches, single-stream back-to-back and the two-stream backward
