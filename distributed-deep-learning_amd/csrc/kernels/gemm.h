@@ -695,8 +695,18 @@ DDL_DEV void run_sub(const P& p, const SubGrid& g, int vb, float* lds, int* flag
   }
 }
 
+// Occupancy hint for the GEMM launches (A/B knob; 0 = the compiler's choice)
+#ifndef DDL_GEMM_WAVES
+#define DDL_GEMM_WAVES 0
+#endif
+#if DDL_GEMM_WAVES > 0
+#define DDL_GEMM_OCC __attribute__((amdgpu_waves_per_eu(DDL_GEMM_WAVES)))
+#else
+#define DDL_GEMM_OCC
+#endif
+
 template <int BM, int BN, int BK, int WM, int WN, class P>
-__global__ void __launch_bounds__(WM * WN * 64)
+__global__ void __launch_bounds__(WM * WN * 64) DDL_GEMM_OCC
 gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets,
                 int xcd) {
   using T = GemmTile<BM, BN, BK, WM, WN, P>;
@@ -809,7 +819,7 @@ struct TailAux {
 // numbering holds).  The tail path must stay under the GEMM paths' VGPR count: at 8 float4
 // per lane it raised the conv4 dual from 113 to 149 VGPRs (3 -> 2 waves/SIMD, +9 us).
 template <class CA, class PA, class CB, class PB, class AUX>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) DDL_GEMM_OCC
 gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut, int bfirst) {
   static_assert(CA::NT == 64 && CB::NT == 64, "dual launch needs one-wave blocks");
   using TA = GemmTile<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>;

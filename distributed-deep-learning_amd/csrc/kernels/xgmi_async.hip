@@ -71,17 +71,18 @@ DDL_DEV bool wait_ge(const uint32_t* f, uint32_t target, long long deadline, int
   }
   return true;
 }
-// The flag that publishes a workgroup's payload: a system-scope RELEASE store.  The payload was
-// stored write-through and drained (vmcnt(0)) by every wave before the barrier, which is the
-// whole release on one device; across GPUs the payload and the flag can travel different fabric
-// paths (and, in the async protocol, the flag goes to host memory while the payload goes to a
-// peer GPU), so the release fence (L2 writeback + wait) is what orders the payload before the
-// flag for every observer.  One wave executes it per workgroup and phase.  The release is one
-// asm statement (system-scope L2 write-back, then the wait for it): the compiler's own release
-// store omits the wait when the scoreboard is already drained (MI355X guide, compiler hazard),
-// and a separate asm wait gets scheduled above the fence's write-back.
+// The flag that publishes a workgroup's payload.  Every payload store is a system-scope
+// (sc0|sc1) write-through store, and every storing wave drains vmcnt(0) before the workgroup
+// barrier that precedes the flag store: a write-through store is counted complete only once the
+// memory side (local HBM, or the peer over xGMI, or host memory) has acknowledged it, so the
+// payload is globally visible before the flag is issued — no L2 write-back is needed (the CDNA
+// guide's G16 write-through hand-off, at system scope).  DDL_XGMI_RELEASE=1 adds the full
+// system release anyway (L2 write-back + wait, as one asm statement: hipcc drops the wait of its
+// own release when the scoreboard is already drained, and schedules a separate asm wait above
+// the write-back); it writes back every dirty line of the XCD's L2 at each flag — the GEMMs'
+// output included — and measured 3.2 -> 5.4 ms/step on the two-ranks-on-one-GPU rehearsal.
 #ifndef DDL_XGMI_RELEASE
-#define DDL_XGMI_RELEASE 1
+#define DDL_XGMI_RELEASE 0
 #endif
 DDL_DEV void flag_store(uint32_t* f, uint32_t v) {
   if (DDL_XGMI_RELEASE) asm volatile("buffer_wbl2 sc0 sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
