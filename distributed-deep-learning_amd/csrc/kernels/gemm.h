@@ -445,13 +445,21 @@ struct GemmTile {
       if (nk > 1) gload(kb + BK);
     }
     if constexpr (!SOLO) __syncthreads();
+#ifndef DDL_STORE_LATE
+#define DDL_STORE_LATE 1
+#endif
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = SOLO ? 0 : (kt & 1);
       fetch_all(As0 + cur * A_ELEMS, Bs0 + cur * B_ELEMS);
       // (SOLO) overwriting the buffer just read is safe: a wave's LDS ops run in order;
       // with two buffers the previous iteration's barrier freed buffer cur^1.
-      if (kt + 1 < nk) sstore(SOLO ? 0 : (cur ^ 1));
-      if (kt + 2 < nk) gload(kb + (kt + 2) * BK);
+      // One-wave blocks stage tile kt+1 AFTER tile kt's MFMAs (below): issued before them, the
+      // LDS writes' vmcnt waits for tile kt+1's global loads sat in front of the MFMA cluster
+      // (its lgkmcnt wait covers the writes), so every K tile paid the load latency again.
+      if (!(SOLO && DDL_STORE_LATE)) {
+        if (kt + 1 < nk) sstore(SOLO ? 0 : (cur ^ 1));
+        if (kt + 2 < nk) gload(kb + (kt + 2) * BK);
+      }
       __builtin_amdgcn_sched_barrier(0);
 #if DDL_MFMA_PRIO
       __builtin_amdgcn_s_setprio(1);
@@ -475,6 +483,11 @@ struct GemmTile {
       __builtin_amdgcn_s_setprio(0);
 #endif
       __builtin_amdgcn_sched_barrier(0);
+      if (SOLO && DDL_STORE_LATE) {
+        if (kt + 1 < nk) sstore(0);
+        if (kt + 2 < nk) gload(kb + (kt + 2) * BK);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       if constexpr (!SOLO) __syncthreads();
     }
     if constexpr (NCH == 2) acc[0][0] += acc2;
@@ -966,11 +979,20 @@ inline size_t gemm_slab_f4(int M, int N, int K, int splits, int workers) {
   return sk > sp ? sk : sp;
 }
 
-// XCD-contiguous split-K numbering: DDL_XCD_REMAP=0/1 (A/B knob, read once)
-inline int xcd_remap_default() {
+// XCD-contiguous split-K numbering (xcd_remap): per policy (`static constexpr bool XCD_CONTIG`,
+// default off), or forced for every launch by DDL_XCD_REMAP=0/1 (A/B knob, read once)
+template <class P, class = void>
+struct XcdOf {
+  static constexpr bool value = false;
+};
+template <class P>
+struct XcdOf<P, std::void_t<decltype(P::XCD_CONTIG)>> {
+  static constexpr bool value = P::XCD_CONTIG;
+};
+inline int xcd_remap_env() {
   static const int v = [] {
     const char* e = getenv("DDL_XCD_REMAP");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : -1;
   }();
   return v;
 }
@@ -997,7 +1019,7 @@ inline SubGrid plan_gemm(const P& p, int splits, int workers, int wide_thr,
   }
   g.gz = splitk_z<BK>(p.K, splits);
   g.kchunk = g.gz > 1 ? splitk_kchunk<BK>(p.K, splits) : p.K;
-  g.xcd = xcd_remap_default();
+  g.xcd = xcd_remap_env() >= 0 ? xcd_remap_env() : (XcdOf<P>::value ? 1 : 0);
   g.mode = g.gz == 1 ? 0 : (g.gz > wide_thr ? 2 : 1);
   if (g.mode == 1 && (long long)g.gx * g.gy > sc.max_tiles) g.mode = 2;  // ticket capacity
   g.nblocks = g.gx * g.gy * g.gz;

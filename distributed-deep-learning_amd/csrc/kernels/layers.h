@@ -520,6 +520,11 @@ struct ConvWgrad {
 // A[m=(tap,ci)][k] = x[b, y+ky-2, x+kx-2, ci] = halo x[b, y+ky, x+kx, ci],
 // B[n=co][k] = halo dpre[b, y+2, x+2, co]; both MN-contiguous (ci / co innermost).
 // ---------------------------------------------------------------------------------------------
+#ifndef DDL_XCD_WGRAD
+#define DDL_XCD_WGRAD 0
+#endif
+constexpr bool XCD_WGRAD = DDL_XCD_WGRAD != 0;
+
 template <int H, int CIN, int COUT>
 struct ConvWgradBM {
   static constexpr bool A_KCONTIG = false;
@@ -539,6 +544,9 @@ struct ConvWgradBM {
   struct KWin {
     int y0, ny, x0, nx, rx;
   };
+  // split-K blocks numbered XCD-contiguous (gemm.h xcd_remap): the m-fastest neighbours are
+  // the taps of one K split, which read the same images' maps — one L2 instead of eight
+  static constexpr bool XCD_CONTIG = XCD_WGRAD;
   int M, N, K;                     // K = k_of(B)
   const float* __restrict__ x;     // [B,H+4,H+4,CIN]
   const float* __restrict__ dpre;  // [B,H+4,H+4,COUT]
