@@ -26,8 +26,11 @@ Engine::Engine() {
   // weight gradient on the basic BK 32 loop instead of the pipelined BK 16 one, 342.8 ->
   // 336.5 us, profiles/r2_runner_tune_halo.log)
   // fc1 forward on the K-wave launch (8 waves per workgroup, LDS reduction, no reduce launch):
-  // 313.4 -> 310.6 us (profiles/r2_runner_tune_kwave.log)
-  static const int defc[OP_COUNT] = {3, 3, 3, 3, CFG_KWAVE, 3, 3, 5, 3, 5, 3, 3, 3, 3, 3, 3, 3};
+  // 313.4 -> 310.6 us (profiles/r2_runner_tune_kwave.log); fc1 data gradient as the K-wave
+  // half of one packed launch with its weight gradient (gemm_pack_kernel, 4 waves), instead
+  // of the one-wave dual launch + wide reduce: 308.7 -> 304.4 us (profiles/r2_runner_tune_pack.log)
+  static const int defc[OP_COUNT] = {3, 3, 3, 3, CFG_KWAVE, 3, 3, 5, CFG_KWAVE, 5,
+                                     3, 3, 3, 3, 3, 3, 3};
   // (re-tuned in the real step with scripts/sched_ab.py after the compact 52-row conv3
   // enumeration and the wgrad row decode: conv3 forward split 4 + in-launch reduce instead of
   // stream-K 3072 workers, 372.4 -> 369.5 us; conv4 weight gradient split 4 instead of 8,

@@ -173,8 +173,24 @@ inline void dual_b(Engine& e, const PA& pa, const PB& pb, int B, hipStream_t st)
 }
 
 // Ops OA and OB (independent) in one launch if both use one-wave tiles, else back to back.
+// OA on the K-wave config (fc data gradients) with OB on a one-wave 32x32 config: one packed
+// launch (gemm.h gemm_pack_kernel; OB's tiles run BK 32 there).
 template <int OA, int OB>
 void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
+  if (e.dual && e.cfg[OA] == CFG_KWAVE && (e.cfg[OB] == 3 || e.cfg[OB] == 5)) {
+    const auto pa = make_policy<OA>(e, B, x, seed, true);
+    const auto pb = make_policy<OB>(e, B, x, seed, true);
+    if constexpr (KWaveOK<std::decay_t<decltype(pa)>>::value) {
+      if constexpr (OA == OP_FC2_DGRAD) {
+        e.flush_tail(st);
+        launch_gemm_pack(pa, e.splits[OA], pb, head_aux(e, B), st);
+      } else {
+        launch_gemm_pack(pa, e.splits[OA], pb, TailAux(e.tail), st);
+        e.tail = UpdTail();
+      }
+      return;
+    }
+  }
   if (!e.dual || !one_wave_cfg(e.cfg[OA]) || !one_wave_cfg(e.cfg[OB])) {
     e.flush_tail(st);
     if constexpr (OA == OP_FC2_DGRAD) e.flush_head_wgrad(B, st);

@@ -495,7 +495,7 @@ struct GemmTile {
 
   // fused epilogue: each lane owns 4 groups of 4 consecutive rows of one column
   static DDL_DEV void epilogue(const P& p, int m_blk, int n_blk, const f32x16 (&acc)[TM][TN]) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = (threadIdx.x & (NT - 1)) >> 6;
     const int wm = wave / WN, wn = wave % WN;
     const int lr = lane & 31, lh = lane >> 5;
 #pragma unroll
@@ -519,7 +519,7 @@ struct GemmTile {
   // partial-fragment image of one block: [wave][frag][g][lane] float4 (coalesced per wave),
   // at float4 index `base` of the slab.  Written and read write-through (sc1): see arrive().
   static DDL_DEV void store_partial(brsrc_t slab, size_t base, const f32x16 (&acc)[TM][TN]) {
-    const int mine = (int)base + (threadIdx.x >> 6) * WPART + (threadIdx.x & 63);
+    const int mine = (int)base + ((threadIdx.x & (NT - 1)) >> 6) * WPART + (threadIdx.x & 63);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -532,7 +532,7 @@ struct GemmTile {
         }
   }
   static DDL_DEV void add_partial(brsrc_t slab, size_t base, f32x16 (&acc)[TM][TN]) {
-    const int src = (int)base + (threadIdx.x >> 6) * WPART + (threadIdx.x & 63);
+    const int src = (int)base + ((threadIdx.x & (NT - 1)) >> 6) * WPART + (threadIdx.x & 63);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -754,15 +754,15 @@ gemm_streamk_kernel(P p, int KI, int gx, long long I, float4* __restrict__ slab,
 // then the KW accumulators are summed through LDS in wave order (deterministic) and the fused
 // epilogue runs in the same launch — no partial slab in HBM and no reduce launch, where the
 // split-K form of the same tile needs a partial round trip plus a dependent kernel boundary.
+// One K-wave tile (bx, by) by the KW waves of this workgroup; wave w stages through the L
+// float4 at lds4 + w * L (L >= the tile's LDS_F4, >= 1024 floats for the reduction image).
 template <int BK, int KW, class P>
-__global__ void __launch_bounds__(KW * 64) gemm_kwave_kernel(P p) {
+DDL_DEV void kwave_body(const P& p, int bx, int by, float4* lds4, int L) {
   using T = GemmTile<32, 32, BK, 1, 1, P>;
   static_assert(KW == 4 || KW == 8 || KW == 16, "4, 8 or 16 waves");
-  static_assert(T::LDS_F4 * 16 >= 16 * 64 * 4, "a wave's reduction image fits its staging area");
-  __shared__ float4 lds4[KW * T::LDS_F4];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int m_blk = blockIdx.x * 32, n_blk = blockIdx.y * 32;
-  float* mine = reinterpret_cast<float*>(lds4 + wave * T::LDS_F4);
+  const int m_blk = bx * 32, n_blk = by * 32;
+  float* mine = reinterpret_cast<float*>(lds4 + wave * L);
   f32x16 acc[1][1];
   if constexpr (T::KM) {
     const typename T::Win w = p.kwin(m_blk, min(p.M, m_blk + 32));
@@ -789,6 +789,65 @@ __global__ void __launch_bounds__(KW * 64) gemm_kwave_kernel(P p) {
     const int n = n_blk + (lane & 31);
     const int m0 = m_blk + 8 * g + 4 * (lane >> 5);
     if (n < p.N && m0 < p.M) p.epi(m0, n, f32x4{v[0], v[1], v[2], v[3]});
+  }
+}
+
+template <int BK, int KW, class P>
+__global__ void __launch_bounds__(KW * 64) gemm_kwave_kernel(P p) {
+  using T = GemmTile<32, 32, BK, 1, 1, P>;
+  static_assert(T::LDS_F4 * 16 >= 16 * 64 * 4, "a wave's reduction image fits its staging area");
+  __shared__ float4 lds4[KW * T::LDS_F4];
+  kwave_body<BK, KW, P>(p, blockIdx.x, blockIdx.y, lds4, T::LDS_F4);
+}
+
+// Packed dual launch for the fc backward (KW-wave workgroups): blocks [0, nA) run problem A —
+// the data gradient, M = batch — as K-wave tiles (no partial slab, no reduce launch); blocks
+// [nA, nA + nB) run KW independent one-wave 32x32 tiles of problem B — the weight gradient,
+// K = batch, unsplit — one per wave; the rest run the auxiliary work (fc3 weight gradient /
+// optimizer tail), one index per wave.  Replaces the one-wave dual launch + A's wide reduce.
+template <int KW, class PA, class PB, class AUX>
+__global__ void __launch_bounds__(KW * 64)
+gemm_pack_kernel(PA pa, int nA, int gxA, PB pb, int nB, int gxB, int ntB, AUX ut) {
+  using TA = GemmTile<32, 32, 32, 1, 1, PA>;
+  using TB = GemmTile<32, 32, 32, 1, 1, PB>;
+  constexpr int L0 = TA::LDS_F4 > TB::LDS_F4 ? TA::LDS_F4 : TB::LDS_F4;
+  constexpr int L = L0 > 256 ? L0 : 256;
+  __shared__ float4 lds4[KW * L];
+  const int b = blockIdx.x, wave = threadIdx.x >> 6;
+  if (b < nA) {
+    kwave_body<32, KW, PA>(pa, b % gxA, b / gxA, lds4, L);
+  } else if (b < nA + nB) {
+    const int t = (b - nA) * KW + wave;
+    if (t >= ntB) return;
+    const int m_blk = (t % gxB) * 32, n_blk = (t / gxB) * 32;
+    f32x16 acc[1][1];
+    TB::mainloop(pb, m_blk, n_blk, 0, pb.K, reinterpret_cast<float*>(lds4 + wave * L), acc);
+    TB::epilogue(pb, m_blk, n_blk, acc);
+  } else {
+    const int i = (b - nA - nB) * KW + wave;
+    if (i < ut.nblk) ut.run(i);
+  }
+}
+
+template <int KW, class PA, class PB, class AUX>
+inline void launch_gemm_pack_w(const PA& pa, const PB& pb, const AUX& ut, hipStream_t stream) {
+  const int gxA = (pa.M + 31) / 32, nA = gxA * ((pa.N + 31) / 32);
+  const int gxB = (pb.M + 31) / 32, ntB = gxB * ((pb.N + 31) / 32);
+  const int nB = (ntB + KW - 1) / KW, nX = (ut.nblk + KW - 1) / KW;
+  if (nA + nB + nX > 0)
+    hipLaunchKernelGGL((gemm_pack_kernel<KW, PA, PB, AUX>), dim3(nA + nB + nX), dim3(KW * 64), 0,
+                       stream, pa, nA, gxA, pb, nB, gxB, ntB, ut);
+}
+
+inline int kwave_waves(int splits);
+
+template <class PA, class PB, class AUX>
+inline void launch_gemm_pack(const PA& pa, int splits_a, const PB& pb, const AUX& ut,
+                             hipStream_t stream) {
+  switch (kwave_waves(splits_a)) {
+    case 4: launch_gemm_pack_w<4>(pa, pb, ut, stream); break;
+    case 8: launch_gemm_pack_w<8>(pa, pb, ut, stream); break;
+    default: launch_gemm_pack_w<16>(pa, pb, ut, stream);
   }
 }
 
