@@ -132,17 +132,28 @@ def main(argv=None):
     candidates = [a.exchange]
     if a.exchange == "auto" and world > 1 and a.mode == "sync" and a.shard == "flat" and cuda:
         candidates = ["xgmi"] if shared_gpu else ["rccl", "xgmi"]
+    if os.environ.get("DDL_AB_CANDIDATES") and world > 1:  # test hook: force an A/B list
+        candidates = os.environ["DDL_AB_CANDIDATES"].split(",")
     ab = {}
     tr = None
     # every trainer built here stays referenced until the process ends: a garbage-collected
     # runner would destroy its RCCL communicator / IPC mappings at a different moment on each
     # rank
     keep = []
+    def digest(p):
+        """Bit-exact digest of a parameter replica: sum of the raw fp32 bit patterns (int64,
+        exact) and whether every value is finite."""
+        bits = int(p.view(torch.int32).to(torch.int64).sum().item())
+        return bits, bool(torch.isfinite(p).all().item())
+
     if len(candidates) > 1:
         # short A/B before the benchmark proper (a wait that times out in the xGMI path raises
         # at the next step on that rank; every rank votes, so a failed candidate is dropped
-        # by all ranks together)
-        best = None
+        # by all ranks together).  Each candidate is also checked for correctness: in a sync
+        # PS step every worker pulls the same parameters, so the replicas must be bitwise equal
+        # on all ranks, finite, and (same init, data and step count) close to the first
+        # candidate's — a data plane that loses or tears an update fails here, not silently.
+        best, ref_params = None, None
         for c in candidates:
             try:
                 t = make_trainer(c)
@@ -153,6 +164,7 @@ def main(argv=None):
             ok, ms = t is not None, None
             if ok:
                 try:
+                    p0 = t.params.clone()
                     for i in range(5):
                         t.train_step(i)
                     sync()
@@ -173,11 +185,31 @@ def main(argv=None):
                 continue
             ms = max_over_ranks(ms)
             ab[c] = {"ms_per_step": round(ms, 4), "exchange": backend_of(t)}
+            dg = [None] * world
+            dist.all_gather_object(dg, digest(t.params))
+            good = all(d[1] for d in dg) and len({d[0] for d in dg}) == 1
+            rel = None
+            if ref_params is None:
+                ref_params = (t.params.clone(), p0)
+            else:
+                moved = (ref_params[0] - ref_params[1]).abs().mean()
+                rel = float(((t.params - ref_params[0]).abs().mean() / moved.clamp_min(1e-30)).item())
+                rel = max_over_ranks(rel)
+                good = good and rel < 0.1
+                ab[c]["mean_diff_vs_" + candidates[0]] = round(rel, 5)
+            ab[c]["replicas_consistent"] = good
+            if not good:
+                continue
             if best is None or ms < best[0]:
                 best = (ms, c, t)
-        if best is None:
-            raise RuntimeError(f"no exchange candidate worked: {ab}")
-        chosen = best[1]
+        if best is not None:
+            chosen = best[1]
+        else:
+            ran = [c for c in candidates if "ms_per_step" in ab.get(c, {})]
+            if not ran:
+                raise RuntimeError(f"no exchange candidate worked: {ab}")
+            chosen = ran[0]
+            ab["note"] = "no candidate passed the replica check; benchmarking the first that ran"
         # a fresh trainer for the benchmark proper: identical initial state for every choice
         tr = make_trainer(chosen)
     else:

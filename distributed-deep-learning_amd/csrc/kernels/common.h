@@ -69,6 +69,10 @@ DDL_DEV float bload1(brsrc_t r, int byte_off) {
   auto v = __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0);
   return __builtin_bit_cast(float, v);
 }
+DDL_DEV float bload1_so(brsrc_t r, int voff_bytes, int soff_bytes) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b32(r, voff_bytes, soff_bytes, 0);
+  return __builtin_bit_cast(float, v);
+}
 
 // Write-through (sc1) 16-B store / load pair for data handed to another workgroup inside
 // one launch (MI355X guide §6 Guideline 16, R1): the stores need no agent-scope release (an

@@ -124,6 +124,25 @@ struct KMapOf<P, std::void_t<decltype(P::KMAP)>> {
   using Win = typename P::KWin;
 };
 
+// A policy whose B operand is MN-contiguous may offer a one-element gather loadB1(info, k0)
+// (element (k0 + kk, n) of prepB(n, kk)); with it the direct-fragment main loop applies.
+template <class P, class = void>
+struct HasLoadB1 : std::false_type {};
+template <class P>
+struct HasLoadB1<P, std::void_t<decltype(std::declval<const P&>().loadB1(
+                        std::declval<const typename P::BInfo&>(), 0))>> : std::true_type {};
+
+// Direct-fragment main loop for one-wave 32x32 tiles (A/B knob, measured and rejected: default
+// off): every lane loads its own MFMA fragments straight from global memory into VGPRs.  A
+// one-wave block gets no operand reuse out of LDS (the MFMA broadcasts inside the wave); LDS
+// only re-lays the tile out, at the price of a store -> read round trip per K tile.  But the
+// fragment layout fixes lane -> row, so each 16-byte gather instruction touches 32 rows (32
+// cache lines, 32 bytes each) where the coalesced LDS-staging gather touches 8 full lines:
+// 0.3045 -> 0.336 ms/step, every conv GEMM slower (docs/DESIGN.md).
+#ifndef DDL_DIRECT
+#define DDL_DIRECT 0
+#endif
+
 // ---- per-tile building blocks shared by the split-K and stream-K drivers ---------------------
 template <int BM, int BN, int BK, int WM, int WN, class P>
 struct GemmTile {
@@ -148,7 +167,11 @@ struct GemmTile {
   // the LDS footprint doubles the resident waves per CU (LDS was the occupancy limit).
   static constexpr bool SOLO = (NT == 64);
   static constexpr int NBUF = SOLO ? 1 : 2;
-  static constexpr int LDS_F4 = (NBUF * (A_ELEMS + B_ELEMS)) / 4;
+  // One-wave single-fragment tiles with a K-contiguous A and a K-contiguous (or one-element
+  // gatherable) B take the direct-fragment loop and need no staging LDS at all.
+  static constexpr bool DIRECT = DDL_DIRECT && SOLO && TM * TN == 1 && BK % 8 == 0 && AK &&
+                                 (BKC || HasLoadB1<P>::value) && !(BK == 16);
+  static constexpr int LDS_F4 = DIRECT ? 0 : (NBUF * (A_ELEMS + B_ELEMS)) / 4;
   // A wave with a single 32x32 fragment alternates two accumulator chains (summed at the
   // end) so consecutive MFMAs are independent.
   static constexpr int NCH = (TM * TN == 1) ? 2 : 1;
@@ -172,8 +195,85 @@ struct GemmTile {
   // [kb, ke) is virtual (window w) for K-map policies
   static DDL_DEV void mainloop(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
                                f32x16 (&acc)[TM][TN], const Win& w = Win()) {
-    if constexpr (PIPE) mainloop_pipe(p, m_blk, n_blk, kb, ke, lds, acc, w);
+    if constexpr (DIRECT) mainloop_direct(p, m_blk, n_blk, kb, ke, acc, w);
+    else if constexpr (PIPE) mainloop_pipe(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else mainloop_basic(p, m_blk, n_blk, kb, ke, lds, acc, w);
+  }
+
+  static DDL_DEV float ldB1(const P& p, const typename P::BInfo& b, int k, const Win& w) {
+    if constexpr (KM) return p.loadB1(b, k, w);
+    else return p.loadB1(b, k);
+  }
+
+  // Direct-fragment loop (one wave, one 32x32 fragment, no LDS).  MFMA s of 8-deep sub-step r
+  // takes k = 8r + 4h + s in lane half h (the LDS path's fragment order), so a K-contiguous
+  // operand's fragments of one sub-step are ONE 16-byte gather per lane (row = lane & 31, k
+  // offset 8r + 4h: the loaders' prep(mn, kk) / load(info, k0 + 8r) protocol, the sub-step
+  // base staying wave-uniform) and an MN-contiguous B's are four one-element gathers whose 32
+  // lanes of a half read 128 contiguous bytes.  Two register sets: tile t+2's loads are issued
+  // right after tile t's MFMAs, so they have tile t+1's MFMA cluster to land.
+  static DDL_DEV void mainloop_direct(const P& p, int m_blk, int n_blk, int kb, int ke,
+                                      f32x16 (&acc)[TM][TN], const Win& w) {
+    const int lane = threadIdx.x & 63;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int nk = (ke - kb + BK - 1) / BK;
+    const typename P::AInfo ai = p.prepA(m_blk + lr, 4 * lh);
+    constexpr int NBI = BKC ? 1 : 4;
+    typename P::BInfo bi[NBI];
+#pragma unroll
+    for (int s = 0; s < NBI; ++s) bi[s] = p.prepB(n_blk + lr, 4 * lh + s);
+    float a0[R][4], b0[R][4], a1[R][4], b1[R][4];
+    auto gl = [&](int k0, float (&a)[R][4], float (&b)[R][4]) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const float4 t = ldA(p, ai, k0 + 8 * r, w);
+        a[r][0] = t.x; a[r][1] = t.y; a[r][2] = t.z; a[r][3] = t.w;
+        if constexpr (BKC) {
+          const float4 u = ldB(p, bi[0], k0 + 8 * r, w);
+          b[r][0] = u.x; b[r][1] = u.y; b[r][2] = u.z; b[r][3] = u.w;
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) b[r][s] = ldB1(p, bi[s], k0 + 8 * r, w);
+        }
+      }
+    };
+    f32x16 c0, c1;  // two independent accumulator chains
+#pragma unroll
+    for (int q = 0; q < 16; ++q) { c0[q] = 0.f; c1[q] = 0.f; }
+    auto mf = [&](const float (&a)[R][4], const float (&b)[R][4]) {
+#if DDL_MFMA_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          if (s & 1) c1 = mfma32x32x2(a[r][s], b[r][s], c1);
+          else c0 = mfma32x32x2(a[r][s], b[r][s], c0);
+        }
+#if DDL_MFMA_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    if (nk > 0) gl(kb, a0, b0);
+    if (nk > 1) gl(kb + BK, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    int kt = 0;
+    for (; kt + 3 < nk; kt += 2) {  // tiles kt (set 0) and kt+1 (set 1); kt+2, kt+3 exist
+      mf(a0, b0);
+      gl(kb + (kt + 2) * BK, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      mf(a1, b1);
+      gl(kb + (kt + 3) * BK, a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int left = nk - kt;  // 0..3 tiles, already loaded or loaded below
+    if (left >= 1) mf(a0, b0);
+    if (left == 3) gl(kb + (kt + 2) * BK, a0, b0);
+    if (left >= 2) mf(a1, b1);
+    if (left == 3) mf(a0, b0);
+    acc[0][0] = c0 + c1;
   }
 
   // Software-pipelined main loop (one wave, one 32x32 fragment, single LDS buffer).
@@ -795,9 +895,11 @@ DDL_DEV void kwave_body(const P& p, int bx, int by, float4* lds4, int L) {
 template <int BK, int KW, class P>
 __global__ void __launch_bounds__(KW * 64) gemm_kwave_kernel(P p) {
   using T = GemmTile<32, 32, BK, 1, 1, P>;
-  static_assert(T::LDS_F4 * 16 >= 16 * 64 * 4, "a wave's reduction image fits its staging area");
-  __shared__ float4 lds4[KW * T::LDS_F4];
-  kwave_body<BK, KW, P>(p, blockIdx.x, blockIdx.y, lds4, T::LDS_F4);
+  // per wave: its staging image (none on the direct-fragment loop) and its 16x64-float
+  // reduction image
+  constexpr int LW = T::LDS_F4 > 256 ? T::LDS_F4 : 256;
+  __shared__ float4 lds4[KW * LW];
+  kwave_body<BK, KW, P>(p, blockIdx.x, blockIdx.y, lds4, LW);
 }
 
 // Packed dual launch for the fc backward (KW-wave workgroups): blocks [0, nA) run problem A —

@@ -206,6 +206,19 @@ struct ConvFwd {
       return bload4(r, good ? (b.off + k0 * COUT) * 4 : kOOB);
     }
   }
+  // one weight (k0 + kk, n): the direct-fragment loop's B gather (gemm.h)
+  DDL_DEV float loadB1(const BInfo& b, int k0) const {
+    const brsrc_t r = make_rsrc(w, 25u * CIN * COUT * 4u);
+    if constexpr (PADIN) {
+      return bload1_so(r, b.ok ? b.off * 4 : kOOB, k0 * COUT * 4);
+    } else {
+      const bool good = b.ok && k0 + b.kk < K;
+      return bload1(r, good ? (b.off + k0 * COUT) * 4 : kOOB);
+    }
+  }
+  DDL_DEV float loadB1(const BInfo& b, int kv, const KWin& win) const {
+    return loadB1(b, kreal(win, kv));
+  }
   // pooled output (halo layout when a conv reads it) and its pool code (no halo)
   DDL_DEV void store_pooled(int b, int py, int px, int n, float best, int arg) const {
     out[map_off<HP, COUT, PADOUT>(b, py, px, n)] = best > 0.f ? best : 0.f;
@@ -683,6 +696,8 @@ struct FcFwd {
     const brsrc_t r = make_rsrc(w, (uint32_t)K * N * 4u);
     return bload4(r, b.ok && k0 + b.kk < K ? (b.off + k0 * N) * 4 : kOOB);
   }
+  // (no loadB1: on the direct-fragment loop the fc forward's guarded gathers cost 24-36 more
+  // VGPRs than the LDS path — a wave per SIMD — and spilled in the 16-wave K-wave launch)
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
     const float bb = bias[n];
     uint32_t key = 0;

@@ -16,7 +16,9 @@ import os
 import sys
 
 _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO_PATH = os.path.join(_PKG_DIR, "_C.so")
+# DDL_SO: an alternative in-tree build of the same extension (same-box A/B of compile-time
+# knobs, e.g. `_C_ab.so` built with DDL_EXTRA_CFLAGS); default the one build.py writes
+SO_PATH = os.path.join(_PKG_DIR, os.environ.get("DDL_SO", "_C.so"))
 
 _mod = None
 _err: str | None = None

@@ -60,3 +60,23 @@ def test_bench_torchrun_two_ranks_json(port):
     assert rec["config"]["parallelism"] == "dp2-ps2-sync-flat"
     # whole-job aggregate: images/s = W * batch * steps / max-over-ranks time
     assert rec["value"] == pytest.approx(2 * 100 / (rec["ms_per_step"] / 1e3), rel=1e-3)
+
+
+@pytest.mark.slow
+def test_bench_torchrun_exchange_ab_checks_replicas(port):
+    """The W > 1 data-plane A/B (RCCL vs xGMI on a GPU node) on CPU ranks: two candidates of
+    the same exchange must both pass the replica check (bitwise-equal parameters on every
+    rank, finite, and identical to the first candidate's after the same steps)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--tta", "0", "--ab-steps", "2"]
+    env = _env()
+    env["DDL_AB_CANDIDATES"] = "rccl,rccl"
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    ab = recs[0]["exchange_ab"]
+    assert ab["rccl"]["replicas_consistent"] is True
+    assert ab["rccl"]["mean_diff_vs_rccl"] == 0.0
+    assert "note" not in ab
