@@ -174,7 +174,12 @@ struct GemmTile {
   static constexpr int LDS_F4 = DIRECT ? 0 : (NBUF * (A_ELEMS + B_ELEMS)) / 4;
   // A wave with a single 32x32 fragment alternates two accumulator chains (summed at the
   // end) so consecutive MFMAs are independent.
-  static constexpr int NCH = (TM * TN == 1) ? 2 : 1;
+  // (DDL_TWO_CHAINS=0: one chain; gfx950 forwards a 32x32 MFMA's result to the next one's
+  // SrcC back to back, so the second chain is only registers — A/B knob)
+#ifndef DDL_TWO_CHAINS
+#define DDL_TWO_CHAINS 1
+#endif
+  static constexpr int NCH = (TM * TN == 1 && DDL_TWO_CHAINS) ? 2 : 1;
   static constexpr int WPART = TM * TN * 4 * 64;  // float4 of one wave's partial fragments
   static constexpr bool KM = KMapOf<P>::value;
   using Win = typename KMapOf<P>::Win;
@@ -248,7 +253,7 @@ struct GemmTile {
       for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          if (s & 1) c1 = mfma32x32x2(a[r][s], b[r][s], c1);
+          if ((s & 1) && NCH == 2) c1 = mfma32x32x2(a[r][s], b[r][s], c1);
           else c0 = mfma32x32x2(a[r][s], b[r][s], c0);
         }
 #if DDL_MFMA_PRIO
@@ -273,7 +278,8 @@ struct GemmTile {
     if (left == 3) gl(kb + (kt + 2) * BK, a0, b0);
     if (left >= 2) mf(a1, b1);
     if (left == 3) mf(a0, b0);
-    acc[0][0] = c0 + c1;
+    if constexpr (NCH == 2) acc[0][0] = c0 + c1;
+    else acc[0][0] = c0;
   }
 
   // Software-pipelined main loop (one wave, one 32x32 fragment, single LDS buffer).
@@ -362,7 +368,7 @@ struct GemmTile {
       for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          if (s & 1) c1 = mfma32x32x2(fa[r][s], fb[r][s], c1);
+          if ((s & 1) && NCH == 2) c1 = mfma32x32x2(fa[r][s], fb[r][s], c1);
           else c0 = mfma32x32x2(fa[r][s], fb[r][s], c0);
         }
     };
@@ -431,7 +437,8 @@ struct GemmTile {
         mfmas(f1a, f1b);
       }
     }
-    acc[0][0] = c0 + c1;
+    if constexpr (NCH == 2) acc[0][0] = c0 + c1;
+    else acc[0][0] = c0;
   }
 
   static DDL_DEV void mainloop_basic(const P& p, int m_blk, int n_blk, int kb, int ke,
