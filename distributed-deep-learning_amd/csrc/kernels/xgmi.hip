@@ -272,7 +272,7 @@ PeerExchange::PeerExchange(float* params, const float* grads, int64_t total, int
   memset(err_, 0, 64);
   X_CHECK(hipDeviceSynchronize());
   const char* t = getenv("DDL_XGMI_TIMEOUT_S");
-  timeout_s_ = t ? atof(t) : 60.0;
+  timeout_s_ = t ? atof(t) : 20.0;  // a healthy wait takes microseconds
 }
 
 PeerExchange::~PeerExchange() {
