@@ -171,7 +171,20 @@ struct GemmTile {
   // gatherable) B take the direct-fragment loop and need no staging LDS at all.
   static constexpr bool DIRECT = DDL_DIRECT && SOLO && TM * TN == 1 && BK % 8 == 0 && AK &&
                                  (BKC || HasLoadB1<P>::value) && !(BK == 16);
-  static constexpr int LDS_F4 = DIRECT ? 0 : (NBUF * (A_ELEMS + B_ELEMS)) / 4;
+  // Hybrid (A/B knob DDL_BDIRECT): A staged through LDS as usual, an MN-contiguous B (the conv
+  // forward's HWIO weights) gathered straight into fragment registers — per MFMA one 4-byte
+  // load whose 32 lanes per half read 128 contiguous bytes (two whole lines per instruction, so
+  // none of the direct loop's texture cost) — one tile ahead in a second register set.  Saves
+  // the B image's LDS stores / 16 ds_read_b32 per K tile and halves the block's LDS.  Measured
+  // and rejected (default off): 0.3050 -> 0.3100 ms/step, each conv forward ~1 us slower — 16
+  // dword loads per K tile cost more issue / latency than the LDS round trip they replace.
+#ifndef DDL_BDIRECT
+#define DDL_BDIRECT 0
+#endif
+  static constexpr bool BDIR = DDL_BDIRECT && !DIRECT && SOLO && TM * TN == 1 && BK % 8 == 0 &&
+                               !(BK == 16) && !BKC && HasLoadB1<P>::value;
+  static constexpr int LDS_F4 =
+      DIRECT ? 0 : (NBUF * (A_ELEMS + (BDIR ? 0 : B_ELEMS))) / 4;
   // A wave with a single 32x32 fragment alternates two accumulator chains (summed at the
   // end) so consecutive MFMAs are independent.
   // (DDL_TWO_CHAINS=0: one chain; gfx950 forwards a 32x32 MFMA's result to the next one's
@@ -472,6 +485,10 @@ struct GemmTile {
     }
 #pragma unroll
     for (int it = 0; it < FB; ++it) {
+      if constexpr (BDIR) {  // (it < 4) the lane's fragment column, k offset 4h + it
+        bi[it] = p.prepB(n_blk + (lane & 31), 4 * (lane >> 5) + it);
+        continue;
+      }
       const int idx = tid + it * NT;
       if constexpr (BKC) {
         const int kq = idx % (BK / 4), row = idx / (BK / 4);
@@ -483,6 +500,8 @@ struct GemmTile {
         b_off[it] = kk * SB + nq * 4;
       }
     }
+    static_assert(!BDIR || FB == 4, "hybrid B: one info per k offset 4h + s");
+    float bn[BDIR ? R : 1][4];  // BDIR: next tile's B fragments (in flight)
 
     // Two register-prefetch stages of the global operands: K tile t+1 is stored to LDS
     // while tile t's fragments are already in VGPRs, and tile t+2 loads during t's MFMAs.
@@ -490,16 +509,25 @@ struct GemmTile {
     auto gload = [&](int k0) {
 #pragma unroll
       for (int it = 0; it < FA; ++it) ra[it] = ldA(p, ai[it], k0, w);
+      if constexpr (BDIR) {
 #pragma unroll
-      for (int it = 0; it < FB; ++it) rb[it] = ldB(p, bi[it], k0, w);
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) bn[r][s] = ldB1(p, bi[s], k0 + 8 * r, w);
+      } else {
+#pragma unroll
+        for (int it = 0; it < FB; ++it) rb[it] = ldB(p, bi[it], k0, w);
+      }
     };
     auto sstore = [&](int buf) {
       float* As = As0 + buf * A_ELEMS;
       float* Bs = Bs0 + buf * B_ELEMS;
 #pragma unroll
       for (int it = 0; it < FA; ++it) *reinterpret_cast<float4*>(As + a_off[it]) = ra[it];
+      if constexpr (!BDIR) {
 #pragma unroll
-      for (int it = 0; it < FB; ++it) *reinterpret_cast<float4*>(Bs + b_off[it]) = rb[it];
+        for (int it = 0; it < FB; ++it) *reinterpret_cast<float4*>(Bs + b_off[it]) = rb[it];
+      }
     };
 
     f32x16 acc2;
@@ -534,6 +562,7 @@ struct GemmTile {
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
+          if constexpr (BDIR) break;  // B fragments arrive by register copy (bcopy)
           const int col = wn * WTN + j * 32 + lr;
           if constexpr (BKC) {
             const float4 t = *reinterpret_cast<const float4*>(Bs + col * SB + r * 8 + 4 * lh);
@@ -546,9 +575,20 @@ struct GemmTile {
       }
     };
 
+    // BDIR: tile t+1's B fragments move from the in-flight set to the MFMA set where tile t+1's
+    // A image is stored to LDS (the same point that waits for tile t+1's loads)
+    auto bcopy = [&]() {
+      if constexpr (BDIR) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) bv[r][0][s] = bn[r][s];
+      }
+    };
     if (nk > 0) {
       gload(kb);
       sstore(0);
+      bcopy();
       if (nk > 1) gload(kb + BK);
     }
     if constexpr (!SOLO) __syncthreads();
@@ -563,6 +603,7 @@ struct GemmTile {
       // One-wave blocks stage tile kt+1 AFTER tile kt's MFMAs (below): issued before them, the
       // LDS writes' vmcnt waits for tile kt+1's global loads sat in front of the MFMA cluster
       // (its lgkmcnt wait covers the writes), so every K tile paid the load latency again.
+      static_assert(!BDIR || DDL_STORE_LATE, "hybrid B needs the late staging order");
       if (!(SOLO && DDL_STORE_LATE)) {
         if (kt + 1 < nk) sstore(SOLO ? 0 : (cur ^ 1));
         if (kt + 2 < nk) gload(kb + (kt + 2) * BK);
@@ -591,7 +632,7 @@ struct GemmTile {
 #endif
       __builtin_amdgcn_sched_barrier(0);
       if (SOLO && DDL_STORE_LATE) {
-        if (kt + 1 < nk) sstore(0);
+        if (kt + 1 < nk) { sstore(0); bcopy(); }
         if (kt + 2 < nk) gload(kb + (kt + 2) * BK);
         __builtin_amdgcn_sched_barrier(0);
       }
