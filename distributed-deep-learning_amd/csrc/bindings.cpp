@@ -103,6 +103,10 @@ class PyEngine {
     e_.concurrent = on;
   }
   void set_dual(bool on) { e_.dual = on; }
+  // per-op bit mask: window-aware split-K (gemm.h KFixOf); no re-allocation needed (the
+  // split-K z never exceeds the balanced split's)
+  void set_kfix(int64_t mask) { e_.kfix = (int)mask; }
+  int64_t get_kfix() const { return e_.kfix; }
   void set_wide_thr(int64_t t) {
     e_.wide_thr = (int)std::max<int64_t>(1, t);
     for (int i = 0; i < ddl::OP_COUNT; ++i) e_.wide[i] = e_.wide_thr;
@@ -554,6 +558,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("get_eval_cfg", &PyEngine::get_eval_cfg)
       .def("set_concurrent", &PyEngine::set_concurrent)
       .def("set_dual", &PyEngine::set_dual)
+      .def("set_kfix", &PyEngine::set_kfix)
+      .def("get_kfix", &PyEngine::get_kfix)
       .def("set_wide_thr", &PyEngine::set_wide_thr)
       .def("set_wide", &PyEngine::set_wide)
       .def("get_wide", &PyEngine::get_wide)

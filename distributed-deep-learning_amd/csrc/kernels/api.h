@@ -97,6 +97,11 @@ struct Engine {
   // (their data gradients are the longer poles; conv4's stream-K loses its XCD-major numbering).
   // DDL_DUAL_BFIRST overrides (scripts/ab_env.sh).
   int dual_bfirst = 1 << OP_CONV2_DGRAD;
+  // bit op: that op's split-K uses one chunk length for every tile, sized so the tile with the
+  // longest tap window gets splits[op] pieces (gemm.h KFixOf; only the K-map conv forwards /
+  // data gradients honour it).  DDL_KFIX overrides.
+  int kfix = 0;
+  int sarg(int op) const { return ((kfix >> op) & 1) ? -splits[op] : splits[op]; }
 
   // workspace carve-out
   float *p1 = nullptr, *p2 = nullptr, *p3 = nullptr, *p4 = nullptr, *h1 = nullptr, *h2 = nullptr;

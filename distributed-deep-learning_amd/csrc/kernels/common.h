@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #define DDL_DEV __device__ __forceinline__
+#define DDL_HD __host__ __device__ __forceinline__
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 

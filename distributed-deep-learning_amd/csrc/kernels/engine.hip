@@ -44,6 +44,7 @@ Engine::Engine() {
   // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
   static const bool inl[OP_COUNT] = {0, 1, 1, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0};
   if (const char* s = getenv("DDL_DUAL_BFIRST")) dual_bfirst = (int)strtol(s, nullptr, 0);
+  if (const char* s = getenv("DDL_KFIX")) kfix = (int)strtol(s, nullptr, 0);
   memcpy(cfg, defc, sizeof(defc));
   memcpy(eval_cfg, defc, sizeof(defc));
   // eval forward at 10k-row chunks (scripts/eval_sweep.py, after the compact conv3 rows):

@@ -34,7 +34,7 @@ inline void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const Spli
                        hipStream_t st) {
   if (c == CFG_KWAVE) {
     if constexpr (KWaveOK<P>::value) {
-      launch_gemm_kwave<32>(p, s, st);
+      launch_gemm_kwave<32>(p, s < 0 ? -s : s, st);
       return;
     }
     c = 3;  // not instantiated for this op: the one-wave 32x32 tile
@@ -120,7 +120,7 @@ void run_op_inst(Engine& e, const float* x, int B, const uint32_t* seed, bool tr
       return;
     }
   }
-  launch_cfg(train ? e.cfg[OP] : e.eval_cfg[OP], p, train ? e.splits[OP] : 1,
+  launch_cfg(train ? e.cfg[OP] : e.eval_cfg[OP], p, train ? e.sarg(OP) : 1,
              train ? e.workers[OP] : 0, e.wide[OP],
              e.scratch[si], st);
 }
@@ -147,8 +147,8 @@ inline HeadWgradAux head_aux(Engine& e, int B) {
 template <class CA, int OA, int OB, class PA, class PB>
 inline void dual_b(Engine& e, const PA& pa, const PB& pb, int B, hipStream_t st) {
 #define DDL_DUAL_B(CB, AUXV) \
-  launch_gemm_dual<CA, PA, TileCfg<CB>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], \
-                                            e.wide[OA], pb, e.splits[OB], e.workers[OB], \
+  launch_gemm_dual<CA, PA, TileCfg<CB>, PB>(pa, e.sarg(OA), e.workers[OA], e.scratch[0], \
+                                            e.wide[OA], pb, e.sarg(OB), e.workers[OB], \
                                             e.scratch[1], e.wide[OB], st, AUXV, nullptr, \
                                             (e.dual_bfirst >> OA) & 1)
   // the fc2 dual carries fc3's weight gradient; the others a pending optimizer tail
@@ -225,11 +225,11 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
   using CA = TileCfg<TILE_3>;
   using CN = TileCfg<TILE_3>;
   SubGrid gb;
-  launch_gemm_dual<CA, PA, CB, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb,
-                                   e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st,
+  launch_gemm_dual<CA, PA, CB, PB>(pa, e.sarg(OA), e.workers[OA], e.scratch[0], e.wide[OA], pb,
+                                   e.sarg(OB), e.workers[OB], e.scratch[1], e.wide[OB], st,
                                    TailAux(e.tail), &gb, (e.dual_bfirst >> OA) & 1);
   e.tail = UpdTail();
-  if (!launch_reduce_with_gemm<CB, PB, CN, PN>(pb, gb, pn, e.splits[ON], e.workers[ON],
+  if (!launch_reduce_with_gemm<CB, PB, CN, PN>(pb, gb, pn, e.sarg(ON), e.workers[ON],
                                                e.wide[ON], e.scratch[0], st)) {
     launch_reduce<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, st);
     run_op_inst<ON>(e, x, B, seed, true, st, 0);

@@ -124,6 +124,21 @@ struct KMapOf<P, std::void_t<decltype(P::KMAP)>> {
   using Win = typename P::KWin;
 };
 
+// Window-aware split-K (KFIX policies: kwin / kvlen callable on the host).  With the balanced
+// K-map split every tile is cut into gz pieces of ITS OWN window length, so the waves of the
+// tiles with the most taps (the map's centre) are the launch's longest pole — up to 2.8x the
+// corner tiles' on the 7x7 map.  A negative split request -s asks instead for one chunk length
+// for all tiles, sized so the LONGEST window is cut into s pieces: heavy tiles get s waves,
+// light ones fewer (their surplus z-slices exit at once with zero partials).
+template <class P, class = void>
+struct KFixOf {
+  static constexpr bool value = false;
+};
+template <class P>
+struct KFixOf<P, std::void_t<decltype(P::KFIX)>> {
+  static constexpr bool value = P::KFIX;
+};
+
 // A policy whose B operand is MN-contiguous may offer a one-element gather loadB1(info, k0)
 // (element (k0 + kk, n) of prepB(n, kk)); with it the direct-fragment main loop applies.
 template <class P, class = void>
@@ -749,7 +764,10 @@ DDL_DEV void splitk_body(const P& p, int kchunk, int mode, float4* __restrict__ 
     // this tile's useful K sub-space, divided over the gz splits (whole BK tiles)
     const typename T::Win w = p.kwin(m_blk, min(p.M, m_blk + BM));
     const int kv = p.kvlen(w);
-    const int kc = gz > 1 ? ((kv + gz - 1) / gz + BK - 1) / BK * BK : kv;
+    // kchunk < 0: one chunk length for every tile (window-aware split, see KFixOf); a z-slice
+    // past this tile's window runs no K tile and contributes a zero partial
+    const int kc = kchunk < 0 ? -kchunk
+                              : (gz > 1 ? ((kv + gz - 1) / gz + BK - 1) / BK * BK : kv);
     const int kb = bz * kc;
     T::mainloop(p, m_blk, n_blk, kb, min(kv, kb + kc), lds, acc, w);
   } else {
@@ -1215,6 +1233,8 @@ inline SubGrid plan_gemm(const P& p, int splits, int workers, int wide_thr,
   SubGrid g;
   g.slab = reinterpret_cast<float4*>(sc.slab);
   g.tickets = sc.tickets;
+  const bool kfix = splits < 0;  // window-aware split request (KFixOf policies only)
+  if (kfix) splits = -splits;
   if (p.M <= 0 || p.N <= 0) return g;
   g.gx = (p.M + BM - 1) / BM;
   g.gy = (p.N + BN - 1) / BN;
@@ -1228,6 +1248,22 @@ inline SubGrid plan_gemm(const P& p, int splits, int workers, int wide_thr,
   }
   g.gz = splitk_z<BK>(p.K, splits);
   g.kchunk = g.gz > 1 ? splitk_kchunk<BK>(p.K, splits) : p.K;
+  if constexpr (KFixOf<P>::value) {
+    if (kfix && g.gz > 1) {
+      int kvmax = BK;
+      for (int t = 0; t < g.gx; ++t) {
+        const int lo = t * BM, hi = lo + BM < p.M ? lo + BM : p.M;
+        const int kv = p.kvlen(p.kwin(lo, hi));
+        kvmax = kv > kvmax ? kv : kvmax;
+      }
+      // z never exceeds the balanced split's (the slab is sized for that)
+      int z = splits < g.gz ? splits : g.gz;
+      int kc = ((kvmax + z - 1) / z + BK - 1) / BK * BK;
+      z = (kvmax + kc - 1) / kc;
+      g.gz = z;
+      g.kchunk = -kc;
+    }
+  }
   g.xcd = xcd_remap_env() >= 0 ? xcd_remap_env() : (XcdOf<P>::value ? 1 : 0);
   g.mode = g.gz == 1 ? 0 : (g.gz > wide_thr ? 2 : 1);
   if (g.mode == 1 && (long long)g.gx * g.gy > sc.max_tiles) g.mode = 2;  // ticket capacity

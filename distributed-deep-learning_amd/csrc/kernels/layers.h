@@ -38,7 +38,7 @@ DDL_DEV int map_off(int b, int y, int x, int c) {
 struct TapWin {
   int ty0, nty, tx0, ntx, rx;
 };
-DDL_DEV TapWin tap_win(int ty0, int ty1, int tx0, int tx1) {  // inclusive bounds
+DDL_HD TapWin tap_win(int ty0, int ty1, int tx0, int tx1) {  // inclusive bounds
   const int nx = tx1 - tx0 + 1;
   return {ty0, ty1 - ty0 + 1, tx0, nx, (65536 + nx - 1) / nx};
 }
@@ -87,6 +87,7 @@ struct ConvFwd {
   // order spreads a tile's gathers over 32 images: 26.1 -> 26.6 us) keep the image-major
   // order m = b*RP + 4g + q.
   static constexpr bool KMAP = PADIN && H <= 7;
+  static constexpr bool KFIX = true;  // kwin / kvlen host-callable: window-aware split-K (gemm.h)
   using KWin = TapWin;
   int M, N, K;
   const float* __restrict__ x;     // [B,H,H,CIN] (+ halo when PADIN)
@@ -105,7 +106,7 @@ struct ConvFwd {
   using BInfo = LinInfo;
 
   // position (y, x) of row r (0..3) of 4-row group g of an image; false = no position
-  static DDL_DEV bool group_row(int g, int r, int& y, int& x) {
+  static DDL_HD bool group_row(int g, int r, int& y, int& x) {
     if (!ODD || g < FULLW) {
       const int w = ODD ? HP - 1 : HP;
       y = 2 * (g / w) + (r >> 1);
@@ -138,7 +139,7 @@ struct ConvFwd {
   }
   DDL_DEV KWin kfull() const { return tap_win(0, 4, 0, 4); }
   // input row y + ky - 2 is inside the image for ky in [2 - y, H + 1 - y]
-  DDL_DEV KWin kwin(int m_lo, int m_hi) const {
+  DDL_HD KWin kwin(int m_lo, int m_hi) const {
     const int nimg = M / RP;
     const int g0 = (m_lo >> 2) / nimg, g1 = ((m_hi - 1) >> 2) / nimg;
     int ylo = H, yhi = 0, xlo = H, xhi = 0;
@@ -152,7 +153,7 @@ struct ConvFwd {
       }
     return tap_win(max(0, 2 - yhi), min(4, H + 1 - ylo), max(0, 2 - xhi), min(4, H + 1 - xlo));
   }
-  DDL_DEV int kvlen(const KWin& w) const { return w.nty * w.ntx * CIN; }
+  DDL_HD int kvlen(const KWin& w) const { return w.nty * w.ntx * CIN; }
   DDL_DEV int kreal(const KWin& w, int kv) const {
     const int t = kv / CIN;
     return tap_of(w, t) * CIN + (kv - t * CIN);
@@ -302,6 +303,7 @@ struct ConvDgrad {
   // conv2 (14x14, 16 % of the taps in the halo) keeps m = (b*H + y)*H + x: the pixel-major
   // order made its dual launch 50.6 -> 58.4 us (gathers spread over 32 images per tile).
   static constexpr bool KMAP = H <= 7;
+  static constexpr bool KFIX = true;  // kwin / kvlen host-callable: window-aware split-K (gemm.h)
   using KWin = TapWin;
   int M, N, K;
   const float* __restrict__ dpre;        // [B,H+4,H+4,COUT] (halo)
@@ -331,14 +333,14 @@ struct ConvDgrad {
   }
   DDL_DEV KWin kfull() const { return tap_win(0, 4, 0, 4); }
   // oy = y - ky + 2 in [0, H) for ky in [y + 3 - H, y + 2]
-  DDL_DEV KWin kwin(int m_lo, int m_hi) const {
+  DDL_HD KWin kwin(int m_lo, int m_hi) const {
     const int nimg = M / (H * H);
     const int p0 = m_lo / nimg, p1 = (m_hi - 1) / nimg;
     const int ylo = p0 / H, yhi = p1 / H;
     const int xlo = ylo == yhi ? p0 - ylo * H : 0, xhi = ylo == yhi ? p1 - yhi * H : H - 1;
     return tap_win(max(0, ylo + 3 - H), min(4, yhi + 2), max(0, xlo + 3 - H), min(4, xhi + 2));
   }
-  DDL_DEV int kvlen(const KWin& w) const { return w.nty * w.ntx * COUT; }
+  DDL_HD int kvlen(const KWin& w) const { return w.nty * w.ntx * COUT; }
   DDL_DEV int kreal(const KWin& w, int kv) const {
     const int t = kv / COUT;
     return tap_of(w, t) * COUT + (kv - t * COUT);

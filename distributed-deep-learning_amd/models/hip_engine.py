@@ -95,6 +95,16 @@ class HipEngine:
         self.eng.set_concurrent(bool(on))
         self.graphs = None
 
+    def set_kfix(self, mask: int) -> None:
+        """Per-op bit mask (ops of csrc/kernels/api.h): window-aware split-K for the K-map conv
+        forwards / data gradients — one chunk length for every tile, the longest tap window
+        cut into splits[op] pieces."""
+        self.eng.set_kfix(int(mask))
+        self.graphs = None
+
+    def get_kfix(self) -> int:
+        return int(self.eng.get_kfix())
+
     def set_dual(self, on: bool) -> None:
         """Single stream: each layer's data- and weight-gradient GEMMs in one launch."""
         self.eng.set_dual(bool(on))

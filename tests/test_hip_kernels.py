@@ -167,6 +167,35 @@ def test_split_k_variants_agree(setup):
             assert err < tol, (t.name, name, err, e32)
 
 
+@pytest.mark.parametrize("mul", [1, 2])
+def test_window_aware_split_matches(setup, mul):
+    """Window-aware split-K (one chunk length per launch, sized by the longest tap window) on
+    the K-map conv forwards / data gradients: same loss and gradients as the balanced split,
+    within fp32 summation-order noise, deterministic across reruns."""
+    eng, flat, params, grads, x, y = setup
+    base, kf = eng.get_splits(), eng.get_kfix()
+    grads.zero_()
+    eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 31)
+    torch.cuda.synchronize()
+    g0 = grads.clone()
+    ops = (2, 3, 10, 12)  # OP_CONV3_FWD, OP_CONV4_FWD, OP_CONV4_DGRAD, OP_CONV3_DGRAD
+    try:
+        eng.set_kfix(sum(1 << o for o in ops))
+        eng.set_splits([max(2, s * mul) if i in ops else s for i, s in enumerate(base)])
+        outs = []
+        for _ in range(2):
+            grads.zero_()
+            eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 31)
+            torch.cuda.synchronize()
+            outs.append(grads.clone())
+        assert torch.equal(outs[0], outs[1])
+        assert not torch.equal(outs[0], g0) or mul == 1  # the schedule really changed
+        check_grads(outs[0], flat, x, y, 0.5, 31)
+    finally:
+        eng.set_kfix(kf)
+        eng.set_splits(base)
+
+
 @pytest.mark.parametrize("cfg", [None, 0, 1, 2, 4, 5, 6, 7, 8])
 def test_stream_k_matches_reference(setup, cfg):
     """Stream-K schedules (several worker counts, every tile config) give the fp64-reference
