@@ -26,6 +26,9 @@ import os
 import sys
 import time
 
+# device-memory kernel arguments before any HIP initialisation (see ddl_amd/__init__)
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 METRIC = "images/sec (whole node) + time-to-target-acc, MNIST CNN sync-sharding at 1/2/4/8 MI355X"
 # Baseline per GPU (the reference publishes no numbers): the strongest stock
 # PyTorch-ROCm version of the same step measured on MI355X — MIOpen-autotuned convs, fused

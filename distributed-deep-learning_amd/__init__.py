@@ -15,6 +15,14 @@ Sub-packages:
 """
 __version__ = "0.1.0"
 
+import os as _os
+
+# Kernel arguments in device memory (read by the dispatcher from HBM instead of host memory
+# over the bus).  The step is ~17 dependent launches: host-resident kernargs measured
+# 0.3255 vs 0.3045 ms/step (docs/DESIGN.md).  This ROCm defaults to device kernargs already;
+# the setting pins it for any runtime whose default differs.  Must precede HIP init.
+_os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 # Presets named after the reference's six variant directories
 # (reference: mnist_*/run.sh:3).
 VARIANTS = {
