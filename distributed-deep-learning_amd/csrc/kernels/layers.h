@@ -64,6 +64,13 @@ struct LinInfo {   // linear operand: element offset of (row, k = 0 + kk), valid
 // N = COUT, K = 25*CIN (k = tap*CIN + ci, tap = ky*5+kx).  Epilogue writes the pooled output
 // and a 1-byte code: argmax q, or 0xFF when the max is <= 0 (ReLU inactive => no gradient).
 // ---------------------------------------------------------------------------------------------
+// Image-major conv launches (conv1 / conv2 forward, conv2 data gradient) with XCD-contiguous
+// split-K numbering (gemm.h xcd_remap): each XCD's L2 then holds only its eighth of the images
+// instead of all of them (A/B knob).
+#ifndef DDL_XCD_IMG
+#define DDL_XCD_IMG 0
+#endif
+
 template <int H, int CIN, int COUT>
 struct ConvFwd {
   static constexpr int HP = (H + 1) / 2;
@@ -88,6 +95,7 @@ struct ConvFwd {
   // order m = b*RP + 4g + q.
   static constexpr bool KMAP = PADIN && H <= 7;
   static constexpr bool KFIX = true;  // kwin / kvlen host-callable: window-aware split-K (gemm.h)
+  static constexpr bool XCD_CONTIG = DDL_XCD_IMG && !KMAP;
   using KWin = TapWin;
   int M, N, K;
   const float* __restrict__ x;     // [B,H,H,CIN] (+ halo when PADIN)
@@ -304,6 +312,7 @@ struct ConvDgrad {
   // order made its dual launch 50.6 -> 58.4 us (gathers spread over 32 images per tile).
   static constexpr bool KMAP = H <= 7;
   static constexpr bool KFIX = true;  // kwin / kvlen host-callable: window-aware split-K (gemm.h)
+  static constexpr bool XCD_CONTIG = DDL_XCD_IMG && !KMAP;
   using KWin = TapWin;
   int M, N, K;
   const float* __restrict__ dpre;        // [B,H+4,H+4,COUT] (halo)

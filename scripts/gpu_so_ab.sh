@@ -14,7 +14,7 @@ if [ -z "${SKIP_TESTS:-}" ]; then
   rc=$?; tail -3 gpurun_out/ab_tests.log; [ $rc -ne 0 ] && exit $rc
 fi
 for i in $(seq $ROUNDS); do
-  for so in _C.so ${SO_B:-_C_ab.so}; do
+  for so in _C.so ${SO_B:-_C_ab.so}; do  # SO_B may list several builds
     DDL_SO=$so timeout -k 10 120 python bench.py --tta 0 --steps 400 --warmup 40 ${BENCH_ARGS:-} > gpurun_out/ab.log 2>&1 || exit $?
     echo "$so $(tail -1 gpurun_out/ab.log | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["ms_per_step"])')"
   done
