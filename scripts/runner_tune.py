@@ -27,6 +27,10 @@ def main():
     ap.add_argument("--steps", type=int, default=250)
     ap.add_argument("--gain", type=float, default=0.004)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--ops", default=None, help="comma-separated op indices to tune (default all)")
+    ap.add_argument("--multiwave", action="store_true",
+                    help="also try the multi-wave block tiles (configs 1, 2, 6, 7, 8) on the "
+                         "forward convolutions (not dual-launched, so any tile config runs)")
     a = ap.parse_args()
     import torch
     from ddl_amd.config import TrainConfig
@@ -83,6 +87,10 @@ def main():
         for c2 in (0, 3, 4, 5):  # the one-wave configs (dual launches instantiate these)
             if c2 != c:
                 out.append(mk(c2, s, w, wd))
+        if a.multiwave and op in (0, 1, 2, 3):
+            for c2 in (1, 2, 6, 7, 8):
+                for s2 in sorted({s, min(2048, s * 2), max(1, s // 2)}):
+                    out.append(mk(c2, s2, 0, wd))
         if op in KWAVE_OK:  # K split over the waves of one workgroup (4 / 8 / 16 waves)
             for s2 in (4, 8, 16):
                 if (c, s) != (13, s2):
@@ -93,6 +101,8 @@ def main():
     print(f"start {base:.1f} us/step", flush=True)
     for p in range(a.passes):
         for op, name in enumerate(OPS):
+            if a.ops and op not in {int(o) for o in a.ops.split(",")}:
+                continue
             best, best_t = None, None
             for cand in cands(op):
                 t = timed(cand)
