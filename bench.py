@@ -26,8 +26,10 @@ import os
 import sys
 import time
 
-# device-memory kernel arguments before any HIP initialisation (see ddl_amd/__init__)
+# device-memory kernel arguments and dmabuf IPC before any HIP initialisation (see
+# ddl_amd/__init__)
 os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 METRIC = "images/sec (whole node) + time-to-target-acc, MNIST CNN sync-sharding at 1/2/4/8 MI355X"
 # Baseline per GPU (the reference publishes no numbers): the strongest stock
@@ -36,6 +38,16 @@ METRIC = "images/sec (whole node) + time-to-target-acc, MNIST CNN sync-sharding 
 # 0.8464 ms/step).  The round-1 faithful-semantics eager baseline (bench.py --engine torch,
 # 51,308.5 img/s) is 2.3x slower still.
 BASELINE_IMG_PER_S_PER_GPU = 118145.4
+
+
+def variant_of(mode: str, policy: str) -> str:
+    """The reference directory whose semantics the run has; the flat and
+    LPT plans are this framework's sharding policies for the sharded variants."""
+    base = {"none": "mnist_{}", "contiguous": "mnist_{}_sharding",
+            "greedy": "mnist_{}_sharding_greedy"}.get(policy)
+    if base:
+        return base.format(mode)
+    return f"mnist_{mode}_sharding ({policy} plan)"
 
 
 def main(argv=None):
@@ -80,6 +92,15 @@ def main(argv=None):
     ap.add_argument("--tta-sync-eval", action="store_true",
                     help="time-to-accuracy run with the eval in line on the training stream "
                          "(default on GPU: side-stream eval from parameter snapshots)")
+    ap.add_argument("--prewarm-steps", type=int, default=-1,
+                    help="untimed training steps BEFORE the --warmup steps (reported in the "
+                         "JSON; default 100 on a GPU, 0 on CPU).  Measured on MI355X: after 5 warmup steps a 20-step window "
+                         "runs 0.321-0.323 ms/step, after 100 0.308-0.312 (the GPU is still "
+                         "ramping up); --steps 200 --warmup 5 amortises it to 0.307")
+    ap.add_argument("--extra-plans", default="contiguous",
+                    help="W > 1 sync: comma-separated shard plans also timed after the headline "
+                         "plan (same steps), reported under 'plans' (BASELINE config 3 names "
+                         "contiguous shards); empty string skips them")
     a = ap.parse_args(argv)
 
     import torch
@@ -95,12 +116,14 @@ def main(argv=None):
     if a.gpus != world and not (a.gpus == 1 and world == 1):
         if env.rank == 0:
             print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    total_steps = a.warmup + a.steps
     cuda = env.device.type == "cuda"
+    n_pre = a.prewarm_steps if a.prewarm_steps >= 0 else (100 if cuda else 0)
+    total_steps = n_pre + a.warmup + a.steps
     data = synthetic_mnist()
 
-    def make_trainer(backend):
-        cfg = TrainConfig(mode=a.mode, shard=a.shard, steps=total_steps, batch_size=a.batch_size,
+    def make_trainer(backend, shard=None):
+        cfg = TrainConfig(mode=a.mode, shard=shard or a.shard, steps=total_steps,
+                          batch_size=a.batch_size,
                           eval_every=0, engine=a.engine, graph=a.graph and not a.no_graph,
                           overlap=not a.no_overlap, quiet=True, data_sharding="stride",
                           native_exchange=not a.no_native_exchange,
@@ -221,22 +244,43 @@ def main(argv=None):
     keep.append(tr)
     cfg = tr.cfg
 
-    if a.mode == "async":
-        tr.exchange.steps = total_steps
-        tr.exchange.start()
-    for i in range(a.warmup):
-        tr.train_step(i)
-    sync()
-    t0 = time.perf_counter()
-    for i in range(a.warmup, total_steps):
-        tr.train_step(i)
-    if a.mode == "async":
-        tr.exchange.join()
-    sync()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
+    def timed_run(t):
+        """prewarm + warmup (untimed), then exactly a.steps steps between barrier+sync pairs;
+        returns the max-over-ranks seconds of the timed window."""
+        if a.mode == "async":
+            t.exchange.steps = total_steps
+            t.exchange.start()
+        for i in range(n_pre + a.warmup):
+            t.train_step(i)
+        sync()
+        t0 = time.perf_counter()
+        for i in range(n_pre + a.warmup, total_steps):
+            t.train_step(i)
+        if a.mode == "async":
+            t.exchange.join()
+        sync()
+        return max_over_ranks(time.perf_counter() - t0)
+
+    elapsed = timed_run(tr)
     ms = 1e3 * elapsed / a.steps
     imgs = world * a.batch_size * a.steps / elapsed
     acc = tr.evaluate()
+
+    # W > 1 sync: the reference's tensor-granular plans on the same harness (RCCL grouped
+    # reduce / broadcast; contiguous puts 59 % of the bytes on the last PS at W = 8)
+    plans = {}
+    extra = [p for p in a.extra_plans.split(",") if p and p != a.shard]
+    if world > 1 and a.mode == "sync" and extra:
+        for p in extra:
+            try:
+                t = make_trainer("rccl", shard=p)
+                keep.append(t)
+                el = timed_run(t)
+                plans[p] = {"ms_per_step": round(1e3 * el / a.steps, 4),
+                            "value": round(world * a.batch_size * a.steps / el, 1),
+                            "exchange": backend_of(t), "num_ps": t.num_ps}
+            except RuntimeError as e:
+                plans[p] = {"error": str(e)[:200]}
 
     tta = None
     if a.tta is not None and a.tta > 0:
@@ -275,7 +319,8 @@ def main(argv=None):
                 "global_batch": world * a.batch_size,
                 "seq_len": None,
                 "parallelism": f"dp{world}-ps{tr.num_ps}-{a.mode}-{tr.plan.policy}",
-                "variant": "mnist_sync_sharding" if a.mode == "sync" else "mnist_async_sharding",
+                "variant": variant_of(a.mode, tr.plan.policy),
+                "plan": tr.plan.policy,
                 "engine": engine_name,
                 "hip_graph": bool(a.graph and not a.no_graph),
                 "overlap": not a.no_overlap,
@@ -284,9 +329,14 @@ def main(argv=None):
                 "optimizer": "adam(1e-4) on PS shards",
             },
             "test_acc_after_run": round(acc, 4),
+            "prewarm": {"steps": n_pre, "note": "untimed steps before the warmup steps: the "
+                        "GPU is still ramping up after a few steps (20-step window after 5 "
+                        "warmup steps: 0.322 vs 0.308 ms/step after 100)"},
         }
         if ab:
             rec["exchange_ab"] = ab
+        if plans:
+            rec["plans"] = plans
         if shared_gpu and world > 1:
             rec["note"] = (f"{world} ranks share ONE GPU (DDL_DIST_BACKEND=gloo rehearsal): "
                            "functional check of the W > 1 path, not a multi-GPU measurement")

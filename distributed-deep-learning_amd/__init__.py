@@ -22,6 +22,12 @@ import os as _os
 # 0.3255 vs 0.3045 ms/step (docs/DESIGN.md).  This ROCm defaults to device kernargs already;
 # the setting pins it for any runtime whose default differs.  Must precede HIP init.
 _os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+# Cross-process GPU memory sharing (RCCL's P2P transports, the xGMI exchanges' IPC handles)
+# through dmabuf: the MI355X hosts this runs on only support dmabuf IPC, and with the legacy
+# mode hipIpcGetMemHandle fails ("invalid argument").  Every launcher script exports it; the
+# setdefault covers a torchrun started without them (e.g. the driver's multi-GPU bench).
+# Must precede HIP init.
+_os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 # Presets named after the reference's six variant directories
 # (reference: mnist_*/run.sh:3).

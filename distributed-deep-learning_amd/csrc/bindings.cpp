@@ -393,6 +393,11 @@ class PyAsyncService {
   }
   int64_t t(int64_t ps) const { return svc_->t((int)ps); }
   int64_t served() const { return svc_->served(); }
+  void pause() {
+    py::gil_scoped_release nogil;
+    svc_->pause();
+  }
+  void resume() { svc_->resume(); }
   std::vector<std::array<int64_t, 4>> provenance() const { return svc_->provenance(); }
 
  private:
@@ -617,6 +622,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("start", &PyAsyncService::start)
       .def("join", &PyAsyncService::join)
       .def("t", &PyAsyncService::t)
+      .def("pause", &PyAsyncService::pause)
+      .def("resume", &PyAsyncService::resume)
       .def("served", &PyAsyncService::served)
       .def("provenance", &PyAsyncService::provenance);
 

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -305,6 +306,10 @@ class AsyncService {
   ~AsyncService();
   void start(int64_t expected);  // serve `expected` tokens on a native thread
   void join();                   // rethrows the thread's error, if any
+  // checkpoint hook: no apply is issued between pause() and resume(), and every issued one has
+  // completed when pause() returns (the PS state is one consistent step); same caller thread
+  void pause();
+  void resume();
   int64_t t(int ps) const;
   int64_t served() const { return served_.load(); }
   // (worker, ps, worker round, PS step) per apply, in service order
@@ -326,6 +331,7 @@ class AsyncService {
   hipStream_t stream_ = nullptr;
   std::thread th_;
   std::string error_;
+  mutable std::mutex pause_mu_;  // held by the service thread while it issues an apply
 };
 
 class SyncRunner {
@@ -382,6 +388,9 @@ class SyncRunner {
   hipEvent_t seg_ev_[kSegments] = {};
   hipEvent_t seg_ev_dev_[kSegments] = {};  // device-scope release (xGMI-only segments)
   bool seg_xgmi_only_[kSegments] = {};
+  bool seg_offstream_[kSegments] = {};     // the segment has units on the comm stream
+  // seg events recorded by the segment's own kernel packets (DDL_EXT_EVENT, default on)
+  bool ext_event_ = true;
   hipEvent_t done_ev_ = nullptr;
   std::vector<RunnerUnit> units_;
   int opt_ = 0;

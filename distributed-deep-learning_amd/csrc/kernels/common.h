@@ -6,6 +6,29 @@
 #define DDL_DEV __device__ __forceinline__
 #define DDL_HD __host__ __device__ __forceinline__
 
+#include <hip/hip_ext.h>
+
+namespace ddl {
+// Completion event bound to the engine's kernel launches (host thread-local).  While set, every
+// DDL_LAUNCH records it through the kernel's OWN dispatch packet (hipExtLaunchKernelGGL stop
+// event) instead of a separate hipEventRecord marker packet: the runner waits on the event after
+// the segment's last launch, so it fires when that kernel completes.  A marker packet after the
+// segment cost ~5 us of compute-queue idle per issue point (forced-rehearsal timelines).
+inline hipEvent_t& launch_stop_event() {
+  static thread_local hipEvent_t ev = nullptr;
+  return ev;
+}
+}  // namespace ddl
+
+#define DDL_LAUNCH(kernel, grid, block, shmem, stream, ...)                                     \
+  do {                                                                                          \
+    if (hipEvent_t ddl_ev_ = ::ddl::launch_stop_event())                                        \
+      hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, nullptr, ddl_ev_, 0,             \
+                            __VA_ARGS__);                                                       \
+    else                                                                                        \
+      hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);                      \
+  } while (0)
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------------------------

@@ -1003,7 +1003,7 @@ inline void launch_gemm_pack_w(const PA& pa, const PB& pb, const AUX& ut, hipStr
   const int gxB = (pb.M + 31) / 32, ntB = gxB * ((pb.N + 31) / 32);
   const int nB = (ntB + KW - 1) / KW, nX = (ut.nblk + KW - 1) / KW;
   if (nA + nB + nX > 0)
-    hipLaunchKernelGGL((gemm_pack_kernel<KW, PA, PB, AUX>), dim3(nA + nB + nX), dim3(KW * 64), 0,
+    DDL_LAUNCH((gemm_pack_kernel<KW, PA, PB, AUX>), dim3(nA + nB + nX), dim3(KW * 64), 0,
                        stream, pa, nA, gxA, pb, nB, gxB, ntB, ut);
 }
 
@@ -1027,10 +1027,10 @@ inline void launch_gemm_kwave(const P& p, int splits, hipStream_t stream) {
   if (p.M <= 0 || p.N <= 0) return;
   const dim3 grid((p.M + 31) / 32, (p.N + 31) / 32);
   switch (kwave_waves(splits)) {
-    case 4: hipLaunchKernelGGL((gemm_kwave_kernel<BK, 4, P>), grid, dim3(256), 0, stream, p); break;
-    case 8: hipLaunchKernelGGL((gemm_kwave_kernel<BK, 8, P>), grid, dim3(512), 0, stream, p); break;
+    case 4: DDL_LAUNCH((gemm_kwave_kernel<BK, 4, P>), grid, dim3(256), 0, stream, p); break;
+    case 8: DDL_LAUNCH((gemm_kwave_kernel<BK, 8, P>), grid, dim3(512), 0, stream, p); break;
     default:
-      hipLaunchKernelGGL((gemm_kwave_kernel<BK, 16, P>), grid, dim3(1024), 0, stream, p);
+      DDL_LAUNCH((gemm_kwave_kernel<BK, 16, P>), grid, dim3(1024), 0, stream, p);
   }
 }
 
@@ -1281,15 +1281,15 @@ inline void launch_reduce(const P& p, const SubGrid& g, hipStream_t stream) {
   const float4* s4 = g.slab;
   if (z > 32) {
     const size_t th = nelem * 64;
-    hipLaunchKernelGGL((splitk_wide_reduce<BM, BN, WM, WN, 64, P>), dim3((th + 255) / 256),
+    DDL_LAUNCH((splitk_wide_reduce<BM, BN, WM, WN, 64, P>), dim3((th + 255) / 256),
                        dim3(256), 0, stream, p, s4, z, g.gx, ntiles);
   } else if (z > 4) {
     const size_t th = nelem * 16;
-    hipLaunchKernelGGL((splitk_wide_reduce<BM, BN, WM, WN, 16, P>), dim3((th + 255) / 256),
+    DDL_LAUNCH((splitk_wide_reduce<BM, BN, WM, WN, 16, P>), dim3((th + 255) / 256),
                        dim3(256), 0, stream, p, s4, z, g.gx, ntiles);
   } else {
     const size_t th = nelem * 4;
-    hipLaunchKernelGGL((splitk_wide_reduce<BM, BN, WM, WN, 4, P>), dim3((th + 255) / 256),
+    DDL_LAUNCH((splitk_wide_reduce<BM, BN, WM, WN, 4, P>), dim3((th + 255) / 256),
                        dim3(256), 0, stream, p, s4, z, g.gx, ntiles);
   }
 }
@@ -1300,11 +1300,11 @@ inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch
   const SubGrid g = plan_gemm<BM, BN, BK>(p, splits, workers, wide_thr, sc);
   if (g.nblocks == 0) return;
   if (g.streamk) {
-    hipLaunchKernelGGL((gemm_streamk_kernel<BM, BN, BK, WM, WN, P>), dim3(g.nblocks),
+    DDL_LAUNCH((gemm_streamk_kernel<BM, BN, BK, WM, WN, P>), dim3(g.nblocks),
                        dim3(WM * WN * 64), 0, stream, p, g.KI, g.gx, g.I, g.slab, g.tickets);
     return;
   }
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, WM, WN, P>), dim3(g.gx, g.gy, g.gz),
+  DDL_LAUNCH((gemm_f32_kernel<BM, BN, BK, WM, WN, P>), dim3(g.gx, g.gy, g.gz),
                      dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets, g.xcd);
   launch_reduce<BM, BN, BK, WM, WN, P>(p, g, stream);
 }
@@ -1325,7 +1325,7 @@ inline bool launch_reduce_with_gemm(const PR& pr, const SubGrid& gr, const PG& p
 #define DDL_RG(RL)                                                                            \
   {                                                                                         \
     const int nrb = (int)((nelem * RL + 63) / 64);                                          \
-    hipLaunchKernelGGL((reduce_gemm_kernel<CR::BM, CR::BN, CR::WM, CR::WN, RL, PR, CG, PG>),  \
+    DDL_LAUNCH((reduce_gemm_kernel<CR::BM, CR::BN, CR::WM, CR::WN, RL, PR, CG, PG>),  \
                        dim3(nrb + gg.nblocks), dim3(64), 0, stream, pr, s4, z, gr.gx, ntiles, nrb, \
                        pg, gg);                                                             \
   }
@@ -1346,7 +1346,7 @@ inline void launch_gemm_dual(const PA& pa, int sa, int wa, const SplitScratch& s
   const SubGrid gb = plan_gemm<CB::BM, CB::BN, CB::BK>(pb, sb, wb, wide_b, scb);
   const int n = ut.nblk + ga.nblocks + gb.nblocks;
   if (n > 0)
-    hipLaunchKernelGGL((gemm_dual_kernel<CA, PA, CB, PB, AUX>), dim3(n), dim3(64), 0, stream, pa,
+    DDL_LAUNCH((gemm_dual_kernel<CA, PA, CB, PB, AUX>), dim3(n), dim3(64), 0, stream, pa,
                        ga, pb, gb, ut, bfirst);
   launch_reduce<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, stream);
   if (defer_b) *defer_b = gb;  // the caller launches B's reduce (launch_reduce_with_gemm)

@@ -159,20 +159,20 @@ head_fused_kernel(const float* __restrict__ h2, const float* __restrict__ w,
 void launch_head_fused(const float* h2, const float* w, const float* bias, const int64_t* labels,
                        int B, const uint32_t* seed, uint32_t seed_v, uint32_t thr24,
                        float inv_keep, float* dlog, float* loss, float* dpre2, hipStream_t st) {
-  hipLaunchKernelGGL(head_fused_kernel, dim3(B), dim3(256), 0, st, h2, w, bias, labels,
+  DDL_LAUNCH(head_fused_kernel, dim3(B), dim3(256), 0, st, h2, w, bias, labels,
                      B, 1.f / (float)B, seed, seed_v, thr24, inv_keep, dlog, loss, dpre2);
 }
 
 void launch_head_wgrad(const float* h2, const float* dlog, int B, float* gw, float* gb,
                        hipStream_t st) {
   const int wblocks = (HK + 1 + 3) / 4;
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(wblocks), dim3(256), 0, st, h2, nullptr, dlog, B,
+  DDL_LAUNCH(head_bwd_kernel, dim3(wblocks), dim3(256), 0, st, h2, nullptr, dlog, B,
                      wblocks, nullptr, 0u, 0u, 1.f, gw, gb, nullptr);
 }
 
 void launch_head_fwd(const float* h2, const float* w, const float* bias, const int64_t* labels,
                      int B, float* dlog, float* loss, int* correct, hipStream_t st) {
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(B), dim3(256), 0, st, h2, w, bias, labels, B,
+  DDL_LAUNCH(head_fwd_kernel, dim3(B), dim3(256), 0, st, h2, w, bias, labels, B,
                      1.f / (float)B, dlog, loss, correct);
 }
 
@@ -182,7 +182,7 @@ void launch_head_bwd(const float* h2, const float* w, const float* dlog, int B,
                      float* dpre2, hipStream_t st) {
   const int wblocks = (HK + 1 + 3) / 4;  // one wave per dW_aug row
   const int dblocks = (B * HK + 255) / 256;
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(wblocks + dblocks), dim3(256), 0, st, h2, w, dlog, B,
+  DDL_LAUNCH(head_bwd_kernel, dim3(wblocks + dblocks), dim3(256), 0, st, h2, w, dlog, B,
                      wblocks, seed, seed_v, thr24, inv_keep, gw, gb, dpre2);
 }
 

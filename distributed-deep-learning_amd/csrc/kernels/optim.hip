@@ -82,10 +82,10 @@ void launch_adam_c(float* w, const float* g, float* m, float* v, int64_t n, floa
   if (n <= 0) return;
   const uintptr_t al = (uintptr_t)w | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v;
   if ((al & 15) == 0) {
-    hipLaunchKernelGGL(adam_vec_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, (float4*)w,
+    DDL_LAUNCH(adam_vec_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, (float4*)w,
                        (const float4*)g, (float4*)m, (float4*)v, n, lr_t, c1, c2, eps, scale);
   } else {
-    hipLaunchKernelGGL(adam_scalar_kernel, dim3(grid_for(n)), dim3(256), 0, st, w, g, m, v, n,
+    DDL_LAUNCH(adam_scalar_kernel, dim3(grid_for(n)), dim3(256), 0, st, w, g, m, v, n,
                        lr_t, c1, c2, eps, scale);
   }
 }
@@ -93,12 +93,12 @@ void launch_adam_c(float* w, const float* g, float* m, float* v, int64_t n, floa
 void launch_momentum(float* w, const float* g, float* m, int64_t n, float lr, float mu,
                      float scale, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(momentum_kernel, dim3(grid_for(n)), dim3(256), 0, st, w, g, m, n, lr, mu,
+  DDL_LAUNCH(momentum_kernel, dim3(grid_for(n)), dim3(256), 0, st, w, g, m, n, lr, mu,
                      scale);
 }
 
 void launch_scale(float* p, int64_t n, float a, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, n, a);
+  DDL_LAUNCH(scale_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, n, a);
 }
 }  // namespace ddl

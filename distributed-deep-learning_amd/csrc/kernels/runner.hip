@@ -28,6 +28,8 @@
 #include <vector>
 
 #include "api.h"
+#include "common.h"
+#include "trace.h"
 
 namespace ddl {
 
@@ -121,6 +123,8 @@ SyncRunner::SyncRunner(Engine* eng, float* params, float* grads, int world, int 
                                       hipEventDisableTiming | hipEventDisableSystemFence));
   }
   HIP_CHECK(hipEventCreateWithFlags(&done_ev_, hipEventDisableTiming));
+  const char* xe = getenv("DDL_EXT_EVENT");
+  ext_event_ = xe ? xe[0] == '1' : true;
 }
 
 SyncRunner::~SyncRunner() {
@@ -184,6 +188,7 @@ void SyncRunner::set_units(const std::vector<RunnerUnit>& units) {
         only &= u.kind == RunnerUnit::XGMI;
       }
     seg_xgmi_only_[sg] = any && only;
+    seg_offstream_[sg] = any;
   }
   // the step's last xGMI unit also waits until every owner's parameters have landed here
   last_xgmi_ = -1;
@@ -327,30 +332,52 @@ void SyncRunner::issue_reduce_group(const std::vector<const RunnerUnit*>& us, co
   RCCL_CHECK(rccl().GroupEnd());
 }
 
+// RAII: engine launches inside the scope carry `ev` as their completion event (common.h)
+struct StopEventScope {
+  explicit StopEventScope(hipEvent_t ev) { launch_stop_event() = ev; }
+  ~StopEventScope() { launch_stop_event() = nullptr; }
+};
+
+static const char* const kBwdRange[SyncRunner::kSegments] = {
+    "ddl.bwd.seg0(head+fc)", "ddl.bwd.seg1(conv4)", "ddl.bwd.seg2(conv3)",
+    "ddl.bwd.seg3(conv2+conv1)"};
+static const char* const kExRange[SyncRunner::kSegments] = {
+    "ddl.exchange.seg0", "ddl.exchange.seg1", "ddl.exchange.seg2", "ddl.exchange.seg3"};
+
 void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t seed_value,
                       const float* lr_t, hipStream_t st) {
+  TraceRange step_range("ddl.step");
   eng_->seed_value = seed_value;  // dropout seed by kernel argument: no seed-upload kernel
   const uint32_t* seed = nullptr;
   // Cross-queue dependencies (event record -> stream wait) cost tens of microseconds of GPU
   // idle each on this stack (measured), so LOCAL updates go straight onto the compute
   // stream in order; only units with collectives use the comm stream, which then overlaps
   // the remaining backward segments.
-  eng_->forward(x, B, seed, true, st);
+  {
+    TraceRange r("ddl.fwd");
+    eng_->forward(x, B, seed, true, st);
+  }
   if (all_local_ && local_on_main_ && use_tail_ && tail_ok_ && opt_ == 0 && coef_ == 1.f) {
     // segment s-1's update rides in segment s's dual launch (flushed as a launch of its own
     // if the segment had no dual launch to take it); the last segment's follows the backward
     for (int s = 0; s < kSegments; ++s) {
+      TraceRange r(kBwdRange[s]);
       if (s > 0 && !seg_pieces_[s - 1].empty()) set_tail(s - 1, lr_t);
       eng_->backward_segment(s, x, labels, B, seed, st);
       eng_->flush_tail(st);
     }
+    TraceRange r("ddl.update.last_segment");
     for (const auto& p : seg_pieces_[kSegments - 1])
       update(w_ + p.r.lo, g_ + p.r.lo, p.m + p.r.state_off, p.v + p.r.state_off,
              p.r.hi - p.r.lo, lr_t[p.ps], st);
     return;
   }
   if (all_local_ && local_on_main_) {
-    for (int s = 0; s < kSegments; ++s) eng_->backward_segment(s, x, labels, B, seed, st);
+    for (int s = 0; s < kSegments; ++s) {
+      TraceRange r(kBwdRange[s]);
+      eng_->backward_segment(s, x, labels, B, seed, st);
+    }
+    TraceRange r("ddl.update");
     if (coef_ != 1.f)
       for (const auto& p : merged_) launch_scale(g_ + p.r.lo, p.r.hi - p.r.lo, coef_, st);
     for (const auto& p : merged_)
@@ -370,8 +397,18 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
   }
   std::vector<const RunnerUnit*> reduces;
   for (int s = 0; s < kSegments; ++s) {
-    eng_->backward_segment(s, x, labels, B, seed, st);
     const bool on_main = last_on_main_ && s == kSegments - 1;
+    hipEvent_t ev = seg_xgmi_only_[s] ? seg_ev_dev_[s] : seg_ev_[s];
+    // the comm stream waits for this segment's gradients: bind the event to the segment's
+    // kernel launches themselves (the wait below is issued after the last one) rather than a
+    // marker packet behind them
+    const bool bind = ext_event_ && !on_main && seg_offstream_[s];
+    {
+      TraceRange r(kBwdRange[s]);
+      StopEventScope scope(bind ? ev : nullptr);
+      eng_->backward_segment(s, x, labels, B, seed, st);
+    }
+    TraceRange ex_range(kExRange[s]);
     hipStream_t xs = on_main ? st : cs_;
     bool waited = on_main;
     reduces.clear();
@@ -383,8 +420,7 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
         continue;
       }
       if (!waited) {
-        hipEvent_t ev = seg_xgmi_only_[s] ? seg_ev_dev_[s] : seg_ev_[s];
-        HIP_CHECK(hipEventRecord(ev, st));
+        if (!bind) HIP_CHECK(hipEventRecord(ev, st));
         HIP_CHECK(hipStreamWaitEvent(cs_, ev, 0));
         waited = true;
       }
@@ -403,6 +439,7 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
     if (!reduces.empty()) issue_reduce_group(reduces, lr_t, xs);
   }
   if (comm_used) {
+    TraceRange r("ddl.exchange.join");
     // the next step's forward reads the updated parameters
     HIP_CHECK(hipEventRecord(done_ev_, cs_));
     HIP_CHECK(hipStreamWaitEvent(st, done_ev_, 0));

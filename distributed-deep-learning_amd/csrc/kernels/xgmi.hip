@@ -146,18 +146,26 @@ __global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a)
   __syncthreads();
   if (tid < W && tid != me) flag_store(T.flags[tid] + arrive_idx(b, me, j), a.epoch);
 
-  // ---- phase 2: every peer's piece of my slice has arrived (one parallel poll)
-  if (tid < W && tid != me)
-    wait_ge(myflags + arrive_idx(b, tid, j), a.epoch, deadline, a.err, 1);
+  // ---- phase 2: every peer's piece of my slice has arrived (one parallel poll).  If any wait
+  // failed (timeout, or another workgroup's recorded error) the slice is NOT updated: summing a
+  // stale inbox would advance m / v and push wrong parameters into every replica.  DONE is still
+  // stored, so the peers do not wait out their own timeouts; the host raises on the error word.
+  __shared__ int arrived;
+  if (tid == 0) arrived = 1;
+  __syncthreads();
+  if (tid < W && tid != me &&
+      !wait_ge(myflags + arrive_idx(b, tid, j), a.epoch, deadline, a.err, 1))
+    arrived = 0;  // benign race: every writer stores 0
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // keep the loads below the poll
+  const int n4u = arrived ? n4 : 0;
 
   const float4* own = reinterpret_cast<const float4*>(a.grads + a.lo + me * a.c + s0);
   const brsrc_t inbox = make_rsrc(T.inbox[me] + a.inbox_off, (uint32_t)(W * a.c * 4));
   float4* m4 = reinterpret_cast<float4*>(a.m + s0);
   float4* v4 = a.v ? reinterpret_cast<float4*>(a.v + s0) : nullptr;
   float4* w4 = reinterpret_cast<float4*>(T.params[me] + a.lo + me * a.c + s0);
-  for (int i = tid; i < n4; i += 256) {
+  for (int i = tid; i < n4u; i += 256) {
     float4 x[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q)

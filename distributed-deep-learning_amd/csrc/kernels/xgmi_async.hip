@@ -39,6 +39,7 @@
 #include <cmath>
 
 #include "api.h"
+#include "trace.h"
 #include "common.h"
 #include "runtime/mailbox.h"
 
@@ -143,13 +144,17 @@ __global__ void __launch_bounds__(256) async_apply_kernel(AsyncTable T, ApplyArg
   const long long deadline = wall_clock64() + a.timeout_ticks;
   const AsyncShard& S = T.shard[a.ps];
   const int j = blockIdx.x, tid = threadIdx.x;
+  // a failed wait (timeout / recorded error) leaves the PS state untouched: applying a stale
+  // inbox slot would advance m / v with the wrong gradient; DONE is still stored (the worker
+  // host then sees the error word instead of waiting out its own timeout)
+  __shared__ int arrived;
   if (tid == 0)
-    wait_ge(T.flags[a.me] + arrive_idx(a.ps, a.worker, j), a.epoch, deadline, a.err, 1);
+    arrived = wait_ge(T.flags[a.me] + arrive_idx(a.ps, a.worker, j), a.epoch, deadline, a.err, 1);
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // keep the loads below the poll
   const int64_t s0 = (int64_t)j * S.slice;
   const int64_t s1 = s0 + S.slice < S.n ? s0 + S.slice : S.n;
-  const int n4 = s0 < s1 ? (int)((s1 - s0) >> 2) : 0;
+  const int n4 = (s0 < s1 && arrived) ? (int)((s1 - s0) >> 2) : 0;
   const brsrc_t in = make_rsrc(T.inbox[a.me] + S.inbox_off + (int64_t)a.worker * S.n + s0,
                                (uint32_t)n4 * 16u);
   const brsrc_t out = make_rsrc(T.params[a.worker] + S.lo + s0, (uint32_t)n4 * 16u);
@@ -447,15 +452,22 @@ void AsyncService::run() {
     X_CHECK(hipSetDevice(device_));
     ShmMailbox box(mbox_name_, 2, false);
     for (int64_t k = 0; k < expected_; ++k) {
-      const int64_t v = box.pop(600.0);
+      int64_t v;
+      {
+        TraceRange r("ddl.async.ps.wait_arrival");
+        v = box.pop(600.0);
+      }
       if (v < 0) throw std::runtime_error("async PS: no arrival within 600 s");
+      TraceRange apply_range("ddl.async.ps.apply");
       const int w = (int)(v >> 20), p = (int)(v & ((1 << 20) - 1));
       AsyncPsState* st = nullptr;
       for (auto& s : ps_)
         if (s.ps == p) st = &s;
       if (!st || w < 0 || w >= world_) throw std::runtime_error("async PS: bad token");
+      std::lock_guard<std::mutex> hold(pause_mu_);  // pause(): no apply while a snapshot is taken
       const uint32_t e = ++epoch_[(size_t)w * kAsyncMaxPs + p];
-      const int64_t t = ++st->t;  // one apply_gradients of this PS per arrival
+      // one apply_gradients of this PS per arrival
+      const int64_t t = __atomic_add_fetch(&st->t, 1, __ATOMIC_ACQ_REL);
       XgmiUpdate u;
       u.opt = opt_;
       u.m = st->m;
@@ -487,9 +499,22 @@ void AsyncService::join() {
   if (!error_.empty()) throw std::runtime_error(error_);
 }
 
+void AsyncService::pause() {
+  pause_mu_.lock();
+  if (stream_) {
+    const hipError_t e = hipStreamSynchronize(stream_);
+    if (e != hipSuccess) {
+      pause_mu_.unlock();
+      throw std::runtime_error(std::string("async service: pause: ") + hipGetErrorString(e));
+    }
+  }
+}
+
+void AsyncService::resume() { pause_mu_.unlock(); }
+
 int64_t AsyncService::t(int ps) const {
-  for (const auto& s : ps_)
-    if (s.ps == ps) return s.t;
+  for (const auto& s : ps_)  // lock-free: also read while paused
+    if (s.ps == ps) return __atomic_load_n(&s.t, __ATOMIC_ACQUIRE);
   throw std::invalid_argument("async service: PS not hosted here");
 }
 

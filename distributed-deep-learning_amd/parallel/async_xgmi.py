@@ -27,6 +27,7 @@ tested on a one-GPU box (``tests/test_xgmi_gpu.py``).
 """
 from __future__ import annotations
 
+import contextlib
 import threading
 from typing import Dict, List, Optional, Tuple
 
@@ -54,7 +55,7 @@ class AsyncPeerExchange:
                  check_provenance: bool = False, optimizer: str = "adam"):
         if not params.is_cuda or not native.available():
             raise AsyncPeerUnavailable("async xGMI exchange needs the extension and a GPU")
-        if optimizer not in ("adam", "momentum"):
+        if optimizer not in ("adam", "momentum", "sgd"):
             raise AsyncPeerUnavailable(f"async xGMI exchange has no '{optimizer}' update")
         P, W, r = plan.num_ps, env.world, env.rank
         for p in range(P):
@@ -64,7 +65,8 @@ class AsyncPeerExchange:
         self.servers = servers
         self.steps = steps_per_worker
         self.grad_scale = 1.0  # the async PS applies each worker's gradient as-is
-        self.opt = 0 if optimizer == "adam" else 1
+        self.opt = 0 if optimizer == "adam" else 1  # sgd: the momentum update with mu = 0
+        self.mu = 0.0 if optimizer == "sgd" else None
         self.ranges: List[Tuple[int, int]] = [plan.ps_segments(p)[0] for p in range(P)]
         self.hosts = [plan.host_rank(p, W) for p in range(P)]
         ops = native.ops()
@@ -188,7 +190,7 @@ class AsyncPeerExchange:
             # between a remote worker's token and its apply kernel
             ps_list = [(p, ps.params, ps.m, ps.v, ps.t) for p, ps in self.servers.items()]
             h = next(iter(self.servers.values())).h
-            mom = next(iter(self.servers.values())).momentum
+            mom = next(iter(self.servers.values())).momentum if self.mu is None else self.mu
             self._svc = native.ops().AsyncService(
                 self.peer, self.mailbox.name, self.env.world, ps_list, self.opt, h.lr, h.beta1,
                 h.beta2, h.eps, mom, self.grad_scale, 1, self.check_provenance)
@@ -209,13 +211,17 @@ class AsyncPeerExchange:
                 e = self.count[(w, p)] + 1
                 self.count[(w, p)] = e
                 ps = self.servers[p]
-                ps.begin()
-                lr_t = adam_coeffs(ps.h, ps.t) if self.opt == 0 else 0.0
-                with torch.cuda.stream(ps.stream):
-                    self.peer.apply(p, w, e, self.opt, ps.params, ps.m, ps.v, lr_t, ps.h.beta1,
-                                    ps.h.beta2, ps.h.eps, ps.h.lr, ps.momentum, self.grad_scale)
+                with ps.lock:  # paused(): no apply while a checkpoint snapshot is taken
+                    ps.begin()
+                    lr_t = adam_coeffs(ps.h, ps.t) if self.opt == 0 else 0.0
+                    with torch.cuda.stream(ps.stream):
+                        self.peer.apply(p, w, e, self.opt, ps.params, ps.m, ps.v, lr_t,
+                                        ps.h.beta1, ps.h.beta2, ps.h.eps, ps.h.lr,
+                                        ps.momentum if self.mu is None else self.mu,
+                                        self.grad_scale)
+                    t = ps.t
                 if self.check_provenance:
-                    self.provenance.append((w, p, e - 2, ps.t))
+                    self.provenance.append((w, p, e - 2, t))
                 self.served += 1
                 if self.peer.error():
                     raise RuntimeError(f"async xGMI wait timed out (code {self.peer.error()})")
@@ -224,16 +230,41 @@ class AsyncPeerExchange:
         except BaseException as e:  # surfaced by join()
             self._error = e
 
+    def _sync_counters(self, svc) -> None:
+        """The native service advances each hosted PS's step counter; mirror it into the
+        Python ParameterServer objects (checkpoints and reports read those)."""
+        for p, ps in self.servers.items():
+            n = svc.t(p) - ps.t
+            ps.t += n
+            ps.updates += n
+
+    @contextlib.contextmanager
+    def paused(self):
+        """Checkpoint hook: no PS update is issued inside the block and every issued one has
+        completed, so each hosted PS's parameters, m, v and t are one consistent step."""
+        svc = self._svc
+        if svc is not None:
+            svc.pause()
+            try:
+                self._sync_counters(svc)
+                yield
+            finally:
+                svc.resume()
+            return
+        with contextlib.ExitStack() as held:
+            for ps in self.servers.values():
+                held.enter_context(ps.lock)
+                if ps._stream is not None:
+                    ps.stream.synchronize()
+            yield
+
     def join(self) -> None:
         if self._svc is not None:
             svc, self._svc = self._svc, None
             try:
                 svc.join()
             finally:
-                for p, ps in self.servers.items():
-                    n = svc.t(p) - ps.t
-                    ps.t += n
-                    ps.updates += n
+                self._sync_counters(svc)
                 self.served = svc.served()
                 if self.check_provenance:
                     self.provenance = [(w, p, e - 2, t) for (w, p, e, t) in svc.provenance()]

@@ -63,16 +63,26 @@ def init_distributed(device: str = "auto") -> DistEnv:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = (device == "cuda") or (device == "auto" and torch.cuda.is_available())
+    backend = None
+    if world > 1:
+        backend = os.environ.get("DDL_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     if use_gpu:
         ndev = torch.cuda.device_count()
-        local_dev = local % ndev if ndev > 0 else local
+        if backend == "gloo" and ndev > 0:
+            local_dev = local % ndev  # several ranks per GPU: the one-box rehearsal only
+        elif local >= ndev:
+            # RCCL refuses two ranks of one communicator on one device: fail here, clearly,
+            # instead of with a late RCCL error or hang
+            raise RuntimeError(f"LOCAL_RANK {local} but only {ndev} GPU(s) visible: start one "
+                               f"process per GPU (or DDL_DIST_BACKEND=gloo for the shared-GPU "
+                               f"rehearsal)")
+        else:
+            local_dev = local
         torch.cuda.set_device(local_dev)
         dev = torch.device("cuda", local_dev)
     else:
         dev = torch.device("cpu")
-    backend = None
     if world > 1:
-        backend = os.environ.get("DDL_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         if not dist.is_initialized():
             kw = {}
             if use_gpu and backend == "nccl":
@@ -412,6 +422,18 @@ class AsyncExchange:
             ts = [t for (_, pp, _, t) in self.provenance if pp == p]
             if ts != sorted(ts) or len(set(ts)) != len(ts):
                 raise RuntimeError(f"provenance: PS {p} step counter not strictly increasing")
+
+    @contextlib.contextmanager
+    def paused(self):
+        """Checkpoint hook: the service thread updates a PS only under its lock (on its
+        stream), so holding every hosted PS's lock with its stream drained is a consistent
+        snapshot of parameters, m, v and t."""
+        with contextlib.ExitStack() as held:
+            for ps in self.servers.values():
+                held.enter_context(ps.lock)
+                if ps._stream is not None:
+                    ps.stream.synchronize()
+            yield
 
     def join(self) -> None:
         if self._thread is not None:

@@ -25,9 +25,11 @@ def main(argv=None, mode_default: str = "sync") -> dict:
     from .comm import init_distributed
     from .roles import Trainer
     env = init_distributed()
-    if a.np_compat is not None and cfg.num_ps is None and cfg.shard != "none" and mode_default != "single":
-        # `parameter_server.py -np P` / `worker.py -np W`: the PS count is what matters here
-        pass
+    if a.np_compat is not None and a.np_compat != env.world and env.rank == 0:
+        # `worker.py -np W` (reference mnist_sync_sharding/worker.py:65): the worker count is
+        # the launcher's process count here (parameter_server.py maps its -np to --num-ps)
+        print(f"[ddl_amd] -np {a.np_compat} ignored: {env.world} worker process(es) were "
+              f"launched (run.sh <num_ps> <num_workers> sets both)", file=sys.stderr)
     tr = Trainer(cfg, env)
     summary = tr.train()
     if a.summary_json and env.rank == 0:

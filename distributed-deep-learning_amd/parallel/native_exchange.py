@@ -53,8 +53,11 @@ class NativeSyncExchange(SyncExchange):
                  grad_reduce: str = "sum", ref_quirks: bool = False, overlap: bool = True,
                  optimizer: str = "adam", hyper=None, momentum: float = 0.9,
                  force_collectives: bool = False, backend: str = "rccl"):
-        if optimizer not in ("adam", "momentum"):
+        if optimizer not in ("adam", "momentum", "sgd"):
             raise NativeUnavailable(f"native runner has no '{optimizer}' update")
+        if optimizer == "sgd":
+            # plain SGD = the fused momentum kernel with mu = 0 (m holds the last gradient)
+            momentum = 0.0
         if not params.is_cuda or getattr(engine, "name", "") != "hip":
             raise NativeUnavailable("native runner needs the HIP engine on a GPU")
         if len(segments) != 4:
@@ -241,7 +244,7 @@ class NativeSyncExchange(SyncExchange):
 
 
 def make_sync_exchange(plan, env, params, grads, segments, servers, engine, cfg, hyper):
-    """Native runner when it applies (HIP engine, sync, adam/momentum), else the Python
+    """Native runner when it applies (HIP engine, sync, adam/momentum/sgd), else the Python
     exchange.  On a multi-GPU job the choice is collective (self-test votes)."""
     if cfg.native_exchange:
         try:

@@ -107,7 +107,11 @@ class ParameterServer:
                 m.mul_(self.momentum).add_(g, alpha=grad_scale)
                 w.sub_(self.h.lr * m)
         elif self.optimizer == "sgd":
-            w.sub_(g, alpha=self.h.lr * grad_scale)
+            if w.is_cuda and self.native_optim:
+                # the fused momentum kernel with mu = 0: w -= lr * (g * scale)
+                native.ops().momentum_flat(w, g, m, self.h.lr, 0.0, grad_scale)
+            else:
+                w.sub_(g * grad_scale if grad_scale != 1.0 else g, alpha=self.h.lr)
         else:
             raise ValueError(self.optimizer)
 

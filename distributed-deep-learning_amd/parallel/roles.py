@@ -37,6 +37,18 @@ from .ps import ParameterServer
 from .sharding import make_plan
 
 
+def _job_id(env: DistEnv) -> str:
+    """Name prefix of this job's POSIX shm segments (mailboxes, completion counters): unique
+    per job on the host.  Rank 0 draws a nonce and broadcasts it, so two jobs with the same
+    MASTER_PORT (or none, at W = 1) never share (or unlink) each other's segments."""
+    import os
+    import secrets
+    nonce = [f"{os.getpid():x}{secrets.token_hex(4)}"]
+    if env.world > 1:
+        dist.broadcast_object_list(nonce, src=0)
+    return f"ddl{nonce[0]}"
+
+
 def resolve_num_ps(cfg: TrainConfig, world: int) -> int:
     if cfg.mode == "single" or cfg.shard == "none":
         return 1
@@ -106,13 +118,11 @@ class Trainer:
             cfg.exchange_backend == "auto" and env.world > 1 and self.engine.name == "hip")
         if want and env.device.type == "cuda":
             from .async_xgmi import AsyncPeerExchange, AsyncPeerUnavailable
-            import os
             try:
                 return AsyncPeerExchange(self.plan, env, self.params, self.grads, self.servers,
                                          steps_per_worker=steps, grad_reduce=cfg.grad_reduce,
                                          check_provenance=cfg.check_provenance,
-                                         optimizer=cfg.optimizer,
-                                         job_id=f"ddl{os.environ.get('MASTER_PORT', '')}")
+                                         optimizer=cfg.optimizer, job_id=_job_id(env))
             except AsyncPeerUnavailable as e:
                 if env.rank == 0:
                     import sys
@@ -120,7 +130,7 @@ class Trainer:
                           file=sys.stderr)
         return AsyncExchange(self.plan, env, self.params, self.grads, self.servers,
                              steps_per_worker=steps, grad_reduce=cfg.grad_reduce,
-                             check_provenance=cfg.check_provenance)
+                             check_provenance=cfg.check_provenance, job_id=_job_id(env))
 
     # ---- one worker step (reference SyncWorker.work + pull + assign) -----------------------------
     def batch(self, step: int):
@@ -258,10 +268,12 @@ class Trainer:
             self.exchange.join()
             if cfg.check_provenance:
                 self.exchange.verify_provenance()
-        if getattr(self.exchange, "native", False) and env.world > 1:
-            self.exchange.check()
+        # drain first: the last steps' exchange kernels may still be running, and a bounded
+        # xGMI wait that times out records its error only when it gives up
         if env.device.type == "cuda":
             torch.cuda.synchronize()
+        if getattr(self.exchange, "native", False) and env.world > 1:
+            self.exchange.check()
         if env.world > 1:
             dist.barrier()
         cpu_t, wall_t = clock.cpu(), clock.wall()

@@ -45,34 +45,35 @@ def _name(i: int, a: int, b: int, n: int) -> str:
 
 
 def save(trainer, path: str) -> None:
+    import contextlib
     import torch.distributed as dist
     os.makedirs(path, exist_ok=True)
     env, plan = trainer.env, trainer.plan
     asyncm = trainer.cfg.mode == "async"
+    ex = trainer.exchange
+    if trainer.params.is_cuda:
+        # every queued step (and its exchange kernels) must have finished, and must not have
+        # failed: a checkpoint of parameters a timed-out exchange left half-updated is refused
+        torch.cuda.synchronize(trainer.params.device)
+    if getattr(ex, "native", False) and hasattr(ex, "check"):
+        ex.check()
+    # async: the PS service keeps applying other workers' pushes.  Snapshot the hosted PS
+    # state (parameters, m, v and the step counter t) with the service paused, so it is one
+    # consistent PS step; the pause ends before any collective below (a peer may be waiting
+    # for this PS to serve its push before it reaches its own checkpoint).
+    pause = getattr(ex, "paused", None)
+    with (pause() if pause is not None else contextlib.nullcontext()):
+        snaps = {p: _ps_snapshot(trainer, plan, ps) for p, ps in trainer.servers.items()}
     if asyncm or env.rank == 0:
         w = {}
         for t in TENSORS:
             o = plan.tensor_offsets[t.index]
             w[f"mnist/v{t.index}"] = trainer.params[o:o + t.numel].detach().view(t.shape).cpu().contiguous()
         save_file(w, os.path.join(path, f"worker{env.rank}.safetensors"))
-    for p, ps in trainer.servers.items():
-        d: Dict[str, torch.Tensor] = {}
-        for (lo, hi), off in zip(ps.segments, ps.seg_off):
-            for i, a, b, po in _pieces(plan, lo, hi):
-                n = TENSORS[i].numel
-                base = _name(i, a, b, n)
-                s0 = off + (po - lo)
-                src = ps.params[s0:s0 + (b - a)] if ps.params is not None else trainer.params[po:po + (b - a)]
-                d[base] = src.detach().cpu().contiguous()
-                d[base + "/Adam"] = ps.m[s0:s0 + (b - a)].detach().cpu().contiguous()
-                if ps.v is not None:
-                    d[base + "/Adam_1"] = ps.v[s0:s0 + (b - a)].detach().cpu().contiguous()
-        b1, b2 = ps.h.beta1 ** ps.t, ps.h.beta2 ** ps.t
-        d["ParameterServer/beta1_power"] = torch.tensor([b1], dtype=torch.float32)
-        d["ParameterServer/beta2_power"] = torch.tensor([b2], dtype=torch.float32)
+    for p, (d, _) in snaps.items():
         save_file(d, os.path.join(path, f"ps{p}.safetensors"))
     # every PS's own step counter (PSes are hosted by different ranks)
-    local_t = {p: s.t for p, s in trainer.servers.items()}
+    local_t = {p: t for p, (_, t) in snaps.items()}
     all_t = [local_t]
     if env.world > 1:
         all_t = [None] * env.world
@@ -87,6 +88,25 @@ def save(trainer, path: str) -> None:
             json.dump(man, f, indent=1)
     if env.world > 1:
         dist.barrier()
+
+
+def _ps_snapshot(trainer, plan, ps) -> Tuple[Dict[str, torch.Tensor], int]:
+    """Host copies of one PS's tensors under the reference's names, and its step counter."""
+    d: Dict[str, torch.Tensor] = {}
+    for (lo, hi), off in zip(ps.segments, ps.seg_off):
+        for i, a, b, po in _pieces(plan, lo, hi):
+            n = TENSORS[i].numel
+            base = _name(i, a, b, n)
+            s0 = off + (po - lo)
+            src = ps.params[s0:s0 + (b - a)] if ps.params is not None else trainer.params[po:po + (b - a)]
+            d[base] = src.detach().cpu().contiguous()
+            d[base + "/Adam"] = ps.m[s0:s0 + (b - a)].detach().cpu().contiguous()
+            if ps.v is not None:
+                d[base + "/Adam_1"] = ps.v[s0:s0 + (b - a)].detach().cpu().contiguous()
+    b1, b2 = ps.h.beta1 ** ps.t, ps.h.beta2 ** ps.t
+    d["ParameterServer/beta1_power"] = torch.tensor([b1], dtype=torch.float32)
+    d["ParameterServer/beta2_power"] = torch.tensor([b2], dtype=torch.float32)
+    return d, ps.t
 
 
 def _stitch(path: str, num_ps: int) -> Tuple[Dict[int, Dict[str, torch.Tensor]], List[float]]:

@@ -72,14 +72,37 @@ def simulate_sync(cfg_kw, world, n_train=600):
     num_ps = 1 if cfg.shard == "none" else (cfg.num_ps or world)
     plan = make_plan(cfg.shard, num_ps)
     steps = cfg.steps * cfg.epochs
+    worker_init = None
+    if cfg.ref_quirks and world > 1:
+        # Q4: every process initialises independently (seed + rank).  A sync PS updates its
+        # host's buffer in place, so the PS state starts as each tensor's host's init, while
+        # the step-0 gradients are computed by every worker at its OWN init
+        # (mnist_sync/parameter_server.py:17-18,31; mnist_sync/model/model.py:112).
+        from ddl_amd.models.layout import TENSORS
+        if not plan.tensor_granular:
+            raise NotImplementedError("quirk simulation covers the tensor-granular plans")
+        worker_init = []
+        for r in range(world):
+            p_r = torch.zeros(TOTAL_NUMEL)
+            init_params_(p_r, CANON_OFFSETS, cfg.seed + r)
+            worker_init.append(p_r)
+        for t in TENSORS:
+            host = plan.host_rank(plan.owner[t.index], world)
+            o = CANON_OFFSETS[t.index]
+            params[o:o + t.numel] = worker_init[host][o:o + t.numel]
     for step in range(steps):
         acc.zero_()
+        ps_params = params.clone() if (worker_init is not None and step == 0) else None
         for r in range(world):
+            if ps_params is not None:
+                params.copy_(worker_init[r])
             lo, hi = batch_indices(step % cfg.steps, cfg.batch_size, data.total_batch, r, world,
                                    cfg.data_sharding)
             eng.forward_backward(data.x_train[lo:hi], data.y_train[lo:hi], cfg.keep_prob,
                                  rng.step_seed(cfg.seed, r, step))
             acc.add_(grads, alpha=quirk_coefficient(plan, r, world, cfg.ref_quirks))
+        if ps_params is not None:
+            params.copy_(ps_params)
         if cfg.grad_reduce == "mean":
             acc.div_(world)
         adam_torch_(params, acc, m, v, h, step + 1)

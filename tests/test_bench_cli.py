@@ -43,6 +43,8 @@ def test_bench_single_process_json():
     assert rec["value"] > 0 and rec["higher_is_better"] is True and rec["scaling"] == "weak"
     assert rec["config"]["global_batch"] == 100
     assert rec["config"]["parallelism"] == "dp1-ps1-sync-flat"
+    assert rec["config"]["variant"] == "mnist_sync_sharding (flat plan)"
+    assert rec["prewarm"]["steps"] == 0  # CPU default; 100 untimed steps on a GPU
 
 
 @pytest.mark.slow
@@ -58,8 +60,13 @@ def test_bench_torchrun_two_ranks_json(port):
     assert KEYS <= rec.keys()
     assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 200
     assert rec["config"]["parallelism"] == "dp2-ps2-sync-flat"
+    assert rec["config"]["plan"] == "flat"
     # whole-job aggregate: images/s = W * batch * steps / max-over-ranks time
     assert rec["value"] == pytest.approx(2 * 100 / (rec["ms_per_step"] / 1e3), rel=1e-3)
+    # the reference's contiguous plan (BASELINE config 3) is timed on the same harness
+    c = rec["plans"]["contiguous"]
+    assert c["num_ps"] == 2 and c["ms_per_step"] > 0
+    assert c["value"] == pytest.approx(2 * 100 / (c["ms_per_step"] / 1e3), rel=1e-3)
 
 
 @pytest.mark.slow

@@ -54,16 +54,61 @@ def test_sync_matches_single_process_simulation(tmp_path, world, kw):
         assert torch.equal(_canon(rec), _canon(recs[0]))
 
 
-@pytest.mark.parametrize("world,shard", [(3, "contiguous"), (2, "none")])
+@pytest.mark.parametrize("world,shard", [(3, "contiguous"), (2, "none"), (3, "greedy")])
 def test_reference_quirks_reproduced(tmp_path, world, shard):
-    # keep_prob=1 + replicated data: every worker's gradient is identical, so the quirks
-    # scale it by 2**(W-1) (Q2) or (W+1) (Q1); seeds differ per rank in quirk mode (Q4),
-    # so compare against a simulation with the quirk coefficients, init seed 0 on rank 0.
-    recs, cfg = _run(tmp_path, world, shard=shard, ref_quirks=True, keep_prob=1.0)
-    # Q4 (independent init) makes ranks start differently; after the first pull all
-    # workers hold the PS parameters, which are identical across ranks.
+    """--ref-quirks: Q1 (the single sync PS adds worker 1's buffer to itself: 2 g_1 + g_2 + ...),
+    Q2 (the sharded sync PS aliases one receive buffer: g_last * 2**(W-1)) and Q4 (independent
+    init per process; the PS starts from its host's init, step-0 gradients from each worker's
+    own) against the single-process simulation of exactly that math."""
+    recs, cfg = _run(tmp_path, world, shard=shard, ref_quirks=True)
+    ref = simulate_sync(cfg, world)
+    for r, rec in enumerate(recs):
+        got = _canon(rec)
+        assert torch.allclose(got, ref, atol=2e-5, rtol=0), (r, float((got - ref).abs().max()))
+    # after the first pull every worker holds the PS parameters
     for rec in recs[1:]:
         assert torch.equal(_canon(rec), _canon(recs[0]))
+
+
+# ---- W = 8: every reference variant at the size of BASELINE configs 3-5 (8 workers) --------
+W8 = dict(steps=2, batch_size=10)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(shard="none"),                            # mnist_sync (1 PS on rank 0, 8 workers)
+    dict(shard="contiguous"),                      # mnist_sync_sharding, P = 8 (4.76x imbalance)
+    dict(shard="greedy"),                          # mnist_sync_sharding_greedy, P = 8
+    dict(shard="flat", data_sharding="stride"),    # the bench plan: RS / AG per bucket
+    dict(shard="contiguous", num_ps=3),            # run.sh 3 8: fewer PS than workers
+    dict(shard="contiguous", num_ps=11),           # run.sh 11 8: PS 8..10 on ranks 0..2
+])
+def test_sync_w8_matches_simulation(tmp_path, kw):
+    recs, cfg = _run(tmp_path, 8, **W8, **kw)
+    ref = simulate_sync(cfg, 8)
+    for r, rec in enumerate(recs):
+        got = _canon(rec)
+        assert torch.allclose(got, ref, atol=2e-5, rtol=0), (r, float((got - ref).abs().max()))
+    for rec in recs[1:]:
+        assert torch.equal(_canon(rec), _canon(recs[0]))
+
+
+@pytest.mark.parametrize("kw", [dict(shard="contiguous"), dict(shard="greedy"),
+                                dict(shard="none")])
+def test_async_w8_provenance(tmp_path, kw):
+    """mnist_async_sharding / _greedy / mnist_async at W = 8: every push served once, in
+    order, with its bytes checksummed at the PS; each PS counts W x steps updates."""
+    recs, cfg = _run(tmp_path, 8, mode="async", check_provenance=True, **W8, **kw)
+    from ddl_amd.parallel.sharding import make_plan
+    num_ps = 1 if kw["shard"] == "none" else 8
+    plan = make_plan(kw["shard"], num_ps)
+    ps_t = {}
+    for r, rec in enumerate(recs):
+        ps_t.update(rec["ps_t"])
+        hosted = sum(1 for p in range(plan.num_ps) if plan.host_rank(p, 8) == r)
+        assert len(rec["provenance"]) == hosted * 7 * cfg["steps"]
+        assert torch.isfinite(rec["params"]).all()
+    assert sorted(ps_t) == list(range(num_ps))
+    assert all(t == 8 * cfg["steps"] for t in ps_t.values()), ps_t
 
 
 @pytest.mark.parametrize("world,shard", [(3, "greedy"), (2, "none"), (3, "contiguous")])
