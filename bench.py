@@ -247,7 +247,8 @@ def main(argv=None):
     def timed_run(t):
         """prewarm + warmup (untimed), then exactly a.steps steps between barrier+sync pairs;
         returns the max-over-ranks seconds of the timed window."""
-        if a.mode == "async":
+        asyncx = a.mode == "async" and not getattr(t, "async_as_sync", False)
+        if asyncx:
             t.exchange.steps = total_steps
             t.exchange.start()
         for i in range(n_pre + a.warmup):
@@ -256,7 +257,7 @@ def main(argv=None):
         t0 = time.perf_counter()
         for i in range(n_pre + a.warmup, total_steps):
             t.train_step(i)
-        if a.mode == "async":
+        if asyncx:
             t.exchange.join()
         sync()
         return max_over_ranks(time.perf_counter() - t0)

@@ -255,7 +255,7 @@ class PyEngine {
 class PyPeer {
  public:
   PyPeer(at::Tensor params, at::Tensor grads, int64_t world, int64_t rank, py::list buckets,
-         int64_t max_slices)
+         int64_t max_slices, int64_t repl_bucket)
       : params_(params), grads_(grads) {
     check_f32_cuda(params, "params");
     check_f32_cuda(grads, "grads");
@@ -268,7 +268,7 @@ class PyPeer {
     c10::hip::HIPGuard guard(params.device().index());
     p_ = std::make_unique<ddl::PeerExchange>(params.data_ptr<float>(), grads.data_ptr<float>(),
                                              params.numel(), (int)world, (int)rank, bk,
-                                             (int)max_slices);
+                                             (int)max_slices, (int)repl_bucket);
   }
   py::bytes handle() const {
     c10::hip::HIPGuard guard(params_.device().index());
@@ -405,6 +405,40 @@ class PyAsyncService {
   std::unique_ptr<ddl::AsyncService> svc_;
 };
 
+// native async worker step (kernels/async_runner.hip)
+class PyAsyncRunner {
+ public:
+  PyAsyncRunner(PyEngine& eng, PyAsyncPeer& peer, int64_t world, int64_t rank,
+                std::vector<int64_t> seg_of_ps, std::vector<int64_t> hosts,
+                std::vector<std::string> boxes, int64_t epoch0)
+      : eng_(eng) {
+    std::vector<int> seg(seg_of_ps.begin(), seg_of_ps.end()), h(hosts.begin(), hosts.end());
+    c10::hip::HIPGuard guard(peer.device());
+    r_ = std::make_unique<ddl::AsyncRunner>(eng.raw(), peer.raw(), (int)world, (int)rank,
+                                            peer.device(), seg, h, boxes, (uint32_t)epoch0);
+  }
+  void step(at::Tensor x, at::Tensor labels, int64_t seed, double timeout_s) {
+    eng_.check_batch(x);
+    TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_cuda(), "labels must be int64 GPU");
+    TORCH_CHECK(labels.numel() == x.size(0), "labels/batch size mismatch");
+    const float* xp = x.data_ptr<float>();
+    const int64_t* lp = labels.data_ptr<int64_t>();
+    const int B = (int)x.size(0);
+    hipStream_t st = cur_stream();
+    py::gil_scoped_release nogil;  // the host wait for the previous round
+    r_->step(xp, lp, B, (uint32_t)(seed & 0xFFFFFFFF), st, timeout_s);
+  }
+  void finish(double timeout_s) {
+    py::gil_scoped_release nogil;
+    r_->finish(timeout_s);
+  }
+  int64_t epoch() const { return r_->epoch(); }
+
+ private:
+  PyEngine& eng_;
+  std::unique_ptr<ddl::AsyncRunner> r_;
+};
+
 class PyRunner {
  public:
   PyRunner(PyEngine& eng, at::Tensor params, at::Tensor grads, int64_t world, int64_t rank)
@@ -466,7 +500,8 @@ class PyRunner {
         ddl::RunnerRange range{rr[0].cast<int64_t>(), rr[1].cast<int64_t>(), rr[2].cast<int64_t>()};
         TORCH_CHECK(0 <= range.lo && range.lo <= range.hi && range.hi <= n, "range out of bounds");
         int64_t len = range.hi - range.lo;
-        if (u.kind == ddl::RunnerUnit::RS || u.kind == ddl::RunnerUnit::XGMI) {
+        if (u.kind == ddl::RunnerUnit::RS || u.kind == ddl::RunnerUnit::XGMI) {  // (AR and
+          // XGMI_REPL update the whole range on every rank: state for all of it)
           // reduce-scatter: this rank updates (and needs state / a shard buffer for) 1/W of it;
           // a remainder would silently get no exchange and no update
           TORCH_CHECK(len % world_ == 0, "RS unit range [", range.lo, ", ", range.hi,
@@ -627,10 +662,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("served", &PyAsyncService::served)
       .def("provenance", &PyAsyncService::provenance);
 
+  py::class_<PyAsyncRunner>(m, "AsyncRunner")
+      .def(py::init<PyEngine&, PyAsyncPeer&, int64_t, int64_t, std::vector<int64_t>,
+                    std::vector<int64_t>, std::vector<std::string>, int64_t>(),
+           py::arg("engine"), py::arg("peer"), py::arg("world"), py::arg("rank"),
+           py::arg("seg_of_ps"), py::arg("hosts"), py::arg("boxes"), py::arg("epoch0"),
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
+      .def("step", &PyAsyncRunner::step)
+      .def("finish", &PyAsyncRunner::finish)
+      .def("epoch", &PyAsyncRunner::epoch);
+
   py::class_<PyPeer>(m, "PeerExchange")
-      .def(py::init<at::Tensor, at::Tensor, int64_t, int64_t, py::list, int64_t>(),
+      .def(py::init<at::Tensor, at::Tensor, int64_t, int64_t, py::list, int64_t, int64_t>(),
            py::arg("params"), py::arg("grads"), py::arg("world"), py::arg("rank"),
-           py::arg("buckets"), py::arg("max_slices") = 128)
+           py::arg("buckets"), py::arg("max_slices") = 128, py::arg("repl_bucket") = -1)
       .def("handle", &PyPeer::handle)
       .def("open", &PyPeer::open)
       .def("error", &PyPeer::error)

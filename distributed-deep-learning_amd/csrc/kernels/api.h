@@ -8,6 +8,9 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -158,7 +161,8 @@ struct RunnerRange {
   int64_t state_off;    // offset of the range's optimizer state in the unit's m / v
 };
 struct RunnerUnit {
-  enum Kind { LOCAL = 0, RS = 1, REDUCE = 2, XGMI = 3 };
+  // AR: all-reduce + update on replicated state (the last bucket); XGMI_REPL: its xGMI form
+  enum Kind { LOCAL = 0, RS = 1, REDUCE = 2, XGMI = 3, AR = 4, XGMI_REPL = 5 };
   int seg = 0;          // backward segment after which the unit's gradients are complete
   int kind = LOCAL;
   int host = 0;         // REDUCE: rank that owns the PS
@@ -190,6 +194,8 @@ struct XgmiLaunch {              // one bucket's kernel arguments
   float lr_t, c1, c2, eps, lr, mu, scale, coef;
   int* err;
   long long timeout_ticks;
+  int check;                     // DDL_XGMI_CHECK: per-(bucket, source, slice) inbox checksums
+  int repl_bucket;               // the replicated bucket (-1: none)
 };
 struct XgmiUpdate {              // owner-side update of one bucket chunk
   int opt = 0;                   // 0 Adam (TF1), 1 momentum, 2 self-test (w := summed g)
@@ -203,8 +209,11 @@ class PeerExchange {
  public:
   // buckets: [lo, hi) ranges of the flat plan buffer, each divisible by 4 * world; rank r owns
   // chunk r of every bucket.  Allocates the inbox (one slot per source rank) and the flags.
+  // repl_bucket >= 0: that bucket is exchanged all-to-all and updated on every rank with
+  // replicated optimizer state (xgmi_repl_kernel), instead of by its chunk owners
   PeerExchange(float* params, const float* grads, int64_t total, int world, int rank,
-               const std::vector<std::pair<int64_t, int64_t>>& buckets, int max_slices);
+               const std::vector<std::pair<int64_t, int64_t>>& buckets, int max_slices,
+               int repl_bucket = -1);
   ~PeerExchange();
   std::string handle() const;                         // this rank's IPC handles, as bytes
   void open(const std::vector<std::string>& handles);  // every rank's, in rank order
@@ -215,9 +224,12 @@ class PeerExchange {
   int nslices(int b) const { return bk_[b].nslice; }
   int64_t chunk(int b) const { return bk_[b].c; }
   int world() const { return world_; }
+  int repl_bucket() const { return repl_; }
 
  private:
   struct Bucket { int64_t lo, c, inbox_off, slice; int nslice; };
+  int repl_ = -1;
+  bool check_ = false;
   float* params_;
   const float* grads_;
   int64_t total_;
@@ -259,6 +271,8 @@ class AsyncPeer {
   void open(const std::vector<std::string>& handles);
   // worker: every PS shard of the gradient (x coef) into its host's inbox slot, round `epoch`
   void push_all(uint32_t epoch, float coef, hipStream_t st);
+  // the same for the listed PS only (one launch)
+  void push_set(const std::vector<int>& ps, uint32_t epoch, float coef, hipStream_t st);
   // the DONE counters: a POSIX shm segment (created by one rank, attached by the others)
   // registered with HIP, so every GPU bumps them and every host polls them directly
   void attach_done(const std::string& name, bool create);
@@ -332,6 +346,52 @@ class AsyncService {
   std::thread th_;
   std::string error_;
   mutable std::mutex pause_mu_;  // held by the service thread while it issues an apply
+};
+
+class ShmMailbox;
+
+// Native asynchronous worker step over the xGMI data plane (async_runner.hip): wait for the
+// previous round's parameters (host), forward, backward with each PS's gradient push launched
+// after the segment that completes its range, tokens posted by a poster thread once each push
+// has completed.
+class AsyncRunner {
+ public:
+  static constexpr int kSegments = 4;
+  // seg_of_ps[p]: backward segment after which PS p's range is complete; hosts[p]: its host
+  // rank; boxes[r]: arrival mailbox name of rank r ("" if it hosts no PS); epoch0: the round
+  // already completed (the set-up self-test)
+  AsyncRunner(Engine* eng, AsyncPeer* peer, int world, int rank, int device,
+              const std::vector<int>& seg_of_ps, const std::vector<int>& hosts,
+              const std::vector<std::string>& boxes, uint32_t epoch0);
+  ~AsyncRunner();
+  void step(const float* x, const int64_t* labels, int B, uint32_t seed, hipStream_t st,
+            double timeout_s);
+  // the last round's parameters are back and every token has been posted
+  void finish(double timeout_s);
+  uint32_t epoch() const { return epoch_; }
+
+ private:
+  struct Posting {
+    hipEvent_t ev = nullptr;
+    std::vector<int> ps;
+  };
+  void post_loop();
+  void wait_round(double timeout_s);
+  Engine* eng_;
+  AsyncPeer* peer_;
+  int world_, rank_, device_;
+  uint32_t epoch_, epoch0_;
+  std::vector<int> seg_ps_[kSegments];
+  std::vector<int> hosts_;
+  std::unique_ptr<ShmMailbox> boxes_[kXgmiMaxPeers];
+  hipEvent_t ev_[kSegments] = {};
+  std::thread poster_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Posting> queue_;
+  int inflight_ = 0;
+  bool stop_ = false;
+  std::string error_;
 };
 
 class SyncRunner {

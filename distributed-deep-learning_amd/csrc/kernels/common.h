@@ -18,6 +18,13 @@ inline hipEvent_t& launch_stop_event() {
   static thread_local hipEvent_t ev = nullptr;
   return ev;
 }
+// RAII: the DDL_LAUNCHes inside the scope carry `ev` as their completion event
+struct StopEventScope {
+  explicit StopEventScope(hipEvent_t ev) { launch_stop_event() = ev; }
+  ~StopEventScope() { launch_stop_event() = nullptr; }
+  StopEventScope(const StopEventScope&) = delete;
+  StopEventScope& operator=(const StopEventScope&) = delete;
+};
 }  // namespace ddl
 
 #define DDL_LAUNCH(kernel, grid, block, shmem, stream, ...)                                     \
@@ -61,6 +68,14 @@ DDL_DEV void adam1(float& w, float g, float& m, float& v, float lr_t, float c1, 
   m += (g - m) * c1;
   v += (g * g - v) * c2;
   w -= lr_t * m / (sqrtf(v) + eps);
+}
+
+// Momentum SGD of one element (mu = 0: plain SGD).  The roundings are pinned (one product, one
+// fma each) so every kernel that applies it — the flat optimizer, the xGMI owner update, the
+// async PS apply — gives the same bits whatever the compiler's contraction choices.
+DDL_DEV void momentum1(float& w, float g, float& m, float lr, float mu, float scale) {
+  m = __fmaf_rn(m, mu, __fmul_rn(g, scale));
+  w = __fmaf_rn(-lr, m, w);
 }
 
 DDL_DEV float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }

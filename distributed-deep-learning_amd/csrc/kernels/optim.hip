@@ -55,9 +55,10 @@ momentum_kernel(float* __restrict__ w, const float* __restrict__ g, float* __res
                 int64_t n, float lr, float mu, float scale) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const float mm = m[i] * mu + g[i] * scale;
+    float ww = w[i], mm = m[i];
+    momentum1(ww, g[i], mm, lr, mu, scale);
     m[i] = mm;
-    w[i] -= lr * mm;
+    w[i] = ww;
   }
 }
 

@@ -18,8 +18,6 @@
 // torch.distributed), so the per-step host cost is a few launches instead of one Python
 // ProcessGroup call per collective — the Python exchange was host-bound (step timeline:
 // 20-45 us GPU idle at every segment boundary).
-#include <dlfcn.h>
-#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -29,72 +27,12 @@
 
 #include "api.h"
 #include "common.h"
+#include "rccl_api.h"
 #include "trace.h"
 
 namespace ddl {
 
-#define RCCL_CHECK(x)                                                                 \
-  do {                                                                                \
-    ncclResult_t r_ = (x);                                                            \
-    if (r_ != ncclSuccess)                                                            \
-      throw std::runtime_error(std::string("RCCL: ") + #x + ": " + rccl().GetErrorString(r_)); \
-  } while (0)
-#define HIP_CHECK(x)                                                                  \
-  do {                                                                                \
-    hipError_t e_ = (x);                                                              \
-    if (e_ != hipSuccess)                                                             \
-      throw std::runtime_error(std::string("HIP: ") + #x + ": " + hipGetErrorString(e_)); \
-  } while (0)
-
 static ncclComm_t as_comm(void* c) { return reinterpret_cast<ncclComm_t>(c); }
-
-// RCCL entry points resolved from the librccl instance torch already loaded (torch's
-// ProcessGroupNCCL and this runner must share ONE RCCL: a second copy from /opt/rocm would
-// run its own proxy threads / shm / device state).  Declarations come from the header; the
-// NCCL API of these calls is identical across the 2.26 (torch) / 2.27 (ROCm 7.2) builds.
-struct RcclApi {
-  decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
-  decltype(&ncclCommInitRank) CommInitRank = nullptr;
-  decltype(&ncclCommDestroy) CommDestroy = nullptr;
-  decltype(&ncclGetErrorString) GetErrorString = nullptr;
-  decltype(&ncclReduceScatter) ReduceScatter = nullptr;
-  decltype(&ncclAllGather) AllGather = nullptr;
-  decltype(&ncclReduce) Reduce = nullptr;
-  decltype(&ncclBroadcast) Broadcast = nullptr;
-  decltype(&ncclGroupStart) GroupStart = nullptr;
-  decltype(&ncclGroupEnd) GroupEnd = nullptr;
-  decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;
-  decltype(&ncclCommAbort) CommAbort = nullptr;
-};
-
-static const RcclApi& rccl() {
-  static RcclApi api = [] {
-    RcclApi a;
-    void* h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
-    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) throw std::runtime_error(std::string("cannot locate librccl: ") + dlerror());
-    auto sym = [&](const char* n) {
-      void* f = dlsym(h, n);
-      if (!f) throw std::runtime_error(std::string("librccl lacks ") + n);
-      return f;
-    };
-    a.GetUniqueId = (decltype(a.GetUniqueId))sym("ncclGetUniqueId");
-    a.CommInitRank = (decltype(a.CommInitRank))sym("ncclCommInitRank");
-    a.CommDestroy = (decltype(a.CommDestroy))sym("ncclCommDestroy");
-    a.GetErrorString = (decltype(a.GetErrorString))sym("ncclGetErrorString");
-    a.ReduceScatter = (decltype(a.ReduceScatter))sym("ncclReduceScatter");
-    a.AllGather = (decltype(a.AllGather))sym("ncclAllGather");
-    a.Reduce = (decltype(a.Reduce))sym("ncclReduce");
-    a.Broadcast = (decltype(a.Broadcast))sym("ncclBroadcast");
-    a.GroupStart = (decltype(a.GroupStart))sym("ncclGroupStart");
-    a.GroupEnd = (decltype(a.GroupEnd))sym("ncclGroupEnd");
-    a.CommGetAsyncError = (decltype(a.CommGetAsyncError))sym("ncclCommGetAsyncError");
-    a.CommAbort = (decltype(a.CommAbort))sym("ncclCommAbort");
-    return a;
-  }();
-  return api;
-}
 
 SyncRunner::SyncRunner(Engine* eng, float* params, float* grads, int world, int rank)
     : eng_(eng), w_(params), g_(grads), world_(world), rank_(rank) {
@@ -165,16 +103,21 @@ void SyncRunner::init_comm(const char id_bytes[128], bool force) {
 void SyncRunner::set_units(const std::vector<RunnerUnit>& units) {
   for (const auto& u : units) {
     if (u.seg < 0 || u.seg >= kSegments) throw std::invalid_argument("unit segment out of range");
-    if (u.kind != RunnerUnit::LOCAL && u.kind != RunnerUnit::XGMI && !comm_)
+    const bool xg = u.kind == RunnerUnit::XGMI || u.kind == RunnerUnit::XGMI_REPL;
+    if (u.kind != RunnerUnit::LOCAL && !xg && !comm_)
       throw std::invalid_argument("collective unit without an RCCL communicator");
+    if (u.kind == RunnerUnit::AR && u.ranges.size() != 1)
+      throw std::invalid_argument("all-reduce unit needs exactly one range");
     if (u.kind == RunnerUnit::RS && (u.ranges.size() != 1 || !u.shard))
       throw std::invalid_argument("RS unit needs exactly one range and a shard buffer");
     if (u.kind == RunnerUnit::RS && (u.ranges[0].hi - u.ranges[0].lo) % world_ != 0)
       throw std::invalid_argument("RS unit range not divisible by the world size");
-    if (u.kind == RunnerUnit::XGMI) {
+    if (xg) {
       if (!peer_) throw std::invalid_argument("xGMI unit without a PeerExchange");
       if (u.bucket < 0 || u.bucket >= peer_->num_buckets())
         throw std::invalid_argument("xGMI unit bucket out of range");
+      if ((u.kind == RunnerUnit::XGMI_REPL) != (u.bucket == peer_->repl_bucket()))
+        throw std::invalid_argument("xGMI unit kind does not match the exchange's replicated bucket");
       if (opt_ == 0 && !u.v) throw std::invalid_argument("xGMI unit without Adam state");
     }
   }
@@ -185,7 +128,7 @@ void SyncRunner::set_units(const std::vector<RunnerUnit>& units) {
     for (const auto& u : units_)
       if (u.seg == sg && !(u.kind == RunnerUnit::LOCAL && local_on_main_)) {
         any = true;
-        only &= u.kind == RunnerUnit::XGMI;
+        only &= u.kind == RunnerUnit::XGMI || u.kind == RunnerUnit::XGMI_REPL;
       }
     seg_xgmi_only_[sg] = any && only;
     seg_offstream_[sg] = any;
@@ -193,7 +136,7 @@ void SyncRunner::set_units(const std::vector<RunnerUnit>& units) {
   // the step's last xGMI unit also waits until every owner's parameters have landed here
   last_xgmi_ = -1;
   for (size_t i = 0; i < units_.size(); ++i)
-    if (units_[i].kind == RunnerUnit::XGMI &&
+    if ((units_[i].kind == RunnerUnit::XGMI || units_[i].kind == RunnerUnit::XGMI_REPL) &&
         (last_xgmi_ < 0 || units_[i].seg >= units_[last_xgmi_].seg))
       last_xgmi_ = (int)i;
   // W = 1 (every unit LOCAL): one stream.  Ranges adjacent in both the parameter buffer and
@@ -298,6 +241,16 @@ void SyncRunner::issue(const RunnerUnit& u, const float* lr_t, hipStream_t st) {
       update(mine, u.shard, u.m + r.state_off, u.v ? u.v + r.state_off : nullptr, c, lt, st);
       RCCL_CHECK(rccl().AllGather(mine, w_ + r.lo, (size_t)c, ncclFloat32, as_comm(comm_), st));
     } break;
+    case RunnerUnit::AR: {
+      // the step's last bucket, replicated: ONE all-reduce, then every rank runs the update on
+      // its replicated optimizer state (one collective instead of reduce-scatter + all-gather
+      // on the exposed end of the step)
+      const auto& r = u.ranges[0];
+      const int64_t n = r.hi - r.lo;
+      RCCL_CHECK(rccl().AllReduce(g_ + r.lo, g_ + r.lo, (size_t)n, ncclFloat32, ncclSum,
+                                  as_comm(comm_), st));
+      update(w_ + r.lo, g_ + r.lo, u.m + r.state_off, u.v ? u.v + r.state_off : nullptr, n, lt, st);
+    } break;
     default:
       throw std::invalid_argument("unknown unit kind");
   }
@@ -331,12 +284,6 @@ void SyncRunner::issue_reduce_group(const std::vector<const RunnerUnit*>& us, co
                                   u->host, as_comm(comm_), st));
   RCCL_CHECK(rccl().GroupEnd());
 }
-
-// RAII: engine launches inside the scope carry `ev` as their completion event (common.h)
-struct StopEventScope {
-  explicit StopEventScope(hipEvent_t ev) { launch_stop_event() = ev; }
-  ~StopEventScope() { launch_stop_event() = nullptr; }
-};
 
 static const char* const kBwdRange[SyncRunner::kSegments] = {
     "ddl.bwd.seg0(head+fc)", "ddl.bwd.seg1(conv4)", "ddl.bwd.seg2(conv3)",
@@ -424,7 +371,7 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
         HIP_CHECK(hipStreamWaitEvent(cs_, ev, 0));
         waited = true;
       }
-      if (u.kind == RunnerUnit::XGMI) {
+      if (u.kind == RunnerUnit::XGMI || u.kind == RunnerUnit::XGMI_REPL) {
         // the final wait orders the next forward after every owner's pushes; only if it runs
         // on the comm stream does the compute stream need the end-of-exchange event
         const bool fin = (int)i == last_xgmi_;

@@ -107,6 +107,83 @@ DDL_DEV float4 scale4(float4 x, float a) {
   return x;
 }
 
+// ---- debug checksums (DDL_XGMI_CHECK=1, the sync analogue of async --check-provenance) ------
+// The pusher of slice j of bucket b stores, next to its ARRIVE word at the owner, the wrapping
+// sum of the 32-bit patterns of exactly the floats it pushed; the owner recomputes that sum over
+// what it reads from its inbox before it uses the slice and records error code 3 (and skips the
+// update) on a mismatch — a stale or torn inbox read is caught where it happens, per (bucket,
+// source, step), instead of as a parameter divergence steps later.
+DDL_DEV int ck_idx(int b, int src, int j) {
+  return 2 * kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices + arrive_idx(b, src, j);
+}
+DDL_DEV uint32_t bits4(float4 v) {
+  return __float_as_uint(v.x) + __float_as_uint(v.y) + __float_as_uint(v.z) + __float_as_uint(v.w);
+}
+// sum over the 256 threads of the workgroup (every thread gets it); red: 4 words of LDS
+DDL_DEV uint32_t block_sum(uint32_t v, uint32_t* red) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const uint32_t t = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return t;
+}
+
+// owner-side check of one source's piece [n4 float4 at byte offset off of `in`]: false (error
+// code 3 recorded) when it differs from the checksum the source published
+DDL_DEV bool check_piece(brsrc_t in, int off, int n4, const uint32_t* ck, int* err,
+                         uint32_t* red) {
+  uint32_t c = 0;
+  for (int i = threadIdx.x; i < n4; i += 256) c += bits4(ld4_sys(in, off + i * 16));
+  const uint32_t got = block_sum(c, red);
+  const uint32_t want = __hip_atomic_load(ck, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (got == want) return true;
+  if (threadIdx.x == 0) __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return false;
+}
+
+// The final wait of a step: every (bucket, owner, slice) DONE word of the step, except the
+// replicated bucket's (it has none), spread over all threads of the launch and polled at once.
+DDL_DEV void final_wait(const XgmiLaunch& a, const uint32_t* myflags, int W, long long deadline) {
+  int total = 0;
+  for (int bb = 0; bb < a.nbuckets; ++bb)
+    if (bb != a.repl_bucket) total += W * a.nslices[bb];
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < total; k += gridDim.x * 256) {
+    int bb = 0, x = k;
+    for (;;) {
+      const int nb = bb == a.repl_bucket ? 0 : W * a.nslices[bb];
+      if (x < nb) break;
+      x -= nb;
+      ++bb;
+    }
+    const int q = x / a.nslices[bb], jj = x - q * a.nslices[bb];
+    wait_ge(myflags + done_idx(bb, q, jj), a.epoch, deadline, a.err, 2);
+  }
+}
+
+// The owner-side optimizer update of one float4 (TF1 Adam, momentum, or the self-test's
+// w := g), shared by the owner kernel and the replicated kernel so both give the same bits.
+DDL_DEV void update4(const XgmiLaunch& a, float4& w, float4 g, float4* m4, float4* v4, int i) {
+  if (a.opt == 0) {  // TF1 Adam (optim.hip form)
+    float4 M = m4[i], V = v4[i];
+    adam1(w.x, g.x * a.scale, M.x, V.x, a.lr_t, a.c1, a.c2, a.eps);
+    adam1(w.y, g.y * a.scale, M.y, V.y, a.lr_t, a.c1, a.c2, a.eps);
+    adam1(w.z, g.z * a.scale, M.z, V.z, a.lr_t, a.c1, a.c2, a.eps);
+    adam1(w.w, g.w * a.scale, M.w, V.w, a.lr_t, a.c1, a.c2, a.eps);
+    m4[i] = M; v4[i] = V;
+  } else if (a.opt == 1) {  // momentum SGD (optim.hip momentum_kernel form)
+    float4 M = m4[i];
+    momentum1(w.x, g.x, M.x, a.lr, a.mu, a.scale);
+    momentum1(w.y, g.y, M.y, a.lr, a.mu, a.scale);
+    momentum1(w.z, g.z, M.z, a.lr, a.mu, a.scale);
+    momentum1(w.w, g.w, M.w, a.lr, a.mu, a.scale);
+    m4[i] = M;
+  } else {  // self-test: parameters := the summed gradient
+    w = g;
+  }
+}
+
 // WT = world size when instantiated for it (loops over ranks fully unrolled: all of an
 // element's remote loads / stores are in flight together), 0 = any world size.
 template <int WT>
@@ -119,10 +196,15 @@ __global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a)
   const int64_t s1 = s0 + a.slice < a.c ? s0 + a.slice : a.c;
   const int n4 = s0 < s1 ? (int)((s1 - s0) >> 2) : 0;
   uint32_t* myflags = T.flags[me];
+  __shared__ uint32_t red[4];
+  __shared__ int arrived;
 
   // ---- phase 1: push my gradient pieces to their owners.  Per element index every owner's
   // load is issued before the first store; workgroup j starts at a different owner so the
   // W-1 links carry traffic at once.
+  uint32_t cs[NQ - 1];
+#pragma unroll
+  for (int k = 0; k < NQ - 1; ++k) cs[k] = 0;
   for (int i = tid; i < n4; i += 256) {
     float4 x[NQ - 1];
 #pragma unroll
@@ -138,7 +220,21 @@ __global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a)
         const int r = (me + 1 + (k + j) % (W - 1)) % W;
         const brsrc_t dst = make_rsrc(T.inbox[r] + a.inbox_off + (int64_t)me * a.c + s0,
                                       (uint32_t)n4 * 16u);
-        st4_sys(dst, i * 16, a.coef != 1.f ? scale4(x[k], a.coef) : x[k]);
+        const float4 v = a.coef != 1.f ? scale4(x[k], a.coef) : x[k];
+        st4_sys(dst, i * 16, v);
+        if (a.check) cs[k] += bits4(v);
+      }
+    }
+  }
+  if (a.check) {  // publish each owner's checksum before the ARRIVE word (same drain covers it)
+#pragma unroll
+    for (int k = 0; k < NQ - 1; ++k) {
+      if (k < W - 1) {
+        const uint32_t t = block_sum(cs[k], red);
+        const int r = (me + 1 + (k + j) % (W - 1)) % W;
+        if (tid == 0)
+          __hip_atomic_store(T.flags[r] + ck_idx(b, me, j), t, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
   }
@@ -150,7 +246,6 @@ __global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a)
   // failed (timeout, or another workgroup's recorded error) the slice is NOT updated: summing a
   // stale inbox would advance m / v and push wrong parameters into every replica.  DONE is still
   // stored, so the peers do not wait out their own timeouts; the host raises on the error word.
-  __shared__ int arrived;
   if (tid == 0) arrived = 1;
   __syncthreads();
   if (tid < W && tid != me &&
@@ -158,10 +253,20 @@ __global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a)
     arrived = 0;  // benign race: every writer stores 0
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // keep the loads below the poll
+
+  const brsrc_t inbox = make_rsrc(T.inbox[me] + a.inbox_off, (uint32_t)(W * a.c * 4));
+  if (a.check && arrived) {
+    bool ok = true;
+    for (int q = 0; q < W; ++q)
+      if (q != me)
+        ok &= check_piece(inbox, (int)(((int64_t)q * a.c + s0) * 4), n4,
+                          myflags + ck_idx(b, q, j), a.err, red);
+    if (!ok && tid == 0) arrived = 0;
+    __syncthreads();
+  }
   const int n4u = arrived ? n4 : 0;
 
   const float4* own = reinterpret_cast<const float4*>(a.grads + a.lo + me * a.c + s0);
-  const brsrc_t inbox = make_rsrc(T.inbox[me] + a.inbox_off, (uint32_t)(W * a.c * 4));
   float4* m4 = reinterpret_cast<float4*>(a.m + s0);
   float4* v4 = a.v ? reinterpret_cast<float4*>(a.v + s0) : nullptr;
   float4* w4 = reinterpret_cast<float4*>(T.params[me] + a.lo + me * a.c + s0);
@@ -173,28 +278,11 @@ __global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a)
         x[q] = q == me ? (a.coef != 1.f ? scale4(own[i], a.coef) : own[i])
                        : ld4_sys(inbox, (int)(((int64_t)q * a.c + s0) * 4) + i * 16);
     float4 w = w4[i];
-    float4 M = f4zero(), V = f4zero();
-    if (a.opt == 0) { M = m4[i]; V = v4[i]; }
-    else if (a.opt == 1) M = m4[i];
     float4 g = f4zero();
 #pragma unroll
     for (int q = 0; q < NQ; ++q)  // rank order: the same sum on every run and every rank count
       if (q < W) { g.x += x[q].x; g.y += x[q].y; g.z += x[q].z; g.w += x[q].w; }
-    if (a.opt == 0) {  // TF1 Adam (optim.hip form)
-      adam1(w.x, g.x * a.scale, M.x, V.x, a.lr_t, a.c1, a.c2, a.eps);
-      adam1(w.y, g.y * a.scale, M.y, V.y, a.lr_t, a.c1, a.c2, a.eps);
-      adam1(w.z, g.z * a.scale, M.z, V.z, a.lr_t, a.c1, a.c2, a.eps);
-      adam1(w.w, g.w * a.scale, M.w, V.w, a.lr_t, a.c1, a.c2, a.eps);
-      m4[i] = M; v4[i] = V;
-    } else if (a.opt == 1) {  // momentum SGD (optim.hip momentum_kernel form)
-      M.x = M.x * a.mu + g.x * a.scale; w.x -= a.lr * M.x;
-      M.y = M.y * a.mu + g.y * a.scale; w.y -= a.lr * M.y;
-      M.z = M.z * a.mu + g.z * a.scale; w.z -= a.lr * M.z;
-      M.w = M.w * a.mu + g.w * a.scale; w.w -= a.lr * M.w;
-      m4[i] = M;
-    } else {  // self-test: parameters := the summed gradient
-      w = g;
-    }
+    update4(a, w, g, m4, v4, i);
     // every rank's copy, this one included: write-through, so a later kernel of any rank
     // (other XCD, other GPU) reads it from memory even while this kernel is still running
 #pragma unroll
@@ -210,18 +298,95 @@ __global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a)
   __syncthreads();
   if (tid < W) flag_store(T.flags[tid] + done_idx(b, me, j), a.epoch);
 
-  // ---- final wait: every bucket's new parameters from every owner have landed here; the
-  // (bucket, owner, slice) words are spread over all threads of the launch and polled at once
-  if (a.final_wait) {
-    int total = 0;
-    for (int bb = 0; bb < a.nbuckets; ++bb) total += W * a.nslices[bb];
-    for (int k = j * 256 + tid; k < total; k += gridDim.x * 256) {
-      int bb = 0, x = k;
-      while (x >= W * a.nslices[bb]) x -= W * a.nslices[bb++];
-      const int q = x / a.nslices[bb], jj = x - q * a.nslices[bb];
-      wait_ge(myflags + done_idx(bb, q, jj), a.epoch, deadline, a.err, 2);
-    }
+  // ---- final wait: every bucket's new parameters from every owner have landed here
+  if (a.final_wait) final_wait(a, myflags, W, deadline);
+}
+
+// The step's LAST bucket, replicated: nothing overlaps its exchange — it is
+// complete only after the final backward launch — so instead of push chunk -> owner update ->
+// push parameters -> DONE (two cross-GPU hops on the critical path), every rank pushes the
+// WHOLE bucket gradient to every peer (W-1 links at once, 208 KB each for conv1+conv2), sums the
+// W contributions in rank order and runs the update itself on replicated optimizer state, then
+// stores only its own parameters.  One hop.  The inbox has two parity slots per source: a peer
+// writes slot (e+1)&1 of step e+1 while this rank may still read slot e&1; it can write slot e&1
+// again only at step e+2, after its final wait of step e+1 saw this rank's DONE of buckets
+// 0..nb-2 at e+1 — issued after this rank's step-e+1 forward, i.e. after this kernel of step e.
+template <int WT>
+__global__ void __launch_bounds__(256) xgmi_repl_kernel(XgmiTable T, XgmiLaunch a) {
+  constexpr int NQ = WT ? WT : kXgmiMaxPeers;
+  const int j = blockIdx.x, tid = threadIdx.x;
+  const int W = WT ? WT : a.world, me = a.rank, b = a.bucket;
+  const long long deadline = wall_clock64() + a.timeout_ticks;
+  const int64_t n = a.c;  // replicated: the whole bucket
+  const int64_t s0 = (int64_t)j * a.slice;
+  const int64_t s1 = s0 + a.slice < n ? s0 + a.slice : n;
+  const int n4 = s0 < s1 ? (int)((s1 - s0) >> 2) : 0;
+  const int par = (int)(a.epoch & 1u);
+  uint32_t* myflags = T.flags[me];
+  __shared__ uint32_t red[4];
+  __shared__ int arrived;
+  const float4* own = reinterpret_cast<const float4*>(a.grads + a.lo + s0);
+  // slot (par, src) of rank r's replicated inbox, this slice
+  auto slot = [&](int r, int src) {
+    return make_rsrc(T.inbox[r] + a.inbox_off + ((int64_t)par * W + src) * n + s0,
+                     (uint32_t)n4 * 16u);
+  };
+
+  // ---- phase 1: my whole slice to every peer
+  uint32_t cs = 0;
+  for (int i = tid; i < n4; i += 256) {
+    float4 x = own[i];
+    if (a.coef != 1.f) x = scale4(x, a.coef);
+    if (a.check) cs += bits4(x);
+#pragma unroll
+    for (int k = 0; k < NQ - 1; ++k)
+      if (k < W - 1) st4_sys(slot((me + 1 + (k + j) % (W - 1)) % W, me), i * 16, x);
   }
+  if (a.check) {
+    const uint32_t t = block_sum(cs, red);
+    if (tid < W && tid != me)
+      __hip_atomic_store(T.flags[tid] + ck_idx(b, me, j), t, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  drain_vm();
+  __syncthreads();
+  if (tid < W && tid != me) flag_store(T.flags[tid] + arrive_idx(b, me, j), a.epoch);
+
+  // ---- phase 2: all peers' slices are here (failed wait: no update, as in xgmi_ps_kernel)
+  if (tid == 0) arrived = 1;
+  __syncthreads();
+  if (tid < W && tid != me &&
+      !wait_ge(myflags + arrive_idx(b, tid, j), a.epoch, deadline, a.err, 1))
+    arrived = 0;
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (a.check && arrived) {
+    bool ok = true;
+    for (int q = 0; q < W; ++q)
+      if (q != me) ok &= check_piece(slot(me, q), 0, n4, myflags + ck_idx(b, q, j), a.err, red);
+    if (!ok && tid == 0) arrived = 0;
+    __syncthreads();
+  }
+  const int n4u = arrived ? n4 : 0;
+  float4* m4 = reinterpret_cast<float4*>(a.m + s0);
+  float4* v4 = a.v ? reinterpret_cast<float4*>(a.v + s0) : nullptr;
+  float4* w4 = reinterpret_cast<float4*>(T.params[me] + a.lo + s0);
+  for (int i = tid; i < n4u; i += 256) {
+    float4 x[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      if (q < W)
+        x[q] = q == me ? (a.coef != 1.f ? scale4(own[i], a.coef) : own[i])
+                       : ld4_sys(slot(me, q), i * 16);
+    float4 g = f4zero();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)  // rank order, as the owner kernel: identical bits
+      if (q < W) { g.x += x[q].x; g.y += x[q].y; g.z += x[q].z; g.w += x[q].w; }
+    float4 w = w4[i];
+    update4(a, w, g, m4, v4, i);
+    w4[i] = w;  // this rank's copy only (the next forward is a later kernel of this stream)
+  }
+  if (a.final_wait) final_wait(a, myflags, W, deadline);
 }
 
 #define X_CHECK(x)                                                                        \
@@ -240,8 +405,10 @@ struct HandleBlob {  // what one rank publishes (exchanged as bytes over the def
 }  // namespace
 
 PeerExchange::PeerExchange(float* params, const float* grads, int64_t total, int world, int rank,
-                           const std::vector<std::pair<int64_t, int64_t>>& buckets, int max_slices)
-    : params_(params), grads_(grads), total_(total), world_(world), rank_(rank) {
+                           const std::vector<std::pair<int64_t, int64_t>>& buckets, int max_slices,
+                           int repl_bucket)
+    : params_(params), grads_(grads), total_(total), world_(world), rank_(rank),
+      repl_(repl_bucket) {
   if (world < 1 || world > kXgmiMaxPeers) throw std::invalid_argument("xgmi: world out of range");
   if (rank < 0 || rank >= world) throw std::invalid_argument("xgmi: rank out of range");
   if (buckets.empty() || (int)buckets.size() > kXgmiMaxBuckets)
@@ -250,14 +417,19 @@ PeerExchange::PeerExchange(float* params, const float* grads, int64_t total, int
     throw std::invalid_argument("xgmi: max_slices out of range");
   if (reinterpret_cast<uintptr_t>(params) % 16 || reinterpret_cast<uintptr_t>(grads) % 16)
     throw std::invalid_argument("xgmi: buffers must be 16-B aligned");
+  if (repl_bucket >= (int)buckets.size()) throw std::invalid_argument("xgmi: replicated bucket");
   int64_t inbox = 0;
-  for (const auto& bk : buckets) {
+  for (size_t bi = 0; bi < buckets.size(); ++bi) {
+    const auto& bk = buckets[bi];
     const int64_t lo = bk.first, hi = bk.second;
+    const bool repl = (int)bi == repl_bucket;
     if (lo < 0 || hi > total || hi <= lo) throw std::invalid_argument("xgmi: bucket out of range");
-    if ((hi - lo) % (4 * world)) throw std::invalid_argument("xgmi: bucket not divisible by 4W");
+    if ((hi - lo) % (repl ? 4 : 4 * world))
+      throw std::invalid_argument("xgmi: bucket not divisible by 4W (replicated: by 4)");
     Bucket B;
     B.lo = lo;
-    B.c = (hi - lo) / world;
+    // owner buckets: this rank's chunk; the replicated bucket: all of it
+    B.c = repl ? hi - lo : (hi - lo) / world;
     B.inbox_off = inbox;
     // >= 1024 elements (4 KB) per workgroup slice, at most max_slices workgroups
     int64_t ns = (B.c + 1023) / 1024;
@@ -265,14 +437,16 @@ PeerExchange::PeerExchange(float* params, const float* grads, int64_t total, int
     if (ns < 1) ns = 1;
     B.slice = ((B.c + ns - 1) / ns + 3) & ~(int64_t)3;
     B.nslice = (int)((B.c + B.slice - 1) / B.slice);
-    if (B.c * 4 * world > 0x7fffffffLL) throw std::invalid_argument("xgmi: bucket too large");
-    inbox += B.c * world;
+    if (B.c * 4 * world * (repl ? 2 : 1) > 0x7fffffffLL)
+      throw std::invalid_argument("xgmi: bucket too large");
+    inbox += B.c * world * (repl ? 2 : 1);  // replicated: two parity slots per source
     bk_.push_back(B);
   }
   inbox_elems_ = inbox;
   X_CHECK(hipMalloc(&inbox_, inbox_elems_ * sizeof(float)));
   X_CHECK(hipMemset(inbox_, 0, inbox_elems_ * sizeof(float)));
-  flag_bytes_ = 2ull * kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices * sizeof(uint32_t);
+  // ARRIVE, DONE and (check mode) checksum words
+  flag_bytes_ = 3ull * kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices * sizeof(uint32_t);
   X_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes_,
                                 hipDeviceMallocUncached));
   X_CHECK(hipMemset(flags_, 0, flag_bytes_));
@@ -281,6 +455,8 @@ PeerExchange::PeerExchange(float* params, const float* grads, int64_t total, int
   X_CHECK(hipDeviceSynchronize());
   const char* t = getenv("DDL_XGMI_TIMEOUT_S");
   timeout_s_ = t ? atof(t) : 20.0;  // a healthy wait takes microseconds
+  const char* ck = getenv("DDL_XGMI_CHECK");
+  check_ = ck && ck[0] == '1';
 }
 
 PeerExchange::~PeerExchange() {
@@ -370,12 +546,25 @@ void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool 
   a.coef = u.coef;
   a.err = err_;
   a.timeout_ticks = (long long)(timeout_s_ * 1e8);  // wall_clock64: 100 MHz
+  a.check = check_ ? 1 : 0;
+  a.repl_bucket = repl_;
+  if (bucket == repl_) {
+    switch (world_) {
+#define X_CASE(N) \
+  case N: DDL_LAUNCH(xgmi_repl_kernel<N>, dim3(B.nslice), dim3(256), 0, st, table_, a); break;
+      X_CASE(2) X_CASE(3) X_CASE(4) X_CASE(5) X_CASE(6) X_CASE(7) X_CASE(8)
+#undef X_CASE
+      default: DDL_LAUNCH(xgmi_repl_kernel<0>, dim3(B.nslice), dim3(256), 0, st, table_, a);
+    }
+    DDL_CHECK_LAUNCH();
+    return;
+  }
   switch (world_) {
 #define X_CASE(N) \
-  case N: hipLaunchKernelGGL(xgmi_ps_kernel<N>, dim3(B.nslice), dim3(256), 0, st, table_, a); break;
+  case N: DDL_LAUNCH(xgmi_ps_kernel<N>, dim3(B.nslice), dim3(256), 0, st, table_, a); break;
     X_CASE(2) X_CASE(3) X_CASE(4) X_CASE(5) X_CASE(6) X_CASE(7) X_CASE(8)
 #undef X_CASE
-    default: hipLaunchKernelGGL(xgmi_ps_kernel<0>, dim3(B.nslice), dim3(256), 0, st, table_, a);
+    default: DDL_LAUNCH(xgmi_ps_kernel<0>, dim3(B.nslice), dim3(256), 0, st, table_, a);
   }
   DDL_CHECK_LAUNCH();
 }

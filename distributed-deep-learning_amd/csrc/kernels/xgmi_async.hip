@@ -101,17 +101,20 @@ DDL_DEV int done_word(int w, int p, int j) { return (w * kAsyncMaxPs + p) * kAsy
 struct PushArgs {
   int world, rank, nps;
   uint32_t epoch;
-  int first_blk[kAsyncMaxPs + 1];  // block range of PS p: [first_blk[p], first_blk[p+1])
+  int first_blk[kAsyncMaxPs + 1];  // block range of entry i: [first_blk[i], first_blk[i+1])
+  int ps[kAsyncMaxPs];             // subset: the PS id of entry i (else entry i is PS i)
+  int subset;
   const float* grads;
   float coef;
 };
 
 __global__ void __launch_bounds__(256) async_push_kernel(AsyncTable T, PushArgs a) {
   const int blk = blockIdx.x, tid = threadIdx.x;
-  int p = 0;
-  while (p + 1 < a.nps && blk >= a.first_blk[p + 1]) ++p;
+  int e = 0;
+  while (e + 1 < a.nps && blk >= a.first_blk[e + 1]) ++e;
+  const int p = a.subset ? a.ps[e] : e;
   const AsyncShard& S = T.shard[p];
-  const int j = blk - a.first_blk[p];
+  const int j = blk - a.first_blk[e];
   const int64_t s0 = (int64_t)j * S.slice;
   const int64_t s1 = s0 + S.slice < S.n ? s0 + S.slice : S.n;
   const int n4 = s0 < s1 ? (int)((s1 - s0) >> 2) : 0;
@@ -173,10 +176,10 @@ __global__ void __launch_bounds__(256) async_apply_kernel(AsyncTable T, ApplyArg
       m4[i] = M; v4[i] = V;
     } else if (a.opt == 1) {
       float4 M = m4[i];
-      M.x = M.x * a.mu + g.x * a.scale; w.x -= a.lr * M.x;
-      M.y = M.y * a.mu + g.y * a.scale; w.y -= a.lr * M.y;
-      M.z = M.z * a.mu + g.z * a.scale; w.z -= a.lr * M.z;
-      M.w = M.w * a.mu + g.w * a.scale; w.w -= a.lr * M.w;
+      momentum1(w.x, g.x, M.x, a.lr, a.mu, a.scale);
+      momentum1(w.y, g.y, M.y, a.lr, a.mu, a.scale);
+      momentum1(w.z, g.z, M.z, a.lr, a.mu, a.scale);
+      momentum1(w.w, g.w, M.w, a.lr, a.mu, a.scale);
       m4[i] = M;
     } else {  // self-test: the PS shard := the pushed gradient
       w = g;
@@ -332,6 +335,31 @@ void AsyncPeer::push_all(uint32_t epoch, float coef, hipStream_t st) {
   a.grads = grads_;
   a.coef = coef;
   hipLaunchKernelGGL(async_push_kernel, dim3(blk), dim3(256), 0, st, table_, a);
+  DDL_CHECK_LAUNCH();
+}
+
+void AsyncPeer::push_set(const std::vector<int>& ps, uint32_t epoch, float coef, hipStream_t st) {
+  if (!opened_ok_) throw std::runtime_error("async xgmi: open() first");
+  if (ps.empty()) return;
+  if ((int)ps.size() > kAsyncMaxPs) throw std::invalid_argument("async xgmi: PS list");
+  PushArgs a;
+  memset(&a, 0, sizeof(a));
+  a.world = world_;
+  a.rank = rank_;
+  a.nps = (int)ps.size();
+  a.epoch = epoch;
+  int blk = 0;
+  for (size_t i = 0; i < ps.size(); ++i) {
+    if (ps[i] < 0 || ps[i] >= nps_) throw std::invalid_argument("async xgmi: PS id");
+    a.ps[i] = ps[i];
+    a.first_blk[i] = blk;
+    blk += table_.shard[ps[i]].nslice;
+  }
+  a.first_blk[ps.size()] = blk;
+  a.grads = grads_;
+  a.coef = coef;
+  a.subset = 1;
+  DDL_LAUNCH(async_push_kernel, dim3(blk), dim3(256), 0, st, table_, a);
   DDL_CHECK_LAUNCH();
 }
 

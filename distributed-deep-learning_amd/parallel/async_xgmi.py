@@ -136,6 +136,43 @@ class AsyncPeerExchange:
         self.served = 0
         self.check_provenance = check_provenance
         self.provenance: List[Tuple[int, int, int, int]] = []
+        self.runner = None
+
+    # -- the native worker step ----------------------------------------------------------------------
+    def attach_runner(self, engine, segments) -> None:
+        """Issue the worker step from C++ (csrc/kernels/async_runner.hip) — forward, the backward
+        segments with each PS's push launched as soon as its range is complete, tokens posted by
+        a native thread after each push completes, the previous round's pull as a host wait at
+        the start of the step — when the engine is the HIP one and every arrival mailbox is a
+        shared-memory ring (one host).  DDL_ASYNC_NATIVE=0 keeps the Python push_pull path."""
+        import os
+        from ..models.layout import TENSORS
+        if getattr(engine, "name", "") != "hip" or os.environ.get("DDL_ASYNC_NATIVE", "1") != "1":
+            return
+        if not all(isinstance(b, mbox.ShmMailbox) for b in self.boxes.values()):
+            return
+        seg_of = {t: s for s, ts in enumerate(segments) for t in ts}
+        off = self.plan.tensor_offsets
+        seg_of_ps = []
+        for lo, hi in self.ranges:
+            ts = [t.index for t in TENSORS if off[t.index] < hi and off[t.index] + t.numel > lo]
+            seg_of_ps.append(max(seg_of[t] for t in ts))
+        W = self.env.world
+        boxes = [self.boxes[r].name if r in self.boxes else "" for r in range(W)]
+        self.runner = native.ops().AsyncRunner(engine.eng, self.peer, W, self.env.rank, seg_of_ps,
+                                               [int(h) for h in self.hosts], boxes, self.epoch)
+
+    def native_step(self, engine, x, y, keep_prob: float, seed: int) -> None:
+        engine._set_keep(keep_prob)
+        self.runner.step(x if x.is_contiguous() else x.contiguous(), y, seed & 0xFFFFFFFF,
+                         self.timeout_s)
+        self.epoch += 1
+
+    def drain_round(self) -> None:
+        """The round in flight (native step) has come back: this worker's parameters are final
+        until its next step (checkpoint hook)."""
+        if self.runner is not None:
+            self.runner.finish(self.timeout_s)
 
     # -- set-up check ------------------------------------------------------------------------------
     def _selftest(self, agree) -> None:
@@ -259,6 +296,7 @@ class AsyncPeerExchange:
             yield
 
     def join(self) -> None:
+        self.drain_round()  # this worker's last round (the reference's final pull)
         if self._svc is not None:
             svc, self._svc = self._svc, None
             try:

@@ -37,7 +37,7 @@ from .comm import DistEnv, SyncExchange
 from .ps import ParameterServer
 from .sharding import ShardPlan
 
-_KIND = {"local": 0, "rs": 1, "reduce": 2, "xgmi": 3}
+_KIND = {"local": 0, "rs": 1, "reduce": 2, "xgmi": 3, "ar": 4, "xgmi_repl": 5}
 
 
 class NativeUnavailable(RuntimeError):
@@ -67,6 +67,19 @@ class NativeSyncExchange(SyncExchange):
         self.engine = engine
         self.optimizer = optimizer
         ops = native.ops()
+        # The step's LAST bucket (conv2 + conv1, 52 k parameters) completes with the backward, so
+        # nothing overlaps its exchange.  Replicate its update: one all-reduce (RCCL) or one
+        # all-to-all push (xGMI) of the whole bucket, every rank sums in rank order and runs the
+        # optimizer on replicated state — one hop on the exposed end of the step instead of
+        # reduce-scatter -> owner update -> all-gather.  The PS objects keep their chunk of that
+        # state for checkpoints (sync_ps_state / load_ps_state).  DDL_REPL_LAST=0: owner form.
+        self.repl = None
+        if (self.collective and plan.bucket_ranges is not None and plan.num_ps == env.world
+                and os.environ.get("DDL_REPL_LAST", "1") == "1"):
+            b = len(plan.bucket_ranges) - 1
+            lo, hi = plan.bucket_ranges[b]
+            z = lambda: torch.zeros(hi - lo, dtype=torch.float32, device=params.device)  # noqa: E731
+            self.repl = (b, int(lo), int(hi), z(), z() if optimizer == "adam" else None)
         self.runner = ops.SyncRunner(engine.eng, params, grads, env.world, env.rank)
         self.backend = "local" if env.world == 1 and not force_collectives else backend
         self.peer = None
@@ -113,14 +126,20 @@ class NativeSyncExchange(SyncExchange):
             offs = u.state_offs or [0] * len(u.ranges)
             ranges = [(int(lo), int(hi), int(off)) for (lo, hi), off in zip(u.ranges, offs)]
             kind = "xgmi" if (self.peer is not None and u.kind == "rs") else u.kind
+            m = srv.m if srv is not None else None
+            v = srv.v if srv is not None else None
+            shard = None if kind == "xgmi" else u.shard_buf
+            if self.repl is not None and u.kind == "rs" and u.bucket == self.repl[0]:
+                kind = "xgmi_repl" if self.peer is not None else "ar"
+                _, lo, hi, m, v = self.repl
+                ranges, shard = [(lo, hi, 0)], None
             units.append((seg_of(u.tensors), _KIND[kind], int(u.host), int(ps), ranges,
-                          srv.m if srv is not None else None,
-                          srv.v if srv is not None else None,
-                          None if kind == "xgmi" else u.shard_buf, int(u.bucket)))
-        self.runner.set_units(units)
+                          m, v, shard, int(u.bucket)))
         h = hyper if hyper is not None else next(iter(servers.values())).h
+        # (before set_units: it checks each unit's optimizer state against the update kind)
         self.runner.set_optimizer(0 if optimizer == "adam" else 1, h.lr, h.beta1, h.beta2, h.eps,
                                   momentum)
+        self.runner.set_units(units)
         self.runner.set_scale(self.grad_scale, self.coef)
         # A/B knob: DDL_LAST_ON_MAIN=0 puts the last segment's collectives back on the comm
         # stream (one event hop more on the critical path of every W > 1 step)
@@ -174,7 +193,8 @@ class NativeSyncExchange(SyncExchange):
         peer, why = None, ""
         try:
             peer = ops.PeerExchange(params, grads, env.world, env.rank,
-                                    [tuple(map(int, b)) for b in plan.bucket_ranges])
+                                    [tuple(map(int, b)) for b in plan.bucket_ranges], 128,
+                                    self.repl[0] if self.repl is not None else -1)
             mine = peer.handle()
         except RuntimeError as e:
             mine, why = None, str(e)
@@ -227,6 +247,39 @@ class NativeSyncExchange(SyncExchange):
         self._n += 1
         if self.env.world > 1 and self._n % 64 == 0:
             self.check()
+
+    # -- replicated last bucket <-> the PS objects (checkpoint / resume) ---------------------------
+    def _repl_chunk(self):
+        b, lo, hi, m, v = self.repl
+        r, W = self.env.rank, self.env.world
+        c = (hi - lo) // W
+        ps = self.servers[r]
+        off = ps.seg_off[b]
+        return r, c, ps, off, m, v
+
+    def sync_ps_state(self) -> None:
+        """Copy this rank's chunk of the replicated last-bucket optimizer state into its PS
+        (every rank holds the same state; the PS owns its chunk in checkpoints)."""
+        if self.repl is None:
+            return
+        r, c, ps, off, m, v = self._repl_chunk()
+        ps.m[off:off + c].copy_(m[r * c:(r + 1) * c])
+        if v is not None:
+            ps.v[off:off + c].copy_(v[r * c:(r + 1) * c])
+
+    def load_ps_state(self) -> None:
+        """After a resume: rebuild the replicated state from every PS's restored chunk."""
+        if self.repl is None:
+            return
+        r, c, ps, off, m, v = self._repl_chunk()
+        mine = (ps.m[off:off + c].cpu(), None if v is None else ps.v[off:off + c].cpu())
+        chunks = [mine]
+        if self.env.world > 1:
+            chunks = [None] * self.env.world
+            dist.all_gather_object(chunks, mine)
+        m.copy_(torch.cat([cm for cm, _ in chunks]).to(m.device))
+        if v is not None:
+            v.copy_(torch.cat([cv for _, cv in chunks]).to(v.device))
 
     def check(self) -> None:
         """Raise if RCCL reported an asynchronous communicator error."""

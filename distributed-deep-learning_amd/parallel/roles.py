@@ -85,10 +85,19 @@ class Trainer:
         hyper = AdamHyper(lr=cfg.lr)
         hosted = [p for p in range(self.num_ps) if self.plan.host_rank(p, W) == r]
         asyncm = cfg.mode == "async"
+        # One worker and its own PS (async, W = 1): every push is applied before the worker's
+        # next step, so the PS parameters ARE the worker's and the math is the sync PS's (one
+        # Adam step per push, test_async_single_worker_equals_sync).  Run it on the sync step
+        # path — the native runner with the update as the optimizer tail of the backward —
+        # instead of a private PS copy plus a copy back per step (0.366 vs 0.307 ms/step).
+        # Not with --ref-quirks (Q4: the PS starts from its own init) or an explicit xGMI
+        # exchange (the W = 1 rehearsal of the async data plane).
+        self.async_as_sync = (asyncm and W == 1 and not cfg.ref_quirks
+                              and cfg.exchange_backend != "xgmi")
         self.servers: Dict[int, ParameterServer] = {}
         for p in hosted:
             own = None
-            if asyncm:
+            if asyncm and not self.async_as_sync:
                 own = self.params
                 if cfg.ref_quirks:  # PS initialised independently of the workers (Q4)
                     tmp = torch.zeros_like(self.params)
@@ -100,8 +109,10 @@ class Trainer:
         self.data = dataset if dataset is not None else get_dataset(cfg.data, seed=1234)
         self.data = self.data.to(dev)
         self.steps = cfg.steps or (self.data.total_batch // cfg.batch_size)
-        if asyncm:
+        if asyncm and not self.async_as_sync:
             self.exchange = self._make_async_exchange(cfg, env)
+            if hasattr(self.exchange, "attach_runner"):
+                self.exchange.attach_runner(self.engine, segs)
         else:
             self.exchange = make_sync_exchange(self.plan, env, self.params, self.grads, segs,
                                                self.servers, self.engine, cfg, hyper)
@@ -142,7 +153,11 @@ class Trainer:
         cfg = self.cfg
         x, y = self.batch(step)
         seed = rng.step_seed(cfg.seed, self.env.rank, self.global_step)
-        if cfg.mode == "async":
+        if cfg.mode == "async" and not self.async_as_sync and \
+                getattr(self.exchange, "runner", None) is not None:
+            with trace_range("step_native_async"):
+                self.exchange.native_step(self.engine, x, y, cfg.keep_prob, seed)
+        elif cfg.mode == "async" and not self.async_as_sync:
             with trace_range("fwd_bwd"):
                 self.engine.forward_backward(x, y, cfg.keep_prob, seed)
             with trace_range("push_pull"):
@@ -208,7 +223,7 @@ class Trainer:
         single = cfg.mode == "single"
         if cfg.resume and cfg.checkpoint_dir:
             ckpt.load(self, cfg.checkpoint_dir)
-        asyncx = cfg.mode == "async"
+        asyncx = cfg.mode == "async" and not self.async_as_sync
         if asyncx:
             self.exchange.start()
         wd = Watchdog(cfg.watchdog_s, name=f"rank{env.rank}", on_timeout=self._on_hang)

@@ -51,12 +51,18 @@ def save(trainer, path: str) -> None:
     env, plan = trainer.env, trainer.plan
     asyncm = trainer.cfg.mode == "async"
     ex = trainer.exchange
+    drain = getattr(ex, "drain_round", None)  # async native step: this worker's round is back
+    if drain is not None:
+        drain()
     if trainer.params.is_cuda:
         # every queued step (and its exchange kernels) must have finished, and must not have
         # failed: a checkpoint of parameters a timed-out exchange left half-updated is refused
         torch.cuda.synchronize(trainer.params.device)
     if getattr(ex, "native", False) and hasattr(ex, "check"):
         ex.check()
+    sync_state = getattr(ex, "sync_ps_state", None)  # replicated optimizer state -> the PS
+    if sync_state is not None:
+        sync_state()
     # async: the PS service keeps applying other workers' pushes.  Snapshot the hosted PS
     # state (parameters, m, v and the step counter t) with the service paused, so it is one
     # consistent PS step; the pause ends before any collective below (a peer may be waiting
@@ -162,3 +168,6 @@ def load(trainer, path: str) -> None:
         same_plan = (man["policy"] == plan.policy and man["num_ps"] == plan.num_ps)
         ps.t = int(man["ps_t"].get(str(p)) or t_resume) if same_plan else t_resume
     trainer.global_step = int(man["global_step"])
+    load_state = getattr(trainer.exchange, "load_ps_state", None)
+    if load_state is not None:  # PS chunks -> the exchange's replicated optimizer state
+        load_state()

@@ -36,6 +36,9 @@ def _run(data, native, steps=6, **kw):
     for i in range(steps):
         tr.train_step(i)
     torch.cuda.synchronize()
+    sync = getattr(tr.exchange, "sync_ps_state", None)  # replicated last-bucket state -> PS
+    if sync is not None:
+        sync()
     state = {p: (s.t, s.m.clone(), None if s.v is None else s.v.clone())
              for p, s in tr.servers.items()}
     return tr.params.clone(), state
@@ -80,6 +83,7 @@ def test_native_runner_trains(data):
     dict(shard="flat", exchange_backend="xgmi"),  # fused xGMI bucket kernels, push to self
     dict(shard="flat", exchange_backend="xgmi", overlap=False),
     dict(shard="flat", exchange_backend="xgmi", optimizer="sgd"),
+    dict(shard="flat", exchange_backend="xgmi", optimizer="momentum"),
 ])
 def test_forced_collectives_on_one_rank_match_local(data, kw):
     """The multi-GPU exchange path on one GPU: torch's librccl resolved by dlsym, a 1-rank

@@ -29,12 +29,22 @@ def _canon(params, offsets):
     return torch.cat([params[offsets[t.index]:offsets[t.index] + t.numel] for t in TENSORS])
 
 
+# Eight processes on ONE card: each pinned to one hardware queue (GPU_MAX_HW_QUEUES=1, HIP
+# reads it at init), so the box runs 8 queues, not 8 x 4 (the oversubscribed regime round 2's
+# W = 8 runs stalled in), and with the inbox checksums on (DDL_XGMI_CHECK=1: every owner
+# verifies every pushed slice against its pusher's checksum, error code 3 on a mismatch).
+W8_ENV = dict(GPU_MAX_HW_QUEUES="1", DDL_XGMI_CHECK="1", DDL_XGMI_TIMEOUT_S="60")
+
+
 def _rank(rank, world, port, outdir, kw):
     if ROOT not in sys.path:
         sys.path.insert(0, ROOT)
+    kw = dict(kw)
+    extra_env = kw.pop("_env", {})
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DDL_DIST_BACKEND="gloo",
                       DDL_XGMI_TIMEOUT_S="20")
+    os.environ.update(extra_env)
     try:
         import torch.distributed as dist
         from ddl_amd.config import TrainConfig
@@ -105,10 +115,9 @@ def _simulate(world, kw):
     (2, {}),
     (3, dict(grad_reduce="mean")),
     (4, dict(overlap=False)),
-    # no W = 8 here: eight processes time-sharing ONE card oversubscribe its hardware queues
-    # (8 x GPU_MAX_HW_QUEUES); runs in that regime timed out, diverged once and once aborted
-    # with an illegal-instruction fault inside the GEMM dual kernel while waves were being
-    # context-switched — a one-box artefact, not the 8-GPU node's regime (one process per GPU)
+    (2, dict(_env=dict(DDL_REPL_LAST="0"))),     # last bucket by its chunk owners
+    (4, dict(_env=dict(DDL_XGMI_CHECK="1"))),
+    pytest.param(8, dict(_env=W8_ENV), id="w8"),  # the 8-worker size of BASELINE configs 3-5
 ])
 def test_xgmi_exchange_matches_simulation(tmp_path, world, kw):
     import torch.multiprocessing as mp
@@ -118,7 +127,7 @@ def test_xgmi_exchange_matches_simulation(tmp_path, world, kw):
         assert torch.equal(rec["params"], recs[0]["params"])
         assert rec["acc"] == recs[0]["acc"]
     assert all(t == STEPS for rec in recs for t in rec["t"].values())
-    ref, ref_sums = _simulate(world, {k: v for k, v in kw.items() if k != "overlap"})
+    ref, ref_sums = _simulate(world, {k: v for k, v in kw.items() if k not in ("overlap", "_env")})
     got = recs[0]["params"]
     diff = float((got - ref).abs().max())
     # per-step parameter checksums localise a divergence (which step, which rank)
@@ -132,9 +141,12 @@ ASYNC_STEPS = 6
 def _async_rank(rank, world, port, outdir, kw):
     if ROOT not in sys.path:
         sys.path.insert(0, ROOT)
+    kw = dict(kw)
+    extra_env = kw.pop("_env", {})
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DDL_DIST_BACKEND="gloo",
                       DDL_XGMI_TIMEOUT_S="20")
+    os.environ.update(extra_env)
     try:
         import torch.distributed as dist
         from ddl_amd.config import TrainConfig
@@ -149,6 +161,8 @@ def _async_rank(rank, world, port, outdir, kw):
                           **kw)
         tr = Trainer(cfg, env, dataset=synthetic_mnist(2000, 500, seed=5))
         assert isinstance(tr.exchange, AsyncPeerExchange), type(tr.exchange)
+        want_native = extra_env.get("DDL_ASYNC_NATIVE", "1") == "1"
+        assert (tr.exchange.runner is not None) == want_native, "native async step not taken"
         s = tr.train()  # verify_provenance runs inside (check_provenance=True)
         torch.cuda.synchronize()
         torch.save({"params": tr.params.cpu(), "served": tr.exchange.served,
@@ -169,6 +183,11 @@ def _async_rank(rank, world, port, outdir, kw):
     (2, dict(shard="contiguous")),               # mnist_async_sharding
     (4, dict(shard="greedy", num_ps=4)),         # mnist_async_sharding_greedy
     (3, dict(shard="contiguous", num_ps=5)),     # several PS per host
+    (2, dict(shard="greedy", _env=dict(DDL_ASYNC_NATIVE="0"))),  # the Python push_pull path
+    pytest.param(8, dict(shard="contiguous", _env=dict(GPU_MAX_HW_QUEUES="1",
+                                                       DDL_XGMI_TIMEOUT_S="60")), id="w8-contig"),
+    pytest.param(8, dict(shard="greedy", _env=dict(GPU_MAX_HW_QUEUES="1",
+                                                   DDL_XGMI_TIMEOUT_S="60")), id="w8-greedy"),
 ])
 def test_async_xgmi_serves_every_push(tmp_path, world, kw):
     import torch.multiprocessing as mp
@@ -187,3 +206,56 @@ def test_async_xgmi_serves_every_push(tmp_path, world, kw):
         for p, (_, ps_params) in rec["ps"].items():
             lo, hi = rec["ranges"][p]
             assert any(torch.equal(o["params"][lo:hi], ps_params) for o in recs), p
+
+
+def _ckpt_rank(rank, world, port, outdir, kw):
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DDL_DIST_BACKEND="gloo",
+                      DDL_XGMI_TIMEOUT_S="20")
+    try:
+        import torch.distributed as dist
+        from ddl_amd.config import TrainConfig
+        from ddl_amd.parallel.comm import init_distributed
+        from ddl_amd.parallel.roles import Trainer
+        from ddl_amd.utils.data import synthetic_mnist
+        env = init_distributed()
+        cfg = TrainConfig(mode="async", steps=6, batch_size=100, eval_every=0, engine="hip",
+                          quiet=True, data_sharding="stride", exchange_backend="xgmi",
+                          checkpoint_dir=os.path.join(outdir, "ck"), watchdog_s=120.0, **kw)
+        tr = Trainer(cfg, env, dataset=synthetic_mnist(2000, 500, seed=5))
+        tr.train()  # checkpoint_every=3: a mid-run snapshot while the PS services run
+        torch.save({"t": {p: s.t for p, s in tr.servers.items()}},
+                   os.path.join(outdir, f"final{rank}.pt"))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
+def test_async_xgmi_midrun_checkpoint_is_consistent(tmp_path):
+    """a mid-run async checkpoint must carry the PS step counters the native service
+    advanced (beta powers consistent with the manifest's t) and a snapshot taken with the
+    service paused; the final one equals the services' end state."""
+    import json
+    import torch.multiprocessing as mp
+    from safetensors.torch import load_file
+    world = 2
+    # the step-3 save runs while the peer's pushes are being served (it must neither deadlock
+    # against the peer nor tear the PS state); the end-of-run save overwrites it and is checked
+    mp.spawn(_ckpt_rank, args=(world, free_port(), str(tmp_path), dict(checkpoint_every=3)),
+             nprocs=world, join=True)
+    man = json.load(open(tmp_path / "ck" / "manifest.json"))
+    final = {}
+    for r in range(world):
+        final.update(torch.load(tmp_path / f"final{r}.pt")["t"])
+    assert {int(k): v for k, v in man["ps_t"].items()} == final   # the end-of-run save
+    assert all(t == world * 6 for t in final.values())
+    for p in range(man["num_ps"]):
+        d = load_file(str(tmp_path / "ck" / f"ps{p}.safetensors"))
+        b1 = float(d["ParameterServer/beta1_power"][0])
+        assert b1 == pytest.approx(0.9 ** man["ps_t"][str(p)], rel=1e-5)
+        for k, v in d.items():
+            assert torch.isfinite(v).all(), k
