@@ -147,9 +147,10 @@ class PyEngine {
     return std::vector<int64_t>(e_.workers, e_.workers + ddl::OP_COUNT);
   }
 
-  void forward(at::Tensor x, at::Tensor seed, bool train) {
+  void forward(at::Tensor x, at::Tensor seed, bool train, bool defer_fc) {
     check_x(x);
-    e_.forward(x.data_ptr<float>(), (int)x.size(0), seed_ptr(seed), train, cur_stream());
+    e_.forward(x.data_ptr<float>(), (int)x.size(0), seed_ptr(seed), train, cur_stream(),
+               defer_fc);
   }
   void backward_segment(int64_t s, at::Tensor x, at::Tensor labels, at::Tensor seed) {
     check_x(x);
@@ -405,6 +406,83 @@ class PyAsyncService {
   std::unique_ptr<ddl::AsyncService> svc_;
 };
 
+// asynchronous PS over point-to-point RCCL sessions (kernels/rccl_async.hip)
+class PyRcclAsync {
+ public:
+  // ps: list of (ps id, private params, m, v | None, t); ranges: [(lo, hi)] per PS
+  PyRcclAsync(at::Tensor params, at::Tensor grads, int64_t world, int64_t rank, py::list ranges,
+              std::vector<int64_t> hosts, py::list ps, int64_t opt, double lr, double b1,
+              double b2, double eps, double mu, bool self_sessions)
+      : params_(params), grads_(grads) {
+    check_f32_cuda(params, "params");
+    check_f32_cuda(grads, "grads");
+    std::vector<std::pair<int64_t, int64_t>> rg;
+    for (auto r : ranges) {
+      auto t = r.cast<py::tuple>();
+      rg.emplace_back(t[0].cast<int64_t>(), t[1].cast<int64_t>());
+    }
+    std::vector<ddl::AsyncPsState> st;
+    for (auto item : ps) {
+      auto t = item.cast<py::tuple>();
+      ddl::AsyncPsState s;
+      s.ps = t[0].cast<int>();
+      at::Tensor w = t[1].cast<at::Tensor>(), m = t[2].cast<at::Tensor>();
+      check_f32_cuda(w, "ps params");
+      check_f32_cuda(m, "m");
+      keep_.push_back(w);
+      keep_.push_back(m);
+      s.params = w.data_ptr<float>();
+      s.m = m.data_ptr<float>();
+      s.v = nullptr;
+      if (!t[3].is_none()) {
+        at::Tensor v = t[3].cast<at::Tensor>();
+        check_f32_cuda(v, "v");
+        keep_.push_back(v);
+        s.v = v.data_ptr<float>();
+      }
+      s.t = t[4].cast<int64_t>();
+      st.push_back(s);
+    }
+    std::vector<int> h(hosts.begin(), hosts.end());
+    c10::hip::HIPGuard guard(params.device().index());
+    r_ = std::make_unique<ddl::RcclAsync>(params.data_ptr<float>(), grads.data_ptr<float>(),
+                                          (int)world, (int)rank, params.device().index(), rg, h,
+                                          st, (int)opt, lr, b1, b2, (float)eps, (float)mu,
+                                          self_sessions);
+  }
+  void init_comm(py::bytes id) {
+    std::string s = id;
+    TORCH_CHECK(s.size() == 128, "RCCL unique id must be 128 bytes");
+    py::gil_scoped_release nogil;  // collective
+    r_->init_comm(s.data());
+  }
+  void attach_shm(std::string job, bool create) { r_->attach_shm(job, create); }
+  void open_boxes(bool own) { r_->open_boxes(own); }
+  void start(int64_t expected, bool provenance) { r_->start(expected, provenance); }
+  void push_pull() {
+    hipStream_t st = cur_stream();
+    py::gil_scoped_release nogil;
+    r_->push_pull(st);
+  }
+  void join() {
+    py::gil_scoped_release nogil;
+    r_->join();
+  }
+  void pause() {
+    py::gil_scoped_release nogil;
+    r_->pause();
+  }
+  void resume() { r_->resume(); }
+  int64_t t(int64_t ps) const { return r_->t((int)ps); }
+  int64_t served() const { return r_->served(); }
+  std::vector<std::array<int64_t, 4>> provenance() const { return r_->provenance(); }
+
+ private:
+  at::Tensor params_, grads_;
+  std::vector<at::Tensor> keep_;
+  std::unique_ptr<ddl::RcclAsync> r_;
+};
+
 // native async worker step (kernels/async_runner.hip)
 class PyAsyncRunner {
  public:
@@ -598,12 +676,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("get_eval_cfg", &PyEngine::get_eval_cfg)
       .def("set_concurrent", &PyEngine::set_concurrent)
       .def("set_dual", &PyEngine::set_dual)
+      .def("set_fc_chain", [](PyEngine& e, bool on) { e.raw()->fc_chain = on; })
+      .def("fc_chain", [](PyEngine& e) { return e.raw()->fc_chain; })
+      .def("fc_chain_error", [](PyEngine& e) { return e.raw()->fc_chain_error(); })
+      .def("set_fc_stamps", [](PyEngine& e, c10::optional<at::Tensor> t) {
+        // int64 [items x 4] device tensor (kept alive by the caller), or None to turn off
+        e.raw()->fc_stamps = t ? reinterpret_cast<long long*>(t->data_ptr<int64_t>()) : nullptr;
+      })
       .def("set_kfix", &PyEngine::set_kfix)
       .def("get_kfix", &PyEngine::get_kfix)
       .def("set_wide_thr", &PyEngine::set_wide_thr)
       .def("set_wide", &PyEngine::set_wide)
       .def("get_wide", &PyEngine::get_wide)
-      .def("forward", &PyEngine::forward)
+      .def("forward", &PyEngine::forward, py::arg("x"), py::arg("seed"), py::arg("train"),
+           py::arg("defer_fc") = false)
       .def("backward_segment", &PyEngine::backward_segment)
       .def("run_op", &PyEngine::run_op)
       .def("zero_correct", &PyEngine::zero_correct)
@@ -661,6 +747,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("resume", &PyAsyncService::resume)
       .def("served", &PyAsyncService::served)
       .def("provenance", &PyAsyncService::provenance);
+
+  py::class_<PyRcclAsync>(m, "RcclAsync")
+      .def(py::init<at::Tensor, at::Tensor, int64_t, int64_t, py::list, std::vector<int64_t>,
+                    py::list, int64_t, double, double, double, double, double, bool>())
+      .def("init_comm", &PyRcclAsync::init_comm)
+      .def("attach_shm", &PyRcclAsync::attach_shm)
+      .def("open_boxes", &PyRcclAsync::open_boxes)
+      .def("start", &PyRcclAsync::start)
+      .def("push_pull", &PyRcclAsync::push_pull)
+      .def("join", &PyRcclAsync::join)
+      .def("pause", &PyRcclAsync::pause)
+      .def("resume", &PyRcclAsync::resume)
+      .def("t", &PyRcclAsync::t)
+      .def("served", &PyRcclAsync::served)
+      .def("provenance", &PyRcclAsync::provenance);
 
   py::class_<PyAsyncRunner>(m, "AsyncRunner")
       .def(py::init<PyEngine&, PyAsyncPeer&, int64_t, int64_t, std::vector<int64_t>,

@@ -21,6 +21,8 @@
 
 namespace ddl {
 
+class ShmMailbox;
+
 // ---- optimizer (optim.hip) -------------------------------------------------------------------
 void launch_adam(float* w, const float* g, float* m, float* v, int64_t n, float lr_t, float b1,
                  float b2, float eps, float scale, hipStream_t st);
@@ -124,6 +126,13 @@ struct Engine {
   UpdTail tail;
   // fc3 weight gradient still to compute (fused head kernel ran): taken by the fc2 dual launch
   int head_wgrad_pending = 0;
+  // training: fc1 forward .. fc1 backward as ONE persistent launch (fc_chain.h) at the start
+  // of backward segment 0 instead of six launches.  Opt-in (DDL_FC_CHAIN=1): measured slower
+  // than the separate launches so far (docs/DESIGN.md "fc chain")
+  bool fc_chain = false;
+  int* fc_ctr = nullptr;     // its work-queue / stage counters (zero between launches)
+  long long* fc_stamps = nullptr;  // diagnostics: per-item wall-clock stamps (null: off)
+  int fc_chain_error() const;  // host read of the chain's timeout word (0: healthy)
 
   Engine();
   ~Engine();
@@ -135,7 +144,11 @@ struct Engine {
   void bind_workspace(void* base);
 
   // forward through fc2 (train: dropout on, configured split-K; eval: no dropout, no split)
-  void forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st);
+  // defer_fc (training, followed by backward_segment(0)): with fc_chain the fc forward runs
+  // inside segment 0's fused fc launch instead
+  void forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st,
+               bool defer_fc = false);
+  bool fc_deferred = false;  // set by forward(defer_fc), consumed by backward_segment(0)
   // backward segment s (0: head+fc, 1: conv4, 2: conv3, 3: conv2+conv1); weight-gradient
   // GEMMs fork onto the side stream and join back at the end of the segment
   void backward_segment(int s, const float* x, const int64_t* labels, int B,
@@ -348,8 +361,6 @@ class AsyncService {
   mutable std::mutex pause_mu_;  // held by the service thread while it issues an apply
 };
 
-class ShmMailbox;
-
 // Native asynchronous worker step over the xGMI data plane (async_runner.hip): wait for the
 // previous round's parameters (host), forward, backward with each PS's gradient push launched
 // after the segment that completes its range, tokens posted by a poster thread once each push
@@ -390,6 +401,73 @@ class AsyncRunner {
   std::condition_variable cv_;
   std::deque<Posting> queue_;
   int inflight_ = 0;
+  bool stop_ = false;
+  std::string error_;
+};
+
+// Asynchronous PS over point-to-point RCCL in exclusive sessions (rccl_async.hip): one
+// communicator, one comm stream and one comm thread per process; a (worker, PS) round trip
+// runs only while its initiator holds both processes' session locks.
+class RcclAsync {
+ public:
+  RcclAsync(float* params, float* grads, int world, int rank, int device,
+            const std::vector<std::pair<int64_t, int64_t>>& ps_ranges,
+            const std::vector<int>& hosts, const std::vector<AsyncPsState>& hosted, int opt,
+            double lr, double b1, double b2, float eps, float mu, bool self_sessions);
+  ~RcclAsync();
+  void init_comm(const char id[128]);               // collective over all ranks
+  void attach_shm(const std::string& job, bool create);  // session locks (rank 0 creates)
+  void open_boxes(bool own);                        // own: create mine; else attach the others
+  void start(int64_t expected_served, bool provenance);
+  void push_pull(hipStream_t compute);              // this worker's round (blocks the caller)
+  void join();
+  void pause();
+  void resume();
+  int64_t t(int ps) const;
+  int64_t served() const { return served_.load(); }
+  // (worker, ps, that worker's round at this PS, PS step) per applied push
+  const std::vector<std::array<int64_t, 4>>& provenance() const { return prov_; }
+
+ private:
+  void loop();
+  bool push_one(int p);
+  void serve(int worker, int p);
+  void apply(int p, int worker, const float* g);
+  bool try_lock_pair(int h);
+  void unlock_pair(int h);
+  uint64_t* lock_word(int r) const;
+  AsyncPsState* state_of(int p);
+  float* w_;
+  float* g_;
+  int world_, rank_, device_;
+  std::vector<std::pair<int64_t, int64_t>> ranges_;
+  std::vector<int> hosts_;
+  std::vector<AsyncPsState> ps_;
+  int opt_;
+  float lr_, b1_, b2_, eps_, mu_;
+  double lrd_, b1d_, b2d_;
+  bool self_;
+  void* comm_ = nullptr;
+  hipStream_t cs_ = nullptr;
+  hipEvent_t ev_ = nullptr;
+  float* gbuf_ = nullptr;
+  uint64_t* locks_ = nullptr;
+  size_t lock_bytes_ = 0;
+  bool lock_owner_ = false;
+  std::string lock_name_, box_name_;
+  std::unique_ptr<ShmMailbox> mine_;
+  std::unique_ptr<ShmMailbox> boxes_[kXgmiMaxPeers];
+  std::vector<int64_t> count_;
+  bool keep_prov_ = false;
+  std::vector<std::array<int64_t, 4>> prov_;
+  std::atomic<int64_t> served_{0};
+  int64_t expected_ = 0;
+  std::thread th_;
+  std::mutex qmu_;               // round queue / stop / error
+  std::mutex pause_mu_;
+  std::condition_variable cv_;
+  std::vector<int> pending_;
+  bool waited_ = false;
   bool stop_ = false;
   std::string error_;
 };

@@ -137,7 +137,7 @@ void AsyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t se
   eng_->seed_value = seed;
   {
     TraceRange r("ddl.fwd");
-    eng_->forward(x, B, nullptr, true, st);
+    eng_->forward(x, B, nullptr, true, st, /*defer_fc=*/true);
   }
   for (int s = 0; s < kSegments; ++s) {
     {

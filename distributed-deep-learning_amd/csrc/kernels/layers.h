@@ -680,7 +680,27 @@ using WgradConv1 = ConvWgrad<28, 1, 32, 28>;
 // M = B, N = NOUT, K = KIN.  Dropout key derived on device from *seed (graph-replayable),
 // or from seed_v when no seed word is given (the native step runner: no seed-upload kernel).
 // ---------------------------------------------------------------------------------------------
-template <bool RELU>
+// Cache-policy flags of the fc policies for the in-launch hand-offs of the fused fc chain
+// (fc_chain.h): LSC1 = the activation operand (and any epilogue read of a handed-off buffer) is
+// loaded sc1, SSC1 = the epilogue stores write-through (sc1), so producer and consumer work
+// groups need no release / acquire fences (MI355X guide §6 Guideline 16, first table row).
+template <bool SC1>
+DDL_DEV float4 ld_op4(brsrc_t r, int off) {
+  if constexpr (SC1) return bload4_sc1(r, off);
+  else return bload4(r, off);
+}
+template <bool SC1>
+DDL_DEV void st_out(float* p, float v) {
+  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <bool SC1>
+DDL_DEV float ld_in(const float* p) {
+  if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+
+template <bool RELU, bool LSC1 = false, bool SSC1 = false>
 struct FcFwd {
   static constexpr bool A_KCONTIG = true;
   static constexpr bool B_KCONTIG = false;
@@ -700,7 +720,7 @@ struct FcFwd {
   DDL_DEV AInfo prepA(int m, int kk) const { return {m * K + kk, kk, m < M}; }
   DDL_DEV float4 loadA(const AInfo& a, int k0) const {
     const brsrc_t r = make_rsrc(in, (uint32_t)M * K * 4u);
-    return bload4(r, a.ok && k0 + a.kk < K ? (a.off + k0) * 4 : kOOB);
+    return ld_op4<LSC1>(r, a.ok && k0 + a.kk < K ? (a.off + k0) * 4 : kOOB);
   }
   DDL_DEV BInfo prepB(int n, int kk) const { return {kk * N + n, kk, n < N}; }
   DDL_DEV float4 loadB(const BInfo& b, int k0) const {
@@ -721,7 +741,7 @@ struct FcFwd {
       if (RELU) val = val > 0.f ? val : 0.f;
       const uint32_t idx = (uint32_t)(m * N + n);
       if (thr24) val = ddl_keep(key, idx, thr24) ? val * inv_keep : 0.f;
-      out[idx] = val;
+      st_out<SSC1>(out + idx, val);
     }
   }
 };
@@ -730,7 +750,8 @@ struct FcFwd {
 // W[i][o] (K-contig).  Epilogue variants:
 //   FcDgradAct  : previous layer was ReLU+dropout (fc1): dpre = hpost > 0 ? g/keep : 0
 //   FcDgradPool : previous layer was the conv4 max-pool (flatten of [B,2,2,256])
-struct FcDgradBase {
+template <bool LSC1 = false>
+struct FcDgradBaseT {
   static constexpr bool A_KCONTIG = true;
   static constexpr bool B_KCONTIG = true;
   int M, N, K;
@@ -741,7 +762,7 @@ struct FcDgradBase {
   DDL_DEV AInfo prepA(int m, int kk) const { return {m * K + kk, kk, m < M}; }
   DDL_DEV float4 loadA(const AInfo& a, int k0) const {
     const brsrc_t r = make_rsrc(dy, (uint32_t)M * K * 4u);
-    return bload4(r, a.ok && k0 + a.kk < K ? (a.off + k0) * 4 : kOOB);
+    return ld_op4<LSC1>(r, a.ok && k0 + a.kk < K ? (a.off + k0) * 4 : kOOB);
   }
   DDL_DEV BInfo prepB(int n, int kk) const { return {n * K + kk, kk, n < N}; }
   DDL_DEV float4 loadB(const BInfo& b, int k0) const {
@@ -750,27 +771,33 @@ struct FcDgradBase {
   }
 };
 
-struct FcDgradAct : FcDgradBase {
+using FcDgradBase = FcDgradBaseT<false>;
+
+template <bool LSC1 = false, bool SSC1 = false>
+struct FcDgradActT : FcDgradBaseT<LSC1> {
   const float* __restrict__ hpost;  // [B,N] post ReLU+dropout activation
   float inv_keep;
   float* __restrict__ dx;           // [B,N]
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
+    const int M = this->M, N = this->N;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = m0 + r;
       if (m >= M) break;
       const size_t o = (size_t)m * N + n;
-      dx[o] = hpost[o] > 0.f ? v[r] * inv_keep : 0.f;
+      st_out<SSC1>(dx + o, ld_in<LSC1>(hpost + o) > 0.f ? v[r] * inv_keep : 0.f);
     }
   }
 };
+using FcDgradAct = FcDgradActT<false, false>;
 
-template <int HP, int C>
-struct FcDgradPool : FcDgradBase {
+template <int HP, int C, bool LSC1 = false>
+struct FcDgradPool : FcDgradBaseT<LSC1> {
   static constexpr int HPREV = 2 * HP;
   const uint8_t* __restrict__ code;    // [B,HP,HP,C] == [B,N]
   float* __restrict__ dpre_prev;       // [B,HPREV,HPREV,C] + halo
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
+    const int M = this->M, N = this->N;
     const int c = n % C;
     const int t = n / C;
     const int px = t % HP, py = t / HP;
@@ -784,7 +811,8 @@ struct FcDgradPool : FcDgradBase {
 };
 
 // fc weight gradient dW_aug[KIN+1, NOUT] = [X;1]^T dY (B2/B4/B6): M = KIN+1, N = NOUT, K = B.
-struct FcWgrad {
+template <bool LSC1 = false>
+struct FcWgradT {
   static constexpr bool A_KCONTIG = false;
   static constexpr bool B_KCONTIG = false;
   int M, N, K;
@@ -803,7 +831,7 @@ struct FcWgrad {
     const int k = k0 + a.kk;
     const bool kin = k < K;
     if ((KIN & 3) == 0) {  // group = all weight rows, or [ones row, 0, 0, 0] / zeros: branch-free
-      float4 v = bload4(r, (a.ok && kin) ? (k * KIN + a.off) * 4 : kOOB);
+      float4 v = ld_op4<LSC1>(r, (a.ok && kin) ? (k * KIN + a.off) * 4 : kOOB);
       if (a.off == KIN) v.x = kin ? 1.f : 0.f;
       return v;
     }
@@ -819,7 +847,7 @@ struct FcWgrad {
   DDL_DEV BInfo prepB(int n, int kk) const { return {kk * N + n, kk, n < N}; }
   DDL_DEV float4 loadB(const BInfo& b, int k0) const {
     const brsrc_t r = make_rsrc(dy, (uint32_t)K * N * 4u);
-    return bload4(r, b.ok && k0 + b.kk < K ? (b.off + k0 * N) * 4 : kOOB);
+    return ld_op4<LSC1>(r, b.ok && k0 + b.kk < K ? (b.off + k0 * N) * 4 : kOOB);
   }
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
 #pragma unroll
@@ -830,15 +858,16 @@ struct FcWgrad {
     }
   }
 };
+using FcWgrad = FcWgradT<false>;
 
 // ops the K-wave launch (gemm.h gemm_kwave_kernel, CFG_KWAVE) is instantiated for
 template <class P>
 struct KWaveOK : std::false_type {};
-template <bool R>
-struct KWaveOK<FcFwd<R>> : std::true_type {};
-template <>
-struct KWaveOK<FcDgradAct> : std::true_type {};
-template <int HP, int C>
-struct KWaveOK<FcDgradPool<HP, C>> : std::true_type {};
+template <bool R, bool L, bool S>
+struct KWaveOK<FcFwd<R, L, S>> : std::true_type {};
+template <bool L, bool S>
+struct KWaveOK<FcDgradActT<L, S>> : std::true_type {};
+template <int HP, int C, bool L>
+struct KWaveOK<FcDgradPool<HP, C, L>> : std::true_type {};
 
 }  // namespace ddl

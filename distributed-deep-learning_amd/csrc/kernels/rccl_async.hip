@@ -42,6 +42,7 @@
 #include <cmath>
 #include <stdexcept>
 #include <string>
+#include <algorithm>
 #include <thread>
 
 #include "api.h"
@@ -56,11 +57,11 @@ static ncclComm_t comm_of(void* c) { return reinterpret_cast<ncclComm_t>(c); }
 RcclAsync::RcclAsync(float* params, float* grads, int world, int rank, int device,
                      const std::vector<std::pair<int64_t, int64_t>>& ps_ranges,
                      const std::vector<int>& hosts, const std::vector<AsyncPsState>& hosted,
-                     int opt, float lr, float b1, float b2, float eps, float mu,
+                     int opt, double lr, double b1, double b2, float eps, float mu,
                      bool self_sessions)
     : w_(params), g_(grads), world_(world), rank_(rank), device_(device), ranges_(ps_ranges),
-      hosts_(hosts), ps_(hosted), opt_(opt), lr_(lr), b1_(b1), b2_(b2), eps_(eps), mu_(mu),
-      self_(self_sessions) {
+      hosts_(hosts), ps_(hosted), opt_(opt), lr_((float)lr), b1_((float)b1), b2_((float)b2),
+      eps_(eps), mu_(mu), lrd_(lr), b1d_(b1), b2d_(b2), self_(self_sessions) {
   if (world < 1 || world > kXgmiMaxPeers) throw std::invalid_argument("rccl async: world");
   if (ranges_.size() != hosts_.size() || ranges_.empty())
     throw std::invalid_argument("rccl async: one host per PS range");
@@ -80,7 +81,7 @@ RcclAsync::RcclAsync(float* params, float* grads, int world, int rank, int devic
 
 RcclAsync::~RcclAsync() {
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<std::mutex> g(qmu_);
     stop_ = true;
   }
   cv_.notify_all();
@@ -171,8 +172,9 @@ void RcclAsync::apply(int p, int worker, const float* g) {
   const int64_t n = ranges_[p].second - ranges_[p].first;
   const int64_t t = __atomic_add_fetch(&st->t, 1, __ATOMIC_ACQ_REL);
   if (opt_ == 0) {
-    const float lr_t = (float)((double)lr_ * std::sqrt(1.0 - std::pow((double)b2_, (double)t)) /
-                               (1.0 - std::pow((double)b1_, (double)t)));
+    // TF1 Adam's lr_t in double, as ops/adam.py adam_coeffs (the same bits as the sync path)
+    const float lr_t = (float)(lrd_ * std::sqrt(1.0 - std::pow(b2d_, (double)t)) /
+                               (1.0 - std::pow(b1d_, (double)t)));
     launch_adam(st->params, g, st->m, st->v, n, lr_t, b1_, b2_, eps_, 1.f, cs_);
   } else {
     launch_momentum(st->params, g, st->m, n, lr_, mu_, 1.f, cs_);
@@ -265,7 +267,7 @@ void RcclAsync::loop() {
       }
       std::vector<int> todo;
       {
-        std::lock_guard<std::mutex> g(mu_);
+        std::lock_guard<std::mutex> g(qmu_);
         if (stop_ && pending_.empty() && served_.load() >= expected_) return;
         todo = pending_;
         if (!todo.empty() && !waited_) {
@@ -276,7 +278,7 @@ void RcclAsync::loop() {
       for (int p : todo) {
         if (!push_one(p)) continue;
         progressed = true;
-        std::lock_guard<std::mutex> g(mu_);
+        std::lock_guard<std::mutex> g(qmu_);
         pending_.erase(std::find(pending_.begin(), pending_.end(), p));
         if (pending_.empty()) cv_.notify_all();
         break;  // back to serving incoming requests between sessions
@@ -284,7 +286,7 @@ void RcclAsync::loop() {
       if (!progressed) std::this_thread::sleep_for(std::chrono::microseconds(5));
     }
   } catch (const std::exception& e) {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<std::mutex> g(qmu_);
     error_ = e.what();
     pending_.clear();
     cv_.notify_all();
@@ -294,7 +296,7 @@ void RcclAsync::loop() {
 void RcclAsync::push_pull(hipStream_t compute) {
   TraceRange r("ddl.async.rccl.push_pull");
   HIP_CHECK(hipEventRecord(ev_, compute));
-  std::unique_lock<std::mutex> g(mu_);
+  std::unique_lock<std::mutex> g(qmu_);
   if (!error_.empty()) throw std::runtime_error("rccl async: " + error_);
   for (int p = 0; p < (int)ranges_.size(); ++p) pending_.push_back(p);
   waited_ = false;
@@ -304,7 +306,7 @@ void RcclAsync::push_pull(hipStream_t compute) {
 
 void RcclAsync::join() {
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<std::mutex> g(qmu_);
     stop_ = true;
   }
   if (th_.joinable()) th_.join();

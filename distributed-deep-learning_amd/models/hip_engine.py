@@ -118,7 +118,8 @@ class HipEngine:
 
     # ---- step ----------------------------------------------------------------------------------
     def _eager(self, x, y, seed_t, on_segment):
-        self.eng.forward(x, seed_t, True)
+        # defer_fc: with the fused fc chain the fc forward runs inside segment 0's launch
+        self.eng.forward(x, seed_t, True, True)
         for s in range(len(self.segments)):
             self.eng.backward_segment(s, x, y, seed_t)
             if on_segment is not None:
@@ -136,7 +137,7 @@ class HipEngine:
                 # thread_local: RCCL's watchdog thread keeps polling events while we capture
                 with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
                     if s == 0:
-                        self.eng.forward(self.x_static, self.seed_static, True)
+                        self.eng.forward(self.x_static, self.seed_static, True, True)
                     self.eng.backward_segment(s, self.x_static, self.y_static, self.seed_static)
                 graphs.append(g)
         torch.cuda.current_stream().wait_stream(side)

@@ -90,10 +90,10 @@ class Trainer:
         # Adam step per push, test_async_single_worker_equals_sync).  Run it on the sync step
         # path — the native runner with the update as the optimizer tail of the backward —
         # instead of a private PS copy plus a copy back per step (0.366 vs 0.307 ms/step).
-        # Not with --ref-quirks (Q4: the PS starts from its own init) or an explicit xGMI
-        # exchange (the W = 1 rehearsal of the async data plane).
+        # Not with --ref-quirks (Q4: the PS starts from its own init) or an explicit exchange
+        # backend (--exchange xgmi / rccl: the W = 1 rehearsals of the async data planes).
         self.async_as_sync = (asyncm and W == 1 and not cfg.ref_quirks
-                              and cfg.exchange_backend != "xgmi")
+                              and cfg.exchange_backend == "auto")
         self.servers: Dict[int, ParameterServer] = {}
         for p in hosted:
             own = None
@@ -121,27 +121,42 @@ class Trainer:
         self.history: List[dict] = []
 
     def _make_async_exchange(self, cfg: TrainConfig, env: DistEnv):
-        """xGMI peer-memory async PS (``async_xgmi.py``) when asked for, or by default at W > 1
-        with the HIP engine; otherwise (or if its collective set-up fails on any rank) the
-        RCCL pair-communicator one (``comm.AsyncExchange``)."""
+        """The async data plane.  On a GPU: the xGMI peer-memory exchange (``async_xgmi.py``,
+        no p2p kernels at all) when asked for, or by default at W > 1 with the HIP engine; else
+        point-to-point RCCL in exclusive sessions (``async_rccl.py``, deadlock-free under any
+        stream-to-hardware-queue mapping).  The round-2 Python RCCL pair-group exchange, whose
+        concurrent p2p kernels could block each other's hardware queues, is NOT a GPU fallback
+        any more; it remains the CPU (gloo) implementation."""
         steps = self.steps * cfg.epochs
-        want = cfg.exchange_backend == "xgmi" or (
+        job = _job_id(env)
+        cuda = env.device.type == "cuda"
+        want_xgmi = cfg.exchange_backend == "xgmi" or (
             cfg.exchange_backend == "auto" and env.world > 1 and self.engine.name == "hip")
-        if want and env.device.type == "cuda":
+        import sys
+        if want_xgmi and cuda:
             from .async_xgmi import AsyncPeerExchange, AsyncPeerUnavailable
             try:
                 return AsyncPeerExchange(self.plan, env, self.params, self.grads, self.servers,
                                          steps_per_worker=steps, grad_reduce=cfg.grad_reduce,
                                          check_provenance=cfg.check_provenance,
-                                         optimizer=cfg.optimizer, job_id=_job_id(env))
+                                         optimizer=cfg.optimizer, job_id=job)
             except AsyncPeerUnavailable as e:
                 if env.rank == 0:
-                    import sys
-                    print(f"[ddl_amd] async xGMI exchange unavailable ({e}); using RCCL pairs",
+                    print(f"[ddl_amd] async xGMI exchange unavailable ({e}); using RCCL sessions",
                           file=sys.stderr)
+        if cuda:
+            from .async_rccl import RcclAsyncExchange, RcclAsyncUnavailable
+            try:
+                return RcclAsyncExchange(self.plan, env, self.params, self.grads, self.servers,
+                                         steps_per_worker=steps, job_id=job,
+                                         optimizer=cfg.optimizer,
+                                         check_provenance=cfg.check_provenance)
+            except RcclAsyncUnavailable as e:
+                raise RuntimeError(f"async mode on GPU: neither the xGMI nor the RCCL-session "
+                                   f"exchange is available ({e})") from e
         return AsyncExchange(self.plan, env, self.params, self.grads, self.servers,
                              steps_per_worker=steps, grad_reduce=cfg.grad_reduce,
-                             check_provenance=cfg.check_provenance, job_id=_job_id(env))
+                             check_provenance=cfg.check_provenance, job_id=job)
 
     # ---- one worker step (reference SyncWorker.work + pull + assign) -----------------------------
     def batch(self, step: int):

@@ -126,6 +126,37 @@ def test_gradients_match_autograd(setup, B):
     assert abs(float(eng.eng.buffer("loss", B).mean()) - float(loss.detach())) < 1e-5
 
 
+@pytest.mark.parametrize("B", [100, 37])
+def test_fc_chain_matches_separate_launches(setup, B):
+    """The fused fc chain (csrc/kernels/fc_chain.h: fc1 fwd .. fc1 bwd as one persistent
+    work-queue launch) against the six separate launches: every gradient, h1 / h2, the loss
+    and the conv4 data gradient agree to fp32 summation-order noise, and no stage wait timed
+    out."""
+    eng, flat, params, grads, x, y = setup
+    x, y = x[:B].to(DEV), y[:B].to(DEV)
+    out = []
+    prev = eng.eng.fc_chain()
+    try:
+        for chain in (True, False):
+            eng.eng.set_fc_chain(chain)
+            grads.zero_()
+            eng.forward_backward(x, y, 0.5, 4321)
+            torch.cuda.synchronize()
+            out.append([grads.clone()] + [eng.eng.buffer(n, B).clone() for n in
+                                          ("h1", "h2", "loss", "d4")])
+    finally:
+        eng.eng.set_fc_chain(prev)
+    assert eng.eng.fc_chain_error() == 0
+    for t, a, b in zip(TENSORS, param_views(out[0][0], CANON_OFFSETS),
+                       param_views(out[1][0], CANON_OFFSETS)):
+        assert rel_err(a, b) < 1e-5, t.name
+    for a, b in zip(out[0][1:], out[1][1:]):
+        assert rel_err(a, b) < 1e-5
+    # dropout masks are the same bits: the zero patterns of h1 / h2 agree exactly
+    assert torch.equal(out[0][1] == 0, out[1][1] == 0)
+    assert torch.equal(out[0][2] == 0, out[1][2] == 0)
+
+
 def test_gradients_no_dropout(setup):
     eng, flat, params, grads, x, y = setup
     grads.zero_()
@@ -301,6 +332,10 @@ def test_backward_modes_match(setup, conc, dual):
     """Single-stream dual launches, single-stream back-to-back and the two-stream backward
     compute the same (bitwise: same schedules, same reduction orders) gradients."""
     eng, flat, params, grads, x, y = setup
+    # (the separate fc launches on both sides: the two-stream mode has no fused fc chain, whose
+    # summation order differs — test_fc_chain_matches_separate_launches covers that one)
+    prev = eng.eng.fc_chain()
+    eng.eng.set_fc_chain(False)
     grads.zero_()
     eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 55)
     torch.cuda.synchronize()
@@ -315,6 +350,7 @@ def test_backward_modes_match(setup, conc, dual):
     finally:
         eng.set_concurrent(False)
         eng.set_dual(True)
+        eng.eng.set_fc_chain(prev)
 
 
 def test_graph_replay_matches_eager(setup):
