@@ -680,7 +680,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("fc_chain", [](PyEngine& e) { return e.raw()->fc_chain; })
       .def("fc_chain_error", [](PyEngine& e) { return e.raw()->fc_chain_error(); })
       .def("set_fc_stamps", [](PyEngine& e, c10::optional<at::Tensor> t) {
-        // int64 [items x 4] device tensor (kept alive by the caller), or None to turn off
+        // int64 [items x 8] device tensor (kept alive by the caller), or None to turn off
         e.raw()->fc_stamps = t ? reinterpret_cast<long long*>(t->data_ptr<int64_t>()) : nullptr;
       })
       .def("set_kfix", &PyEngine::set_kfix)

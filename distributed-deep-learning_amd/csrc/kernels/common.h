@@ -78,6 +78,38 @@ DDL_DEV void momentum1(float& w, float g, float& m, float lr, float mu, float sc
   w = __fmaf_rn(-lr, m, w);
 }
 
+// Sum over aligned groups of RL lanes (RL = 1, 2, 4, ..., 64), returned in every lane of the
+// group.  DPP adds inside each 16-lane row (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror: after the quad steps every lane of a quad holds the quad's sum, so the mirrors
+// pair whole partial sums), then the row sums of a 32 / 64 group by v_readlane.  Replaces
+// __shfl_xor trees: each step of those is a ds_bpermute through the LDS pipe, and hipcc issued
+// chains of them one lgkmcnt(0) wait at a time (the fused head spent ~4.6 us per sample on 60
+// of them).  All 64 lanes of the wave must be active.
+template <int CTRL>
+DDL_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               CTRL, 0xF, 0xF, true));
+}
+DDL_DEV float rdlane_f(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+template <int RL>
+DDL_DEV float group_sum(float v) {
+  static_assert(RL >= 1 && RL <= 64 && (RL & (RL - 1)) == 0, "power-of-two lane groups");
+  if constexpr (RL >= 2) v += dpp_f<0xB1>(v);
+  if constexpr (RL >= 4) v += dpp_f<0x4E>(v);
+  if constexpr (RL >= 8) v += dpp_f<0x141>(v);
+  if constexpr (RL >= 16) v += dpp_f<0x140>(v);
+  if constexpr (RL == 32) {
+    const float lo = rdlane_f(v, 0) + rdlane_f(v, 16), hi = rdlane_f(v, 32) + rdlane_f(v, 48);
+    v = (threadIdx.x & 32) ? hi : lo;
+  }
+  if constexpr (RL == 64)
+    v = (rdlane_f(v, 0) + rdlane_f(v, 16)) + (rdlane_f(v, 32) + rdlane_f(v, 48));
+  return v;
+}
+DDL_DEV float wave_sum(float v) { return group_sum<64>(v); }
+
 DDL_DEV float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
 // ---------------------------------------------------------------------------------------------
@@ -124,6 +156,20 @@ DDL_DEV void bstore4_sc1(brsrc_t r, int byte_off, float4 v) {
 DDL_DEV float4 bload4_sc1(brsrc_t r, int byte_off) {
   auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
   return *reinterpret_cast<float4*>(&v);
+}
+
+// 4-byte forms of the same pair (and plain 4-byte store / int load through a descriptor)
+DDL_DEV float bload1_sc1(brsrc_t r, int byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 16));
+}
+DDL_DEV void bstore1_sc1(brsrc_t r, int byte_off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, byte_off, 0, 16);
+}
+DDL_DEV void bstore1(brsrc_t r, int byte_off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, byte_off, 0, 0);
+}
+DDL_DEV int bload1i(brsrc_t r, int byte_off) {
+  return (int)__builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0);
 }
 
 DDL_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }

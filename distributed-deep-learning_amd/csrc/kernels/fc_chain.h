@@ -69,6 +69,7 @@ struct FcChain {
   int* ctr;
   long long timeout_ticks;
   long long* stamps;                   // diagnostics (null: off): per item dequeue / ready / end
+                                       // / block / 4 item-specific, 8 per item
 };
 
 // item ranges
@@ -89,6 +90,9 @@ DDL_DEV int fc_ctr_load(const int* p) {
 
 // lane 0 of wave 0 waits until ctr[i] >= target (bounded: a timeout records FC_ERR and lets
 // the item run on whatever is there, so a bug shows as a wrong result, never as a hang)
+#ifndef DDL_FC_SLEEP
+#define DDL_FC_SLEEP 32
+#endif
 DDL_DEV void fc_wait(const FcChain& a, int i, int target, long long deadline, int it) {
   if (threadIdx.x == 0) {
     while (fc_ctr_load(a.ctr + i) < target) {
@@ -96,9 +100,9 @@ DDL_DEV void fc_wait(const FcChain& a, int i, int target, long long deadline, in
         __hip_atomic_store(a.ctr + FC_ERR, 1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(DDL_FC_SLEEP);
     }
-    if (a.stamps) a.stamps[it * 4 + 1] = wall_clock64();
+    if (a.stamps) a.stamps[it * 8 + 1] = wall_clock64();
   }
   __syncthreads();
 }
@@ -113,99 +117,127 @@ DDL_DEV void fc_publish(const FcChain& a, int i0, int i1 = -1) {
   }
 }
 
-// classifier head of up to 32 samples (row tile mi), one wave per sample, 4 per wave: logits
-// (lane l sums h2 columns 8l .. 8l+7 for the 10 classes, then a butterfly), softmax cross
-// entropy, dlogits = (softmax - onehot) / B, and dpre2 = (dlogits W3^T) with fc2's dropout
-// backward — every handed-off buffer read / written sc1
-DDL_DEV void fc_head(const FcChain& a, int mi) {
+// classifier head of up to 32 samples (row tile mi), one wave per sample, 4 per wave.  W3 is
+// staged once per item into LDS transposed ([HC][HK]) so lane l owns h2 columns l + 64k
+// (coalesced h2 reads / dpre2 stores, conflict-free LDS reads); the 4 rows' h2 loads are all in
+// flight before the first row's math.  Logits (+ butterfly), softmax cross entropy, dlogits =
+// (softmax - onehot) / B, and dpre2 = (dlogits W3^T) with fc2's dropout backward — every
+// handed-off buffer read / written sc1.  Every access goes through a buffer descriptor: with
+// plain pointers the compiler emitted flat loads / stores, each waited for on its own
+// (vmcnt(0) + lgkmcnt(0)), and the item ran 22-40 us.
+DDL_DEV void fc_head(const FcChain& a, int mi, float* w3t, long long* st) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int kT = kFcWaves * 64;
+  static_assert((HK * HC) % kT == 0, "W3 staging: whole rounds");
+  const brsrc_t w3r = make_rsrc(a.w3, HK * HC * 4u), b3r = make_rsrc(a.b3, HC * 4u);
+  const brsrc_t h2r = make_rsrc(a.f2.out, (uint32_t)a.B * HK * 4u);
+  const brsrc_t dpr = make_rsrc(a.dpre2, (uint32_t)a.B * HK * 4u);
+  const brsrc_t dlr = make_rsrc(a.dlog, (uint32_t)a.B * HC * 4u);
+  const brsrc_t lsr = make_rsrc(a.loss, (uint32_t)a.B * 4u);
+  const brsrc_t lbr = make_rsrc(a.labels, (uint32_t)a.B * 8u);
+  const int row0 = mi * 32 + wave * 4;
+#pragma unroll
+  for (int r = 0; r < HK * HC / kT; ++r) {
+    const int j = r * kT + threadIdx.x, i = j / HC, c = j - i * HC;
+    w3t[c * HK + i] = bload1(w3r, j * 4);
+  }
+  // fc2's dropout key (layer 2), as FcFwd / head_fused_kernel derive it
+  const uint32_t key =
+      a.thr24 ? ddl_mix32((a.f2.seed ? *a.f2.seed : a.f2.seed_v) + 2u * 0x9E3779B9u) : 0u;
+  __syncthreads();
+  if (st && threadIdx.x == 0) st[4] = wall_clock64();
+  float b3v[HC];
+#pragma unroll
+  for (int c = 0; c < HC; ++c) b3v[c] = bload1(b3r, c * 4);
+  float hv[HK / 64], hn[HK / 64];
+#pragma unroll
+  for (int k = 0; k < HK / 64; ++k) hn[k] = bload1_sc1(h2r, (row0 * HK + k * 64 + lane) * 4);
   for (int s = 0; s < 4; ++s) {
-    const int row = mi * 32 + wave * 4 + s;
+    const int row = row0 + s;
     if (row >= a.B) break;
-    const brsrc_t hr = make_rsrc(a.f2.out + (size_t)row * HK, HK * 4u);
-    const float4 h0 = bload4_sc1(hr, lane * 32), h1 = bload4_sc1(hr, lane * 32 + 16);
-    const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int k = 0; k < HK / 64; ++k) hv[k] = hn[k];
+    if (s + 1 < 4) {  // (rows past B read 0 through the range check)
+#pragma unroll
+      for (int k = 0; k < HK / 64; ++k)
+        hn[k] = bload1_sc1(h2r, ((row + 1) * HK + k * 64 + lane) * 4);
+    }
     float lg[HC];
 #pragma unroll
-    for (int c = 0; c < HC; ++c) lg[c] = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float* wr = a.w3 + (lane * 8 + k) * HC;
-#pragma unroll
-      for (int c = 0; c < HC; ++c) lg[c] = fmaf(hv[k], wr[c], lg[c]);
-    }
-#pragma unroll
     for (int c = 0; c < HC; ++c) {
-      float v = lg[c];
+      float v = 0.f;
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-      lg[c] = v + a.b3[c];
+      for (int k = 0; k < HK / 64; ++k) v = fmaf(hv[k], w3t[c * HK + k * 64 + lane], v);
+      lg[c] = v;
     }
+#pragma unroll
+    for (int c = 0; c < HC; ++c) lg[c] = wave_sum(lg[c]) + b3v[c];
     float mx = lg[0];
 #pragma unroll
     for (int c = 1; c < HC; ++c) mx = lg[c] > mx ? lg[c] : mx;
     float se = 0.f;
 #pragma unroll
     for (int c = 0; c < HC; ++c) se += __expf(lg[c] - mx);
-    const int lab = (int)a.labels[row];
-    // fc2's dropout key (layer 2), as FcFwd / head_fused_kernel derive it
-    const uint32_t key =
-        a.thr24 ? ddl_mix32((a.f2.seed ? *a.f2.seed : a.f2.seed_v) + 2u * 0x9E3779B9u) : 0u;
+    const int lab = bload1i(lbr, row * 8);  // int64 labels: low word
+    const float inv_se = 1.f / se;
     float dl[HC];
 #pragma unroll
-    for (int c = 0; c < HC; ++c) dl[c] = (__expf(lg[c] - mx) / se - (c == lab ? 1.f : 0.f)) * a.inv_batch;
+    for (int c = 0; c < HC; ++c)
+      dl[c] = (__expf(lg[c] - mx) * inv_se - (c == lab ? 1.f : 0.f)) * a.inv_batch;
     if (lane == 0) {
       float ll = 0.f;
 #pragma unroll
       for (int c = 0; c < HC; ++c)
         if (c == lab) ll = lg[c];
-      a.loss[row] = (mx + __logf(se)) - ll;
+      bstore1(lsr, row * 4, (mx + __logf(se)) - ll);
     }
     if (lane < HC) {
       float v = 0.f;
 #pragma unroll
       for (int c = 0; c < HC; ++c)
         if (c == lane) v = dl[c];
-      st_out<true>(a.dlog + (size_t)row * HC + lane, v);
+      bstore1_sc1(dlr, (row * HC + lane) * 4, v);
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int i = lane * 8 + k;
+    for (int k = 0; k < HK / 64; ++k) {
+      const int i = k * 64 + lane;
       float g = 0.f;
 #pragma unroll
-      for (int c = 0; c < HC; ++c) g = fmaf(dl[c], a.w3[i * HC + c], g);
+      for (int c = 0; c < HC; ++c) g = fmaf(dl[c], w3t[c * HK + i], g);
       const int idx = row * HK + i;
       if (a.thr24) g = ddl_keep(key, (uint32_t)idx, a.thr24) ? g * a.inv_keep : 0.f;
-      st_out<true>(a.dpre2 + idx, g);
+      bstore1_sc1(dpr, idx * 4, g);
     }
+    if (st && threadIdx.x == 0 && s < 3) st[5 + s] = wall_clock64();
   }
 }
 
-// fc3 weight gradient row i (head.h head_wgrad_row with sc1 reads of h2 / dlog)
+// fc3 weight gradient row i (head.h head_wgrad_row with sc1 reads of h2 / dlog), all of a
+// lane's loads in flight at once (B <= 128: two samples per lane)
 DDL_DEV void fc_head_wgrad_row(const FcChain& a, int i) {
   const int lane = threadIdx.x & 63;
+  const brsrc_t h2r = make_rsrc(a.f2.out, (uint32_t)a.B * HK * 4u);
+  const brsrc_t dlr = make_rsrc(a.dlog, (uint32_t)a.B * HC * 4u);
+  float hv[2], dv[2][HC];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int b = lane + 64 * q;
+    hv[q] = i < HK ? bload1_sc1(h2r, (b * HK + i) * 4) : (b < a.B ? 1.f : 0.f);
+#pragma unroll
+    for (int c = 0; c < HC; ++c) dv[q][c] = bload1_sc1(dlr, (b * HC + c) * 4);
+  }
   float acc[HC];
 #pragma unroll
-  for (int c = 0; c < HC; ++c) acc[c] = 0.f;
-  for (int b = lane; b < a.B; b += 64) {
-    const float hv = i < HK ? ld_in<true>(a.f2.out + (size_t)b * HK + i) : 1.f;
+  for (int c = 0; c < HC; ++c) acc[c] = fmaf(hv[1], dv[1][c], hv[0] * dv[0][c]);
 #pragma unroll
-    for (int c = 0; c < HC; ++c) acc[c] = fmaf(hv, ld_in<true>(a.dlog + (size_t)b * HC + c), acc[c]);
-  }
-#pragma unroll
-  for (int c = 0; c < HC; ++c) {
-    float v = acc[c];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    acc[c] = v;
-  }
+  for (int c = 0; c < HC; ++c) acc[c] = wave_sum(acc[c]);
   if (lane < HC) {
     float v = 0.f;
 #pragma unroll
     for (int c = 0; c < HC; ++c)
       if (c == lane) v = acc[c];
-    if (i < HK) a.gw3[i * HC + lane] = v;
-    else a.gb3[lane] = v;
+    if (i < HK) bstore1(make_rsrc(a.gw3, HK * HC * 4u), (i * HC + lane) * 4, v);
+    else bstore1(make_rsrc(a.gb3, HC * 4u), lane * 4, v);
   }
 }
 
@@ -235,7 +267,9 @@ template <class P>
 DDL_FC_ITEM void fc_item_kwave(const P& p, int mi, int nj, float4* lds4, int L) {
   kwave_body<32, kFcWaves>(p, mi, nj, lds4, L);
 }
-DDL_FC_ITEM void fc_item_head(const FcChain& a, int mi) { fc_head(a, mi); }
+DDL_FC_ITEM void fc_item_head(const FcChain& a, int mi, float* w3t, long long* st) {
+  fc_head(a, mi, w3t, st);
+}
 DDL_FC_ITEM void fc_item_head_wgrad(const FcChain& a, int i) {
   if (i <= HK) fc_head_wgrad_row(a, i);
 }
@@ -246,6 +280,7 @@ DDL_FC_ITEM void fc_item_tile(const P& p, int t, int ntiles, int gx, float4* lds
 
 template <int L>
 __global__ void __launch_bounds__(kFcWaves * 64) fc_chain_kernel(FcChain a) {
+  static_assert(kFcWaves * L * 4 >= HK * HC, "the head stages W3 in the staging images");
   __shared__ float4 lds4[kFcWaves * L + 1];  // staging / reduction images + the item word
   int* item_s = reinterpret_cast<int*>(lds4 + kFcWaves * L);
   const long long deadline = wall_clock64() + a.timeout_ticks;
@@ -259,8 +294,8 @@ __global__ void __launch_bounds__(kFcWaves * 64) fc_chain_kernel(FcChain a) {
     if (it >= kFcItems) break;
     const int wave = threadIdx.x >> 6;
     if (a.stamps && threadIdx.x == 0) {
-      a.stamps[it * 4 + 0] = wall_clock64();
-      a.stamps[it * 4 + 3] = blockIdx.x;
+      a.stamps[it * 8 + 0] = wall_clock64();
+      a.stamps[it * 8 + 3] = blockIdx.x;
     }
     if (it < kFcOffB) {                      // A: fc1 forward
       const int mi = it % kFcRowTiles, nj = it / kFcRowTiles;
@@ -274,7 +309,7 @@ __global__ void __launch_bounds__(kFcWaves * 64) fc_chain_kernel(FcChain a) {
     } else if (it < kFcOffD) {               // C: head
       const int mi = it - kFcOffC;
       fc_wait(a, FC_H2 + mi, 16, deadline, it);
-      fc_item_head(a, mi);
+      fc_item_head(a, mi, reinterpret_cast<float*>(lds4), a.stamps ? a.stamps + it * 8 : nullptr);
       fc_publish(a, FC_HD + mi);
     } else if (it < kFcOffE) {               // D: fc2 data gradient (+ fc1 act. backward)
       const int j = it - kFcOffD, mi = j % kFcRowTiles, nj = j / kFcRowTiles;
@@ -298,7 +333,7 @@ __global__ void __launch_bounds__(kFcWaves * 64) fc_chain_kernel(FcChain a) {
       if (mt < 33) fc_item_tile(a.w1, nj * 33 + mt, 33 * 32, 33, lds4, L);
     }
     __syncthreads();  // the staging images are reused by the next item
-    if (a.stamps && threadIdx.x == 0) a.stamps[it * 4 + 2] = wall_clock64();
+    if (a.stamps && threadIdx.x == 0) a.stamps[it * 8 + 2] = wall_clock64();
   }
   // the last workgroup out re-arms every counter for the next launch (all others have taken
   // their final item id: they added to DONE after it)

@@ -1108,13 +1108,10 @@ DDL_DEV void wide_reduce_body(const P& p, const float4* __restrict__ slab, int S
     const float4 t = slab[z * zstride + e];
     s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
   }
-#pragma unroll
-  for (int off = RL / 2; off > 0; off >>= 1) {
-    s.x += __shfl_xor(s.x, off, 64);
-    s.y += __shfl_xor(s.y, off, 64);
-    s.z += __shfl_xor(s.z, off, 64);
-    s.w += __shfl_xor(s.w, off, 64);
-  }
+  s.x = group_sum<RL>(s.x);  // (no lane has left yet: every lane of the wave is active)
+  s.y = group_sum<RL>(s.y);
+  s.z = group_sum<RL>(s.z);
+  s.w = group_sum<RL>(s.w);
   if (!valid || sub != 0) return;
   const int tile = e / G::PART4;
   int r = e % G::PART4;

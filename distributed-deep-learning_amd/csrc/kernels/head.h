@@ -25,10 +25,7 @@ DDL_DEV void head_wgrad_row(const float* __restrict__ h2, const float* __restric
   }
 #pragma unroll
   for (int c = 0; c < HC; ++c) {
-    float v = acc[c];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    acc[c] = v;
+    acc[c] = wave_sum(acc[c]);
   }
   if (lane < HC) {
     float v = 0.f;

@@ -35,9 +35,7 @@ DDL_DEV void head_logits(const float* __restrict__ hr, const float* __restrict__
   }
 #pragma unroll
   for (int c = 0; c < HC; ++c) {
-    float v = acc[c];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    const float v = wave_sum(acc[c]);
     if (lane == 0) part[wave][c] = v;
   }
   __syncthreads();

@@ -22,12 +22,13 @@ def main():
     init_params_(params, CANON_OFFSETS, 0)
     grads = torch.zeros_like(params)
     eng = HipEngine(params, grads, CANON_OFFSETS, batch=100, graph=False, eval_chunk=100)
+    eng.eng.set_fc_chain(True)  # opt-in (api.h)
     x = torch.rand(100, 784, device=dev)
     y = torch.randint(0, 10, (100,), device=dev)
     for i in range(20):
         eng.forward_backward(x, y, 0.5, i)
     n = sum(c for _, c in STAGES)
-    st = torch.zeros(n, 4, dtype=torch.int64, device=dev)
+    st = torch.zeros(n, 8, dtype=torch.int64, device=dev)
     for rep in range(3):
         eng.eng.set_fc_stamps(st)
         eng.forward_backward(x, y, 0.5, 100 + rep)
@@ -49,6 +50,11 @@ def main():
                   f"wait med {wait.median():5.1f} max {wait.max():5.1f}  "
                   f"compute med {comp.median():5.1f} max {comp.max():5.1f}  "
                   f"done {end.min():6.1f}-{end.max():6.1f} us")
+            if name.startswith("C"):
+                for q in range(4):
+                    ph = [(int(r[q, j]) - int(r[q, 1])) / 100 for j in (4, 5, 6, 7)]
+                    print("    head item %d: staged %.1f, rows done %.1f %.1f %.1f us after ready"
+                          % (q, *ph))
             off += cnt
 
 

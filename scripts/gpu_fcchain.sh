@@ -15,7 +15,8 @@ for r in 1 2 3; do
     echo "DDL_FC_CHAIN=$v $(tail -1 gpurun_out/fcab.log | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["ms_per_step"])')"
   done
 done
+timeout -k 10 120 python scripts/fc_chain_probe.py || exit $?
 rm -rf gpurun_out/proft
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/proft -o prof -- python3 bench.py --steps 60 --warmup 10 --tta 0 > gpurun_out/proft.log 2>&1 || exit $?
+DDL_FC_CHAIN=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/proft -o prof -- python3 bench.py --steps 60 --warmup 10 --tta 0 > gpurun_out/proft.log 2>&1 || exit $?
 python3 scripts/step_timeline.py $(find gpurun_out/proft -name "*.db" | head -n 1) --step 40 > gpurun_out/timeline_t.txt 2>&1 || exit $?
 cat gpurun_out/timeline_t.txt
