@@ -22,8 +22,11 @@ import sysconfig
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "distributed-deep-learning_amd")
 CSRC = os.path.join(PKG, "csrc")
-BUILD = os.path.join(PKG, "_build")
-OUT = os.path.join(PKG, "_C.so")
+# DDL_BUILD_TAG=x: a side build (objects in _build_x/, extension _C_x.so) with the compile-time
+# knobs of DDL_EXTRA_CFLAGS, loaded at run time with DDL_SO=_C_x.so (same-box A/B)
+_TAG = os.environ.get("DDL_BUILD_TAG", "")
+BUILD = os.path.join(PKG, "_build" + (f"_{_TAG}" if _TAG else ""))
+OUT = os.path.join(PKG, f"_C_{_TAG}.so" if _TAG else "_C.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")

@@ -172,6 +172,40 @@ DDL_DEV int bload1i(brsrc_t r, int byte_off) {
   return (int)__builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0);
 }
 
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA (MI355X guide: `buffer_load_dwordx4 ... lds`): a 16-byte gather per lane that lands
+// in LDS at (wave-uniform base + lane * 16) without passing through VGPRs.  Issued from inline
+// asm so hipcc's wait-count pass does not see an LDS write it cannot disambiguate (the builtin
+// made it wait vmcnt(0) before every ds_read, draining tiles still in flight): the caller counts
+// completion itself (vm_wait<N>) and retires its own reads of a buffer (lgkm_wait0) before
+// re-staging it.  M0 is written and restored inside the statement (guide: M0 is reserved).
+// ---------------------------------------------------------------------------------------------
+struct Gather16 {  // what a policy's 16-byte operand load reads: descriptor + offsets
+  brsrc_t r;
+  int voff;  // per lane (kOOB: the range check returns zeros)
+  int soff;  // wave-uniform
+};
+DDL_DEV uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+DDL_DEV void dma16(const Gather16& g, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g.voff), "s"(g.r), "s"(lds_dst), "s"(__builtin_amdgcn_readfirstlane(g.soff))
+      : "memory");
+}
+template <int N>
+DDL_DEV void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N == 0 || N == 8, "add the count you need");
+}
+DDL_DEV void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 DDL_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 DDL_DEV float f4get(const float4& v, int i) {

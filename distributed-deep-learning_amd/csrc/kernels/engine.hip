@@ -39,7 +39,10 @@ Engine::Engine() {
   // (round 2, with the tap-skipping K maps of conv3/conv4: conv4 data gradient split-K 4 with
   // a separate reduce instead of stream-K over the full K, 322.2 -> 313.3 us,
   // profiles/r2_runner_tune_kmap.log)
-  static const int defs[OP_COUNT] = {1, 2, 4, 8, 8, 16, 4, 1, 4, 1, 4, 4, 8, 12, 4, 32, 1024};
+  // (round 3, conv forwards on the LDS-DMA main loop: conv2 / conv3 / conv4 forward split-K
+  // 3 / 3 / 6 instead of 2 / 4 / 8, 302.5 -> 299.0 us fwd+bwd, scripts/sched_ab.py
+  // --splits-variants, profiles/r3_sched_ab_ldsdma.log)
+  static const int defs[OP_COUNT] = {1, 3, 3, 6, 8, 16, 4, 1, 4, 1, 4, 4, 8, 12, 4, 32, 1024};
   static const int defw[OP_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
   static const bool inl[OP_COUNT] = {0, 1, 1, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0};

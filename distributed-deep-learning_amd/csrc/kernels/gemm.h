@@ -158,6 +158,24 @@ struct HasLoadB1<P, std::void_t<decltype(std::declval<const P&>().loadB1(
 #define DDL_DIRECT 0
 #endif
 
+// LDS-DMA staging of the one-wave 32x32 tiles (mainloop_dma): 0 off, 1 one LDS image per block
+// (8 KB), 2 two images (16 KB, the next tile's fragment reads overlap this tile's MFMAs).
+// Policies opt in per op with a constexpr DMA and srcA / srcB (the 16-byte gathers of their
+// loadA / loadB): the conv forward (DDL_LDSDMA_FWD) and conv data gradient (DDL_LDSDMA_DGRAD).
+#ifndef DDL_LDSDMA
+#define DDL_LDSDMA 1
+#endif
+#ifndef DDL_LDSDMA_FWD
+#define DDL_LDSDMA_FWD 1
+#endif
+#ifndef DDL_LDSDMA_DGRAD
+#define DDL_LDSDMA_DGRAD 0
+#endif
+template <class P, class = void>
+struct HasDma : std::false_type {};
+template <class P>
+struct HasDma<P, std::void_t<decltype(P::DMA)>> : std::bool_constant<P::DMA> {};
+
 // ---- per-tile building blocks shared by the split-K and stream-K drivers ---------------------
 template <int BM, int BN, int BK, int WM, int WN, class P>
 struct GemmTile {
@@ -198,8 +216,14 @@ struct GemmTile {
 #endif
   static constexpr bool BDIR = DDL_BDIRECT && !DIRECT && SOLO && TM * TN == 1 && BK % 8 == 0 &&
                                !(BK == 16) && !BKC && HasLoadB1<P>::value;
+  // LDS-DMA staging (mainloop_dma): unpadded 32x32 images, swizzled through the gather
+  // addresses (the DMA writes lane-linearly), DDL_LDSDMA images of A + B per block
+  static constexpr bool DMA = DDL_LDSDMA > 0 && HasDma<P>::value && SOLO && TM * TN == 1 &&
+                              BM == 32 && BN == 32 && BK == 32 && AK && !DIRECT && !BDIR;
+  static constexpr int DMA_NB = DDL_LDSDMA > 0 ? DDL_LDSDMA : 1;
   static constexpr int LDS_F4 =
-      DIRECT ? 0 : (NBUF * (A_ELEMS + (BDIR ? 0 : B_ELEMS))) / 4;
+      DMA ? DMA_NB * 512
+          : DIRECT ? 0 : (NBUF * (A_ELEMS + (BDIR ? 0 : B_ELEMS))) / 4;
   // A wave with a single 32x32 fragment alternates two accumulator chains (summed at the
   // end) so consecutive MFMAs are independent.
   // (DDL_TWO_CHAINS=0: one chain; gfx950 forwards a 32x32 MFMA's result to the next one's
@@ -228,7 +252,8 @@ struct GemmTile {
   // [kb, ke) is virtual (window w) for K-map policies
   static DDL_DEV void mainloop(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
                                f32x16 (&acc)[TM][TN], const Win& w = Win()) {
-    if constexpr (DIRECT) mainloop_direct(p, m_blk, n_blk, kb, ke, acc, w);
+    if constexpr (DMA) mainloop_dma(p, m_blk, n_blk, kb, ke, lds, acc, w);
+    else if constexpr (DIRECT) mainloop_direct(p, m_blk, n_blk, kb, ke, acc, w);
     else if constexpr (PIPE) mainloop_pipe(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else mainloop_basic(p, m_blk, n_blk, kb, ke, lds, acc, w);
   }
@@ -467,6 +492,144 @@ struct GemmTile {
     }
     if constexpr (NCH == 2) acc[0][0] = c0 + c1;
     else acc[0][0] = c0;
+  }
+
+  static DDL_DEV Gather16 srcA(const P& p, const typename P::AInfo& a, int k, const Win& w) {
+    if constexpr (KM) return p.srcA(a, k, w);
+    else return p.srcA(a, k);
+  }
+  static DDL_DEV Gather16 srcB(const P& p, const typename P::BInfo& b, int k, const Win& w) {
+    if constexpr (KM) return p.srcB(b, k, w);
+    else return p.srcB(b, k);
+  }
+
+  // LDS-DMA loop (one wave, one 32x32 fragment, BK = 32).  Each K tile is 8 DMA instructions
+  // (A and B: 4 x 1 KB) straight into an unpadded LDS image; no staging VGPRs and no ds_write.
+  // The image is lane-linear, so the conflict-free layout is made on the GATHER side (guide
+  // rule 21): a K-contiguous operand's 16-byte quad q of row r sits at quad q ^ ((r >> 1) & 7)
+  // (the 16 lanes of a ds_read_b128 pass then hit 16 different bank groups), an MN-contiguous
+  // operand's k-row k at row k ^ ((k >> 2) & 1) (the two lane halves of a fragment read, k and
+  // k + 4, land in opposite bank halves).  The MFMA order (k pairs, two accumulator chains) is
+  // the basic loop's, so both give the same bits.
+  // NB = 2: tile t+2 is DMA'd while tile t's MFMAs run and tile t+1's fragments are read, in
+  // a second LDS image and a second fragment register set (the loop is unrolled by two so
+  // both stay static).  NB = 1: tile t+1 is DMA'd into the one image once tile t's fragments
+  // are in registers.  Completion is counted by hand (vm_wait: 8 DMAs per tile).
+  static DDL_DEV void mainloop_dma(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
+                                   f32x16 (&acc)[TM][TN], const Win& w) {
+    static_assert(FA == 4 && FB == 4 && R == 4, "32x32x32 one-wave tile");
+    const int lane = threadIdx.x & 63;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int nk = (ke - kb + BK - 1) / BK;
+    typename P::AInfo ai[4];
+    typename P::BInfo bi[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int sl = it * 64 + lane, row = sl >> 3, q = sl & 7;
+      ai[it] = p.prepA(m_blk + row, (q ^ ((row >> 1) & 7)) * 4);
+      if constexpr (BKC) bi[it] = p.prepB(n_blk + row, (q ^ ((row >> 1) & 7)) * 4);
+      else bi[it] = p.prepB(n_blk + q * 4, row ^ ((row >> 2) & 1));
+    }
+    const uint32_t base = lds_addr(lds);
+    auto dma = [&](int k0, int buf) {
+      const uint32_t b0 = base + buf * 8192;
+#pragma unroll
+      for (int it = 0; it < 4; ++it) dma16(srcA(p, ai[it], k0, w), b0 + it * 1024);
+#pragma unroll
+      for (int it = 0; it < 4; ++it) dma16(srcB(p, bi[it], k0, w), b0 + 4096 + it * 1024);
+    };
+    // fragments of K step (r, s): lane half h holds k = 8r + 4h + s (the basic loop's order)
+    auto rd = [&](int buf, float (&av)[R][4], float (&bv)[R][4]) {
+      const float* As = lds + buf * 2048;
+      const float* Bs = As + 1024;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int q = (2 * r + lh) ^ ((lr >> 1) & 7);
+        const float4 t = *reinterpret_cast<const float4*>(As + lr * 32 + q * 4);
+        av[r][0] = t.x; av[r][1] = t.y; av[r][2] = t.z; av[r][3] = t.w;
+        if constexpr (BKC) {
+          const float4 u = *reinterpret_cast<const float4*>(Bs + lr * 32 + q * 4);
+          bv[r][0] = u.x; bv[r][1] = u.y; bv[r][2] = u.z; bv[r][3] = u.w;
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) bv[r][s] = Bs[((8 * r + 4 * lh + s) ^ lh) * 32 + lr];
+        }
+      }
+    };
+    f32x16 acc2;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      acc2[q] = 0.f;
+      acc[0][0][q] = 0.f;
+    }
+    // K steps [r0, r1) of a tile (inline asm is a scheduling barrier, so the split decides
+    // where the next tile's wait + fragment reads sit inside the MFMA stream)
+    auto mma = [&](const float (&av)[R][4], const float (&bv)[R][4], int r0 = 0, int r1 = R) {
+#if DDL_MFMA_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+      for (int r = r0; r < r1; ++r)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          if constexpr (NCH == 2) {
+            if (s & 1) acc2 = mfma32x32x2(av[r][s], bv[r][s], acc2);
+            else acc[0][0] = mfma32x32x2(av[r][s], bv[r][s], acc[0][0]);
+          } else {
+            acc[0][0] = mfma32x32x2(av[r][s], bv[r][s], acc[0][0]);
+          }
+        }
+#if DDL_MFMA_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
+    };
+    if (nk > 0) {
+      float a0[R][4], b0[R][4];
+      if constexpr (DMA_NB == 1) {
+        dma(kb, 0);
+        for (int kt = 0; kt < nk; ++kt) {
+          vm_wait<0>();   // tile kt is in the image
+          rd(0, a0, b0);
+          lgkm_wait0();   // its fragments are in registers: the image may be restaged
+          if (kt + 1 < nk) dma(kb + (kt + 1) * BK, 0);
+          mma(a0, b0);
+        }
+      } else {
+        float a1[R][4], b1[R][4];
+        dma(kb, 0);
+        if (nk > 1) {
+          dma(kb + BK, 1);
+          vm_wait<8>();
+        } else {
+          vm_wait<0>();
+        }
+        rd(0, a0, b0);
+        // (half of a tile's MFMAs are issued before the wait for the next tile's DMA, so the
+        // wave never stalls on it with an empty MFMA pipe)
+        for (int kt = 0; kt < nk; kt += 2) {
+          lgkm_wait0();  // set 0 (tile kt) in registers, image 0 free
+          if (kt + 2 < nk) dma(kb + (kt + 2) * BK, 0);
+          mma(a0, b0, 0, R / 2);
+          if (kt + 1 < nk) {
+            if (kt + 2 < nk) vm_wait<8>();
+            else vm_wait<0>();
+            rd(1, a1, b1);  // tile kt+1's reads overlap tile kt's MFMAs
+          }
+          mma(a0, b0, R / 2, R);
+          if (kt + 1 >= nk) break;
+          lgkm_wait0();  // set 1 (tile kt+1) in registers, image 1 free
+          if (kt + 3 < nk) dma(kb + (kt + 3) * BK, 1);
+          mma(a1, b1, 0, R / 2);
+          if (kt + 2 < nk) {
+            if (kt + 3 < nk) vm_wait<8>();
+            else vm_wait<0>();
+            rd(0, a0, b0);
+          }
+          mma(a1, b1, R / 2, R);
+        }
+      }
+    }
+    if constexpr (NCH == 2) acc[0][0] += acc2;
   }
 
   static DDL_DEV void mainloop_basic(const P& p, int m_blk, int n_blk, int kb, int ke,
@@ -889,8 +1052,10 @@ __global__ void __launch_bounds__(WM * WN * 64) DDL_GEMM_OCC
 gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets,
                 int xcd) {
   using T = GemmTile<BM, BN, BK, WM, WN, P>;
-  __shared__ float4 lds4[T::LDS_F4 + 1];  // staging images + last-arriver flag (one array:
-                                          // guide §5 trap 4a)
+  // staging images; the last-arriver flag reuses the first word (arrive() runs after the main
+  // loop, whose last LDS reads have retired) — one array (guide §5 trap 4a), and no extra 16 B
+  // that would push an 8 / 16 KB LDS-DMA block past an occupancy step
+  __shared__ float4 lds4[T::LDS_F4 > 0 ? T::LDS_F4 : 1];
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   if (xcd) {  // linear id (x fastest, the dispatch order) -> XCD-contiguous virtual id
     const int gx = gridDim.x, gy = gridDim.y;
@@ -901,7 +1066,7 @@ gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __res
   }
   splitk_body<BM, BN, BK, WM, WN, P>(p, kchunk, mode, slab, tickets, bx, by, bz, gridDim.x,
                                      gridDim.y, gridDim.z, reinterpret_cast<float*>(lds4),
-                                     reinterpret_cast<int*>(lds4 + T::LDS_F4));
+                                     reinterpret_cast<int*>(lds4));
 }
 
 template <int BM, int BN, int BK, int WM, int WN, class P>
@@ -909,10 +1074,10 @@ __global__ void __launch_bounds__(WM * WN * 64)
 gemm_streamk_kernel(P p, int KI, int gx, long long I, float4* __restrict__ slab,
                     int* __restrict__ tickets) {
   using T = GemmTile<BM, BN, BK, WM, WN, P>;
-  __shared__ float4 lds4[T::LDS_F4 + 1];
+  __shared__ float4 lds4[T::LDS_F4 > 0 ? T::LDS_F4 : 1];  // (flag in the first word: see above)
   streamk_body<BM, BN, BK, WM, WN, P>(p, KI, gx, I, slab, tickets, blockIdx.x, gridDim.x,
                                       reinterpret_cast<float*>(lds4),
-                                      reinterpret_cast<int*>(lds4 + T::LDS_F4));
+                                      reinterpret_cast<int*>(lds4));
 }
 
 // K split inside ONE workgroup, for the skinny GEMMs (the fc layers at M = batch): KW waves each
@@ -1064,10 +1229,11 @@ gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut, int bfirst) {
   static_assert(CA::NT == 64 && CB::NT == 64, "dual launch needs one-wave blocks");
   using TA = GemmTile<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>;
   using TB = GemmTile<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>;
-  constexpr int L = TA::LDS_F4 > TB::LDS_F4 ? TA::LDS_F4 : TB::LDS_F4;
-  __shared__ float4 lds4[L + 1];
+  constexpr int L0 = TA::LDS_F4 > TB::LDS_F4 ? TA::LDS_F4 : TB::LDS_F4;
+  constexpr int L = L0 > 0 ? L0 : 1;
+  __shared__ float4 lds4[L];  // (the last-arriver flag in the first word: gemm_f32_kernel)
   float* lds = reinterpret_cast<float*>(lds4);
-  int* flag = reinterpret_cast<int*>(lds4 + L);
+  int* flag = reinterpret_cast<int*>(lds4);
   const int gemm_blocks = ga.nblocks + gb.nblocks;
   int b = blockIdx.x;
   if (ut.first_) {

@@ -179,12 +179,27 @@ struct ConvFwd {
     a.voff = (a.ok ? (b * HI + a.y) * HI * CIN + a.x * CIN + kk : kk) * 4;
     return a;
   }
+  // the 16-byte gather of the halo-input forms (also the LDS-DMA source, gemm.h mainloop_dma)
+  static constexpr bool DMA = PADIN && DDL_LDSDMA_FWD;
+  DDL_DEV Gather16 srcA(const AInfo& a, int k0) const {
+    const int tap = k0 / CIN, cib = k0 - tap * CIN;
+    const int ky = tap / 5, kx = tap - ky * 5;
+    return {make_rsrc(x, x_bytes()), a.voff, ((ky * HI + kx) * CIN + cib) * 4};
+  }
+  DDL_DEV Gather16 srcA(const AInfo& a, int kv, const KWin& win) const {
+    return srcA(a, kreal(win, kv));
+  }
+  DDL_DEV Gather16 srcB(const BInfo& b, int k0) const {
+    return {make_rsrc(w, 25u * CIN * COUT * 4u), b.ok ? b.off * 4 : kOOB, k0 * COUT * 4};
+  }
+  DDL_DEV Gather16 srcB(const BInfo& b, int kv, const KWin& win) const {
+    return srcB(b, kreal(win, kv));
+  }
   DDL_DEV float4 loadA(const AInfo& a, int k0) const {
     const brsrc_t r = make_rsrc(x, x_bytes());
     if constexpr (PADIN) {
-      const int tap = k0 / CIN, cib = k0 - tap * CIN;
-      const int ky = tap / 5, kx = tap - ky * 5;
-      return bload4_so(r, a.voff, ((ky * HI + kx) * CIN + cib) * 4);
+      const Gather16 g = srcA(a, k0);
+      return bload4_so(g.r, g.voff, g.soff);
     } else {  // CIN == 1: k = tap, 4 taps per float4
       float v[4];
 #pragma unroll
@@ -209,7 +224,8 @@ struct ConvFwd {
   DDL_DEV float4 loadB(const BInfo& b, int k0) const {
     const brsrc_t r = make_rsrc(w, 25u * CIN * COUT * 4u);
     if constexpr (PADIN) {  // K = 25*CIN is a whole number of tiles (loop-invariant guard)
-      return bload4_so(r, b.ok ? b.off * 4 : kOOB, k0 * COUT * 4);
+      const Gather16 g = srcB(b, k0);
+      return bload4_so(g.r, g.voff, g.soff);
     } else {
       const bool good = b.ok && k0 + b.kk < K;
       return bload4(r, good ? (b.off + k0 * COUT) * 4 : kOOB);
@@ -360,17 +376,32 @@ struct ConvDgrad {
     return {(((b * HI + y) * HI + x) * COUT + kk) * 4};
   }
   // output gradient at (y - ky + 2, x - kx + 2) = halo pixel (y + 4 - ky, x + 4 - kx)
-  DDL_DEV float4 loadA(const AInfo& a, int k0) const {
-    const brsrc_t r = make_rsrc(dpre, (uint32_t)(M / (H * H)) * HI * HI * COUT * 4u);
+  static constexpr bool DMA = DDL_LDSDMA_DGRAD;
+  DDL_DEV Gather16 srcA(const AInfo& a, int k0) const {
     const int tap = k0 / COUT, cob = k0 - tap * COUT;
     const int ky = tap / 5, kx = tap - ky * 5;
-    return bload4_so(r, a.voff, (((2 * kHalo - ky) * HI + (2 * kHalo - kx)) * COUT + cob) * 4);
+    return {make_rsrc(dpre, (uint32_t)(M / (H * H)) * HI * HI * COUT * 4u), a.voff,
+            (((2 * kHalo - ky) * HI + (2 * kHalo - kx)) * COUT + cob) * 4};
   }
   DDL_DEV BInfo prepB(int n, int kk) const { return {n * COUT + kk, kk, n < N}; }
-  DDL_DEV float4 loadB(const BInfo& b, int k0) const {
-    const brsrc_t r = make_rsrc(w, 25u * CIN * COUT * 4u);
+  DDL_DEV Gather16 srcB(const BInfo& b, int k0) const {
     const int tap = k0 / COUT, cob = k0 - tap * COUT;
-    return bload4_so(r, b.ok ? b.off * 4 : kOOB, (tap * CIN * COUT + cob) * 4);
+    return {make_rsrc(w, 25u * CIN * COUT * 4u), b.ok ? b.off * 4 : kOOB,
+            (tap * CIN * COUT + cob) * 4};
+  }
+  DDL_DEV Gather16 srcA(const AInfo& a, int kv, const KWin& win) const {
+    return srcA(a, kreal(win, kv));
+  }
+  DDL_DEV Gather16 srcB(const BInfo& b, int kv, const KWin& win) const {
+    return srcB(b, kreal(win, kv));
+  }
+  DDL_DEV float4 loadA(const AInfo& a, int k0) const {
+    const Gather16 g = srcA(a, k0);
+    return bload4_so(g.r, g.voff, g.soff);
+  }
+  DDL_DEV float4 loadB(const BInfo& b, int k0) const {
+    const Gather16 g = srcB(b, k0);
+    return bload4_so(g.r, g.voff, g.soff);
   }
   DDL_DEV float4 loadA(const AInfo& a, int kv, const KWin& win) const {
     return loadA(a, kreal(win, kv));

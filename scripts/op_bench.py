@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--m1-max", type=int, default=32,
                     help="also sweep split-K with the in-launch reduce for splits <= this")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--ops", default="", help="comma-separated op names (default: all)")
+    ap.add_argument("--no-step", action="store_true", help="skip the whole-step timing")
     a = ap.parse_args()
     from ddl_amd.models.layout import CANON_OFFSETS, TOTAL_NUMEL
     from ddl_amd.models.mnist_cnn import init_params_
@@ -63,7 +65,10 @@ def main():
     base_cfg = eng.get_cfg()
     base_w = eng.get_workers()
     best_cfg, best_split, best_w = list(base_cfg), list(base), list(base_w)
+    only = set(a.ops.split(",")) if a.ops else None
     for op, name in enumerate(OPS):
+        if only is not None and name not in only:
+            continue
         M, N, K = eng.eng.op_shape(op, B)
         flop = 2.0 * M * N * K
         row = {}
@@ -113,7 +118,7 @@ def main():
     eng.set_workers(best_w)
     eng.set_wide(best_wide)
     # whole step eager vs graph
-    for g in (False, True):
+    for g in ((False, True) if not a.no_step else ()):
         e2 = HipEngine(params, grads, CANON_OFFSETS, batch=B, graph=g, eval_chunk=B)
         e2.set_concurrent(False)
         e2.set_cfg(best_cfg)

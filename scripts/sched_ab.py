@@ -18,6 +18,8 @@ def main():
     ap.add_argument("tuned", nargs="*")
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--splits-variants", default="",
+                    help="';'-separated split overrides of the defaults, each 'op=s,op=s'")
     a = ap.parse_args()
     import torch
     from ddl_amd.config import TrainConfig
@@ -34,6 +36,12 @@ def main():
                           "workers": e.get_workers(), "wide": e.get_wide()}}
     for p in a.tuned:
         scheds[os.path.basename(p)] = json.load(open(p))
+    for v in filter(None, a.splits_variants.split(";")):
+        sp = list(scheds["default"]["splits"])
+        for kv in v.split(","):
+            op, val = kv.split("=")
+            sp[int(op)] = int(val)
+        scheds["splits[" + v + "]"] = dict(scheds["default"], splits=sp)
     res = {k: [] for k in scheds}
     step = 0
     for _ in range(a.rounds):
