@@ -530,6 +530,7 @@ class SyncRunner {
   hipEvent_t seg_ev_dev_[kSegments] = {};  // device-scope release (xGMI-only segments)
   bool seg_xgmi_only_[kSegments] = {};
   bool seg_offstream_[kSegments] = {};     // the segment has units on the comm stream
+  int seg_launches_[kSegments] = {};       // kernel launches of the segment in the last step
   // seg events recorded by the segment's own kernel packets (DDL_EXT_EVENT, default on)
   bool ext_event_ = true;
   hipEvent_t done_ev_ = nullptr;

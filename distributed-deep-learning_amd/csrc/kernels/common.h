@@ -9,19 +9,41 @@
 #include <hip/hip_ext.h>
 
 namespace ddl {
-// Completion event bound to the engine's kernel launches (host thread-local).  While set, every
+// Completion event bound to the engine's kernel launches (host thread-local).  While set, a
 // DDL_LAUNCH records it through the kernel's OWN dispatch packet (hipExtLaunchKernelGGL stop
-// event) instead of a separate hipEventRecord marker packet: the runner waits on the event after
-// the segment's last launch, so it fires when that kernel completes.  A marker packet after the
-// segment cost ~5 us of compute-queue idle per issue point (forced-rehearsal timelines).
-inline hipEvent_t& launch_stop_event() {
-  static thread_local hipEvent_t ev = nullptr;
-  return ev;
+// event) instead of a separate hipEventRecord marker packet.  A marker after the segment cost
+// ~5 us of compute-queue idle per issue point (forced-rehearsal timelines) — and so does every
+// kernel that carries the event, so a scope binds it to ONE launch: `target` (its index in the
+// scope), or every launch when target < 0.  The scope reports how many launches it saw and
+// which one got the event, so a caller that predicted the last launch wrong can fall back to
+// a marker (SyncRunner::step).
+struct StopCtl {
+  hipEvent_t ev = nullptr;
+  int target = -1;  // launch index to bind (< 0: all)
+  int n = 0;        // launches issued in the scope
+  int bound = -1;   // index of the last launch that got the event
+};
+inline StopCtl& stop_ctl() {
+  static thread_local StopCtl c;
+  return c;
 }
-// RAII: the DDL_LAUNCHes inside the scope carry `ev` as their completion event
+// the event for the next launch, or null (advances the scope's launch count)
+inline hipEvent_t take_stop_event() {
+  StopCtl& c = stop_ctl();
+  if (!c.ev) return nullptr;
+  const int i = c.n++;
+  if (c.target >= 0 && i != c.target) return nullptr;
+  c.bound = i;
+  return c.ev;
+}
+// RAII: the DDL_LAUNCHes inside the scope carry `ev` (launch `target` only, or all)
 struct StopEventScope {
-  explicit StopEventScope(hipEvent_t ev) { launch_stop_event() = ev; }
-  ~StopEventScope() { launch_stop_event() = nullptr; }
+  explicit StopEventScope(hipEvent_t ev, int target = -1) {
+    stop_ctl() = StopCtl{ev, target, 0, -1};
+  }
+  ~StopEventScope() { stop_ctl() = StopCtl{}; }
+  int launches() const { return stop_ctl().n; }
+  int bound() const { return stop_ctl().bound; }
   StopEventScope(const StopEventScope&) = delete;
   StopEventScope& operator=(const StopEventScope&) = delete;
 };
@@ -29,7 +51,7 @@ struct StopEventScope {
 
 #define DDL_LAUNCH(kernel, grid, block, shmem, stream, ...)                                     \
   do {                                                                                          \
-    if (hipEvent_t ddl_ev_ = ::ddl::launch_stop_event())                                        \
+    if (hipEvent_t ddl_ev_ = ::ddl::take_stop_event())                                          \
       hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, nullptr, ddl_ev_, 0,             \
                             __VA_ARGS__);                                                       \
     else                                                                                        \

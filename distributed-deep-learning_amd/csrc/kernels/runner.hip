@@ -350,10 +350,19 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
     // kernel launches themselves (the wait below is issued after the last one) rather than a
     // marker packet behind them
     const bool bind = ext_event_ && !on_main && seg_offstream_[s];
+    // bound to the segment's LAST launch (its count is learned from the previous step; a
+    // wrong or unknown count falls back to a marker record below, which supersedes the binding)
+    bool marker = !bind;
     {
       TraceRange r(kBwdRange[s]);
-      StopEventScope scope(bind ? ev : nullptr);
+      StopEventScope scope(bind ? ev : nullptr, seg_launches_[s] > 0 ? seg_launches_[s] - 1
+                                                                      : 1 << 30);
       eng_->backward_segment(s, x, labels, B, seed, st);
+      if (bind) {
+        const int n = scope.launches();
+        if (scope.bound() != n - 1) marker = true;
+        seg_launches_[s] = n;
+      }
     }
     TraceRange ex_range(kExRange[s]);
     hipStream_t xs = on_main ? st : cs_;
@@ -367,7 +376,7 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
         continue;
       }
       if (!waited) {
-        if (!bind) HIP_CHECK(hipEventRecord(ev, st));
+        if (marker) HIP_CHECK(hipEventRecord(ev, st));
         HIP_CHECK(hipStreamWaitEvent(cs_, ev, 0));
         waited = true;
       }
