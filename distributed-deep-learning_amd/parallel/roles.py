@@ -70,7 +70,20 @@ class Trainer:
             raise ValueError("mode 'single' runs in one process")
         self.num_ps = resolve_num_ps(cfg, W)
         segs = engine_segments(cfg.engine, env.device)
-        buckets = segs if (cfg.shard == "flat" and cfg.overlap and cfg.mode == "sync") else None
+        asyncm = cfg.mode == "async"
+        # One worker and its own PS (async, W = 1): every push is applied before the worker's
+        # next step, so the PS parameters ARE the worker's and the math is the sync PS's (one
+        # Adam step per push, test_async_single_worker_equals_sync).  Run it on the sync step
+        # path — the native runner with the update as the optimizer tail of the backward —
+        # instead of a private PS copy plus a copy back per step (0.366 vs 0.307 ms/step), and
+        # with the sync path's per-segment buckets (one end-of-step update instead of the
+        # backward's optimizer tails: 0.307 vs 0.300).  Not with --ref-quirks (Q4: the PS
+        # starts from its own init) or an explicit exchange backend (--exchange xgmi / rccl:
+        # the W = 1 rehearsals of the async data planes).
+        self.async_as_sync = (asyncm and W == 1 and not cfg.ref_quirks
+                              and cfg.exchange_backend == "auto")
+        sync_step = cfg.mode == "sync" or self.async_as_sync
+        buckets = segs if (cfg.shard == "flat" and cfg.overlap and sync_step) else None
         shard = "none" if cfg.mode == "single" else cfg.shard
         self.plan = make_plan(shard, self.num_ps, buckets=buckets)
         dev = env.device
@@ -84,16 +97,6 @@ class Trainer:
                                   dev, cfg.batch_size, graph=cfg.graph)
         hyper = AdamHyper(lr=cfg.lr)
         hosted = [p for p in range(self.num_ps) if self.plan.host_rank(p, W) == r]
-        asyncm = cfg.mode == "async"
-        # One worker and its own PS (async, W = 1): every push is applied before the worker's
-        # next step, so the PS parameters ARE the worker's and the math is the sync PS's (one
-        # Adam step per push, test_async_single_worker_equals_sync).  Run it on the sync step
-        # path — the native runner with the update as the optimizer tail of the backward —
-        # instead of a private PS copy plus a copy back per step (0.366 vs 0.307 ms/step).
-        # Not with --ref-quirks (Q4: the PS starts from its own init) or an explicit exchange
-        # backend (--exchange xgmi / rccl: the W = 1 rehearsals of the async data planes).
-        self.async_as_sync = (asyncm and W == 1 and not cfg.ref_quirks
-                              and cfg.exchange_backend == "auto")
         self.servers: Dict[int, ParameterServer] = {}
         for p in hosted:
             own = None

@@ -1,7 +1,8 @@
 // Cost of a cross-stream hand-off point on the producer stream: a hipEventRecord marker between
 // two kernels vs the same event attached to the producing kernel's launch (hipExtLaunchKernelGGL
-// stopEvent, the kernel's own completion signal).  The consumer stream waits on the event and
-// runs a short kernel each time, like the W > 1 step's exchange stream.
+// stopEvent, the kernel's own completion signal), over event flags and consumer set-ups.  The
+// consumer stream waits on the event and runs a short kernel each time, like the W > 1 step's
+// exchange stream.  Prints us per step (4 producer kernels, 3 hand-offs) per variant, twice.
 //   hipcc --offload-arch=gfx950 -O3 -o /tmp/event_probe scripts/event_probe.hip && /tmp/event_probe
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
@@ -23,39 +24,63 @@ __global__ void work(float* out, int iters) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = a;
 }
 
+struct Variant {
+  const char* name;
+  int handoff;      // 0 none, 1 marker (hipEventRecord), 2 stop event on the kernel launch
+  unsigned flags;   // event creation flags
+  int consumer;     // 0: nobody waits, 1: consumer stream waits + runs a kernel
+  int hiprio;       // consumer stream at high priority (the runner's comm stream)
+};
+
 int main() {
   float *buf, *buf2;
   CK(hipMalloc(&buf, 4096 * 256 * sizeof(float)));
   CK(hipMalloc(&buf2, 64 * 256 * sizeof(float)));
-  hipStream_t s1, s2;
+  int lo = 0, hi = 0;
+  CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  hipStream_t s1, s2, s2h;
   CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-  hipEvent_t ev[4], t0, t1;
-  for (int i = 0; i < 4; ++i)
-    CK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming | hipEventDisableSystemFence));
+  CK(hipStreamCreateWithPriority(&s2h, hipStreamNonBlocking, hi));
+  hipEvent_t t0, t1;
   CK(hipEventCreate(&t0));
   CK(hipEventCreate(&t1));
+  const unsigned DT = hipEventDisableTiming;
+  const Variant vs[] = {
+      {"no hand-off", 0, DT, 0, 0},
+      {"marker, sysfence, consumer", 1, DT, 1, 1},
+      {"marker, no-sysfence, consumer", 1, DT | hipEventDisableSystemFence, 1, 1},
+      {"stop, sysfence, consumer", 2, DT, 1, 1},
+      {"stop, no-sysfence, consumer", 2, DT | hipEventDisableSystemFence, 1, 1},
+      {"stop, release-to-device, consumer", 2, DT | hipEventReleaseToDevice, 1, 1},
+      {"stop, no-sysfence, no consumer", 2, DT | hipEventDisableSystemFence, 0, 1},
+      {"marker, no-sysfence, no consumer", 1, DT | hipEventDisableSystemFence, 0, 1},
+      {"stop, no-sysfence, consumer lo-prio", 2, DT | hipEventDisableSystemFence, 1, 0},
+  };
   const int blocks = 2048, iters = 4000, steps = 200, seg = 4;
-  for (int mode = 0; mode < 3; ++mode) {
-    for (int rep = 0; rep < 2; ++rep) {
+  for (int rep = 0; rep < 2; ++rep) {
+    for (const Variant& v : vs) {
+      hipEvent_t ev[4];
+      for (int i = 0; i < 4; ++i) CK(hipEventCreateWithFlags(&ev[i], v.flags));
+      hipStream_t sc = v.hiprio ? s2h : s2;
       CK(hipDeviceSynchronize());
       CK(hipEventRecord(t0, s1));
       for (int st = 0; st < steps; ++st) {
         for (int k = 0; k < seg; ++k) {
-          if (mode == 2 && k < seg - 1) {  // stop event on the kernel's own completion signal
+          const bool h = v.handoff && k < seg - 1;
+          if (h && v.handoff == 2)
             hipExtLaunchKernelGGL(work, dim3(blocks), dim3(256), 0, s1, nullptr, ev[k], 0, buf,
                                   iters);
-          } else {
+          else
             hipLaunchKernelGGL(work, dim3(blocks), dim3(256), 0, s1, buf, iters);
-          }
-          if (mode == 1 && k < seg - 1) CK(hipEventRecord(ev[k], s1));  // marker packet
-          if (mode > 0 && k < seg - 1) {
-            CK(hipStreamWaitEvent(s2, ev[k], 0));
-            hipLaunchKernelGGL(work, dim3(64), dim3(256), 0, s2, buf2, iters / 4);
+          if (h && v.handoff == 1) CK(hipEventRecord(ev[k], s1));
+          if (h && v.consumer) {
+            CK(hipStreamWaitEvent(sc, ev[k], 0));
+            hipLaunchKernelGGL(work, dim3(64), dim3(256), 0, sc, buf2, iters / 4);
           }
         }
-        if (mode > 0) {  // the producer waits for the consumer at the end of the step
-          CK(hipEventRecord(ev[3], s2));
+        if (v.handoff && v.consumer) {  // the producer waits for the consumer at step end
+          CK(hipEventRecord(ev[3], sc));
           CK(hipStreamWaitEvent(s1, ev[3], 0));
         }
       }
@@ -63,8 +88,8 @@ int main() {
       CK(hipEventSynchronize(t1));
       float ms;
       CK(hipEventElapsedTime(&ms, t0, t1));
-      const char* name[] = {"no hand-off", "hipEventRecord marker", "ext-launch stop event"};
-      printf("%-24s %.2f us/step\n", name[mode], 1e3f * ms / steps);
+      printf("%-40s %8.2f us/step\n", v.name, 1e3f * ms / steps);
+      for (int i = 0; i < 4; ++i) CK(hipEventDestroy(ev[i]));
     }
   }
   return 0;
