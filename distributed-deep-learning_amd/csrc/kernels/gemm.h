@@ -171,6 +171,15 @@ struct HasLoadB1<P, std::void_t<decltype(std::declval<const P&>().loadB1(
 #ifndef DDL_LDSDMA_DGRAD
 #define DDL_LDSDMA_DGRAD 0
 #endif
+#ifndef DDL_LDSDMA_WGRAD
+#define DDL_LDSDMA_WGRAD 0
+#endif
+// a policy whose A operand has rows that are not in memory (the weight gradients' ones row)
+template <class P, class = void>
+struct HasOnesA : std::false_type {};
+template <class P>
+struct HasOnesA<P, std::void_t<decltype(std::declval<const P&>().ones_group(
+                       std::declval<const typename P::AInfo&>()))>> : std::true_type {};
 template <class P, class = void>
 struct HasDma : std::false_type {};
 template <class P>
@@ -219,7 +228,7 @@ struct GemmTile {
   // LDS-DMA staging (mainloop_dma): unpadded 32x32 images, swizzled through the gather
   // addresses (the DMA writes lane-linearly), DDL_LDSDMA images of A + B per block
   static constexpr bool DMA = DDL_LDSDMA > 0 && HasDma<P>::value && SOLO && TM * TN == 1 &&
-                              BM == 32 && BN == 32 && BK == 32 && AK && !DIRECT && !BDIR;
+                              BM == 32 && BN == 32 && BK == 32 && !DIRECT && !BDIR;
   static constexpr int DMA_NB = DDL_LDSDMA > 0 ? DDL_LDSDMA : 1;
   static constexpr int LDS_F4 =
       DMA ? DMA_NB * 512
@@ -510,7 +519,9 @@ struct GemmTile {
   // (the 16 lanes of a ds_read_b128 pass then hit 16 different bank groups), an MN-contiguous
   // operand's k-row k at row k ^ ((k >> 2) & 1) (the two lane halves of a fragment read, k and
   // k + 4, land in opposite bank halves).  The MFMA order (k pairs, two accumulator chains) is
-  // the basic loop's, so both give the same bits.
+  // the basic loop's, so both give the same bits.  A's rows that are not in memory (HasOnesA:
+  // the weight gradients' ones row) arrive as zeros and are patched in the image with one
+  // ds_write per holding lane once the tile has landed, before the fragment reads.
   // NB = 2: tile t+2 is DMA'd while tile t's MFMAs run and tile t+1's fragments are read, in
   // a second LDS image and a second fragment register set (the loop is unrolled by two so
   // both stay static).  NB = 1: tile t+1 is DMA'd into the one image once tile t's fragments
@@ -518,6 +529,7 @@ struct GemmTile {
   static DDL_DEV void mainloop_dma(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
                                    f32x16 (&acc)[TM][TN], const Win& w) {
     static_assert(FA == 4 && FB == 4 && R == 4, "32x32x32 one-wave tile");
+    static_assert(!(HasOnesA<P>::value && AK), "ones-row patch: MN-contiguous A");
     const int lane = threadIdx.x & 63;
     const int lr = lane & 31, lh = lane >> 5;
     const int nk = (ke - kb + BK - 1) / BK;
@@ -526,10 +538,20 @@ struct GemmTile {
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int sl = it * 64 + lane, row = sl >> 3, q = sl & 7;
-      ai[it] = p.prepA(m_blk + row, (q ^ ((row >> 1) & 7)) * 4);
+      if constexpr (AK) ai[it] = p.prepA(m_blk + row, (q ^ ((row >> 1) & 7)) * 4);
+      else ai[it] = p.prepA(m_blk + q * 4, row ^ ((row >> 2) & 1));
       if constexpr (BKC) bi[it] = p.prepB(n_blk + row, (q ^ ((row >> 1) & 7)) * 4);
       else bi[it] = p.prepB(n_blk + q * 4, row ^ ((row >> 2) & 1));
     }
+    // the image float that lane's DMA `it` of A fills first (its .x), for the ones-row patch
+    auto patch = [&](int k0, int buf) {
+      if constexpr (HasOnesA<P>::value) {
+        float* As = lds + buf * 2048;
+#pragma unroll
+        for (int it = 0; it < 4; ++it)
+          if (p.ones_group(ai[it])) As[(it * 64 + lane) * 4] = p.ones_value(ai[it], k0, w);
+      }
+    };
     const uint32_t base = lds_addr(lds);
     auto dma = [&](int k0, int buf) {
       const uint32_t b0 = base + buf * 8192;
@@ -545,8 +567,13 @@ struct GemmTile {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int q = (2 * r + lh) ^ ((lr >> 1) & 7);
-        const float4 t = *reinterpret_cast<const float4*>(As + lr * 32 + q * 4);
-        av[r][0] = t.x; av[r][1] = t.y; av[r][2] = t.z; av[r][3] = t.w;
+        if constexpr (AK) {
+          const float4 t = *reinterpret_cast<const float4*>(As + lr * 32 + q * 4);
+          av[r][0] = t.x; av[r][1] = t.y; av[r][2] = t.z; av[r][3] = t.w;
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) av[r][s] = As[((8 * r + 4 * lh + s) ^ lh) * 32 + lr];
+        }
         if constexpr (BKC) {
           const float4 u = *reinterpret_cast<const float4*>(Bs + lr * 32 + q * 4);
           bv[r][0] = u.x; bv[r][1] = u.y; bv[r][2] = u.z; bv[r][3] = u.w;
@@ -589,6 +616,7 @@ struct GemmTile {
         dma(kb, 0);
         for (int kt = 0; kt < nk; ++kt) {
           vm_wait<0>();   // tile kt is in the image
+          patch(kb + kt * BK, 0);
           rd(0, a0, b0);
           lgkm_wait0();   // its fragments are in registers: the image may be restaged
           if (kt + 1 < nk) dma(kb + (kt + 1) * BK, 0);
@@ -603,6 +631,7 @@ struct GemmTile {
         } else {
           vm_wait<0>();
         }
+        patch(kb, 0);
         rd(0, a0, b0);
         // (half of a tile's MFMAs are issued before the wait for the next tile's DMA, so the
         // wave never stalls on it with an empty MFMA pipe)
@@ -613,6 +642,7 @@ struct GemmTile {
           if (kt + 1 < nk) {
             if (kt + 2 < nk) vm_wait<8>();
             else vm_wait<0>();
+            patch(kb + (kt + 1) * BK, 1);
             rd(1, a1, b1);  // tile kt+1's reads overlap tile kt's MFMAs
           }
           mma(a0, b0, R / 2, R);
@@ -623,6 +653,7 @@ struct GemmTile {
           if (kt + 2 < nk) {
             if (kt + 3 < nk) vm_wait<8>();
             else vm_wait<0>();
+            patch(kb + (kt + 2) * BK, 0);
             rd(0, a0, b0);
           }
           mma(a1, b1, R / 2, R);

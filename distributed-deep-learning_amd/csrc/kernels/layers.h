@@ -657,8 +657,11 @@ struct ConvWgradBM {
     const int ky = tap / 5, kx = tap - ky * 5;
     return {m, (ky * HI + kx) * CIN + ci, kk, m + 3 < KW};
   }
-  DDL_DEV float4 loadA(const AInfo& a, int k0, const KWin& win) const {
-    const brsrc_t r = make_rsrc(x, (uint32_t)nimg * HI * HI * CIN * 4u);
+  // the 16-byte gathers (also the LDS-DMA sources, gemm.h mainloop_dma); A's ones row (the
+  // bias gradient) is not in memory: the group starting at row KW gathers zeros and its .x is
+  // patched — in registers by loadA, in the LDS image by the DMA loop (ones_group / ones_value)
+  static constexpr bool DMA = DDL_LDSDMA_WGRAD;
+  DDL_DEV Gather16 srcA(const AInfo& a, int k0, const KWin& win) const {
     const int pos0 = (int)__umulhi((uint32_t)k0, mag);
     int y0, x0, y1, x1;
     vpos(win, pos0, y0, x0);
@@ -670,13 +673,24 @@ struct ConvWgradBM {
     // the offset is computed unconditionally and pushed out of range by an add (a select of
     // the whole address lets hipcc branch around its computation per load)
     const int off = ((int)__umul24(b, HI * HI * CIN) + (w ? p1 : p0) + a.tapoff) * 4;
-    float4 v = bload4(r, off + ((a.vec & kin) ? 0 : kOOB));
-    if (a.m == KW) v.x = kin ? 1.f : 0.f;  // ones row: bias gradient
+    return {make_rsrc(x, (uint32_t)nimg * HI * HI * CIN * 4u), off + ((a.vec & kin) ? 0 : kOOB),
+            0};
+  }
+  DDL_DEV bool ones_group(const AInfo& a) const { return a.m == KW; }
+  DDL_DEV float ones_value(const AInfo& a, int k0, const KWin& win) const {
+    int b;
+    bool w, kin;
+    slot(k0, a.kk, win.ny * win.nx, b, w, kin);
+    return kin ? 1.f : 0.f;
+  }
+  DDL_DEV float4 loadA(const AInfo& a, int k0, const KWin& win) const {
+    const Gather16 g = srcA(a, k0, win);
+    float4 v = bload4(g.r, g.voff);
+    if (a.m == KW) v.x = ones_value(a, k0, win);  // ones row: bias gradient
     return v;
   }
   DDL_DEV BInfo prepB(int n, int kk) const { return {n, kk, n < N}; }
-  DDL_DEV float4 loadB(const BInfo& bi, int k0, const KWin& win) const {
-    const brsrc_t r = make_rsrc(dpre, (uint32_t)nimg * HI * HI * COUT * 4u);
+  DDL_DEV Gather16 srcB(const BInfo& bi, int k0, const KWin& win) const {
     const int pos0 = (int)__umulhi((uint32_t)k0, mag);
     int y0, x0, y1, x1;
     vpos(win, pos0, y0, x0);
@@ -687,7 +701,12 @@ struct ConvWgradBM {
     bool w, kin;
     slot(k0, bi.kk, win.ny * win.nx, b, w, kin);
     const int off = ((int)__umul24(b, HI * HI * COUT) + (w ? q1 : q0) + bi.n) * 4;
-    return bload4(r, off + ((bi.ok & kin) ? 0 : kOOB));
+    return {make_rsrc(dpre, (uint32_t)nimg * HI * HI * COUT * 4u),
+            off + ((bi.ok & kin) ? 0 : kOOB), 0};
+  }
+  DDL_DEV float4 loadB(const BInfo& bi, int k0, const KWin& win) const {
+    const Gather16 g = srcB(bi, k0, win);
+    return bload4(g.r, g.voff);
   }
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
 #pragma unroll
