@@ -605,6 +605,7 @@ class PyRunner {
   void set_local_on_main(bool on) { r_->set_local_on_main(on); }
   void set_last_on_main(bool on) { r_->set_last_on_main(on); }
   void set_use_tail(bool on) { r_->set_use_tail(on); }
+  void set_final_in_reduce(bool on) { r_->set_final_in_reduce(on); }
   void set_tail_cfg(int64_t first, int64_t f4) { r_->set_tail_cfg((int)first, (int)f4); }
   void step(at::Tensor x, at::Tensor labels, int64_t seed, std::vector<double> lr_t) {
     eng_.check_batch(x);
@@ -678,6 +679,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_dual", &PyEngine::set_dual)
       .def("set_fc_chain", [](PyEngine& e, bool on) { e.raw()->fc_chain = on; })
       .def("fc_chain", [](PyEngine& e) { return e.raw()->fc_chain; })
+      .def("set_head_slab", [](PyEngine& e, bool on) { e.raw()->head_slab = on; })
+      .def("head_slab", [](PyEngine& e) { return e.raw()->head_slab; })
       .def("fc_chain_error", [](PyEngine& e) { return e.raw()->fc_chain_error(); })
       .def("set_fc_stamps", [](PyEngine& e, c10::optional<at::Tensor> t) {
         // int64 [items x 8] device tensor (kept alive by the caller), or None to turn off
@@ -714,6 +717,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_local_on_main", &PyRunner::set_local_on_main)
       .def("set_last_on_main", &PyRunner::set_last_on_main)
       .def("set_use_tail", &PyRunner::set_use_tail)
+      .def("set_final_in_reduce", &PyRunner::set_final_in_reduce)
       .def("set_tail_cfg", &PyRunner::set_tail_cfg)
       .def("step", &PyRunner::step)
       .def("selftest", &PyRunner::selftest)

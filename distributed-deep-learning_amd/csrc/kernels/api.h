@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -41,6 +42,13 @@ void launch_head_fwd(const float* h2, const float* w, const float* bias, const i
 void launch_head_fused(const float* h2, const float* w, const float* bias, const int64_t* labels,
                        int B, const uint32_t* seed, uint32_t seed_v, uint32_t thr24,
                        float inv_keep, float* dlog, float* loss, float* dpre2, hipStream_t st);
+// the same, with fc2's split-K reduce (+ bias, dropout; h2 stored) folded in: reads fc2's
+// mode-2 partial slab (S in (4, 16], 32x32 tiles, gx row tiles, ntiles tiles) instead of h2
+void launch_head_fused_slab(const float* slab, int S, int gx, int ntiles, const float* b2,
+                            float* h2, const float* w, const float* bias, const int64_t* labels,
+                            int B, const uint32_t* seed, uint32_t seed_v, uint32_t thr24,
+                            float inv_keep, float* dlog, float* loss, float* dpre2,
+                            hipStream_t st);
 void launch_head_wgrad(const float* h2, const float* dlog, int B, float* gw, float* gb,
                        hipStream_t st);
 void launch_head_bwd(const float* h2, const float* w, const float* dlog, int B,
@@ -124,6 +132,22 @@ struct Engine {
   // optimizer tail (tail.h) for the next dual launch; consumed (and cleared) by it, or by
   // flush_tail() as a launch of its own when no dual launch takes it
   UpdTail tail;
+  // the LAST segment's update (W = 1 tail path): conv1's part applied by its weight-gradient
+  // reduce epilogue, the rest as tail blocks of that launch (engine_impl.h dual_then_b).
+  // Cleared when taken; the runner launches it as before when it is still pending.
+  UpdTail final_upd;
+  // training step (forward with defer_fc): fc2's forward leaves its split-K partials and the
+  // fused head reduces them (launch_head_fused_slab: one launch fewer).  Opt-in
+  // (DDL_HEAD_SLAB=1): measured 0.2999-0.3007 -> 0.3068-0.3073 ms/step — 100 head workgroups
+  // reading 16 strided partials per element are slower than the 3200-wave reduce launch
+  bool head_slab = [] {
+    const char* e = getenv("DDL_HEAD_SLAB");
+    return e && e[0] == '1';
+  }();
+  struct {
+    const float* slab = nullptr;
+    int S = 0, gx = 0, ntiles = 0;
+  } fc2_part;               // pending partials (slab null: none)
   // fc3 weight gradient still to compute (fused head kernel ran): taken by the fc2 dual launch
   int head_wgrad_pending = 0;
   // training: fc1 forward .. fc1 backward as ONE persistent launch (fc_chain.h) at the start
@@ -554,10 +578,18 @@ class SyncRunner {
   std::vector<Piece> seg_pieces_[kSegments];
   bool tail_ok_ = false;
   bool use_tail_ = true;
-  void set_tail(int seg, const float* lr_t);
+  bool final_in_reduce_ = [] {
+    const char* e = getenv("DDL_FINAL_IN_REDUCE");
+    return e && e[0] == '1';
+  }();
+  void set_tail(int seg, const float* lr_t, int f4_per_block = 0);
 
  public:
   void set_use_tail(bool on) { use_tail_ = on; }
+  // the last segment's update inside conv1's weight-gradient reduce launch (tail path only).
+  // Opt-in (DDL_FINAL_IN_REDUCE=1): measured neutral to slightly slower, 0.2999-0.3007 vs
+  // 0.3006-0.3009 ms/step (the stand-alone Adam launch is not what bounds the step's end)
+  void set_final_in_reduce(bool on) { final_in_reduce_ = on; }
   // tail placement (1: before the GEMM blocks) and float4 per tail block (tuning)
   void set_tail_cfg(int first, int f4_per_block) {
     tail_first_ = first;

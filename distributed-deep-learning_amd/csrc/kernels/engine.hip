@@ -220,7 +220,14 @@ void Engine::forward(const float* x, int B, const uint32_t* seed, bool train, hi
   // training with the fused fc chain: the fc forward runs inside backward segment 0's launch
   fc_deferred = defer_fc && train && fc_chain && !concurrent && B <= 128;
   const int last = fc_deferred ? OP_CONV4_FWD : OP_FC2_FWD;
-  for (int op = OP_CONV1_FWD; op <= last; ++op) run_op(op, x, B, seed, train, st, 0);
+  fc2_part.slab = nullptr;
+  for (int op = OP_CONV1_FWD; op <= last; ++op) {
+    // followed by backward segment 0 on one stream: fc2's split-K reduce moves into the head
+    if (op == OP_FC2_FWD && defer_fc && train && head_slab && !concurrent && dual &&
+        run_fc2_fwd_partials(*this, x, B, seed, st))
+      continue;
+    run_op(op, x, B, seed, train, st, 0);
+  }
 }
 
 // The side stream waits for everything enqueued on `st` so far.
@@ -282,8 +289,14 @@ void Engine::backward_segment(int s, const float* x, const int64_t* labels, int 
   switch (s) {
     case 0:
       // one head launch (per-sample fwd + dlogits + dh2); fc3's dW/db ride in the fc2 dual
-      launch_head_fused(h2, P[12], P[13], labels, B, seed, seed_value, thr24, inv_keep, dlog,
-                        loss, dpre2fc, st);
+      if (fc2_part.slab)
+        launch_head_fused_slab(fc2_part.slab, fc2_part.S, fc2_part.gx, fc2_part.ntiles, P[11],
+                               h2, P[12], P[13], labels, B, seed, seed_value, thr24, inv_keep,
+                               dlog, loss, dpre2fc, st);
+      else
+        launch_head_fused(h2, P[12], P[13], labels, B, seed, seed_value, thr24, inv_keep, dlog,
+                          loss, dpre2fc, st);
+      fc2_part.slab = nullptr;
       head_wgrad_pending = 1;
       run_dual_inst<OP_FC2_DGRAD, OP_FC2_WGRAD>(*this, x, B, seed, st);
       flush_head_wgrad(B, st);

@@ -210,6 +210,64 @@ void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipSt
   }
 }
 
+// Split the last segment's update `in` into conv1's weight / bias spans (applied by the
+// epilogue of conv1's weight-gradient reduce: `pa`) and the remaining ranges (`rest`, tail
+// blocks of that launch).  false: the layout does not allow it (the caller keeps `in`).
+template <class PN>
+inline bool final_split(const Engine& e, const UpdTail& in, const PN& pn, WgradAdam<PN>& pa,
+                        UpdTail& rest) {
+  struct Span { const float* w; int64_t n; float *pw = nullptr, *pm = nullptr, *pv = nullptr;
+                float lr_t = 0.f; };
+  Span sp[2] = {{e.P[0], (int64_t)PN::KW * pn.N}, {e.P[1], (int64_t)pn.N}};
+  rest = in;
+  rest.npieces = 0;
+  int blk = 0;
+  auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  auto keep = [&](const UpdPiece& p, int64_t lo, int64_t hi) {
+    if (hi <= lo) return true;
+    if ((hi - lo) % 4 || rest.npieces >= kTailPieces) return false;
+    UpdPiece q = p;
+    q.w = p.w + lo; q.g = p.g + lo; q.m = p.m + lo; q.v = p.v + lo;
+    if (!a16(q.w) || !a16(q.g) || !a16(q.m) || !a16(q.v)) return false;
+    q.n = hi - lo;
+    q.blk0 = blk;
+    blk += (int)((q.n / 4 + in.f4_per_block - 1) / in.f4_per_block);
+    rest.p[rest.npieces++] = q;
+    return true;
+  };
+  for (int i = 0; i < in.npieces; ++i) {
+    const UpdPiece& p = in.p[i];
+    // the spans inside this piece, in address order
+    int64_t cuts[2][2];
+    int nc = 0;
+    for (Span& s : sp) {
+      const int64_t o = s.w - p.w;
+      if (o + s.n <= 0 || o >= p.n) continue;       // disjoint
+      if (o < 0 || o + s.n > p.n) return false;      // straddles the piece edge
+      s.pw = p.w + o; s.pm = p.m + o; s.pv = p.v + o; s.lr_t = p.lr_t;
+      cuts[nc][0] = o; cuts[nc][1] = o + s.n; ++nc;
+    }
+    if (nc == 2 && cuts[1][0] < cuts[0][0]) {
+      std::swap(cuts[0][0], cuts[1][0]);
+      std::swap(cuts[0][1], cuts[1][1]);
+    }
+    int64_t at = 0;
+    for (int c = 0; c < nc; ++c) {
+      if (!keep(p, at, cuts[c][0])) return false;
+      at = cuts[c][1];
+    }
+    if (!keep(p, at, p.n)) return false;
+  }
+  if (!sp[0].pw || !sp[1].pw || sp[0].lr_t != sp[1].lr_t) return false;
+  rest.nblocks = blk;
+  static_cast<PN&>(pa) = pn;
+  pa.w_w = sp[0].pw; pa.w_m = sp[0].pm; pa.w_v = sp[0].pv;
+  pa.b_w = sp[1].pw; pa.b_m = sp[1].pm; pa.b_v = sp[1].pv;
+  pa.lr_t = sp[0].lr_t;
+  pa.c1 = in.c1; pa.c2 = in.c2; pa.eps = in.eps; pa.scale = in.scale;
+  return true;
+}
+
 // Dual launch OA + OB, then op ON with OB's wide split-K reduce fused into ON's launch (both
 // need only what the dual wrote; saves one dependent boundary: conv2 dual -> [conv2 wgrad
 // reduce | conv1 wgrad GEMM]).  Instantiated for the tuned configs (OA: 32x32, OB: 32x32
@@ -229,10 +287,28 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
                                    e.sarg(OB), e.workers[OB], e.scratch[1], e.wide[OB], st,
                                    TailAux(e.tail), &gb, (e.dual_bfirst >> OA) & 1);
   e.tail = UpdTail();
+  constexpr bool kFinal = ON == OP_CONV1_WGRAD;
+  const bool fin = kFinal && e.final_upd.npieces > 0;
+  SubGrid gn;
   if (!launch_reduce_with_gemm<CB, PB, CN, PN>(pb, gb, pn, e.sarg(ON), e.workers[ON],
-                                               e.wide[ON], e.scratch[0], st)) {
+                                               e.wide[ON], e.scratch[0], st,
+                                               fin ? &gn : nullptr)) {
     launch_reduce<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, st);
     run_op_inst<ON>(e, x, B, seed, true, st, 0);
+    return;
+  }
+  if constexpr (kFinal) {
+    if (fin) {
+      // conv1's weight-gradient reduce applies conv1's update in its epilogue and carries the
+      // rest of the last segment's update as tail blocks: no stand-alone optimizer launch
+      WgradAdam<PN> pa;
+      UpdTail rest;
+      if (final_split(e, e.final_upd, pn, pa, rest) &&
+          launch_reduce_tail<CN::BM, CN::BN, CN::BK, CN::WM, CN::WN>(pa, gn, rest, st))
+        e.final_upd = UpdTail();
+      else
+        launch_reduce<CN::BM, CN::BN, CN::BK, CN::WM, CN::WN, PN>(pn, gn, st);
+    }
   }
 }
 

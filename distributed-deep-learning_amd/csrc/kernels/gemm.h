@@ -1331,6 +1331,23 @@ splitk_wide_reduce(P p, const float4* __restrict__ slab, int S, int gx, int ntil
   wide_reduce_body<BM, BN, WM, WN, RL, P>(p, slab, S, gx, ntiles, blockIdx.x * 256 + threadIdx.x);
 }
 
+// The step's last launch at W = 1: the wide reduce of conv1's weight gradient (blocks
+// [0, nrb); its policy's epilogue applies the optimizer to the elements it just summed, see
+// layers.h WgradAdam) followed by the optimizer tail of every other range of the last
+// segment (conv2: its gradients are final one launch earlier), four one-wave tail blocks per
+// 256-thread block.  Replaces reduce -> stand-alone Adam launch (one dependent boundary).
+template <int BM, int BN, int WM, int WN, int RL, class P>
+__global__ void __launch_bounds__(256)
+splitk_wide_reduce_tail(P p, const float4* __restrict__ slab, int S, int gx, int ntiles, int nrb,
+                        UpdTail t) {
+  if ((int)blockIdx.x < nrb) {
+    wide_reduce_body<BM, BN, WM, WN, RL, P>(p, slab, S, gx, ntiles, blockIdx.x * 256 + threadIdx.x);
+    return;
+  }
+  const int tb = ((int)blockIdx.x - nrb) * 4 + (int)(threadIdx.x >> 6);
+  if (tb < t.nblocks) tail_body(t, tb);
+}
+
 // The wide reduce of one mode-2 split-K problem (R, tile geometry RBM x RBN / RWM x RWN) and
 // an independent one-wave GEMM problem G in ONE launch: G's blocks, then nrb reduce blocks
 // (64 threads each).  Saves a dependent kernel boundary at the end of the
@@ -1488,6 +1505,27 @@ inline void launch_reduce(const P& p, const SubGrid& g, hipStream_t stream) {
   }
 }
 
+// launch_reduce with an optimizer tail riding behind it (splitk_wide_reduce_tail).  false
+// (nothing launched) unless g is a pending mode-2 split-K reduce.
+template <int BM, int BN, int BK, int WM, int WN, class P>
+inline bool launch_reduce_tail(const P& p, const SubGrid& g, const UpdTail& t,
+                               hipStream_t stream) {
+  if (g.streamk || g.mode != 2 || g.nblocks == 0) return false;
+  using G = TileGeo<BM, BN, WM, WN>;
+  const int ntiles = g.gx * g.gy, z = g.gz;
+  const size_t nelem = (size_t)ntiles * G::PART4;
+  const int ntb = (t.nblocks + 3) / 4;
+#define DDL_RT(RL)                                                                              \
+  {                                                                                           \
+    const int nrb = (int)((nelem * RL + 255) / 256);                                          \
+    DDL_LAUNCH((splitk_wide_reduce_tail<BM, BN, WM, WN, RL, P>), dim3(nrb + ntb), dim3(256), 0, \
+               stream, p, g.slab, z, g.gx, ntiles, nrb, t);                                   \
+  }
+  if (z > 32) DDL_RT(64) else if (z > 4) DDL_RT(16) else DDL_RT(4)
+#undef DDL_RT
+  return true;
+}
+
 template <int BM, int BN, int BK, int WM, int WN, class P>
 inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch& sc,
                         hipStream_t stream, int workers = 0) {
@@ -1506,9 +1544,11 @@ inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch
 // Launch R's pending wide reduce (SubGrid gr of a mode-2 split-K launch, tile config CR) fused
 // with GEMM problem G (config CG, its own schedule/scratch); G's own mode-2 reduce follows.
 // Returns false (nothing launched) when R has no pending wide reduce or G is stream-K.
+// defer_g: G's own reduce is left to the caller (its SubGrid is returned there).
 template <class CR, class PR, class CG, class PG>
 inline bool launch_reduce_with_gemm(const PR& pr, const SubGrid& gr, const PG& pg, int sg, int wg,
-                                    int wide_g, const SplitScratch& scg, hipStream_t stream) {
+                                    int wide_g, const SplitScratch& scg, hipStream_t stream,
+                                    SubGrid* defer_g = nullptr) {
   if (gr.streamk || gr.mode != 2 || gr.nblocks == 0) return false;
   const SubGrid gg = plan_gemm<CG::BM, CG::BN, CG::BK>(pg, sg, wg, wide_g, scg);
   if (gg.streamk || gg.nblocks == 0) return false;
@@ -1525,7 +1565,8 @@ inline bool launch_reduce_with_gemm(const PR& pr, const SubGrid& gr, const PG& p
   }
   if (z > 32) DDL_RG(64) else if (z > 4) DDL_RG(16) else DDL_RG(4)
 #undef DDL_RG
-  launch_reduce<CG::BM, CG::BN, CG::BK, CG::WM, CG::WN, PG>(pg, gg, stream);
+  if (defer_g) *defer_g = gg;
+  else launch_reduce<CG::BM, CG::BN, CG::BK, CG::WM, CG::WN, PG>(pg, gg, stream);
   return true;
 }
 

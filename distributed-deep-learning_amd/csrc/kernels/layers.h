@@ -725,6 +725,33 @@ using WgradConv3 = ConvWgradBM<7, 64, 128>;
 using WgradConv2 = ConvWgradBM<14, 32, 64>;
 using WgradConv1 = ConvWgrad<28, 1, 32, 28>;
 
+// A ConvWgrad whose reduce epilogue also runs the optimizer (Adam, TF1 form, common.h adam1)
+// on every element it has just summed: with one worker the update of conv1 (the step's last
+// gradients) needs no launch of its own (gemm.h splitk_wide_reduce_tail).  The gradient is
+// still stored.  w/m/v: conv1's weight [25*CIN*COUT] and bias [COUT] parameter / Adam-state
+// spans, in the same layout as gw / gb.
+template <class P>
+struct WgradAdam : P {
+  float *w_w, *w_m, *w_v;  // weight span
+  float *b_w, *b_m, *b_v;  // bias span
+  float lr_t, c1, c2, eps, scale;
+  DDL_DEV void epi(int m0, int n, f32x4 v) const {
+    constexpr int KW = P::KW;  // gw is [KW, N] (N = COUT)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + r;
+      float *pw, *pm, *pv;
+      size_t i;
+      if (m < KW) { i = (size_t)m * this->N + n; pw = w_w; pm = w_m; pv = w_v; this->gw[i] = v[r]; }
+      else if (m == KW) { i = (size_t)n; pw = b_w; pm = b_m; pv = b_v; this->gb[i] = v[r]; }
+      else continue;
+      float W = pw[i], M = pm[i], V = pv[i];
+      adam1(W, v[r] * scale, M, V, lr_t, c1, c2, eps);
+      pw[i] = W; pm[i] = M; pv[i] = V;
+    }
+  }
+};
+
 // ---------------------------------------------------------------------------------------------
 // fully connected forward (model.py:70 fc1: +b, ReLU, dropout; :79,82 fc2: +b, dropout)
 // M = B, N = NOUT, K = KIN.  Dropout key derived on device from *seed (graph-replayable),

@@ -183,10 +183,10 @@ void SyncRunner::set_units(const std::vector<RunnerUnit>& units) {
 }
 
 // Segment `seg`'s Adam as the optimizer tail of the engine's next dual launch.
-void SyncRunner::set_tail(int seg, const float* lr_t) {
+void SyncRunner::set_tail(int seg, const float* lr_t, int f4_per_block) {
   UpdTail t;
   t.first = tail_first_;
-  t.f4_per_block = tail_f4_;
+  t.f4_per_block = f4_per_block > 0 ? f4_per_block : tail_f4_;
   t.c1 = 1.f - b1_;
   t.c2 = 1.f - b2_;
   t.eps = eps_;
@@ -201,7 +201,7 @@ void SyncRunner::set_tail(int seg, const float* lr_t) {
     q.n = p.r.hi - p.r.lo;
     q.lr_t = lr_t[p.ps];
     q.blk0 = blk;
-    blk += (int)((q.n / 4 + tail_f4_ - 1) / tail_f4_);
+    blk += (int)((q.n / 4 + t.f4_per_block - 1) / t.f4_per_block);
   }
   t.nblocks = (blk + 7) & ~7;
   eng_->tail = t;
@@ -310,9 +310,22 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
     for (int s = 0; s < kSegments; ++s) {
       TraceRange r(kBwdRange[s]);
       if (s > 0 && !seg_pieces_[s - 1].empty()) set_tail(s - 1, lr_t);
+      // the last segment's own update rides in its final launch when the engine can take it
+      // (conv1's weight-gradient reduce: engine_impl.h dual_then_b)
+      if (s == kSegments - 1 && final_in_reduce_ && !seg_pieces_[s].empty()) {
+        // one pass per tail block (2 float4 per lane): on the step's critical path the update
+        // wants width, not the long blocks that hide beside a dual launch's GEMM blocks
+        const UpdTail keep = eng_->tail;
+        set_tail(s, lr_t, kTailF4PerBlock);
+        eng_->final_upd = eng_->tail;
+        eng_->tail = keep;
+      }
       eng_->backward_segment(s, x, labels, B, seed, st);
       eng_->flush_tail(st);
     }
+    if (eng_->final_upd.npieces == 0 && final_in_reduce_ && !seg_pieces_[kSegments - 1].empty())
+      return;  // taken by the last launch
+    eng_->final_upd = UpdTail();
     TraceRange r("ddl.update.last_segment");
     for (const auto& p : seg_pieces_[kSegments - 1])
       update(w_ + p.r.lo, g_ + p.r.lo, p.m + p.r.state_off, p.v + p.r.state_off,

@@ -157,6 +157,30 @@ def test_fc_chain_matches_separate_launches(setup, B):
     assert torch.equal(out[0][2] == 0, out[1][2] == 0)
 
 
+@pytest.mark.parametrize("B", [100, 37])
+def test_head_slab_bit_identical(setup, B):
+    """fc2's split-K reduce folded into the fused head (head.hip head_fused_kernel<true>: the
+    head sums fc2's partial slab with the wide reduce's own association, adds the bias and
+    dropout, stores h2) gives the same bits as the reduce launch + head: every gradient, h2,
+    the loss and dlogits."""
+    eng, flat, params, grads, x, y = setup
+    x, y = x[:B].to(DEV), y[:B].to(DEV)
+    out = []
+    prev = eng.eng.head_slab()
+    try:
+        for on in (True, False):
+            eng.eng.set_head_slab(on)
+            grads.zero_()
+            eng.forward_backward(x, y, 0.5, 777)
+            torch.cuda.synchronize()
+            out.append([grads.clone()] + [eng.eng.buffer(n, B).clone() for n in
+                                          ("h2", "loss", "dlog")])
+    finally:
+        eng.eng.set_head_slab(prev)
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
+
+
 def test_gradients_no_dropout(setup):
     eng, flat, params, grads, x, y = setup
     grads.zero_()

@@ -123,22 +123,27 @@ def test_rccl_probe_resolves_torch_librccl():
 @pytest.mark.parametrize("shard", ["flat", "contiguous"])
 def test_optimizer_tail_matches_end_of_step_update(data, shard):
     """W = 1: segment s's Adam riding as extra blocks of segment s+1's dual GEMM launch
-    (csrc/kernels/tail.h) gives bit-identical parameters and moments to one coalesced Adam
+    (csrc/kernels/tail.h), and the last segment's Adam inside conv1's weight-gradient reduce
+    launch (conv1's in the reduce epilogue, conv2's as tail blocks: gemm.h
+    splitk_wide_reduce_tail), give bit-identical parameters and moments to one coalesced Adam
     launch after the backward."""
     out = []
-    for tail in (True, False):
+    # (tail, last segment's update inside conv1's weight-gradient reduce launch)
+    for tail, final in ((True, True), (True, False), (False, False)):
         env = DistEnv(0, 1, 0, torch.device("cuda", 0))
         cfg = TrainConfig(mode="sync", shard=shard, steps=5, batch_size=100, eval_every=0,
                           engine="hip", quiet=True)
         tr = Trainer(cfg, env, dataset=data)
         tr.exchange.runner.set_use_tail(tail)
+        tr.exchange.runner.set_final_in_reduce(final)
         for i in range(5):
             tr.train_step(i)
         torch.cuda.synchronize()
         s = tr.servers[0]
         out.append((tr.params.clone(), s.m.clone(), s.v.clone()))
-    for a, b in zip(*out):
-        assert torch.equal(a, b)
+    for ref in out[1:]:
+        for a, b in zip(out[0], ref):
+            assert torch.equal(a, b)
 
 
 def _train_async(data, **kw):
