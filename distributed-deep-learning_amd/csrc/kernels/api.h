@@ -34,6 +34,11 @@ void launch_momentum(float* w, const float* g, float* m, int64_t n, float lr, fl
                      float scale, hipStream_t st);
 void launch_scale(float* p, int64_t n, float a, hipStream_t st);
 
+// ---- conv1 forward as a direct LDS-staged kernel (conv1.hip) --------------------------------
+// x [B,784], w [25,32], bias [32] -> pooled p1 [B,18,18,32] (halo layout) + codes [B,14,14,32]
+void launch_conv1_fwd(const float* x, const float* w, const float* bias, float* out,
+                      uint8_t* code, int B, hipStream_t st);
+
 // ---- classifier head (head.hip) --------------------------------------------------------------
 void launch_head_fwd(const float* h2, const float* w, const float* bias, const int64_t* labels,
                      int B, float* dlog, float* loss, int* correct, hipStream_t st);
@@ -136,6 +141,12 @@ struct Engine {
   // reduce epilogue, the rest as tail blocks of that launch (engine_impl.h dual_then_b).
   // Cleared when taken; the runner launches it as before when it is still pending.
   UpdTail final_upd;
+  // conv1 forward on the direct LDS-staged kernel (conv1.hip) instead of the GEMM engine's
+  // gather-bound K = 25 launch.  DDL_CONV1_DIRECT=0: the GEMM path
+  bool conv1_direct = [] {
+    const char* e = getenv("DDL_CONV1_DIRECT");
+    return !e || e[0] != '0';
+  }();
   // training step (forward with defer_fc): fc2's forward leaves its split-K partials and the
   // fused head reduces them (launch_head_fused_slab: one launch fewer).  Opt-in
   // (DDL_HEAD_SLAB=1): measured 0.2999-0.3007 -> 0.3068-0.3073 ms/step — 100 head workgroups

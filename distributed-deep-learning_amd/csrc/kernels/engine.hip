@@ -188,6 +188,10 @@ int Engine::fc_chain_error() const {
 
 void Engine::run_op(int op, const float* x, int B, const uint32_t* seed, bool train,
                     hipStream_t st, int si) {
+  if (op == OP_CONV1_FWD && conv1_direct) {
+    launch_conv1_fwd(x, P[0], P[1], p1, c1, B, st);
+    return;
+  }
   switch (op) {
 #define DDL_RUN(OPC) \
   case OPC: run_op_inst<OPC>(*this, x, B, seed, train, st, si); break;

@@ -158,6 +158,29 @@ def test_fc_chain_matches_separate_launches(setup, B):
 
 
 @pytest.mark.parametrize("B", [100, 37])
+def test_conv1_direct_matches_gemm_path(setup, B):
+    """conv1 forward on the direct LDS-staged kernel (csrc/kernels/conv1.hip) against the GEMM
+    engine's ConvFwd<28, 1, 32> launch: pooled p1 to fp32 summation-order noise (the two
+    accumulate the 25 taps in different MFMA pairings) and the pool / ReLU codes equal except
+    on exact near-ties."""
+    eng, flat, params, grads, x, y = setup
+    xb = x[:B].to(DEV)
+    seed_t = torch.tensor([5], dtype=torch.int32, device=DEV)
+    out = []
+    prev = eng.eng.conv1_direct()
+    try:
+        for on in (True, False):
+            eng.eng.set_conv1_direct(on)
+            eng.eng.forward(xb, seed_t, True)
+            torch.cuda.synchronize()
+            out.append((eng.eng.buffer("p1", B).clone(), eng.eng.buffer("c1", B).clone()))
+    finally:
+        eng.eng.set_conv1_direct(prev)
+    assert rel_err(out[0][0], out[1][0]) < 1e-6
+    assert (out[0][1] == out[1][1]).float().mean().item() > 0.9999
+
+
+@pytest.mark.parametrize("B", [100, 37])
 def test_head_slab_bit_identical(setup, B):
     """fc2's split-K reduce folded into the fused head (head.hip head_fused_kernel<true>: the
     head sums fc2's partial slab with the wide reduce's own association, adds the bias and
