@@ -681,6 +681,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("fc_chain", [](PyEngine& e) { return e.raw()->fc_chain; })
       .def("set_conv1_direct", [](PyEngine& e, bool on) { e.raw()->conv1_direct = on; })
       .def("conv1_direct", [](PyEngine& e) { return e.raw()->conv1_direct; })
+      .def("set_conv1_wgrad_direct", [](PyEngine& e, bool on) { e.raw()->conv1_wgrad_direct = on; })
+      .def("conv1_wgrad_direct", [](PyEngine& e) { return e.raw()->conv1_wgrad_direct; })
       .def("set_head_slab", [](PyEngine& e, bool on) { e.raw()->head_slab = on; })
       .def("head_slab", [](PyEngine& e) { return e.raw()->head_slab; })
       .def("fc_chain_error", [](PyEngine& e) { return e.raw()->fc_chain_error(); })

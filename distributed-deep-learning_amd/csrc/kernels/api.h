@@ -38,6 +38,12 @@ void launch_scale(float* p, int64_t n, float a, hipStream_t st);
 // x [B,784], w [25,32], bias [32] -> pooled p1 [B,18,18,32] (halo layout) + codes [B,14,14,32]
 void launch_conv1_fwd(const float* x, const float* w, const float* bias, float* out,
                       uint8_t* code, int B, hipStream_t st);
+// conv1's weight / bias gradient, direct kernel with in-launch reduce (conv1.h); part /
+// tickets: c1w_scratch_floats(B) floats and c1w_groups(B) + 1 zeroed ints of scratch
+void launch_conv1_wgrad_only(const float* x, const float* d1, int B, float* gw, float* gb,
+                             float* part, int* tickets, hipStream_t st);
+size_t conv1_wgrad_scratch_floats(int B);
+int conv1_wgrad_tickets(int B);
 
 // ---- classifier head (head.hip) --------------------------------------------------------------
 void launch_head_fwd(const float* h2, const float* w, const float* bias, const int64_t* labels,
@@ -145,6 +151,13 @@ struct Engine {
   // gather-bound K = 25 launch.  DDL_CONV1_DIRECT=0: the GEMM path
   bool conv1_direct = [] {
     const char* e = getenv("DDL_CONV1_DIRECT");
+    return !e || e[0] != '0';
+  }();
+  // conv1's weight gradient on the direct kernel with its in-launch reduce (conv1.h), riding
+  // with conv2's weight-gradient reduce, instead of the GEMM launch + wide reduce launch.
+  // DDL_CONV1_WGRAD_DIRECT=0: the GEMM path
+  bool conv1_wgrad_direct = [] {
+    const char* e = getenv("DDL_CONV1_WGRAD_DIRECT");
     return !e || e[0] != '0';
   }();
   // training step (forward with defer_fc): fc2's forward leaves its split-K partials and the

@@ -13,6 +13,7 @@
 #include "api.h"
 #include "common.h"
 #include "layers.h"
+#include "conv1.h"
 
 namespace ddl {
 
@@ -87,6 +88,17 @@ void launch_conv1_fwd(const float* x, const float* w, const float* bias, float* 
                       uint8_t* code, int B, hipStream_t st) {
   if (B <= 0) return;
   DDL_LAUNCH(conv1_fwd_kernel, dim3(B, 2), dim3(64 * kC1Tiles), 0, st, x, w, bias, out, code);
+}
+
+size_t conv1_wgrad_scratch_floats(int B) { return c1w_scratch_floats(B); }
+int conv1_wgrad_tickets(int B) { return c1w_groups(B) + 1; }
+
+// conv1's weight gradient alone (conv1.h; no reduce of another problem in the launch)
+void launch_conv1_wgrad_only(const float* x, const float* d1, int B, float* gw, float* gb,
+                             float* part, int* tickets, hipStream_t st) {
+  if (B <= 0) return;
+  using C = TileCfg<32, 32, 32, 1, 1>;
+  launch_conv1_wgrad<C, WgradConv1>(WgradConv1{}, SubGrid(), x, d1, B, gw, gb, part, tickets, st);
 }
 
 }  // namespace ddl

@@ -192,6 +192,13 @@ void Engine::run_op(int op, const float* x, int B, const uint32_t* seed, bool tr
     launch_conv1_fwd(x, P[0], P[1], p1, c1, B, st);
     return;
   }
+  // (the dual path fuses it with conv2's weight-gradient reduce: engine_impl.h dual_then_b)
+  if (op == OP_CONV1_WGRAD && conv1_wgrad_direct && conv1_wgrad_scratch_floats(B) <= slab_floats &&
+      conv1_wgrad_tickets(B) <= scratch[si].max_tiles) {
+    launch_conv1_wgrad_only(x, d1, B, G[0], G[1], static_cast<float*>(scratch[si].slab),
+                            scratch[si].tickets, st);
+    return;
+  }
   switch (op) {
 #define DDL_RUN(OPC) \
   case OPC: run_op_inst<OPC>(*this, x, B, seed, train, st, si); break;

@@ -10,6 +10,7 @@
 #include "api.h"
 #include "layers.h"
 #include "head.h"
+#include "conv1.h"
 #include "engine_decl.h"
 
 namespace ddl {
@@ -268,6 +269,47 @@ inline bool final_split(const Engine& e, const UpdTail& in, const PN& pn, WgradA
   return true;
 }
 
+// The Adam spans (parameter, m, v, lr_t) of [w, w + n) inside the update pieces of `t`.
+inline bool find_span(const UpdTail& t, const float* w, int64_t n, float*& pw, float*& pm,
+                      float*& pv, float& lr) {
+  for (int i = 0; i < t.npieces; ++i) {
+    const UpdPiece& p = t.p[i];
+    const int64_t o = w - p.w;
+    if (o >= 0 && o + n <= p.n) {
+      pw = p.w + o; pm = p.m + o; pv = p.v + o; lr = p.lr_t;
+      return true;
+    }
+  }
+  return false;
+}
+
+// Split the last segment's update into conv2's (weight-gradient reduce epilogue: `pa`) and
+// conv1's (final reduce level of the direct kernel: `ad`); false unless the pieces are exactly
+// those four tensors with one step size.
+template <class PB>
+inline bool final_split_conv12(const Engine& e, const UpdTail& in, const PB& pb,
+                               WgradAdam<PB>& pa, C1Adam& ad) {
+  const int64_t n2w = (int64_t)PB::KW * pb.N, n2b = pb.N, n1w = 800, n1b = 32;
+  int64_t total = 0;
+  for (int i = 0; i < in.npieces; ++i) total += in.p[i].n;
+  if (total != n2w + n2b + n1w + n1b) return false;
+  float lr[4];
+  static_cast<PB&>(pa) = pb;
+  if (!find_span(in, e.P[2], n2w, pa.w_w, pa.w_m, pa.w_v, lr[0]) ||
+      !find_span(in, e.P[3], n2b, pa.b_w, pa.b_m, pa.b_v, lr[1]) ||
+      !find_span(in, e.P[0], n1w, ad.w_w, ad.w_m, ad.w_v, lr[2]) ||
+      !find_span(in, e.P[1], n1b, ad.b_w, ad.b_m, ad.b_v, lr[3]))
+    return false;
+  if (lr[1] != lr[0] || lr[2] != lr[0] || lr[3] != lr[0]) return false;
+  pa.lr_t = ad.lr_t = lr[0];
+  pa.c1 = ad.c1 = in.c1;
+  pa.c2 = ad.c2 = in.c2;
+  pa.eps = ad.eps = in.eps;
+  pa.scale = ad.scale = in.scale;
+  ad.on = 1;
+  return true;
+}
+
 // Dual launch OA + OB, then op ON with OB's wide split-K reduce fused into ON's launch (both
 // need only what the dual wrote; saves one dependent boundary: conv2 dual -> [conv2 wgrad
 // reduce | conv1 wgrad GEMM]).  Instantiated for the tuned configs (OA: 32x32, OB: 32x32
@@ -288,13 +330,37 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
                                    TailAux(e.tail), &gb, (e.dual_bfirst >> OA) & 1);
   e.tail = UpdTail();
   constexpr bool kFinal = ON == OP_CONV1_WGRAD;
+  if constexpr (kFinal) {
+    // conv1's weight gradient on the direct kernel (conv1.h), sharing its launch with OB's
+    // pending reduce; scratch[0] is free here (OA's split-K finished inside the dual launch
+    // or in its own reduce before this point)
+    if (e.conv1_wgrad_direct && (size_t)c1w_scratch_floats(B) <= e.slab_floats &&
+        c1w_groups(B) + 1 <= e.scratch[0].max_tiles) {
+      float* part = static_cast<float*>(e.scratch[0].slab);
+      // the last segment's update (W = 1 tail path) inside this launch: conv2's in its weight-
+      // gradient reduce epilogue, conv1's in the final reduce level; no Adam launch follows
+      if (e.final_upd.npieces > 0 && !gb.streamk && gb.mode == 2) {
+        WgradAdam<PB> pa;
+        C1Adam ad;
+        if (final_split_conv12(e, e.final_upd, pb, pa, ad)) {
+          launch_conv1_wgrad<CB, WgradAdam<PB>>(pa, gb, x, e.d1, B, e.G[0], e.G[1], part,
+                                                e.scratch[0].tickets, st, ad);
+          e.final_upd = UpdTail();
+          return;
+        }
+      }
+      launch_conv1_wgrad<CB, PB>(pb, gb, x, e.d1, B, e.G[0], e.G[1], part, e.scratch[0].tickets,
+                                 st);
+      return;
+    }
+  }
   const bool fin = kFinal && e.final_upd.npieces > 0;
   SubGrid gn;
   if (!launch_reduce_with_gemm<CB, PB, CN, PN>(pb, gb, pn, e.sarg(ON), e.workers[ON],
                                                e.wide[ON], e.scratch[0], st,
                                                fin ? &gn : nullptr)) {
     launch_reduce<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, st);
-    run_op_inst<ON>(e, x, B, seed, true, st, 0);
+    e.run_op(ON, x, B, seed, true, st, 0);
     return;
   }
   if constexpr (kFinal) {
@@ -319,7 +385,7 @@ void run_dual_then_inst(Engine& e, const float* x, int B, const uint32_t* seed, 
   const int cb = e.cfg[OB];
   if (!e.dual || e.cfg[OA] != 3 || (cb != 3 && cb != 5) || e.cfg[ON] != 3 || e.workers[ON] > 0) {
     run_dual_inst<OA, OB>(e, x, B, seed, st);
-    run_op_inst<ON>(e, x, B, seed, true, st, 0);
+    e.run_op(ON, x, B, seed, true, st, 0);
     return;
   }
   if (cb == 3) dual_then_b<OA, OB, ON, TileCfg<TILE_3>>(e, x, B, seed, st);

@@ -181,6 +181,35 @@ def test_conv1_direct_matches_gemm_path(setup, B):
 
 
 @pytest.mark.parametrize("B", [100, 37])
+def test_conv1_wgrad_direct_matches_gemm_path(setup, B):
+    """conv1's weight / bias gradient on the direct kernel with its two-level in-launch reduce
+    (csrc/kernels/conv1.h, sharing the launch with conv2's weight-gradient reduce) against the
+    split-K GEMM + wide reduce: conv1's dW / db to fp32 summation-order noise, every other
+    gradient bit-identical."""
+    eng, flat, params, grads, x, y = setup
+    xb, yb = x[:B].to(DEV), y[:B].to(DEV)
+    out = []
+    prev = eng.eng.conv1_wgrad_direct()
+    try:
+        for on in (True, False, True):
+            eng.eng.set_conv1_wgrad_direct(on)
+            grads.zero_()
+            eng.forward_backward(xb, yb, 0.5, 4242)
+            torch.cuda.synchronize()
+            out.append(grads.clone())
+    finally:
+        eng.eng.set_conv1_wgrad_direct(prev)
+    # deterministic: the same launch twice gives the same bits
+    assert torch.equal(out[0], out[2])
+    va, vb = param_views(out[0], CANON_OFFSETS), param_views(out[1], CANON_OFFSETS)
+    for t, a, b in zip(TENSORS, va, vb):
+        if t.index < 2:
+            assert rel_err(a, b) < 2e-6, t.name
+        else:
+            assert torch.equal(a, b), t.name
+
+
+@pytest.mark.parametrize("B", [100, 37])
 def test_head_slab_bit_identical(setup, B):
     """fc2's split-K reduce folded into the fused head (head.hip head_fused_kernel<true>: the
     head sums fc2's partial slab with the wide reduce's own association, adds the bias and
