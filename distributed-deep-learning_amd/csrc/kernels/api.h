@@ -604,15 +604,17 @@ class SyncRunner {
   bool use_tail_ = true;
   bool final_in_reduce_ = [] {
     const char* e = getenv("DDL_FINAL_IN_REDUCE");
-    return e && e[0] == '1';
+    return !e || e[0] != '0';
   }();
   void set_tail(int seg, const float* lr_t, int f4_per_block = 0);
 
  public:
   void set_use_tail(bool on) { use_tail_ = on; }
-  // the last segment's update inside conv1's weight-gradient reduce launch (tail path only).
-  // Opt-in (DDL_FINAL_IN_REDUCE=1): measured neutral to slightly slower, 0.2999-0.3007 vs
-  // 0.3006-0.3009 ms/step (the stand-alone Adam launch is not what bounds the step's end)
+  // the last segment's update inside conv1's weight-gradient launch (tail path only): with the
+  // direct conv1 kernel conv2's Adam runs in its weight-gradient reduce epilogue and conv1's in
+  // the final reduce level (engine_impl.h final_split_conv12): 0.2988 -> 0.2973 ms/step; with
+  // the GEMM conv1 path as tail blocks of the wide reduce (measured neutral).
+  // DDL_FINAL_IN_REDUCE=0: the stand-alone Adam launch
   void set_final_in_reduce(bool on) { final_in_reduce_ = on; }
   // tail placement (1: before the GEMM blocks) and float4 per tail block (tuning)
   void set_tail_cfg(int first, int f4_per_block) {

@@ -290,9 +290,30 @@ template <class PB>
 inline bool final_split_conv12(const Engine& e, const UpdTail& in, const PB& pb,
                                WgradAdam<PB>& pa, C1Adam& ad) {
   const int64_t n2w = (int64_t)PB::KW * pb.N, n2b = pb.N, n1w = 800, n1b = 32;
-  int64_t total = 0;
-  for (int i = 0; i < in.npieces; ++i) total += in.p[i].n;
-  if (total != n2w + n2b + n1w + n1b) return false;
+  // every element of the pieces is one of the four tensors or the alignment padding that
+  // follows a tensor in the plan buffer (< kPad elements: zero gradient and state, so skipping
+  // its update changes nothing)
+  constexpr int64_t kPad = 64;
+  const float* sw[4] = {e.P[0], e.P[1], e.P[2], e.P[3]};
+  const int64_t sn[4] = {n1w, n1b, n2w, n2b};
+  for (int i = 0; i < in.npieces; ++i) {
+    const UpdPiece& p = in.p[i];
+    int64_t pos = 0;
+    bool first = true;
+    while (pos < p.n) {
+      int k = -1;
+      for (int j = 0; j < 4; ++j) {
+        const int64_t o = sw[j] - p.w;
+        if (o >= pos && o + sn[j] <= p.n && (k < 0 || o < sw[k] - p.w)) k = j;
+      }
+      if (k < 0) break;
+      const int64_t gap = (sw[k] - p.w) - pos;
+      if (gap >= kPad || (first && gap != 0)) return false;
+      pos = (sw[k] - p.w) + sn[k];
+      first = false;
+    }
+    if (first || p.n - pos >= kPad) return false;
+  }
   float lr[4];
   static_cast<PB&>(pa) = pb;
   if (!find_span(in, e.P[2], n2w, pa.w_w, pa.w_m, pa.w_v, lr[0]) ||
