@@ -42,8 +42,7 @@ void launch_conv1_fwd(const float* x, const float* w, const float* bias, float* 
 // tickets: c1w_scratch_floats(B) floats and c1w_groups(B) + 1 zeroed ints of scratch
 void launch_conv1_wgrad_only(const float* x, const float* d1, int B, float* gw, float* gb,
                              float* part, int* tickets, hipStream_t st);
-size_t conv1_wgrad_scratch_floats(int B);
-int conv1_wgrad_tickets(int B);
+bool conv1_wgrad_fits(int B, size_t slab_floats, int max_tickets);
 
 // ---- classifier head (head.hip) --------------------------------------------------------------
 void launch_head_fwd(const float* h2, const float* w, const float* bias, const int64_t* labels,

@@ -38,6 +38,13 @@ DDL_HD size_t c1w_scratch_floats(int B) {
   return (size_t)(2 * B + c1w_groups(B)) * kC1wElems;
 }
 
+// the direct kernel's preconditions: scratch for the partials and tickets, 32-bit buffer
+// offsets into d1 [B, 28, 28, 32]
+inline bool conv1_wgrad_direct_ok(int B, size_t slab_floats, int max_tickets) {
+  return B > 0 && c1w_scratch_floats(B) <= slab_floats && c1w_groups(B) + 1 <= max_tickets &&
+         (uint64_t)B * 784u * 32u * 4u < (1ull << 31);
+}
+
 DDL_DEV bool c1w_arrive(int* ticket, int count, int* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();

@@ -90,8 +90,9 @@ void launch_conv1_fwd(const float* x, const float* w, const float* bias, float* 
   DDL_LAUNCH(conv1_fwd_kernel, dim3(B, 2), dim3(64 * kC1Tiles), 0, st, x, w, bias, out, code);
 }
 
-size_t conv1_wgrad_scratch_floats(int B) { return c1w_scratch_floats(B); }
-int conv1_wgrad_tickets(int B) { return c1w_groups(B) + 1; }
+bool conv1_wgrad_fits(int B, size_t slab_floats, int max_tickets) {
+  return conv1_wgrad_direct_ok(B, slab_floats, max_tickets);
+}
 
 // conv1's weight gradient alone (conv1.h; no reduce of another problem in the launch)
 void launch_conv1_wgrad_only(const float* x, const float* d1, int B, float* gw, float* gb,

@@ -193,8 +193,8 @@ void Engine::run_op(int op, const float* x, int B, const uint32_t* seed, bool tr
     return;
   }
   // (the dual path fuses it with conv2's weight-gradient reduce: engine_impl.h dual_then_b)
-  if (op == OP_CONV1_WGRAD && conv1_wgrad_direct && conv1_wgrad_scratch_floats(B) <= slab_floats &&
-      conv1_wgrad_tickets(B) <= scratch[si].max_tiles) {
+  if (op == OP_CONV1_WGRAD && conv1_wgrad_direct &&
+      conv1_wgrad_fits(B, slab_floats, scratch[si].max_tiles)) {
     launch_conv1_wgrad_only(x, d1, B, G[0], G[1], static_cast<float*>(scratch[si].slab),
                             scratch[si].tickets, st);
     return;

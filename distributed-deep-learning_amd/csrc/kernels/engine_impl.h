@@ -355,8 +355,7 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
     // conv1's weight gradient on the direct kernel (conv1.h), sharing its launch with OB's
     // pending reduce; scratch[0] is free here (OA's split-K finished inside the dual launch
     // or in its own reduce before this point)
-    if (e.conv1_wgrad_direct && (size_t)c1w_scratch_floats(B) <= e.slab_floats &&
-        c1w_groups(B) + 1 <= e.scratch[0].max_tiles) {
+    if (e.conv1_wgrad_direct && conv1_wgrad_direct_ok(B, e.slab_floats, e.scratch[0].max_tiles)) {
       float* part = static_cast<float*>(e.scratch[0].slab);
       // the last segment's update (W = 1 tail path) inside this launch: conv2's in its weight-
       // gradient reduce epilogue, conv1's in the final reduce level; no Adam launch follows

@@ -2,7 +2,8 @@
 """Per-step kernel timeline from a rocprofv3 rocpd database (which stream ran what, when).
 
 usage: python scripts/step_timeline.py <results.db> [--step N] [--anchor SUBSTR]
-A step starts at each launch of the anchor kernel (default: the conv1 forward GEMM).
+A step starts at each launch of the anchor kernel (default: the conv1 forward kernel, direct
+conv1_fwd_kernel or the GEMM ConvFwd<28, 1, 32>).
 Prints start offset, duration, gap since the previous kernel end on the same queue, queue id.
 """
 import re
@@ -23,9 +24,12 @@ def short(name):
 def main():
     db = sys.argv[1]
     step = int(sys.argv[sys.argv.index("--step") + 1]) if "--step" in sys.argv else 50
-    anchor = sys.argv[sys.argv.index("--anchor") + 1] if "--anchor" in sys.argv else "ConvFwd<28, 1, 32>"
+    anchor = sys.argv[sys.argv.index("--anchor") + 1] if "--anchor" in sys.argv else None
     c = sqlite3.connect(db)
     rows = c.execute("select name, start, end, queue_id from kernels order by start").fetchall()
+    if anchor is None:
+        anchor = "conv1_fwd_kernel" if any("conv1_fwd_kernel" in r[0] for r in rows) \
+            else "ConvFwd<28, 1, 32>"
     starts = [i for i, r in enumerate(rows) if anchor in r[0]]
     # skip eval launches (huge grids) by requiring the next anchor to be close
     i0, i1 = starts[step], starts[step + 1]
