@@ -171,7 +171,7 @@ DDL_DEV void conv1_wgrad_block(const float* __restrict__ x, const float* __restr
 // float4)]
 template <int BM, int BN, int WM, int WN, int RL, class PR>
 __global__ void __launch_bounds__(256)
-conv1_wgrad_kernel(PR pr, const float4* __restrict__ rslab, int S, int rgx, int rntiles, int nrb,
+conv1_wgrad_kernel(PR pr, const float4* __restrict__ rslab, int S, int rgx, int rntiles,
                    const float* __restrict__ x, const float* __restrict__ d1, int B,
                    float* __restrict__ gw, float* __restrict__ gb, float* __restrict__ part,
                    int* __restrict__ tickets, C1Adam ad) {
@@ -202,7 +202,7 @@ inline void launch_conv1_wgrad(const PR& pr, const SubGrid& gr, const float* x, 
   {                                                                                         \
     const int nrb = (int)((nelem * RL + 255) / 256);                                        \
     DDL_LAUNCH((conv1_wgrad_kernel<CR::BM, CR::BN, CR::WM, CR::WN, RL, PR>),                \
-               dim3(nrb + 2 * B), dim3(256), 0, st, pr, gr.slab, z, gr.gx, ntiles, nrb, x, d1, \
+               dim3(nrb + 2 * B), dim3(256), 0, st, pr, gr.slab, z, gr.gx, ntiles, x, d1,      \
                B, gw, gb, part, tickets, ad);                                               \
   }
   if (z > 32) DDL_C1W(64) else if (z > 4) DDL_C1W(16) else DDL_C1W(4)

@@ -189,7 +189,7 @@ int Engine::fc_chain_error() const {
 void Engine::run_op(int op, const float* x, int B, const uint32_t* seed, bool train,
                     hipStream_t st, int si) {
   if (op == OP_CONV1_FWD && conv1_direct) {
-    launch_conv1_fwd(x, P[0], P[1], p1, c1, B, st);
+    launch_conv1_fwd(x, P[0], P[1], p1, train ? c1 : nullptr, B, st);
     return;
   }
   // (the dual path fuses it with conv2's weight-gradient reduce: engine_impl.h dual_then_b)

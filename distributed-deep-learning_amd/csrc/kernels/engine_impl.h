@@ -71,13 +71,15 @@ inline auto make_policy(const Engine& e, int B, const float* x, const uint32_t* 
   const uint32_t thr = train ? e.thr24 : 0u;
   const float* const* P = e.P;
   float* const* G = e.G;
-  if constexpr (OP == OP_CONV1_FWD) return ConvFwd<28, 1, 32>{M, N, K, x, P[0], P[1], e.p1, e.c1};
+  // pool / ReLU codes only feed the backward: an eval forward skips their stores
+  if constexpr (OP == OP_CONV1_FWD)
+    return ConvFwd<28, 1, 32>{M, N, K, x, P[0], P[1], e.p1, train ? e.c1 : nullptr};
   else if constexpr (OP == OP_CONV2_FWD)
-    return ConvFwd<14, 32, 64>{M, N, K, e.p1, P[2], P[3], e.p2, e.c2};
+    return ConvFwd<14, 32, 64>{M, N, K, e.p1, P[2], P[3], e.p2, train ? e.c2 : nullptr};
   else if constexpr (OP == OP_CONV3_FWD)
-    return ConvFwd<7, 64, 128>{M, N, K, e.p2, P[4], P[5], e.p3, e.c3};
+    return ConvFwd<7, 64, 128>{M, N, K, e.p2, P[4], P[5], e.p3, train ? e.c3 : nullptr};
   else if constexpr (OP == OP_CONV4_FWD)
-    return ConvFwd<4, 128, 256>{M, N, K, e.p3, P[6], P[7], e.p4, e.c4};
+    return ConvFwd<4, 128, 256>{M, N, K, e.p3, P[6], P[7], e.p4, train ? e.c4 : nullptr};
   else if constexpr (OP == OP_FC1_FWD)
     return FcFwd<true>{M, N, K, e.p4, P[8], P[9], e.h1, seed, 1u, thr, e.inv_keep, e.seed_value};
   else if constexpr (OP == OP_FC2_FWD)
