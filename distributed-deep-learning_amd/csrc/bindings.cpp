@@ -85,7 +85,10 @@ class PyEngine {
     for (int i = 0; i < ddl::OP_COUNT; ++i) {
       // the eval-only large tiles exist for the conv2-4 forward ops only
       const bool big = i == ddl::OP_CONV2_FWD || i == ddl::OP_CONV3_FWD || i == ddl::OP_CONV4_FWD;
-      TORCH_CHECK(c[i] >= 0 && c[i] < (big ? ddl::NUM_EVAL_TILE_CFGS : ddl::NUM_TILE_CFGS),
+      // (CFG_KWAVE: the K-wave launch; ops without a K-wave instantiation fall back to the
+      // one-wave 32x32 tile, engine_impl.h launch_cfg)
+      TORCH_CHECK(c[i] == ddl::CFG_KWAVE ||
+                      (c[i] >= 0 && c[i] < (big ? ddl::NUM_EVAL_TILE_CFGS : ddl::NUM_TILE_CFGS)),
                   "tile config out of range");
       e_.eval_cfg[i] = (int)c[i];
     }

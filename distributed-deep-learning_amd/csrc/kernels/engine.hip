@@ -29,7 +29,9 @@ Engine::Engine() {
   // 313.4 -> 310.6 us (profiles/r2_runner_tune_kwave.log); fc1 data gradient as the K-wave
   // half of one packed launch with its weight gradient (gemm_pack_kernel, 4 waves), instead
   // of the one-wave dual launch + wide reduce: 308.7 -> 304.4 us (profiles/r2_runner_tune_pack.log)
-  static const int defc[OP_COUNT] = {3, 3, 3, 3, CFG_KWAVE, 3, 3, 5, CFG_KWAVE, 5,
+  // (round 3, after the direct conv1 kernels: fc2 data gradient on the K-wave half of a packed
+  // launch with its weight gradient, like fc1's: 292.8 -> 291.5 us, profiles/r3_runner_tune.log)
+  static const int defc[OP_COUNT] = {3, 3, 3, 3, CFG_KWAVE, 3, CFG_KWAVE, 5, CFG_KWAVE, 5,
                                      3, 3, 3, 3, 3, 3, 3};
   // (re-tuned in the real step with scripts/sched_ab.py after the compact 52-row conv3
   // enumeration and the wgrad row decode: conv3 forward split 4 + in-launch reduce instead of
@@ -56,9 +58,12 @@ Engine::Engine() {
   // conv3 on the eval-only 128x128 block (2x2 waves of 64x64), 6.62 -> 6.53 ms (108 TF) —
   // the larger eval tiles (9-12) gain at most 1.4 %, so the eval is bound by the main loop,
   // not by tile shape (profiles/r2_eval_sweep_big_tiles.log)
-  eval_cfg[OP_CONV2_FWD] = 6;
-  eval_cfg[OP_CONV3_FWD] = 9;
-  eval_cfg[OP_CONV4_FWD] = 6;
+  // round 3 (scripts/eval_sweep.py on the current build, profiles/r3_eval_sweep.log): the
+  // one-wave 64x64 tile (4 fragments per wave, no LDS sharing between waves) for conv2-4,
+  // full test-set eval 5.04 -> 4.64 ms
+  eval_cfg[OP_CONV2_FWD] = 0;
+  eval_cfg[OP_CONV3_FWD] = 0;
+  eval_cfg[OP_CONV4_FWD] = 0;
   memcpy(splits, defs, sizeof(defs));
   memcpy(workers, defw, sizeof(defw));
   for (int op = 0; op < OP_COUNT; ++op) wide[op] = inl[op] ? (1 << 20) : 1;
