@@ -174,6 +174,11 @@ struct HasLoadB1<P, std::void_t<decltype(std::declval<const P&>().loadB1(
 #ifndef DDL_LDSDMA_WGRAD
 #define DDL_LDSDMA_WGRAD 0
 #endif
+// LDS-DMA staging of one-wave MULTI-fragment tiles (64x64 / 32x64, BN = 64: the eval forward's
+// one-wave 64x64 tiles) for K-contiguous A / MN-contiguous B policies with DMA (mainloop_dma_mf)
+#ifndef DDL_LDSDMA_MF
+#define DDL_LDSDMA_MF 1
+#endif
 // a policy whose A operand has rows that are not in memory (the weight gradients' ones row)
 template <class P, class = void>
 struct HasOnesA : std::false_type {};
@@ -230,8 +235,12 @@ struct GemmTile {
   static constexpr bool DMA = DDL_LDSDMA > 0 && HasDma<P>::value && SOLO && TM * TN == 1 &&
                               BM == 32 && BN == 32 && BK == 32 && !DIRECT && !BDIR;
   static constexpr int DMA_NB = DDL_LDSDMA > 0 ? DDL_LDSDMA : 1;
+  static constexpr bool DMA_MF = DDL_LDSDMA_MF > 0 && HasDma<P>::value && SOLO && TM * TN > 1 &&
+                                 BN == 64 && BK == 32 && AK && !BKC && !DIRECT && !BDIR &&
+                                 !HasOnesA<P>::value;
   static constexpr int LDS_F4 =
       DMA ? DMA_NB * 512
+          : DMA_MF ? (BM * BK + BK * BN) / 4
           : DIRECT ? 0 : (NBUF * (A_ELEMS + (BDIR ? 0 : B_ELEMS))) / 4;
   // A wave with a single 32x32 fragment alternates two accumulator chains (summed at the
   // end) so consecutive MFMAs are independent.
@@ -262,6 +271,7 @@ struct GemmTile {
   static DDL_DEV void mainloop(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
                                f32x16 (&acc)[TM][TN], const Win& w = Win()) {
     if constexpr (DMA) mainloop_dma(p, m_blk, n_blk, kb, ke, lds, acc, w);
+    else if constexpr (DMA_MF) mainloop_dma_mf(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else if constexpr (DIRECT) mainloop_direct(p, m_blk, n_blk, kb, ke, acc, w);
     else if constexpr (PIPE) mainloop_pipe(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else mainloop_basic(p, m_blk, n_blk, kb, ke, lds, acc, w);
@@ -661,6 +671,90 @@ struct GemmTile {
       }
     }
     if constexpr (NCH == 2) acc[0][0] += acc2;
+  }
+
+  // LDS-DMA loop of a one-wave tile with TM x TN fragments (K-contiguous A: BM rows of 8 quads,
+  // quad q of row r at q ^ ((r >> 1) & 7); MN-contiguous B, BN = 64: k-row k of 16 quads, the
+  // two 32-column halves swapped on rows with bit 2 set, so the lane halves' reads of rows k and
+  // k + 4 land in opposite bank halves).  One image: tile t+1 is DMA'd once tile t's fragments
+  // are in registers, under tile t's TM*TN*16 MFMAs.  Same MFMA order as mainloop_basic.
+  static DDL_DEV void mainloop_dma_mf(const P& p, int m_blk, int n_blk, int kb, int ke,
+                                      float* lds, f32x16 (&acc)[TM][TN], const Win& w) {
+    constexpr int NDA = BM * BK / 4 / 64, NDB = BK * BN / 4 / 64;  // 1 KB DMAs per tile
+    const int lane = threadIdx.x & 63;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int nk = (ke - kb + BK - 1) / BK;
+    typename P::AInfo ai[NDA];
+    typename P::BInfo bi[NDB];
+#pragma unroll
+    for (int it = 0; it < NDA; ++it) {
+      const int sl = it * 64 + lane, row = sl >> 3, q = sl & 7;
+      ai[it] = p.prepA(m_blk + row, (q ^ ((row >> 1) & 7)) * 4);
+    }
+#pragma unroll
+    for (int it = 0; it < NDB; ++it) {
+      const int sl = it * 64 + lane, k = sl >> 4, q = sl & 15;
+      bi[it] = p.prepB(n_blk + (q ^ (((k >> 2) & 1) << 3)) * 4, k);
+    }
+    const uint32_t base = lds_addr(lds);
+    auto dma = [&](int k0) {
+#pragma unroll
+      for (int it = 0; it < NDA; ++it) dma16(srcA(p, ai[it], k0, w), base + it * 1024);
+#pragma unroll
+      for (int it = 0; it < NDB; ++it)
+        dma16(srcB(p, bi[it], k0, w), base + BM * BK * 4 + it * 1024);
+    };
+    const float* As = lds;
+    const float* Bs = lds + BM * BK;
+    float av[R][TM][4], bv[R][TN][4];
+    auto rd = [&]() {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = i * 32 + lr;
+          const int q = (2 * r + lh) ^ ((row >> 1) & 7);
+          const float4 t = *reinterpret_cast<const float4*>(As + row * BK + q * 4);
+          av[r][i][0] = t.x; av[r][i][1] = t.y; av[r][i][2] = t.z; av[r][i][3] = t.w;
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const int k = 8 * r + 4 * lh + s;
+            bv[r][j][s] = Bs[k * BN + ((j * 32 + lr) ^ (((k >> 2) & 1) << 5))];
+          }
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+    if (nk <= 0) return;
+    dma(kb);
+    for (int kt = 0; kt < nk; ++kt) {
+      vm_wait<0>();   // tile kt is in the image
+      rd();
+      lgkm_wait0();   // its fragments are in registers: the image may be restaged
+      if (kt + 1 < nk) dma(kb + (kt + 1) * BK);
+#if DDL_MFMA_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = mfma32x32x2(av[r][i][s], bv[r][j][s], acc[i][j]);
+#if DDL_MFMA_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
+    }
   }
 
   static DDL_DEV void mainloop_basic(const P& p, int m_blk, int n_blk, int kb, int ke,
