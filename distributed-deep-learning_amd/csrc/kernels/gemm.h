@@ -1171,6 +1171,15 @@ DDL_DEV void run_sub(const P& p, const SubGrid& g, int vb, float* lds, int* flag
 #else
 #define DDL_GEMM_OCC
 #endif
+// the same for the dual (data + weight gradient) launches only
+#ifndef DDL_DUAL_WAVES
+#define DDL_DUAL_WAVES 0
+#endif
+#if DDL_DUAL_WAVES > 0
+#define DDL_DUAL_OCC __attribute__((amdgpu_waves_per_eu(DDL_DUAL_WAVES)))
+#else
+#define DDL_DUAL_OCC DDL_GEMM_OCC
+#endif
 
 template <int BM, int BN, int BK, int WM, int WN, class P>
 __global__ void __launch_bounds__(WM * WN * 64) DDL_GEMM_OCC
@@ -1349,7 +1358,7 @@ struct TailAux {
 // numbering holds).  The tail path must stay under the GEMM paths' VGPR count: at 8 float4
 // per lane it raised the conv4 dual from 113 to 149 VGPRs (3 -> 2 waves/SIMD, +9 us).
 template <class CA, class PA, class CB, class PB, class AUX>
-__global__ void __launch_bounds__(64) DDL_GEMM_OCC
+__global__ void __launch_bounds__(64) DDL_DUAL_OCC
 gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut, int bfirst) {
   static_assert(CA::NT == 64 && CB::NT == 64, "dual launch needs one-wave blocks");
   using TA = GemmTile<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>;
