@@ -209,6 +209,40 @@ def test_conv1_wgrad_direct_matches_gemm_path(setup, B):
             assert torch.equal(a, b), t.name
 
 
+@pytest.mark.parametrize("B", [8, 13, 130])
+def test_conv1_direct_kernels_odd_batches(B):
+    """The direct conv1 kernels at batch sizes that exercise their edges: two full reduce groups
+    of 8 blocks (B = 8), a partial last group (B = 13: 26 blocks), and more than 32 groups
+    (B = 130: the final reduce level loops over two chunks) — against the GEMM path, and conv1's
+    dW / db against the fp64 autograd reference."""
+    from ddl_amd.models.hip_engine import HipEngine
+    torch.manual_seed(B)
+    flat = torch.zeros(TOTAL_NUMEL)
+    init_params_(flat, CANON_OFFSETS, seed=11)
+    params = flat.to(DEV)
+    grads = torch.zeros_like(params)
+    eng = HipEngine(params, grads, CANON_OFFSETS, batch=B, graph=False, eval_chunk=500,
+                    keep_prob=1.0)
+    x = torch.rand(B, 784)
+    y = torch.randint(0, 10, (B,))
+    out = []
+    for on in (True, False):
+        eng.eng.set_conv1_direct(on)
+        eng.eng.set_conv1_wgrad_direct(on)
+        grads.zero_()
+        eng.forward_backward(x.to(DEV), y.to(DEV), 1.0, 0)
+        torch.cuda.synchronize()
+        out.append((grads.clone(), eng.eng.buffer("p1", B).clone()))
+    va, vb = param_views(out[0][0], CANON_OFFSETS), param_views(out[1][0], CANON_OFFSETS)
+    for t, a, b in zip(TENSORS, va, vb):
+        assert rel_err(a, b) < 1e-5, t.name
+    assert rel_err(out[0][1], out[1][1]) < 1e-6
+    _, r64 = ref_grads(flat, x, y, 1.0, 0, torch.float64)
+    for t in TENSORS[:2]:
+        o = CANON_OFFSETS[t.index]
+        assert rel_err(out[0][0][o:o + t.numel], r64[t.index].reshape(-1)) < 5e-3, t.name
+
+
 @pytest.mark.parametrize("B", [100, 37])
 def test_head_slab_bit_identical(setup, B):
     """fc2's split-K reduce folded into the fused head (head.hip head_fused_kernel<true>: the
