@@ -121,6 +121,10 @@ struct Engine {
   // (their data gradients are the longer poles; conv4's stream-K loses its XCD-major numbering).
   // DDL_DUAL_BFIRST overrides (scripts/ab_env.sh).
   int dual_bfirst = 1 << OP_CONV2_DGRAD;
+  // bit op: that dual launch interleaves its two problems' blocks in proportion instead
+  // (overrides dual_bfirst; DDL_DUAL_MIX)
+  int dual_mix = 0;
+  int dual_order(int op) const { return ((dual_mix >> op) & 1) ? 2 : ((dual_bfirst >> op) & 1); }
   // bit op: that op's split-K uses one chunk length for every tile, sized so the tile with the
   // longest tap window gets splits[op] pieces (gemm.h KFixOf; only the K-map conv forwards /
   // data gradients honour it).  DDL_KFIX overrides.

@@ -49,6 +49,7 @@ Engine::Engine() {
   // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
   static const bool inl[OP_COUNT] = {0, 1, 1, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0};
   if (const char* s = getenv("DDL_DUAL_BFIRST")) dual_bfirst = (int)strtol(s, nullptr, 0);
+  if (const char* s = getenv("DDL_DUAL_MIX")) dual_mix = (int)strtol(s, nullptr, 0);
   if (const char* s = getenv("DDL_FC_CHAIN")) fc_chain = s[0] == '1';
   if (const char* s = getenv("DDL_KFIX")) kfix = (int)strtol(s, nullptr, 0);
   memcpy(cfg, defc, sizeof(defc));

@@ -153,7 +153,7 @@ inline void dual_b(Engine& e, const PA& pa, const PB& pb, int B, hipStream_t st)
   launch_gemm_dual<CA, PA, TileCfg<CB>, PB>(pa, e.sarg(OA), e.workers[OA], e.scratch[0], \
                                             e.wide[OA], pb, e.sarg(OB), e.workers[OB], \
                                             e.scratch[1], e.wide[OB], st, AUXV, nullptr, \
-                                            (e.dual_bfirst >> OA) & 1)
+                                            e.dual_order(OA))
   // the fc2 dual carries fc3's weight gradient; the others a pending optimizer tail
 #define DDL_DUAL_SW(AUXV)                      \
   switch (e.cfg[OB]) {                         \
@@ -350,7 +350,7 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
   SubGrid gb;
   launch_gemm_dual<CA, PA, CB, PB>(pa, e.sarg(OA), e.workers[OA], e.scratch[0], e.wide[OA], pb,
                                    e.sarg(OB), e.workers[OB], e.scratch[1], e.wide[OB], st,
-                                   TailAux(e.tail), &gb, (e.dual_bfirst >> OA) & 1);
+                                   TailAux(e.tail), &gb, e.dual_order(OA));
   e.tail = UpdTail();
   constexpr bool kFinal = ON == OP_CONV1_WGRAD;
   if constexpr (kFinal) {

@@ -1380,15 +1380,27 @@ gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut, int bfirst) {
     ut.run(b - gemm_blocks);
     return;
   }
-  // bfirst: problem B's blocks are dispatched first (longest-first ordering shortens the
-  // launch's tail when B's blocks run longer)
-  const bool is_a = bfirst ? (b >= gb.nblocks) : (b < ga.nblocks);
+  // bfirst 1: problem B's blocks are dispatched first (longest-first ordering shortens the
+  // launch's tail when B's blocks run longer); 0: A's first; 2: the two interleaved in
+  // proportion (block b is A's iff floor((b + 1) na / n) > floor(b na / n): A's blocks spread
+  // evenly over the dispatch order)
+  int ia, ib;
+  bool is_a;
+  if (bfirst == 2) {
+    const int na = ga.nblocks, n = gemm_blocks;
+    const int lo = (int)(((long long)b * na) / n), hi = (int)(((long long)(b + 1) * na) / n);
+    is_a = hi > lo;
+    ia = lo;
+    ib = b - lo;
+  } else {
+    is_a = bfirst ? (b >= gb.nblocks) : (b < ga.nblocks);
+    ia = bfirst ? b - gb.nblocks : b;
+    ib = bfirst ? b : b - ga.nblocks;
+  }
   if (is_a)
-    run_sub<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, bfirst ? b - gb.nblocks : b, lds,
-                                                        flag);
+    run_sub<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, ia, lds, flag);
   else
-    run_sub<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, bfirst ? b : b - ga.nblocks, lds,
-                                                        flag);
+    run_sub<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, ib, lds, flag);
 }
 
 // Wide split-K reduce (mode 2): RL lanes cooperate on one float4 output element; `gid` is the
