@@ -21,6 +21,14 @@
 namespace ddl {
 
 constexpr int kC1wGroup = 8;       // block partials per first-level group
+// staged image row pitch: a half-wave's ds_read_b32 reads one pixel at the 25 tap offsets
+// ky * pitch + kx; pitch 37 (5 mod 32) puts the five tap rows in disjoint bank ranges
+// (pitch 32: 5-way conflicts)
+#ifndef DDL_C1W_PITCH
+#define DDL_C1W_PITCH 37
+#endif
+constexpr int kC1wPitch = DDL_C1W_PITCH;
+constexpr int kC1wLdsBand = 18 * kC1wPitch + 2;  // (+2: keeps the partials 16-B aligned)
 
 // optional optimizer on conv1's weight / bias as the final reduce writes them (the W = 1 tail
 // path: the last segment's update needs no launch of its own); on = 0: gradients only
@@ -116,12 +124,12 @@ DDL_DEV void conv1_wgrad_block(const float* __restrict__ x, const float* __restr
                                float* __restrict__ part, int* __restrict__ tickets, float* lds,
                                int* flag, const C1Adam& ad) {
   const int b = blk >> 1, h = blk & 1;
-  float* T = lds;              // [18][32] image band
-  float* R = lds + 18 * 32;    // [4 waves][1024] wave partials
+  float* T = lds;                   // [18][kC1wPitch] image band
+  float* R = lds + kC1wLdsBand;     // [4 waves][1024] wave partials
   const int y0 = 14 * h - 2;
   const float* img = x + (size_t)b * 784;
-  for (int e = threadIdx.x; e < 18 * 32; e += 256) {
-    const int iy = y0 + (e >> 5), ix = (e & 31) - 2;
+  for (int e = threadIdx.x; e < 18 * kC1wPitch; e += 256) {
+    const int iy = y0 + e / kC1wPitch, ix = e % kC1wPitch - 2;
     T[e] = ((unsigned)iy < 28u && (unsigned)ix < 28u) ? img[iy * 28 + ix] : 0.f;
   }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -134,7 +142,7 @@ DDL_DEV void conv1_wgrad_block(const float* __restrict__ x, const float* __restr
 #pragma unroll
   for (int s = 0; s < 49; ++s) bv[s] = bload1(dr, (pbase + (98 * wave + 2 * s + hk) * 32 + col) * 4);
   // A operand row `col` = tap (ky, kx), row 25 = ones (db), rows 26..31 = 0
-  const int toff = col < 25 ? (col / 5) * 32 + col % 5 : 0;
+  const int toff = col < 25 ? (col / 5) * kC1wPitch + col % 5 : 0;
   const float arow = col == 25 ? 1.f : 0.f;
   __syncthreads();
   f32x16 acc;
@@ -144,7 +152,7 @@ DDL_DEV void conv1_wgrad_block(const float* __restrict__ x, const float* __restr
   for (int s = 0; s < 49; ++s) {
     const int p = 98 * wave + 2 * s + hk;
     const int py = p / 28, px = p - py * 28;
-    const float t = T[py * 32 + px + toff];
+    const float t = T[py * kC1wPitch + px + toff];
     acc = mfma32x32x2(col < 25 ? t : arow, bv[s], acc);
   }
   // wave partials -> LDS [wave][row 8g + 4hk + r][col]; block sum in a fixed order
@@ -175,7 +183,7 @@ conv1_wgrad_kernel(PR pr, const float4* __restrict__ rslab, int S, int rgx, int 
                    const float* __restrict__ x, const float* __restrict__ d1, int B,
                    float* __restrict__ gw, float* __restrict__ gb, float* __restrict__ part,
                    int* __restrict__ tickets, C1Adam ad) {
-  __shared__ float lds[18 * 32 + 4 * 1024];
+  __shared__ float lds[kC1wLdsBand + 4 * 1024];
   __shared__ int flag;
   // conv1's blocks first: their MFMA pass + two reduce levels are the launch's critical path,
   // the independent reduce blocks fill the CUs behind them
