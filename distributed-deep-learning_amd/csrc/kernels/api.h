@@ -150,6 +150,11 @@ struct Engine {
   // reduce epilogue, the rest as tail blocks of that launch (engine_impl.h dual_then_b).
   // Cleared when taken; the runner launches it as before when it is still pending.
   UpdTail final_upd;
+  // eval forward: conv2 on the tap-skipping K map (DDL_EVAL_KMAP2=0: the image-major GEMM)
+  bool eval_kmap2 = [] {
+    const char* e = getenv("DDL_EVAL_KMAP2");
+    return !e || e[0] != '0';
+  }();
   // conv1 forward on the direct LDS-staged kernel (conv1.hip) instead of the GEMM engine's
   // gather-bound K = 25 launch.  DDL_CONV1_DIRECT=0: the GEMM path
   bool conv1_direct = [] {

@@ -112,6 +112,14 @@ template <int OP>
 void run_op_inst(Engine& e, const float* x, int B, const uint32_t* seed, bool train,
                      hipStream_t st, int si) {
   const auto p = make_policy<OP>(e, B, x, seed, train);
+  if constexpr (OP == OP_CONV2_FWD) {
+    // eval: conv2 on the tap-skipping K map (group-major rows), one-wave 64x64 tiles
+    if (!train && e.eval_kmap2 && e.eval_cfg[OP] == 0) {
+      const ConvFwd<14, 32, 64, true> pk{p.M, p.N, p.K, p.x, p.w, p.bias, p.out, p.code};
+      launch_gemm<TILE_0>(pk, 1, 1, e.scratch[si], st, 0);
+      return;
+    }
+  }
   if constexpr (OP == OP_CONV2_FWD || OP == OP_CONV3_FWD || OP == OP_CONV4_FWD) {
     if (!train && e.eval_cfg[OP] >= NUM_TILE_CFGS) {  // eval-only large tiles, no split
       switch (e.eval_cfg[OP]) {

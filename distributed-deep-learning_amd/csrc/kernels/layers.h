@@ -71,7 +71,10 @@ struct LinInfo {   // linear operand: element offset of (row, k = 0 + kk), valid
 #define DDL_XCD_IMG 0
 #endif
 
-template <int H, int CIN, int COUT>
+// KM: the K map (tap skipping, group-major rows) — on by default for the small maps (H <= 7);
+// the eval forward also takes it for conv2 (ConvFwd<14, 32, 64, true>: its border pool windows
+// skip 11 % of the taps, and at 10k images the group-major tiles keep their parallelism)
+template <int H, int CIN, int COUT, bool KM = (H <= 7)>
 struct ConvFwd {
   static constexpr int HP = (H + 1) / 2;
   static constexpr bool ODD = (H % 2) == 1;
@@ -93,7 +96,7 @@ struct ConvFwd {
   // tile) and conv2 (14x14: only 16 % of the taps fall in the halo, while the group-major
   // order spreads a tile's gathers over 32 images: 26.1 -> 26.6 us) keep the image-major
   // order m = b*RP + 4g + q.
-  static constexpr bool KMAP = PADIN && H <= 7;
+  static constexpr bool KMAP = PADIN && KM;
   static constexpr bool KFIX = true;  // kwin / kvlen host-callable: window-aware split-K (gemm.h)
   static constexpr bool XCD_CONTIG = DDL_XCD_IMG && !KMAP;
   using KWin = TapWin;
