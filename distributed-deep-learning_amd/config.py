@@ -48,7 +48,8 @@ class TrainConfig:
     log_jsonl: Optional[str] = None
     checkpoint_dir: Optional[str] = None
     checkpoint_every: int = 0
-    resume: bool = False
+    resume: bool = False            # continue from checkpoint_dir at its global step
+    max_steps: Optional[int] = None  # stop after this many global steps (a preempted run)
     target_acc: Optional[float] = None
     quiet: bool = False
     watchdog_s: float = 600.0
@@ -100,7 +101,11 @@ def add_args(p: argparse.ArgumentParser, mode_default: str = "sync") -> argparse
     p.add_argument("--log-jsonl", default=None)
     p.add_argument("--checkpoint-dir", default=None)
     p.add_argument("--checkpoint-every", type=int, default=0)
-    p.add_argument("--resume", action="store_true")
+    p.add_argument("--resume", action="store_true",
+                   help="continue from --checkpoint-dir: same data index, eval cadence and "
+                        "dropout seeds as an uninterrupted run")
+    p.add_argument("--max-steps", type=int, default=None,
+                   help="stop after this many global steps (checkpointed if --checkpoint-dir)")
     p.add_argument("--target-acc", type=float, default=None)
     p.add_argument("--quiet", action="store_true")
     p.add_argument("--watchdog-s", type=float, default=d.watchdog_s)
@@ -121,4 +126,4 @@ def from_args(a: argparse.Namespace) -> TrainConfig:
         check_provenance=a.check_provenance, overlap=not a.no_overlap, log_jsonl=a.log_jsonl,
         exchange_backend=a.exchange_backend,
         checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
-        resume=a.resume, target_acc=a.target_acc, quiet=a.quiet, watchdog_s=a.watchdog_s)
+        resume=a.resume, max_steps=a.max_steps, target_acc=a.target_acc, quiet=a.quiet, watchdog_s=a.watchdog_s)

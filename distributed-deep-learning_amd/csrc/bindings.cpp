@@ -70,7 +70,8 @@ class PyEngine {
   void set_cfg(std::vector<int64_t> c) {
     TORCH_CHECK((int)c.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " tile configs");
     for (int i = 0; i < ddl::OP_COUNT; ++i) {
-      TORCH_CHECK((c[i] >= 0 && c[i] < ddl::NUM_TILE_CFGS) || c[i] == ddl::CFG_KWAVE,
+      TORCH_CHECK((c[i] >= 0 && c[i] < ddl::NUM_TILE_CFGS) || c[i] == ddl::CFG_KWAVE ||
+                      c[i] == ddl::CFG_MF16,
                   "tile config out of range");
       e_.cfg[i] = (int)c[i];
     }
@@ -477,6 +478,7 @@ class PyRcclAsync {
   }
   void resume() { r_->resume(); }
   int64_t t(int64_t ps) const { return r_->t((int)ps); }
+  void set_t(int64_t ps, int64_t t) { r_->set_t((int)ps, t); }
   int64_t served() const { return r_->served(); }
   std::vector<std::array<int64_t, 4>> provenance() const { return r_->provenance(); }
 
@@ -653,11 +655,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("w"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr_t"), py::arg("b1"),
         py::arg("b2"), py::arg("eps"), py::arg("scale") = 1.0);
   m.def("momentum_flat", &momentum_flat, "Fused momentum SGD on a flat shard");
-  m.def("mfma_peak", [](at::Tensor out, int64_t blocks, int64_t iters) {
+  m.def("mfma_peak", [](at::Tensor out, int64_t blocks, int64_t iters, int64_t kind) {
     check_f32_cuda(out, "out");
     TORCH_CHECK(out.numel() >= blocks * 64, "out too small");
-    ddl::launch_mfma_peak(out.data_ptr<float>(), (int)blocks, (int)iters, cur_stream());
-  }, "diagnostic: 2 chains of v_mfma_f32_32x32x2_f32 per wave (2*iters MFMAs)");
+    ddl::launch_mfma_peak(out.data_ptr<float>(), (int)blocks, (int)iters, cur_stream(), (int)kind);
+  }, "diagnostic: per iteration 2 chains of v_mfma_f32_32x32x2_f32 (kind 0) or 4 of "
+     "v_mfma_f32_16x16x4_f32 (kind 1), the same FLOPs", py::arg("out"), py::arg("blocks"),
+     py::arg("iters"), py::arg("kind") = 0);
   m.def("gemm_nomem", [](at::Tensor out, at::Tensor slab, int64_t M, int64_t N, int64_t K,
                          int64_t splits) {
     ddl::launch_gemm_nomem(out.data_ptr<float>(), (int)M, (int)N, (int)K, (int)splits,
@@ -771,6 +775,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("pause", &PyRcclAsync::pause)
       .def("resume", &PyRcclAsync::resume)
       .def("t", &PyRcclAsync::t)
+      .def("set_t", &PyRcclAsync::set_t)
       .def("served", &PyRcclAsync::served)
       .def("provenance", &PyRcclAsync::provenance);
 

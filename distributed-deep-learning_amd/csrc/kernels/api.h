@@ -66,7 +66,7 @@ void launch_head_bwd(const float* h2, const float* w, const float* dlog, int B,
                      float* gw, float* gb, float* dpre2, hipStream_t st);
 
 // ---- diagnostics (diag.hip) -------------------------------------------------------------------
-void launch_mfma_peak(float* out, int blocks, int iters, hipStream_t st);
+void launch_mfma_peak(float* out, int blocks, int iters, hipStream_t st, int kind = 0);
 void launch_gemm_nomem(float* out, int M, int N, int K, int splits, void* slab, int* tickets,
                        hipStream_t st);
 
@@ -95,6 +95,10 @@ constexpr int NUM_EVAL_TILE_CFGS = 13;
 // training-only: 32x32 one-wave tiles with the K range split over the waves of ONE workgroup
 // (gemm.h gemm_kwave_kernel; `splits` picks 4 / 8 / 16 waves); fc layers only
 constexpr int CFG_KWAVE = 13;
+// training-only: the one-wave 32x32x32 tile on v_mfma_f32_16x16x4_f32 with LDS-DMA staging
+// (gemm.h GemmTile::mainloop_dma16); conv2-4 forward / data gradient / weight gradient only
+// (other ops fall back to config 3)
+constexpr int CFG_MF16 = 14;
 
 struct Engine {
   const float* P[14] = {};   // parameter tensors v0..v13 (any flat layout)
@@ -483,6 +487,9 @@ class RcclAsync {
   void pause();
   void resume();
   int64_t t(int ps) const;
+  // a hosted PS's step counter before start() (resume: the checkpoint's t, restored after the
+  // object was built — Adam's bias correction continues instead of restarting at t = 1)
+  void set_t(int ps, int64_t t);
   int64_t served() const { return served_.load(); }
   // (worker, ps, that worker's round at this PS, PS step) per applied push
   const std::vector<std::array<int64_t, 4>>& provenance() const { return prov_; }

@@ -20,8 +20,25 @@ __global__ void __launch_bounds__(64) mfma_peak_kernel(float* out, int iters) {
   out[blockIdx.x * 64 + threadIdx.x] = s;
 }
 
-void launch_mfma_peak(float* out, int blocks, int iters, hipStream_t st) {
-  hipLaunchKernelGGL(mfma_peak_kernel, dim3(blocks), dim3(64), 0, st, out, iters);
+// the same FLOPs per iteration on v_mfma_f32_16x16x4_f32: four independent 16x16 accumulators
+__global__ void __launch_bounds__(64) mfma16_peak_kernel(float* out, int iters) {
+  f32x4 acc[4] = {};
+  float a = 1.0f + 1e-7f * threadIdx.x, b = 0.999f;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
+  out[blockIdx.x * 64 + threadIdx.x] = s;
+}
+
+void launch_mfma_peak(float* out, int blocks, int iters, hipStream_t st, int kind) {
+  if (kind == 1)
+    hipLaunchKernelGGL(mfma16_peak_kernel, dim3(blocks), dim3(64), 0, st, out, iters);
+  else
+    hipLaunchKernelGGL(mfma_peak_kernel, dim3(blocks), dim3(64), 0, st, out, iters);
 }
 
 }  // namespace ddl

@@ -29,6 +29,8 @@ namespace ddl {
 #define TILE_10 128, 64, 32, 2, 2
 #define TILE_11 256, 64, 32, 4, 1
 #define TILE_12 128, 128, 32, 4, 1
+// training: one-wave 32x32x32 on 16x16x4 MFMAs with LDS-DMA staging (CFG_MF16)
+#define TILE_14 32, 32, 32, 1, 1, 1
 
 template <class P>
 inline void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const SplitScratch& sc,
@@ -39,6 +41,13 @@ inline void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const Spli
       return;
     }
     c = 3;  // not instantiated for this op: the one-wave 32x32 tile
+  }
+  if (c == CFG_MF16) {
+    if constexpr (Mf16OK<P>::value) {
+      launch_gemm<TILE_14>(p, s, wide_thr, sc, st, w);
+      return;
+    }
+    c = 3;
   }
   switch (c) {
     case 0: launch_gemm<TILE_0>(p, s, wide_thr, sc, st, w); break;
@@ -138,7 +147,7 @@ void run_op_inst(Engine& e, const float* x, int B, const uint32_t* seed, bool tr
 
 // ---- dual launches: data- and weight-gradient GEMM of one layer in one kernel -----------------
 // dual launches are instantiated for these one-wave configs (others run back to back)
-inline bool one_wave_cfg(int c) { return c == 0 || c == 3 || c == 4 || c == 5; }
+inline bool one_wave_cfg(int c) { return c == 0 || c == 3 || c == 4 || c == 5 || c == CFG_MF16; }
 
 // fc3's weight gradient as aux blocks (head.h), pending after the fused head kernel
 inline HeadWgradAux head_aux(Engine& e, int B) {
@@ -162,13 +171,31 @@ inline void dual_b(Engine& e, const PA& pa, const PB& pb, int B, hipStream_t st)
                                             e.wide[OA], pb, e.sarg(OB), e.workers[OB], \
                                             e.scratch[1], e.wide[OB], st, AUXV, nullptr, \
                                             e.dual_order(OA))
-  // the fc2 dual carries fc3's weight gradient; the others a pending optimizer tail
-#define DDL_DUAL_SW(AUXV)                      \
-  switch (e.cfg[OB]) {                         \
-    case 0: DDL_DUAL_B(TILE_0, AUXV); break;   \
-    case 3: DDL_DUAL_B(TILE_3, AUXV); break;   \
-    case 4: DDL_DUAL_B(TILE_4, AUXV); break;   \
-    default: DDL_DUAL_B(TILE_5, AUXV); break;  \
+  // the fc2 dual carries fc3's weight gradient; the others a pending optimizer tail.
+  // CFG_MF16 pairs with the 32x32 configs 3 / 5 / 14 only (instantiation count); A on 14
+  // (CA::V == 1) takes B on 3, 5 or 14.
+#define DDL_DUAL_SW(AUXV)                                                         \
+  if constexpr (CA::V == 1) {                                                     \
+    switch (e.cfg[OB]) {                                                          \
+      case CFG_MF16:                                                              \
+        if constexpr (Mf16OK<PB>::value) { DDL_DUAL_B(TILE_14, AUXV); break; }    \
+        [[fallthrough]];                                                          \
+      case 3: DDL_DUAL_B(TILE_3, AUXV); break;                                    \
+      default: DDL_DUAL_B(TILE_5, AUXV); break;                                   \
+    }                                                                             \
+  } else {                                                                        \
+    switch (e.cfg[OB]) {                                                          \
+      case 0: DDL_DUAL_B(TILE_0, AUXV); break;                                    \
+      case CFG_MF16:                                                              \
+        if constexpr (Mf16OK<PB>::value && CA::BM == 32 && CA::BN == 32) {        \
+          DDL_DUAL_B(TILE_14, AUXV);                                              \
+          break;                                                                  \
+        }                                                                         \
+        [[fallthrough]];                                                          \
+      case 3: DDL_DUAL_B(TILE_3, AUXV); break;                                    \
+      case 4: DDL_DUAL_B(TILE_4, AUXV); break;                                    \
+      default: DDL_DUAL_B(TILE_5, AUXV); break;                                   \
+    }                                                                             \
   }
   if constexpr (OA == OP_FC2_DGRAD) {
     e.flush_tail(st);
@@ -215,6 +242,12 @@ void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipSt
   using PB = std::decay_t<decltype(pb)>;
   switch (e.cfg[OA]) {
     case 0: dual_b<TileCfg<TILE_0>, OA, OB, PA, PB>(e, pa, pb, B, st); break;
+    case CFG_MF16:
+      if constexpr (Mf16OK<PA>::value) {
+        dual_b<TileCfg<TILE_14>, OA, OB, PA, PB>(e, pa, pb, B, st);
+        break;
+      }
+      [[fallthrough]];
     case 3: dual_b<TileCfg<TILE_3>, OA, OB, PA, PB>(e, pa, pb, B, st); break;
     case 4: dual_b<TileCfg<TILE_4>, OA, OB, PA, PB>(e, pa, pb, B, st); break;
     default: dual_b<TileCfg<TILE_5>, OA, OB, PA, PB>(e, pa, pb, B, st); break;
@@ -345,7 +378,7 @@ inline bool final_split_conv12(const Engine& e, const UpdTail& in, const PB& pb,
 // need only what the dual wrote; saves one dependent boundary: conv2 dual -> [conv2 wgrad
 // reduce | conv1 wgrad GEMM]).  Instantiated for the tuned configs (OA: 32x32, OB: 32x32
 // BK 16 pipelined, ON: 32x32 split-K); any other schedule takes the unfused sequence.
-template <int OA, int OB, int ON, class CB>
+template <int OA, int OB, int ON, class CA, class CB>
 void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
   const auto pa = make_policy<OA>(e, B, x, seed, true);
   const auto pb = make_policy<OB>(e, B, x, seed, true);
@@ -353,7 +386,6 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
   using PA = std::decay_t<decltype(pa)>;
   using PB = std::decay_t<decltype(pb)>;
   using PN = std::decay_t<decltype(pn)>;
-  using CA = TileCfg<TILE_3>;
   using CN = TileCfg<TILE_3>;
   SubGrid gb;
   launch_gemm_dual<CA, PA, CB, PB>(pa, e.sarg(OA), e.workers[OA], e.scratch[0], e.wide[OA], pb,
@@ -412,14 +444,25 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
 // split-K; any other schedule takes the unfused sequence.
 template <int OA, int OB, int ON>
 void run_dual_then_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
-  const int cb = e.cfg[OB];
-  if (!e.dual || e.cfg[OA] != 3 || (cb != 3 && cb != 5) || e.cfg[ON] != 3 || e.workers[ON] > 0) {
+  const int ca = e.cfg[OA], cb = e.cfg[OB];
+  if (!e.dual || (ca != 3 && ca != CFG_MF16) || (cb != 3 && cb != 5 && cb != CFG_MF16) ||
+      e.cfg[ON] != 3 || e.workers[ON] > 0) {
     run_dual_inst<OA, OB>(e, x, B, seed, st);
     e.run_op(ON, x, B, seed, true, st, 0);
     return;
   }
-  if (cb == 3) dual_then_b<OA, OB, ON, TileCfg<TILE_3>>(e, x, B, seed, st);
-  else dual_then_b<OA, OB, ON, TileCfg<TILE_5>>(e, x, B, seed, st);
+  using C3 = TileCfg<TILE_3>;
+  using C5 = TileCfg<TILE_5>;
+  using C14 = TileCfg<TILE_14>;
+  if (ca == CFG_MF16) {
+    if (cb == CFG_MF16) dual_then_b<OA, OB, ON, C14, C14>(e, x, B, seed, st);
+    else if (cb == 3) dual_then_b<OA, OB, ON, C14, C3>(e, x, B, seed, st);
+    else dual_then_b<OA, OB, ON, C14, C5>(e, x, B, seed, st);
+  } else {
+    if (cb == CFG_MF16) dual_then_b<OA, OB, ON, C3, C14>(e, x, B, seed, st);
+    else if (cb == 3) dual_then_b<OA, OB, ON, C3, C3>(e, x, B, seed, st);
+    else dual_then_b<OA, OB, ON, C3, C5>(e, x, B, seed, st);
+  }
 }
 
 }  // namespace ddl

@@ -191,7 +191,9 @@ template <class P>
 struct HasDma<P, std::void_t<decltype(P::DMA)>> : std::bool_constant<P::DMA> {};
 
 // ---- per-tile building blocks shared by the split-K and stream-K drivers ---------------------
-template <int BM, int BN, int BK, int WM, int WN, class P>
+// V (tile-config variant): 0 = the 32x32x2 MFMA loops below; 1 = the one-wave 32x32x32 tile on
+// v_mfma_f32_16x16x4_f32 with LDS-DMA staging (mainloop_dma16)
+template <int BM, int BN, int BK, int WM, int WN, class P, int V = 0>
 struct GemmTile {
   using G = TileGeo<BM, BN, WM, WN>;
   static constexpr int NT = WM * WN * 64;
@@ -232,14 +234,19 @@ struct GemmTile {
                                !(BK == 16) && !BKC && HasLoadB1<P>::value;
   // LDS-DMA staging (mainloop_dma): unpadded 32x32 images, swizzled through the gather
   // addresses (the DMA writes lane-linearly), DDL_LDSDMA images of A + B per block
+  // 16x16x4 MFMA + LDS-DMA one-wave tile (variant 1): any policy with 16-byte gathers
+  // (instantiated only for policies with the 16-byte gathers srcA / srcB: layers.h Mf16OK)
+  static constexpr bool DMA16 = V == 1 && SOLO && BM == 32 && BN == 32 && BK == 32;
+  static_assert(V == 0 || DMA16, "variant 1 is the one-wave 32x32x32 tile");
   static constexpr bool DMA = DDL_LDSDMA > 0 && HasDma<P>::value && SOLO && TM * TN == 1 &&
-                              BM == 32 && BN == 32 && BK == 32 && !DIRECT && !BDIR;
+                              BM == 32 && BN == 32 && BK == 32 && !DIRECT && !BDIR && !DMA16;
   static constexpr int DMA_NB = DDL_LDSDMA > 0 ? DDL_LDSDMA : 1;
   static constexpr bool DMA_MF = DDL_LDSDMA_MF > 0 && HasDma<P>::value && SOLO && TM * TN > 1 &&
                                  BN == 64 && BK == 32 && AK && !BKC && !DIRECT && !BDIR &&
                                  !HasOnesA<P>::value;
   static constexpr int LDS_F4 =
-      DMA ? DMA_NB * 512
+      DMA16 ? 512
+      : DMA ? DMA_NB * 512
           : DMA_MF ? (BM * BK + BK * BN) / 4
           : DIRECT ? 0 : (NBUF * (A_ELEMS + (BDIR ? 0 : B_ELEMS))) / 4;
   // A wave with a single 32x32 fragment alternates two accumulator chains (summed at the
@@ -270,7 +277,8 @@ struct GemmTile {
   // [kb, ke) is virtual (window w) for K-map policies
   static DDL_DEV void mainloop(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
                                f32x16 (&acc)[TM][TN], const Win& w = Win()) {
-    if constexpr (DMA) mainloop_dma(p, m_blk, n_blk, kb, ke, lds, acc, w);
+    if constexpr (DMA16) mainloop_dma16(p, m_blk, n_blk, kb, ke, lds, acc, w);
+    else if constexpr (DMA) mainloop_dma(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else if constexpr (DMA_MF) mainloop_dma_mf(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else if constexpr (DIRECT) mainloop_direct(p, m_blk, n_blk, kb, ke, acc, w);
     else if constexpr (PIPE) mainloop_pipe(p, m_blk, n_blk, kb, ke, lds, acc, w);
@@ -673,6 +681,138 @@ struct GemmTile {
     if constexpr (NCH == 2) acc[0][0] += acc2;
   }
 
+  // One-wave 32x32x32 tile on v_mfma_f32_16x16x4_f32 (variant 1).  The
+  // 32x32 tile is four 16x16 sub-tiles, each with its own 4-register accumulator: 16
+  // accumulator registers instead of the 32 of two 32x32 chains, and four independent
+  // accumulation chains (consecutive MFMAs never depend on each other), so the wave fits in
+  // <= 96 VGPR+AGPR with LDS-DMA staging (no staging registers) — 5 waves per SIMD with the 8 KB
+  // image, where the 32x32x2 tiles sit at 3.
+  //  * k assignment: MFMA step s (0..7) of a K tile feeds k = 8h + s from lane group h = l >> 4
+  //    (the MFMA's own k index is h), so a lane's A / B values of a whole tile are 8
+  //    consecutive k — two ds_read_b128 per row for a K-contiguous operand.
+  //  * images: K-contiguous operand as mainloop_dma (quad q of row r at q ^ ((r >> 1) & 7): the
+  //    16 rows of a read hit 16 distinct bank groups).  MN-contiguous operand [k][32 mn] with
+  //    logical k-row k at physical row k ^ ((k >> 4) & 1) and its two 16-column halves swapped
+  //    when bit 3 of k is set: the four lane groups of one ds_read_b32 (k = s, 8+s, 16+s, 24+s)
+  //    then read four distinct 16-bank windows.  The DMA writes lane-linearly, so both layouts
+  //    are made on the gather side (slot (row, quad) fetches the logical element it holds).
+  //  * the accumulators are re-laid out through LDS into the 32x32 MFMA layout at the end of
+  //    the tile (4 ds_write_b128 + 4 ds_read_b128 per lane, column-major image with pitch 36),
+  //    so epilogues, split-K partials and the wide reduce are unchanged.
+  static DDL_DEV void mainloop_dma16(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
+                                     f32x16 (&acc)[TM][TN], const Win& w) {
+    static_assert(FA == 4 && FB == 4, "32x32x32 one-wave tile");
+    static_assert(!(HasOnesA<P>::value && AK), "ones-row patch: MN-contiguous A");
+    const int lane = threadIdx.x & 63;
+    const int nk = (ke - kb + BK - 1) / BK;
+    // gather side: DMA slot sl = it * 64 + lane is image quad sl (row sl >> 3, quad sl & 7)
+    auto kc_of = [](int sl, int& row, int& kk) {  // K-contiguous: (mn row, k offset)
+      row = sl >> 3;
+      kk = ((sl & 7) ^ ((row >> 1) & 7)) * 4;
+    };
+    auto mn_of = [](int sl, int& mn, int& k) {  // MN-contiguous: (mn offset, k row)
+      const int pr = sl >> 3;
+      k = pr ^ ((pr >> 4) & 1);
+      mn = ((sl & 7) ^ (((k >> 3) & 1) << 2)) * 4;
+    };
+    typename P::AInfo ai[4];
+    typename P::BInfo bi[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int sl = it * 64 + lane;
+      int x, y;
+      if constexpr (AK) { kc_of(sl, x, y); ai[it] = p.prepA(m_blk + x, y); }
+      else { mn_of(sl, x, y); ai[it] = p.prepA(m_blk + x, y); }
+      if constexpr (BKC) { kc_of(sl, x, y); bi[it] = p.prepB(n_blk + x, y); }
+      else { mn_of(sl, x, y); bi[it] = p.prepB(n_blk + x, y); }
+    }
+    auto patch = [&](int k0) {
+      if constexpr (HasOnesA<P>::value) {
+#pragma unroll
+        for (int it = 0; it < 4; ++it)
+          if (p.ones_group(ai[it])) lds[(it * 64 + lane) * 4] = p.ones_value(ai[it], k0, w);
+      }
+    };
+    const uint32_t base = lds_addr(lds);
+    auto dma = [&](int k0) {
+#pragma unroll
+      for (int it = 0; it < 4; ++it) dma16(srcA(p, ai[it], k0, w), base + it * 1024);
+#pragma unroll
+      for (int it = 0; it < 4; ++it) dma16(srcB(p, bi[it], k0, w), base + 4096 + it * 1024);
+    };
+    // read side: lane (h = lane >> 4, c = lane & 15) of sub-tile row / column block i
+    const int h = lane >> 4, c = lane & 15;
+    auto rd = [&](const float* img, bool kcontig, float (&v)[2][8]) {
+      if (kcontig) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row = i * 16 + c, sw = (row >> 1) & 7;
+          const float4 lo = *reinterpret_cast<const float4*>(img + row * 32 + ((2 * h) ^ sw) * 4);
+          const float4 hi =
+              *reinterpret_cast<const float4*>(img + row * 32 + ((2 * h + 1) ^ sw) * 4);
+          v[i][0] = lo.x; v[i][1] = lo.y; v[i][2] = lo.z; v[i][3] = lo.w;
+          v[i][4] = hi.x; v[i][5] = hi.y; v[i][6] = hi.z; v[i][7] = hi.w;
+        }
+      } else {
+        // k = 8h + s sits at physical row 8h + (s ^ (h >> 1)), column (16i + c) ^ 16 (h & 1)
+        const int t = h >> 1;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int col = (i * 16 + c) ^ ((h & 1) << 4);
+#pragma unroll
+          for (int s2 = 0; s2 < 8; ++s2) v[i][s2] = img[(8 * h + (s2 ^ t)) * 32 + col];
+        }
+      }
+    };
+    f32x4 c4[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) c4[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (nk > 0) {
+      float av[2][8], bv[2][8];
+      dma(kb);
+      for (int kt = 0; kt < nk; ++kt) {
+        vm_wait<0>();  // tile kt is in the image
+        patch(kb + kt * BK);
+        rd(lds, AK, av);
+        rd(lds + 1024, BKC, bv);
+        lgkm_wait0();  // its fragments are in registers: the image may be restaged
+        if (kt + 1 < nk) dma(kb + (kt + 1) * BK);
+#if DDL_MFMA_PRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) c4[i][j] = mfma16x16x4(av[i][s2], bv[j][s2], c4[i][j]);
+#if DDL_MFMA_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
+      }
+    }
+    // 16x16 layout (lane: column 16j + c, rows 16i + 4h .. +3) -> 32x32 layout (lane: column
+    // l & 31, rows 8g + 4 (l >> 5) .. +3), through a column-major [32][36] image
+    constexpr int PC = 36;
+    lgkm_wait0();
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        *reinterpret_cast<float4*>(lds + (16 * j + c) * PC + 16 * i + 4 * h) =
+            make_float4(c4[i][j][0], c4[i][j][1], c4[i][j][2], c4[i][j][3]);
+    const int col = lane & 31, lh = lane >> 5;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 t = *reinterpret_cast<const float4*>(lds + col * PC + 8 * g + 4 * lh);
+      acc[0][0][4 * g] = t.x; acc[0][0][4 * g + 1] = t.y;
+      acc[0][0][4 * g + 2] = t.z; acc[0][0][4 * g + 3] = t.w;
+    }
+    lgkm_wait0();  // the image is free again (split-K flag word, the next tile's DMA)
+  }
+
   // LDS-DMA loop of a one-wave tile with TM x TN fragments (K-contiguous A: BM rows of 8 quads,
   // quad q of row r at q ^ ((r >> 1) & 7); MN-contiguous B, BN = 64: k-row k of 16 quads, the
   // two 32-column halves swapped on rows with bit 2 set, so the lane halves' reads of rows k and
@@ -1039,11 +1179,11 @@ struct GemmTile {
 // Classic split-K: virtual grid (gx, gy, gz); split bz covers K range
 // [bz*kchunk, (bz+1)*kchunk).  mode 0: no split; mode 1: in-launch last-arriver reduction of
 // the gz partials (in z order, deterministic); mode 2: partials only (splitk_wide_reduce).
-template <int BM, int BN, int BK, int WM, int WN, class P>
+template <int BM, int BN, int BK, int WM, int WN, class P, int V = 0>
 DDL_DEV void splitk_body(const P& p, int kchunk, int mode, float4* __restrict__ slab,
                          int* __restrict__ tickets, int bx, int by, int bz, int gx, int gy,
                          int gz, float* lds, int* flag) {
-  using T = GemmTile<BM, BN, BK, WM, WN, P>;
+  using T = GemmTile<BM, BN, BK, WM, WN, P, V>;
   using G = typename T::G;
   const int m_blk = bx * BM;
   const int n_blk = by * BN;
@@ -1086,10 +1226,10 @@ DDL_DEV void splitk_body(const P& p, int kchunk, int mode, float4* __restrict__ 
 // split-K reduction happens inside the same launch, with no separate reduce kernel.
 // Workers are numbered XCD-major (hardware dispatches block b to XCD b % 8), so the
 // neighbours that share a boundary tile, and adjacent tiles' operands, stay in one L2.
-template <int BM, int BN, int BK, int WM, int WN, class P>
+template <int BM, int BN, int BK, int WM, int WN, class P, int V = 0>
 DDL_DEV void streamk_body(const P& p, int KI, int gx, long long I, float4* __restrict__ slab,
                           int* __restrict__ tickets, int bid, int W, float* lds, int* flag) {
-  using T = GemmTile<BM, BN, BK, WM, WN, P>;
+  using T = GemmTile<BM, BN, BK, WM, WN, P, V>;
   using G = typename T::G;
   const int w = (bid & 7) * (W >> 3) + (bid >> 3);  // W % 8 == 0 (host)
   const brsrc_t sr = make_rsrc(slab, (uint32_t)W * 2u * G::PART4 * 16u);
@@ -1149,16 +1289,18 @@ DDL_DEV int xcd_remap(int b, int n) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
-template <int BM, int BN, int BK, int WM, int WN, class P>
+// SK = false: no stream-K body in the kernel (its register count would set the launch's
+// occupancy even when the split-K body runs; the dual launch's 16x16x4 sub-problems)
+template <int BM, int BN, int BK, int WM, int WN, class P, int V = 0, bool SK = true>
 DDL_DEV void run_sub(const P& p, const SubGrid& g, int vb, float* lds, int* flag) {
-  if (g.streamk) {
-    streamk_body<BM, BN, BK, WM, WN, P>(p, g.KI, g.gx, g.I, g.slab, g.tickets, vb, g.nblocks,
-                                        lds, flag);
+  if (SK && g.streamk) {
+    streamk_body<BM, BN, BK, WM, WN, P, V>(p, g.KI, g.gx, g.I, g.slab, g.tickets, vb,
+                                           g.nblocks, lds, flag);
   } else {
     if (g.xcd) vb = xcd_remap(vb, g.nblocks);
     const int bx = vb % g.gx, t = vb / g.gx;
-    splitk_body<BM, BN, BK, WM, WN, P>(p, g.kchunk, g.mode, g.slab, g.tickets, bx, t % g.gy,
-                                       t / g.gy, g.gx, g.gy, g.gz, lds, flag);
+    splitk_body<BM, BN, BK, WM, WN, P, V>(p, g.kchunk, g.mode, g.slab, g.tickets, bx, t % g.gy,
+                                          t / g.gy, g.gx, g.gy, g.gz, lds, flag);
   }
 }
 
@@ -1181,11 +1323,11 @@ DDL_DEV void run_sub(const P& p, const SubGrid& g, int vb, float* lds, int* flag
 #define DDL_DUAL_OCC DDL_GEMM_OCC
 #endif
 
-template <int BM, int BN, int BK, int WM, int WN, class P>
+template <int BM, int BN, int BK, int WM, int WN, class P, int V = 0>
 __global__ void __launch_bounds__(WM * WN * 64) DDL_GEMM_OCC
 gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets,
                 int xcd) {
-  using T = GemmTile<BM, BN, BK, WM, WN, P>;
+  using T = GemmTile<BM, BN, BK, WM, WN, P, V>;
   // staging images; the last-arriver flag reuses the first word (arrive() runs after the main
   // loop, whose last LDS reads have retired) — one array (guide §5 trap 4a), and no extra 16 B
   // that would push an 8 / 16 KB LDS-DMA block past an occupancy step
@@ -1198,20 +1340,20 @@ gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __res
     by = (v / gx) % gy;
     bz = v / (gx * gy);
   }
-  splitk_body<BM, BN, BK, WM, WN, P>(p, kchunk, mode, slab, tickets, bx, by, bz, gridDim.x,
-                                     gridDim.y, gridDim.z, reinterpret_cast<float*>(lds4),
-                                     reinterpret_cast<int*>(lds4));
+  splitk_body<BM, BN, BK, WM, WN, P, V>(p, kchunk, mode, slab, tickets, bx, by, bz, gridDim.x,
+                                        gridDim.y, gridDim.z, reinterpret_cast<float*>(lds4),
+                                        reinterpret_cast<int*>(lds4));
 }
 
-template <int BM, int BN, int BK, int WM, int WN, class P>
+template <int BM, int BN, int BK, int WM, int WN, class P, int V = 0>
 __global__ void __launch_bounds__(WM * WN * 64)
 gemm_streamk_kernel(P p, int KI, int gx, long long I, float4* __restrict__ slab,
                     int* __restrict__ tickets) {
-  using T = GemmTile<BM, BN, BK, WM, WN, P>;
+  using T = GemmTile<BM, BN, BK, WM, WN, P, V>;
   __shared__ float4 lds4[T::LDS_F4 > 0 ? T::LDS_F4 : 1];  // (flag in the first word: see above)
-  streamk_body<BM, BN, BK, WM, WN, P>(p, KI, gx, I, slab, tickets, blockIdx.x, gridDim.x,
-                                      reinterpret_cast<float*>(lds4),
-                                      reinterpret_cast<int*>(lds4));
+  streamk_body<BM, BN, BK, WM, WN, P, V>(p, KI, gx, I, slab, tickets, blockIdx.x, gridDim.x,
+                                         reinterpret_cast<float*>(lds4),
+                                         reinterpret_cast<int*>(lds4));
 }
 
 // K split inside ONE workgroup, for the skinny GEMMs (the fc layers at M = batch): KW waves each
@@ -1333,9 +1475,9 @@ inline void launch_gemm_kwave(const P& p, int splits, hipStream_t stream) {
   }
 }
 
-template <int BM_, int BN_, int BK_, int WM_, int WN_>
+template <int BM_, int BN_, int BK_, int WM_, int WN_, int V_ = 0>
 struct TileCfg {
-  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_;
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_, V = V_;
   static constexpr int NT = WM * WN * 64;
 };
 
@@ -1361,8 +1503,8 @@ template <class CA, class PA, class CB, class PB, class AUX>
 __global__ void __launch_bounds__(64) DDL_DUAL_OCC
 gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut, int bfirst) {
   static_assert(CA::NT == 64 && CB::NT == 64, "dual launch needs one-wave blocks");
-  using TA = GemmTile<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>;
-  using TB = GemmTile<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>;
+  using TA = GemmTile<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA, CA::V>;
+  using TB = GemmTile<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB, CB::V>;
   constexpr int L0 = TA::LDS_F4 > TB::LDS_F4 ? TA::LDS_F4 : TB::LDS_F4;
   constexpr int L = L0 > 0 ? L0 : 1;
   __shared__ float4 lds4[L];  // (the last-arriver flag in the first word: gemm_f32_kernel)
@@ -1398,9 +1540,9 @@ gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut, int bfirst) {
     ib = bfirst ? b : b - ga.nblocks;
   }
   if (is_a)
-    run_sub<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA>(pa, ga, ia, lds, flag);
+    run_sub<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA, CA::V, CA::V == 0>(pa, ga, ia, lds, flag);
   else
-    run_sub<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, ib, lds, flag);
+    run_sub<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB, CB::V, CB::V == 0>(pb, gb, ib, lds, flag);
 }
 
 // Wide split-K reduce (mode 2): RL lanes cooperate on one float4 output element; `gid` is the
@@ -1473,7 +1615,7 @@ __global__ void __launch_bounds__(64)
 reduce_gemm_kernel(PR pr, const float4* __restrict__ rslab, int S, int rgx, int rntiles, int nrb,
                    PG pg, SubGrid gg) {
   static_assert(CG::NT == 64, "one-wave GEMM blocks");
-  using TG = GemmTile<CG::BM, CG::BN, CG::BK, CG::WM, CG::WN, PG>;
+  using TG = GemmTile<CG::BM, CG::BN, CG::BK, CG::WM, CG::WN, PG, CG::V>;
   __shared__ float4 lds4[TG::LDS_F4 + 1];
   // GEMM blocks first (the longer pole: dispatched first), the reduce fills in behind them
   const int b = blockIdx.x;
@@ -1482,8 +1624,8 @@ reduce_gemm_kernel(PR pr, const float4* __restrict__ rslab, int S, int rgx, int 
                                                  (b - gg.nblocks) * 64 + threadIdx.x);
     return;
   }
-  run_sub<CG::BM, CG::BN, CG::BK, CG::WM, CG::WN, PG>(pg, gg, b, reinterpret_cast<float*>(lds4),
-                                                      reinterpret_cast<int*>(lds4 + TG::LDS_F4));
+  run_sub<CG::BM, CG::BN, CG::BK, CG::WM, CG::WN, PG, CG::V>(
+      pg, gg, b, reinterpret_cast<float*>(lds4), reinterpret_cast<int*>(lds4 + TG::LDS_F4));
 }
 
 template <int BK>
@@ -1641,17 +1783,17 @@ inline bool launch_reduce_tail(const P& p, const SubGrid& g, const UpdTail& t,
   return true;
 }
 
-template <int BM, int BN, int BK, int WM, int WN, class P>
+template <int BM, int BN, int BK, int WM, int WN, int V = 0, class P>
 inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch& sc,
                         hipStream_t stream, int workers = 0) {
   const SubGrid g = plan_gemm<BM, BN, BK>(p, splits, workers, wide_thr, sc);
   if (g.nblocks == 0) return;
   if (g.streamk) {
-    DDL_LAUNCH((gemm_streamk_kernel<BM, BN, BK, WM, WN, P>), dim3(g.nblocks),
+    DDL_LAUNCH((gemm_streamk_kernel<BM, BN, BK, WM, WN, P, V>), dim3(g.nblocks),
                        dim3(WM * WN * 64), 0, stream, p, g.KI, g.gx, g.I, g.slab, g.tickets);
     return;
   }
-  DDL_LAUNCH((gemm_f32_kernel<BM, BN, BK, WM, WN, P>), dim3(g.gx, g.gy, g.gz),
+  DDL_LAUNCH((gemm_f32_kernel<BM, BN, BK, WM, WN, P, V>), dim3(g.gx, g.gy, g.gz),
                      dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets, g.xcd);
   launch_reduce<BM, BN, BK, WM, WN, P>(p, g, stream);
 }
@@ -1692,8 +1834,9 @@ inline void launch_gemm_dual(const PA& pa, int sa, int wa, const SplitScratch& s
                              const PB& pb, int sb, int wb, const SplitScratch& scb, int wide_b,
                              hipStream_t stream, const AUX& ut = AUX(),
                              SubGrid* defer_b = nullptr, int bfirst = 0) {
-  const SubGrid ga = plan_gemm<CA::BM, CA::BN, CA::BK>(pa, sa, wa, wide_a, sca);
-  const SubGrid gb = plan_gemm<CB::BM, CB::BN, CB::BK>(pb, sb, wb, wide_b, scb);
+  // (a 16x16x4 sub-problem runs split-K only in a dual launch: see run_sub's SK)
+  const SubGrid ga = plan_gemm<CA::BM, CA::BN, CA::BK>(pa, sa, CA::V ? 0 : wa, wide_a, sca);
+  const SubGrid gb = plan_gemm<CB::BM, CB::BN, CB::BK>(pb, sb, CB::V ? 0 : wb, wide_b, scb);
   const int n = ut.nblk + ga.nblocks + gb.nblocks;
   if (n > 0)
     DDL_LAUNCH((gemm_dual_kernel<CA, PA, CB, PB, AUX>), dim3(n), dim3(64), 0, stream, pa,

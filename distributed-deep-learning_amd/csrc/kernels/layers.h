@@ -940,6 +940,17 @@ struct FcWgradT {
 };
 using FcWgrad = FcWgradT<false>;
 
+// ops the 16x16x4 LDS-DMA tile (CFG_MF16, gemm.h mainloop_dma16) is instantiated for: the
+// halo-layout convolutions, whose 16-byte gathers srcA / srcB are the DMA sources
+template <class P>
+struct Mf16OK : std::false_type {};
+template <int H, int CIN, int COUT, bool KM>
+struct Mf16OK<ConvFwd<H, CIN, COUT, KM>> : std::bool_constant<CIN % kBK == 0> {};
+template <int H, int CIN, int COUT, int HPREV>
+struct Mf16OK<ConvDgrad<H, CIN, COUT, HPREV>> : std::true_type {};
+template <int H, int CIN, int COUT>
+struct Mf16OK<ConvWgradBM<H, CIN, COUT>> : std::true_type {};
+
 // ops the K-wave launch (gemm.h gemm_kwave_kernel, CFG_KWAVE) is instantiated for
 template <class P>
 struct KWaveOK : std::false_type {};

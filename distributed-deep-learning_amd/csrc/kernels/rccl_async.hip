@@ -324,6 +324,12 @@ void RcclAsync::pause() {
 
 void RcclAsync::resume() { pause_mu_.unlock(); }
 
+void RcclAsync::set_t(int p, int64_t t) {
+  if (th_.joinable()) throw std::runtime_error("rccl async: set_t after start()");
+  if (t < 0) throw std::invalid_argument("rccl async: negative step counter");
+  __atomic_store_n(&state_of(p)->t, t, __ATOMIC_RELEASE);
+}
+
 int64_t RcclAsync::t(int p) const {
   for (const auto& s : ps_)
     if (s.ps == p) return __atomic_load_n(&s.t, __ATOMIC_ACQUIRE);

@@ -118,6 +118,11 @@ void SyncRunner::set_units(const std::vector<RunnerUnit>& units) {
         throw std::invalid_argument("xGMI unit bucket out of range");
       if ((u.kind == RunnerUnit::XGMI_REPL) != (u.bucket == peer_->repl_bucket()))
         throw std::invalid_argument("xGMI unit kind does not match the exchange's replicated bucket");
+      // the replicated kernel has no DONE words (the final wait cannot see it) and reuses its
+      // parity slots on the next-but-one step: only the compute stream's program order after
+      // the last backward segment makes both safe
+      if (u.kind == RunnerUnit::XGMI_REPL && u.seg != kSegments - 1)
+        throw std::invalid_argument("the replicated xGMI bucket must be the last segment's");
       if (opt_ == 0 && !u.v) throw std::invalid_argument("xGMI unit without Adam state");
     }
   }

@@ -309,8 +309,10 @@ __global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a)
 // W contributions in rank order and runs the update itself on replicated optimizer state, then
 // stores only its own parameters.  One hop.  The inbox has two parity slots per source: a peer
 // writes slot (e+1)&1 of step e+1 while this rank may still read slot e&1; it can write slot e&1
-// again only at step e+2, after its final wait of step e+1 saw this rank's DONE of buckets
-// 0..nb-2 at e+1 — issued after this rank's step-e+1 forward, i.e. after this kernel of step e.
+// again only at step e+2, after its final wait of step e+1 saw this rank's DONE of every owner
+// bucket at e+1 — issued after this rank's step-e+1 forward, i.e. after this kernel of step e.
+// This needs the replicated bucket to be the one the last backward segment completes (conv1 +
+// conv2, launched on the compute stream): parallel/native_exchange.py last_segment_bucket.
 template <int WT>
 __global__ void __launch_bounds__(256) xgmi_repl_kernel(XgmiTable T, XgmiLaunch a) {
   constexpr int NQ = WT ? WT : kXgmiMaxPeers;

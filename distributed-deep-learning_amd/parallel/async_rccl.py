@@ -89,6 +89,10 @@ class RcclAsyncExchange:
         return sum(1 for hh in self.hosts if hh == r) * (W - 1) * self.steps
 
     def start(self) -> None:
+        # the PS step counters may have been restored (checkpoint load) after the native object
+        # copied them in __init__: hand the current ones over before the service runs
+        for p, ps in self.servers.items():
+            self.svc.set_t(p, int(ps.t))
         self.svc.start(self._expected(), self.check_provenance)
 
     def push_pull(self) -> None:

@@ -45,6 +45,10 @@ class DistEnv:
     local_rank: int = 0
     device: torch.device = field(default_factory=lambda: torch.device("cpu"))
     backend: Optional[str] = None
+    # host-only (gloo) group for control messages that must never queue behind GPU work: with
+    # an RCCL default group a collective kernel can sit on a hardware queue in front of an async
+    # PS's serve / apply kernel that a peer is waiting for (checkpoint metadata in async mode)
+    ctrl: Optional[object] = None
 
     @property
     def distributed(self) -> bool:
@@ -88,7 +92,10 @@ def init_distributed(device: str = "auto") -> DistEnv:
             if use_gpu and backend == "nccl":
                 kw["device_id"] = dev
             dist.init_process_group(backend, rank=rank, world_size=world, **kw)
-    return DistEnv(rank, world, local, dev, backend)
+    ctrl = None
+    if world > 1 and backend != "gloo":
+        ctrl = dist.new_group(backend="gloo")  # collective: every rank, same point
+    return DistEnv(rank, world, local, dev, backend, ctrl)
 
 
 def _stream_ctx(s):

@@ -44,6 +44,28 @@ class NativeUnavailable(RuntimeError):
     pass
 
 
+def last_segment_bucket(plan: ShardPlan, segments: Sequence[Sequence[int]]) -> int:
+    """Index of the bucket whose gradients complete LAST (the final backward segment's).
+
+    ``make_plan`` orders buckets by their smallest tensor id, so for the HIP engine's segments
+    ([fc], [conv4], [conv3], [conv2 + conv1]) the last-completed bucket is bucket 0, not the
+    last index: replicating ``len - 1`` (round 3) replicated the 1.58 M-parameter fc bucket —
+    the FIRST to complete, on the comm stream, with no DONE words for the final wait to see —
+    instead of the 52 k-parameter conv1 + conv2 bucket on the step's exposed end."""
+    last = sorted(int(t) for t in segments[-1])
+    buckets = plan.meta.get("buckets")
+    if buckets is None or last not in buckets:
+        raise NativeUnavailable("flat plan buckets do not match the engine's segments")
+    b = buckets.index(last)
+    lo, hi = plan.bucket_ranges[b]
+    offs = plan.tensor_offsets
+    from ..models.layout import TENSORS
+    want_lo = min(offs[t] for t in last)
+    want_hi = max(offs[t] + TENSORS[t].numel for t in last)
+    assert lo <= want_lo and want_hi <= hi, (b, (lo, hi), (want_lo, want_hi))
+    return b
+
+
 class NativeSyncExchange(SyncExchange):
     native = True
     uses_side = False  # collectives go on the C++ runner's own comm stream
@@ -76,7 +98,7 @@ class NativeSyncExchange(SyncExchange):
         self.repl = None
         if (self.collective and plan.bucket_ranges is not None and plan.num_ps == env.world
                 and os.environ.get("DDL_REPL_LAST", "1") == "1"):
-            b = len(plan.bucket_ranges) - 1
+            b = last_segment_bucket(plan, segments)
             lo, hi = plan.bucket_ranges[b]
             z = lambda: torch.zeros(hi - lo, dtype=torch.float32, device=params.device)  # noqa: E731
             self.repl = (b, int(lo), int(hi), z(), z() if optimizer == "adam" else None)

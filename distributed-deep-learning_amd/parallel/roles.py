@@ -155,8 +155,13 @@ class Trainer:
                                          optimizer=cfg.optimizer,
                                          check_provenance=cfg.check_provenance)
             except RcclAsyncUnavailable as e:
-                raise RuntimeError(f"async mode on GPU: neither the xGMI nor the RCCL-session "
-                                   f"exchange is available ({e})") from e
+                if env.world > 1 and env.backend == "nccl":
+                    raise RuntimeError(f"async mode on GPU: neither the xGMI nor the RCCL-"
+                                       f"session exchange is available ({e})") from e
+                # a non-RCCL default group (the shared-GPU gloo rehearsal after an xGMI set-up
+                # failure) keeps the host-driven exchange, as before round 3
+                print(f"[ddl_amd] async RCCL-session exchange unavailable ({e}); using the "
+                      f"host-driven exchange", file=sys.stderr)
         return AsyncExchange(self.plan, env, self.params, self.grads, self.servers,
                              steps_per_worker=steps, grad_reduce=cfg.grad_reduce,
                              check_provenance=cfg.check_provenance, job_id=job)
@@ -239,10 +244,21 @@ class Trainer:
         cfg, env = self.cfg, self.env
         clock = metrics.Clock()
         single = cfg.mode == "single"
+        # Resume continues the run (reference loop mnist_sync/worker.py:58-72): the restored
+        # global step is the position in the epoch loop, so the data index (cnt), the eval
+        # cadence (cnt % eval_every) and the dropout seeds (global_step) all pick up where the
+        # checkpointed run stopped — a resumed run is the uninterrupted run, not a new epoch.
         if cfg.resume and cfg.checkpoint_dir:
             ckpt.load(self, cfg.checkpoint_dir)
+        first = self.global_step
+        last = cfg.epochs * self.steps
+        if cfg.max_steps is not None:
+            last = min(last, cfg.max_steps)
         asyncx = cfg.mode == "async" and not self.async_as_sync
         if asyncx:
+            # the PS services expect exactly this run's pushes (every worker runs the same
+            # window), and resume their step counters from the checkpoint (load above)
+            self.exchange.steps = max(0, last - first)
             self.exchange.start()
         wd = Watchdog(cfg.watchdog_s, name=f"rank{env.rank}", on_timeout=self._on_hang)
         t_target = None
@@ -273,7 +289,15 @@ class Trainer:
             if aeval is not None:
                 aeval.start()
             for epoch in range(cfg.epochs):
+                if (epoch + 1) * self.steps <= first:
+                    continue
+                if self.global_step >= last:
+                    break
                 for cnt in range(self.steps):
+                    if epoch * self.steps + cnt < first:
+                        continue  # done before the checkpoint
+                    if self.global_step >= last:
+                        break
                     t0 = time.perf_counter()
                     self.train_step(cnt)
                     wd.kick()
@@ -317,7 +341,7 @@ class Trainer:
         wd.stop()
         if cfg.checkpoint_dir:
             ckpt.save(self, cfg.checkpoint_dir)
-        imgs = self.global_step * cfg.batch_size
+        imgs = (self.global_step - first) * cfg.batch_size  # this run's steps (resume)
         summary = dict(final_acc=acc, cpu_time=cpu_t, wall_time=wall_t, train_wall=train_wall,
                        images=imgs, images_per_s=imgs / max(train_wall, 1e-9),
                        time_to_target=t_target, steps=self.global_step, plan=self.plan.describe())

@@ -78,12 +78,16 @@ def save(trainer, path: str) -> None:
         save_file(w, os.path.join(path, f"worker{env.rank}.safetensors"))
     for p, (d, _) in snaps.items():
         save_file(d, os.path.join(path, f"ps{p}.safetensors"))
-    # every PS's own step counter (PSes are hosted by different ranks)
+    # every PS's own step counter (PSes are hosted by different ranks), over the host-only
+    # control group: in async mode a peer may still need this rank's PS service (an RCCL
+    # session or an xGMI apply) to finish its round before it reaches its own save, and an RCCL
+    # collective here could queue on a hardware queue in front of that serve kernel
     local_t = {p: t for p, (_, t) in snaps.items()}
     all_t = [local_t]
+    grp = getattr(env, "ctrl", None)
     if env.world > 1:
         all_t = [None] * env.world
-        dist.all_gather_object(all_t, local_t)
+        dist.all_gather_object(all_t, local_t, group=grp)
     if env.rank == 0:
         ps_t = {}
         for d in all_t:
@@ -93,7 +97,7 @@ def save(trainer, path: str) -> None:
         with open(os.path.join(path, "manifest.json"), "w") as f:
             json.dump(man, f, indent=1)
     if env.world > 1:
-        dist.barrier()
+        dist.barrier(group=grp)
 
 
 def _ps_snapshot(trainer, plan, ps) -> Tuple[Dict[str, torch.Tensor], int]:

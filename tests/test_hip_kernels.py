@@ -437,6 +437,58 @@ def test_kwave_config_matches_reference(setup, waves, packed):
         eng.set_workers(base_w)
 
 
+# conv2-4 forward, conv4..conv2 data / weight gradient (csrc/kernels/api.h op order)
+MF16_OPS = (1, 2, 3, 10, 11, 12, 13, 14, 15)
+
+
+@pytest.mark.parametrize("mode", ["default", "split1", "wide", "streamk", "nodual", "mixed"])
+def test_mf16_config_matches_reference(setup, mode):
+    """CFG_MF16 = 14 (gemm.h mainloop_dma16: one-wave 32x32x32 tile on v_mfma_f32_16x16x4_f32,
+    LDS-DMA staging with the 16x16 image swizzles, accumulators re-laid out through LDS into the
+    32x32 layout) on every conv GEMM: the fp32 / fp64 autograd gradients (check_grads) under
+    every schedule that consumes its accumulators — fused epilogue (split 1), in-launch
+    last-arriver reduce, separate wide reduce, stream-K partial hand-off, dual and back-to-back
+    launches, and mixed with the 32x32x2 tiles in one dual launch — bit-deterministic across
+    reruns, and the forward activations within fp32 noise of the reference."""
+    eng, flat, params, grads, x, y = setup
+    base = (eng.get_cfg(), eng.get_splits(), eng.get_workers(), eng.get_wide())
+    cfg, spl, wrk, wide = (list(v) for v in base)
+    ops = MF16_OPS if mode != "mixed" else (1, 3, 10, 13, 14)  # the others stay on 32x32x2
+    for op in ops:
+        cfg[op] = 14
+        if mode == "split1":
+            spl[op] = 1
+        elif mode == "wide":
+            spl[op], wide[op] = max(2, spl[op]), 1
+        elif mode == "streamk":
+            wrk[op] = 1024
+    try:
+        eng.set_cfg(cfg)
+        eng.set_splits(spl)
+        eng.set_workers(wrk)
+        eng.set_wide(wide)
+        eng.set_dual(mode != "nodual")
+        outs = []
+        for _ in range(2):
+            grads.zero_()
+            eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 66)
+            torch.cuda.synchronize()
+            outs.append(grads.clone())
+        assert torch.equal(outs[0], outs[1])
+        check_grads(outs[0], flat, x, y, 0.5, 66)
+        pv = param_views(flat, CANON_OFFSETS)
+        pooled, _, _ = ref_intermediates(pv, x, 0.5, 66)
+        for name, ref in zip(["p1", "p2", "p3", "p4"], pooled):
+            got = eng.eng.buffer(name, x.shape[0])
+            assert rel_err(got.reshape(ref.shape), ref) < 2e-5, name
+    finally:
+        eng.set_dual(True)
+        eng.set_cfg(base[0])
+        eng.set_splits(base[1])
+        eng.set_workers(base[2])
+        eng.set_wide(base[3])
+
+
 @pytest.mark.parametrize("conc,dual", [(False, True), (False, False), (True, False)])
 def test_backward_modes_match(setup, conc, dual):
     """Single-stream dual launches, single-stream back-to-back and the two-stream backward
