@@ -107,10 +107,6 @@ class PyEngine {
     e_.concurrent = on;
   }
   void set_dual(bool on) { e_.dual = on; }
-  // per-op bit mask: window-aware split-K (gemm.h KFixOf); no re-allocation needed (the
-  // split-K z never exceeds the balanced split's)
-  void set_kfix(int64_t mask) { e_.kfix = (int)mask; }
-  int64_t get_kfix() const { return e_.kfix; }
   void set_wide_thr(int64_t t) {
     e_.wide_thr = (int)std::max<int64_t>(1, t);
     for (int i = 0; i < ddl::OP_COUNT; ++i) e_.wide[i] = e_.wide_thr;
@@ -151,10 +147,9 @@ class PyEngine {
     return std::vector<int64_t>(e_.workers, e_.workers + ddl::OP_COUNT);
   }
 
-  void forward(at::Tensor x, at::Tensor seed, bool train, bool defer_fc) {
+  void forward(at::Tensor x, at::Tensor seed, bool train) {
     check_x(x);
-    e_.forward(x.data_ptr<float>(), (int)x.size(0), seed_ptr(seed), train, cur_stream(),
-               defer_fc);
+    e_.forward(x.data_ptr<float>(), (int)x.size(0), seed_ptr(seed), train, cur_stream());
   }
   void backward_segment(int64_t s, at::Tensor x, at::Tensor labels, at::Tensor seed) {
     check_x(x);
@@ -684,26 +679,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("get_eval_cfg", &PyEngine::get_eval_cfg)
       .def("set_concurrent", &PyEngine::set_concurrent)
       .def("set_dual", &PyEngine::set_dual)
-      .def("set_fc_chain", [](PyEngine& e, bool on) { e.raw()->fc_chain = on; })
-      .def("fc_chain", [](PyEngine& e) { return e.raw()->fc_chain; })
       .def("set_conv1_direct", [](PyEngine& e, bool on) { e.raw()->conv1_direct = on; })
       .def("conv1_direct", [](PyEngine& e) { return e.raw()->conv1_direct; })
       .def("set_conv1_wgrad_direct", [](PyEngine& e, bool on) { e.raw()->conv1_wgrad_direct = on; })
       .def("conv1_wgrad_direct", [](PyEngine& e) { return e.raw()->conv1_wgrad_direct; })
-      .def("set_head_slab", [](PyEngine& e, bool on) { e.raw()->head_slab = on; })
-      .def("head_slab", [](PyEngine& e) { return e.raw()->head_slab; })
-      .def("fc_chain_error", [](PyEngine& e) { return e.raw()->fc_chain_error(); })
-      .def("set_fc_stamps", [](PyEngine& e, c10::optional<at::Tensor> t) {
-        // int64 [items x 8] device tensor (kept alive by the caller), or None to turn off
-        e.raw()->fc_stamps = t ? reinterpret_cast<long long*>(t->data_ptr<int64_t>()) : nullptr;
-      })
-      .def("set_kfix", &PyEngine::set_kfix)
-      .def("get_kfix", &PyEngine::get_kfix)
       .def("set_wide_thr", &PyEngine::set_wide_thr)
       .def("set_wide", &PyEngine::set_wide)
       .def("get_wide", &PyEngine::get_wide)
-      .def("forward", &PyEngine::forward, py::arg("x"), py::arg("seed"), py::arg("train"),
-           py::arg("defer_fc") = false)
+      .def("forward", &PyEngine::forward, py::arg("x"), py::arg("seed"), py::arg("train"))
       .def("backward_segment", &PyEngine::backward_segment)
       .def("run_op", &PyEngine::run_op)
       .def("zero_correct", &PyEngine::zero_correct)

@@ -17,6 +17,7 @@
 #include <thread>
 #include <vector>
 
+#include "runtime/session.h"
 #include "scratch.h"
 #include "tail.h"
 
@@ -52,13 +53,6 @@ void launch_head_fwd(const float* h2, const float* w, const float* bias, const i
 void launch_head_fused(const float* h2, const float* w, const float* bias, const int64_t* labels,
                        int B, const uint32_t* seed, uint32_t seed_v, uint32_t thr24,
                        float inv_keep, float* dlog, float* loss, float* dpre2, hipStream_t st);
-// the same, with fc2's split-K reduce (+ bias, dropout; h2 stored) folded in: reads fc2's
-// mode-2 partial slab (S in (4, 16], 32x32 tiles, gx row tiles, ntiles tiles) instead of h2
-void launch_head_fused_slab(const float* slab, int S, int gx, int ntiles, const float* b2,
-                            float* h2, const float* w, const float* bias, const int64_t* labels,
-                            int B, const uint32_t* seed, uint32_t seed_v, uint32_t thr24,
-                            float inv_keep, float* dlog, float* loss, float* dpre2,
-                            hipStream_t st);
 void launch_head_wgrad(const float* h2, const float* dlog, int B, float* gw, float* gb,
                        hipStream_t st);
 void launch_head_bwd(const float* h2, const float* w, const float* dlog, int B,
@@ -123,17 +117,8 @@ struct Engine {
   // bit op: that dual launch dispatches its second problem first.  conv2's (weight gradient
   // split 32 ways, the longer pole) measured 0.3663 -> 0.3650 ms/step; conv4's / conv3's worse
   // (their data gradients are the longer poles; conv4's stream-K loses its XCD-major numbering).
-  // DDL_DUAL_BFIRST overrides (scripts/ab_env.sh).
   int dual_bfirst = 1 << OP_CONV2_DGRAD;
-  // bit op: that dual launch interleaves its two problems' blocks in proportion instead
-  // (overrides dual_bfirst; DDL_DUAL_MIX)
-  int dual_mix = 0;
-  int dual_order(int op) const { return ((dual_mix >> op) & 1) ? 2 : ((dual_bfirst >> op) & 1); }
-  // bit op: that op's split-K uses one chunk length for every tile, sized so the tile with the
-  // longest tap window gets splits[op] pieces (gemm.h KFixOf; only the K-map conv forwards /
-  // data gradients honour it).  DDL_KFIX overrides.
-  int kfix = 0;
-  int sarg(int op) const { return ((kfix >> op) & 1) ? -splits[op] : splits[op]; }
+  int dual_order(int op) const { return (dual_bfirst >> op) & 1; }
 
   // workspace carve-out
   float *p1 = nullptr, *p2 = nullptr, *p3 = nullptr, *p4 = nullptr, *h1 = nullptr, *h2 = nullptr;
@@ -172,27 +157,8 @@ struct Engine {
     const char* e = getenv("DDL_CONV1_WGRAD_DIRECT");
     return !e || e[0] != '0';
   }();
-  // training step (forward with defer_fc): fc2's forward leaves its split-K partials and the
-  // fused head reduces them (launch_head_fused_slab: one launch fewer).  Opt-in
-  // (DDL_HEAD_SLAB=1): measured 0.2999-0.3007 -> 0.3068-0.3073 ms/step — 100 head workgroups
-  // reading 16 strided partials per element are slower than the 3200-wave reduce launch
-  bool head_slab = [] {
-    const char* e = getenv("DDL_HEAD_SLAB");
-    return e && e[0] == '1';
-  }();
-  struct {
-    const float* slab = nullptr;
-    int S = 0, gx = 0, ntiles = 0;
-  } fc2_part;               // pending partials (slab null: none)
   // fc3 weight gradient still to compute (fused head kernel ran): taken by the fc2 dual launch
   int head_wgrad_pending = 0;
-  // training: fc1 forward .. fc1 backward as ONE persistent launch (fc_chain.h) at the start
-  // of backward segment 0 instead of six launches.  Opt-in (DDL_FC_CHAIN=1): measured slower
-  // than the separate launches so far (docs/DESIGN.md "fc chain")
-  bool fc_chain = false;
-  int* fc_ctr = nullptr;     // its work-queue / stage counters (zero between launches)
-  long long* fc_stamps = nullptr;  // diagnostics: per-item wall-clock stamps (null: off)
-  int fc_chain_error() const;  // host read of the chain's timeout word (0: healthy)
 
   Engine();
   ~Engine();
@@ -204,11 +170,7 @@ struct Engine {
   void bind_workspace(void* base);
 
   // forward through fc2 (train: dropout on, configured split-K; eval: no dropout, no split)
-  // defer_fc (training, followed by backward_segment(0)): with fc_chain the fc forward runs
-  // inside segment 0's fused fc launch instead
-  void forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st,
-               bool defer_fc = false);
-  bool fc_deferred = false;  // set by forward(defer_fc), consumed by backward_segment(0)
+  void forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st);
   // backward segment s (0: head+fc, 1: conv4, 2: conv3, 3: conv2+conv1); weight-gradient
   // GEMMs fork onto the side stream and join back at the end of the segment
   void backward_segment(int s, const float* x, const int64_t* labels, int B,
@@ -449,7 +411,8 @@ class AsyncRunner {
     hipEvent_t ev = nullptr;
     std::vector<int> ps;
   };
-  void post_loop();
+  void wait_push(const Posting& job);   // poster thread: the push kernel has completed
+  void post_tokens(const Posting& job); // poster thread: its (worker, ps) tokens, PS order
   void wait_round(double timeout_s);
   Engine* eng_;
   AsyncPeer* peer_;
@@ -459,13 +422,9 @@ class AsyncRunner {
   std::vector<int> hosts_;
   std::unique_ptr<ShmMailbox> boxes_[kXgmiMaxPeers];
   hipEvent_t ev_[kSegments] = {};
-  std::thread poster_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::deque<Posting> queue_;
-  int inflight_ = 0;
-  bool stop_ = false;
-  std::string error_;
+  // the poster thread and its FIFO (runtime/session.h; CPU-stress-tested under ASan/UBSan);
+  // declared last: destroyed (joined) first, before the events it waits on
+  std::unique_ptr<PostQueue<Posting>> posts_;
 };
 
 // Asynchronous PS over point-to-point RCCL in exclusive sessions (rccl_async.hip): one
@@ -499,9 +458,6 @@ class RcclAsync {
   bool push_one(int p);
   void serve(int worker, int p);
   void apply(int p, int worker, const float* g);
-  bool try_lock_pair(int h);
-  void unlock_pair(int h);
-  uint64_t* lock_word(int r) const;
   AsyncPsState* state_of(int p);
   float* w_;
   float* g_;
@@ -517,10 +473,8 @@ class RcclAsync {
   hipStream_t cs_ = nullptr;
   hipEvent_t ev_ = nullptr;
   float* gbuf_ = nullptr;
-  uint64_t* locks_ = nullptr;
-  size_t lock_bytes_ = 0;
-  bool lock_owner_ = false;
-  std::string lock_name_, box_name_;
+  SessionLocks locks_;  // runtime/session.h (CPU-stress-tested protocol)
+  std::string box_name_;
   std::unique_ptr<ShmMailbox> mine_;
   std::unique_ptr<ShmMailbox> boxes_[kXgmiMaxPeers];
   std::vector<int64_t> count_;

@@ -22,6 +22,7 @@
 // a token is posted only after its push has completed, and the only wait for remote work is
 // the host wait of step 1.  Staleness stays one round per worker.
 #include <chrono>
+#include <thread>
 #include <stdexcept>
 #include <string>
 
@@ -60,54 +61,40 @@ AsyncRunner::AsyncRunner(Engine* eng, AsyncPeer* peer, int world, int rank, int 
     if (!boxes[r].empty()) boxes_[r] = std::make_unique<ShmMailbox>(boxes[r], 2, false);
   for (int s = 0; s < kSegments; ++s)
     A_CHECK(hipEventCreateWithFlags(&ev_[s], hipEventDisableTiming));
-  poster_ = std::thread([this] { post_loop(); });
+  posts_ = std::make_unique<PostQueue<Posting>>([this](const Posting& j) { wait_push(j); },
+                                                [this](const Posting& j) { post_tokens(j); });
 }
 
 AsyncRunner::~AsyncRunner() {
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    stop_ = true;
-  }
-  cv_.notify_all();
-  if (poster_.joinable()) poster_.join();
+  posts_.reset();  // joins the poster before the events go
   for (auto& e : ev_)
     if (e) (void)hipEventDestroy(e);
 }
 
-// Waits for each queued push's completion event, then posts its tokens in PS order.
-void AsyncRunner::post_loop() {
-  try {
+// Poster thread: the push kernel of a job has completed.  A query loop, not
+// hipEventSynchronize: the token post is on the round trip of every async step, and a
+// blocking event wait adds its wake-up latency to it.
+void AsyncRunner::wait_push(const Posting& job) {
+  thread_local int dev = -1;
+  if (dev != device_) {
     A_CHECK(hipSetDevice(device_));
-    for (;;) {
-      Posting job;
-      {
-        std::unique_lock<std::mutex> g(mu_);
-        cv_.wait(g, [this] { return stop_ || !queue_.empty(); });
-        if (queue_.empty()) return;  // stop_
-        job = queue_.front();
-        queue_.pop_front();
-      }
-      {
-        TraceRange r("ddl.async.worker.push_wait");
-        A_CHECK(hipEventSynchronize(job.ev));
-      }
-      for (int p : job.ps) {
-        const int64_t token = ((int64_t)rank_ << 20) | p;  // parallel/mailbox.py encode()
-        if (!boxes_[hosts_[p]]->push(token, 600.0))
-          throw std::runtime_error("arrival mailbox of rank " + std::to_string(hosts_[p]) +
-                                   " full for 600 s");
-      }
-      {
-        std::lock_guard<std::mutex> g(mu_);
-        --inflight_;
-      }
-      cv_.notify_all();
-    }
-  } catch (const std::exception& e) {
-    std::lock_guard<std::mutex> g(mu_);
-    error_ = e.what();
-    inflight_ = 0;
-    cv_.notify_all();
+    dev = device_;
+  }
+  TraceRange r("ddl.async.worker.push_wait");
+  for (int spins = 0;; ++spins) {
+    const hipError_t e = hipEventQuery(job.ev);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) A_CHECK(e);
+    if (spins > 64) std::this_thread::yield();
+  }
+}
+
+void AsyncRunner::post_tokens(const Posting& job) {
+  for (int p : job.ps) {
+    const int64_t token = ((int64_t)rank_ << 20) | p;  // parallel/mailbox.py encode()
+    if (!boxes_[hosts_[p]]->push(token, 600.0))
+      throw std::runtime_error("arrival mailbox of rank " + std::to_string(hosts_[p]) +
+                               " full for 600 s");
   }
 }
 
@@ -115,21 +102,19 @@ void AsyncRunner::wait_round(double timeout_s) {
   if (epoch_ == epoch0_) return;  // no round in flight yet
   TraceRange r("ddl.async.worker.pull_wait");
   if (!peer_->wait_done(epoch_, timeout_s)) {
-    std::lock_guard<std::mutex> g(mu_);
+    const std::string pe = posts_->error();
     throw std::runtime_error("async runner: round " + std::to_string(epoch_) +
                              " did not come back (kernel error code " +
                              std::to_string(peer_->error()) + ")" +
-                             (error_.empty() ? "" : "; poster: " + error_));
+                             (pe.empty() ? "" : "; poster: " + pe));
   }
 }
 
 void AsyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t seed,
                        hipStream_t st, double timeout_s) {
   TraceRange step_range("ddl.async.step");
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    if (!error_.empty()) throw std::runtime_error("async runner poster: " + error_);
-  }
+  if (const std::string pe = posts_->error(); !pe.empty())
+    throw std::runtime_error("async runner poster: " + pe);
   // (1) the previous round's parameters are in place (this also means every token of it was
   // posted, so the segment events are free to record again)
   wait_round(timeout_s);
@@ -137,7 +122,7 @@ void AsyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t se
   eng_->seed_value = seed;
   {
     TraceRange r("ddl.fwd");
-    eng_->forward(x, B, nullptr, true, st, /*defer_fc=*/true);
+    eng_->forward(x, B, nullptr, true, st);
   }
   for (int s = 0; s < kSegments; ++s) {
     {
@@ -151,21 +136,14 @@ void AsyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t se
       StopEventScope bind(ev_[s]);
       peer_->push_set(seg_ps_[s], epoch_, 1.f, st);
     }
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      queue_.push_back({ev_[s], seg_ps_[s]});
-      ++inflight_;
-    }
-    cv_.notify_all();
+    posts_->push({ev_[s], seg_ps_[s]});
   }
   eng_->flush_tail(st);  // (no tails are set on this path; keeps the engine state clean)
 }
 
 void AsyncRunner::finish(double timeout_s) {
   wait_round(timeout_s);
-  std::unique_lock<std::mutex> g(mu_);
-  cv_.wait(g, [this] { return inflight_ == 0; });
-  if (!error_.empty()) throw std::runtime_error("async runner poster: " + error_);
+  posts_->finish();
 }
 
 }  // namespace ddl

@@ -48,10 +48,6 @@ Engine::Engine() {
   static const int defw[OP_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
   static const bool inl[OP_COUNT] = {0, 1, 1, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0};
-  if (const char* s = getenv("DDL_DUAL_BFIRST")) dual_bfirst = (int)strtol(s, nullptr, 0);
-  if (const char* s = getenv("DDL_DUAL_MIX")) dual_mix = (int)strtol(s, nullptr, 0);
-  if (const char* s = getenv("DDL_FC_CHAIN")) fc_chain = s[0] == '1';
-  if (const char* s = getenv("DDL_KFIX")) kfix = (int)strtol(s, nullptr, 0);
   memcpy(cfg, defc, sizeof(defc));
   memcpy(eval_cfg, defc, sizeof(defc));
   // eval forward at 10k-row chunks (scripts/eval_sweep.py, after the compact conv3 rows):
@@ -162,7 +158,6 @@ size_t Engine::workspace_bytes() const {
   for (size_t c : kCodePer) f += al256(B * c);
   f += 256;                          // correct counter
   f += 2 * al256(4 * kMaxTickets);   // split-K arrival tickets (two streams)
-  f += 256;                          // fc chain counters
   return f;
 }
 
@@ -184,13 +179,6 @@ void Engine::bind_workspace(void* base) {
     scratch[s].tickets = (int*)take(4 * kMaxTickets);
     scratch[s].max_tiles = kMaxTickets;
   }
-  fc_ctr = (int*)take(256);
-}
-
-int Engine::fc_chain_error() const {
-  int v = 0;
-  if (fc_ctr) (void)hipMemcpy(&v, fc_ctr + 2, sizeof(int), hipMemcpyDeviceToHost);
-  return v;
 }
 
 void Engine::run_op(int op, const float* x, int B, const uint32_t* seed, bool train,
@@ -233,19 +221,8 @@ void Engine::flush_head_wgrad(int B, hipStream_t st) {
   head_wgrad_pending = 0;
 }
 
-void Engine::forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st,
-                     bool defer_fc) {
-  // training with the fused fc chain: the fc forward runs inside backward segment 0's launch
-  fc_deferred = defer_fc && train && fc_chain && !concurrent && B <= 128;
-  const int last = fc_deferred ? OP_CONV4_FWD : OP_FC2_FWD;
-  fc2_part.slab = nullptr;
-  for (int op = OP_CONV1_FWD; op <= last; ++op) {
-    // followed by backward segment 0 on one stream: fc2's split-K reduce moves into the head
-    if (op == OP_FC2_FWD && defer_fc && train && head_slab && !concurrent && dual &&
-        run_fc2_fwd_partials(*this, x, B, seed, st))
-      continue;
-    run_op(op, x, B, seed, train, st, 0);
-  }
+void Engine::forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st) {
+  for (int op = OP_CONV1_FWD; op <= OP_FC2_FWD; ++op) run_op(op, x, B, seed, train, st, 0);
 }
 
 // The side stream waits for everything enqueued on `st` so far.
@@ -298,23 +275,11 @@ void Engine::backward_segment(int s, const float* x, const int64_t* labels, int 
     return;
   }
   // single stream: each layer's dgrad + wgrad as one dual launch
-  if (s == 0 && fc_deferred) {
-    fc_deferred = false;
-    flush_tail(st);
-    run_fc_chain(*this, labels, B, seed, st);
-    return;
-  }
   switch (s) {
     case 0:
       // one head launch (per-sample fwd + dlogits + dh2); fc3's dW/db ride in the fc2 dual
-      if (fc2_part.slab)
-        launch_head_fused_slab(fc2_part.slab, fc2_part.S, fc2_part.gx, fc2_part.ntiles, P[11],
-                               h2, P[12], P[13], labels, B, seed, seed_value, thr24, inv_keep,
-                               dlog, loss, dpre2fc, st);
-      else
-        launch_head_fused(h2, P[12], P[13], labels, B, seed, seed_value, thr24, inv_keep, dlog,
-                          loss, dpre2fc, st);
-      fc2_part.slab = nullptr;
+      launch_head_fused(h2, P[12], P[13], labels, B, seed, seed_value, thr24, inv_keep, dlog,
+                        loss, dpre2fc, st);
       head_wgrad_pending = 1;
       run_dual_inst<OP_FC2_DGRAD, OP_FC2_WGRAD>(*this, x, B, seed, st);
       flush_head_wgrad(B, st);

@@ -12,10 +12,5 @@ template <int OA, int OB>
 void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st);
 template <int OA, int OB, int ON>
 void run_dual_then_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st);
-// fc2 forward as mode-2 split-K partials only (the slab-reading head reduces them); false:
-// the schedule does not allow it, nothing launched
-bool run_fc2_fwd_partials(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st);
-// fc1 forward .. fc1 backward as one persistent launch (fc_chain.h; engine_ops_fcchain.hip)
-void run_fc_chain(Engine& e, const int64_t* labels, int B, const uint32_t* seed, hipStream_t st);
 
 }  // namespace ddl

@@ -140,14 +140,15 @@ void run_op_inst(Engine& e, const float* x, int B, const uint32_t* seed, bool tr
       return;
     }
   }
-  launch_cfg(train ? e.cfg[OP] : e.eval_cfg[OP], p, train ? e.sarg(OP) : 1,
+  launch_cfg(train ? e.cfg[OP] : e.eval_cfg[OP], p, train ? e.splits[OP] : 1,
              train ? e.workers[OP] : 0, e.wide[OP],
              e.scratch[si], st);
 }
 
 // ---- dual launches: data- and weight-gradient GEMM of one layer in one kernel -----------------
-// dual launches are instantiated for these one-wave configs (others run back to back)
-inline bool one_wave_cfg(int c) { return c == 0 || c == 3 || c == 4 || c == 5 || c == CFG_MF16; }
+// dual launches are instantiated for the one-wave 32x32 configs (others run back to back: the
+// one-wave 64x64 / 32x64 tiles, 180-230 VGPRs, never won a dual launch in the real-step tuner)
+inline bool one_wave_cfg(int c) { return c == 3 || c == 5 || c == CFG_MF16; }
 
 // fc3's weight gradient as aux blocks (head.h), pending after the fused head kernel
 inline HeadWgradAux head_aux(Engine& e, int B) {
@@ -167,35 +168,18 @@ inline HeadWgradAux head_aux(Engine& e, int B) {
 template <class CA, int OA, int OB, class PA, class PB>
 inline void dual_b(Engine& e, const PA& pa, const PB& pb, int B, hipStream_t st) {
 #define DDL_DUAL_B(CB, AUXV) \
-  launch_gemm_dual<CA, PA, TileCfg<CB>, PB>(pa, e.sarg(OA), e.workers[OA], e.scratch[0], \
-                                            e.wide[OA], pb, e.sarg(OB), e.workers[OB], \
+  launch_gemm_dual<CA, PA, TileCfg<CB>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], \
+                                            e.wide[OA], pb, e.splits[OB], e.workers[OB], \
                                             e.scratch[1], e.wide[OB], st, AUXV, nullptr, \
                                             e.dual_order(OA))
-  // the fc2 dual carries fc3's weight gradient; the others a pending optimizer tail.
-  // CFG_MF16 pairs with the 32x32 configs 3 / 5 / 14 only (instantiation count); A on 14
-  // (CA::V == 1) takes B on 3, 5 or 14.
-#define DDL_DUAL_SW(AUXV)                                                         \
-  if constexpr (CA::V == 1) {                                                     \
-    switch (e.cfg[OB]) {                                                          \
-      case CFG_MF16:                                                              \
-        if constexpr (Mf16OK<PB>::value) { DDL_DUAL_B(TILE_14, AUXV); break; }    \
-        [[fallthrough]];                                                          \
-      case 3: DDL_DUAL_B(TILE_3, AUXV); break;                                    \
-      default: DDL_DUAL_B(TILE_5, AUXV); break;                                   \
-    }                                                                             \
-  } else {                                                                        \
-    switch (e.cfg[OB]) {                                                          \
-      case 0: DDL_DUAL_B(TILE_0, AUXV); break;                                    \
-      case CFG_MF16:                                                              \
-        if constexpr (Mf16OK<PB>::value && CA::BM == 32 && CA::BN == 32) {        \
-          DDL_DUAL_B(TILE_14, AUXV);                                              \
-          break;                                                                  \
-        }                                                                         \
-        [[fallthrough]];                                                          \
-      case 3: DDL_DUAL_B(TILE_3, AUXV); break;                                    \
-      case 4: DDL_DUAL_B(TILE_4, AUXV); break;                                    \
-      default: DDL_DUAL_B(TILE_5, AUXV); break;                                   \
-    }                                                                             \
+  // the fc2 dual carries fc3's weight gradient; the others a pending optimizer tail
+#define DDL_DUAL_SW(AUXV)                                                       \
+  switch (e.cfg[OB]) {                                                          \
+    case CFG_MF16:                                                              \
+      if constexpr (Mf16OK<PB>::value) { DDL_DUAL_B(TILE_14, AUXV); break; }    \
+      [[fallthrough]];                                                          \
+    case 3: DDL_DUAL_B(TILE_3, AUXV); break;                                    \
+    default: DDL_DUAL_B(TILE_5, AUXV); break;                                   \
   }
   if constexpr (OA == OP_FC2_DGRAD) {
     e.flush_tail(st);
@@ -241,7 +225,6 @@ void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipSt
   using PA = std::decay_t<decltype(pa)>;
   using PB = std::decay_t<decltype(pb)>;
   switch (e.cfg[OA]) {
-    case 0: dual_b<TileCfg<TILE_0>, OA, OB, PA, PB>(e, pa, pb, B, st); break;
     case CFG_MF16:
       if constexpr (Mf16OK<PA>::value) {
         dual_b<TileCfg<TILE_14>, OA, OB, PA, PB>(e, pa, pb, B, st);
@@ -249,7 +232,6 @@ void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipSt
       }
       [[fallthrough]];
     case 3: dual_b<TileCfg<TILE_3>, OA, OB, PA, PB>(e, pa, pb, B, st); break;
-    case 4: dual_b<TileCfg<TILE_4>, OA, OB, PA, PB>(e, pa, pb, B, st); break;
     default: dual_b<TileCfg<TILE_5>, OA, OB, PA, PB>(e, pa, pb, B, st); break;
   }
 }
@@ -388,8 +370,8 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
   using PN = std::decay_t<decltype(pn)>;
   using CN = TileCfg<TILE_3>;
   SubGrid gb;
-  launch_gemm_dual<CA, PA, CB, PB>(pa, e.sarg(OA), e.workers[OA], e.scratch[0], e.wide[OA], pb,
-                                   e.sarg(OB), e.workers[OB], e.scratch[1], e.wide[OB], st,
+  launch_gemm_dual<CA, PA, CB, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb,
+                                   e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st,
                                    TailAux(e.tail), &gb, e.dual_order(OA));
   e.tail = UpdTail();
   constexpr bool kFinal = ON == OP_CONV1_WGRAD;
@@ -418,7 +400,7 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
   }
   const bool fin = kFinal && e.final_upd.npieces > 0;
   SubGrid gn;
-  if (!launch_reduce_with_gemm<CB, PB, CN, PN>(pb, gb, pn, e.sarg(ON), e.workers[ON],
+  if (!launch_reduce_with_gemm<CB, PB, CN, PN>(pb, gb, pn, e.splits[ON], e.workers[ON],
                                                e.wide[ON], e.scratch[0], st,
                                                fin ? &gn : nullptr)) {
     launch_reduce<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, st);

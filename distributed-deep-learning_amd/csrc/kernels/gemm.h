@@ -44,10 +44,8 @@
 
 #include "common.h"
 
-// s_setprio 1 around each K tile's MFMA cluster in the basic main loop (A/B knob)
-#ifndef DDL_MFMA_PRIO
+// s_setprio 1 around each K tile's MFMA cluster (guide T5; measured 0.3753 -> 0.3747 ms/step)
 #define DDL_MFMA_PRIO 1
-#endif
 #include "scratch.h"
 #include "tail.h"
 
@@ -124,61 +122,12 @@ struct KMapOf<P, std::void_t<decltype(P::KMAP)>> {
   using Win = typename P::KWin;
 };
 
-// Window-aware split-K (KFIX policies: kwin / kvlen callable on the host).  With the balanced
-// K-map split every tile is cut into gz pieces of ITS OWN window length, so the waves of the
-// tiles with the most taps (the map's centre) are the launch's longest pole — up to 2.8x the
-// corner tiles' on the 7x7 map.  A negative split request -s asks instead for one chunk length
-// for all tiles, sized so the LONGEST window is cut into s pieces: heavy tiles get s waves,
-// light ones fewer (their surplus z-slices exit at once with zero partials).
-template <class P, class = void>
-struct KFixOf {
-  static constexpr bool value = false;
-};
-template <class P>
-struct KFixOf<P, std::void_t<decltype(P::KFIX)>> {
-  static constexpr bool value = P::KFIX;
-};
-
-// A policy whose B operand is MN-contiguous may offer a one-element gather loadB1(info, k0)
-// (element (k0 + kk, n) of prepB(n, kk)); with it the direct-fragment main loop applies.
-template <class P, class = void>
-struct HasLoadB1 : std::false_type {};
-template <class P>
-struct HasLoadB1<P, std::void_t<decltype(std::declval<const P&>().loadB1(
-                        std::declval<const typename P::BInfo&>(), 0))>> : std::true_type {};
-
-// Direct-fragment main loop for one-wave 32x32 tiles (A/B knob, measured and rejected: default
-// off): every lane loads its own MFMA fragments straight from global memory into VGPRs.  A
-// one-wave block gets no operand reuse out of LDS (the MFMA broadcasts inside the wave); LDS
-// only re-lays the tile out, at the price of a store -> read round trip per K tile.  But the
-// fragment layout fixes lane -> row, so each 16-byte gather instruction touches 32 rows (32
-// cache lines, 32 bytes each) where the coalesced LDS-staging gather touches 8 full lines:
-// 0.3045 -> 0.336 ms/step, every conv GEMM slower (docs/DESIGN.md).
-#ifndef DDL_DIRECT
-#define DDL_DIRECT 0
-#endif
-
-// LDS-DMA staging of the one-wave 32x32 tiles (mainloop_dma): 0 off, 1 one LDS image per block
-// (8 KB), 2 two images (16 KB, the next tile's fragment reads overlap this tile's MFMAs).
-// Policies opt in per op with a constexpr DMA and srcA / srcB (the 16-byte gathers of their
-// loadA / loadB): the conv forward (DDL_LDSDMA_FWD) and conv data gradient (DDL_LDSDMA_DGRAD).
-#ifndef DDL_LDSDMA
-#define DDL_LDSDMA 1
-#endif
-#ifndef DDL_LDSDMA_FWD
-#define DDL_LDSDMA_FWD 1
-#endif
-#ifndef DDL_LDSDMA_DGRAD
-#define DDL_LDSDMA_DGRAD 0
-#endif
-#ifndef DDL_LDSDMA_WGRAD
-#define DDL_LDSDMA_WGRAD 0
-#endif
-// LDS-DMA staging of one-wave MULTI-fragment tiles (64x64 / 32x64, BN = 64: the eval forward's
-// one-wave 64x64 tiles) for K-contiguous A / MN-contiguous B policies with DMA (mainloop_dma_mf)
-#ifndef DDL_LDSDMA_MF
-#define DDL_LDSDMA_MF 1
-#endif
+// LDS-DMA staging of the one-wave 32x32 tiles (mainloop_dma, one 8 KB image per block) for
+// policies that opt in with a constexpr DMA and srcA / srcB (the 16-byte gathers of their loadA /
+// loadB): the halo-layout conv forwards.  The one-wave MULTI-fragment tiles (64x64 / 32x64,
+// BN = 64: the eval forward) stage the same way (mainloop_dma_mf).  The variants measured and
+// rejected — two images per block, DMA for the conv data / weight gradients on the 32x32x2 tile,
+// direct-to-register fragments, register-gathered B — are recorded in docs/DESIGN.md.
 // a policy whose A operand has rows that are not in memory (the weight gradients' ones row)
 template <class P, class = void>
 struct HasOnesA : std::false_type {};
@@ -216,47 +165,22 @@ struct GemmTile {
   // the LDS footprint doubles the resident waves per CU (LDS was the occupancy limit).
   static constexpr bool SOLO = (NT == 64);
   static constexpr int NBUF = SOLO ? 1 : 2;
-  // One-wave single-fragment tiles with a K-contiguous A and a K-contiguous (or one-element
-  // gatherable) B take the direct-fragment loop and need no staging LDS at all.
-  static constexpr bool DIRECT = DDL_DIRECT && SOLO && TM * TN == 1 && BK % 8 == 0 && AK &&
-                                 (BKC || HasLoadB1<P>::value) && !(BK == 16);
-  // Hybrid (A/B knob DDL_BDIRECT): A staged through LDS as usual, an MN-contiguous B (the conv
-  // forward's HWIO weights) gathered straight into fragment registers — per MFMA one 4-byte
-  // load whose 32 lanes per half read 128 contiguous bytes (two whole lines per instruction, so
-  // none of the direct loop's texture cost) — one tile ahead in a second register set.  Saves
-  // the B image's LDS stores / 16 ds_read_b32 per K tile and halves the block's LDS.  Measured
-  // and rejected (default off): 0.3050 -> 0.3100 ms/step, each conv forward ~1 us slower — 16
-  // dword loads per K tile cost more issue / latency than the LDS round trip they replace.
-#ifndef DDL_BDIRECT
-#define DDL_BDIRECT 0
-#endif
-  static constexpr bool BDIR = DDL_BDIRECT && !DIRECT && SOLO && TM * TN == 1 && BK % 8 == 0 &&
-                               !(BK == 16) && !BKC && HasLoadB1<P>::value;
-  // LDS-DMA staging (mainloop_dma): unpadded 32x32 images, swizzled through the gather
-  // addresses (the DMA writes lane-linearly), DDL_LDSDMA images of A + B per block
-  // 16x16x4 MFMA + LDS-DMA one-wave tile (variant 1): any policy with 16-byte gathers
-  // (instantiated only for policies with the 16-byte gathers srcA / srcB: layers.h Mf16OK)
+  // 16x16x4 MFMA + LDS-DMA one-wave tile (variant 1; instantiated only for policies with the
+  // 16-byte gathers srcA / srcB: layers.h Mf16OK)
   static constexpr bool DMA16 = V == 1 && SOLO && BM == 32 && BN == 32 && BK == 32;
   static_assert(V == 0 || DMA16, "variant 1 is the one-wave 32x32x32 tile");
-  static constexpr bool DMA = DDL_LDSDMA > 0 && HasDma<P>::value && SOLO && TM * TN == 1 &&
-                              BM == 32 && BN == 32 && BK == 32 && !DIRECT && !BDIR && !DMA16;
-  static constexpr int DMA_NB = DDL_LDSDMA > 0 ? DDL_LDSDMA : 1;
-  static constexpr bool DMA_MF = DDL_LDSDMA_MF > 0 && HasDma<P>::value && SOLO && TM * TN > 1 &&
-                                 BN == 64 && BK == 32 && AK && !BKC && !DIRECT && !BDIR &&
-                                 !HasOnesA<P>::value;
-  static constexpr int LDS_F4 =
-      DMA16 ? 512
-      : DMA ? DMA_NB * 512
-          : DMA_MF ? (BM * BK + BK * BN) / 4
-          : DIRECT ? 0 : (NBUF * (A_ELEMS + (BDIR ? 0 : B_ELEMS))) / 4;
+  // LDS-DMA staging (mainloop_dma): unpadded 32x32 images, swizzled through the gather
+  // addresses (the DMA writes lane-linearly), one image of A + B per block
+  static constexpr bool DMA = HasDma<P>::value && SOLO && TM * TN == 1 && BM == 32 && BN == 32 &&
+                              BK == 32 && !DMA16;
+  static constexpr bool DMA_MF = HasDma<P>::value && SOLO && TM * TN > 1 && BN == 64 &&
+                                 BK == 32 && AK && !BKC && !HasOnesA<P>::value;
+  static constexpr int LDS_F4 = (DMA16 || DMA) ? 512
+                                : DMA_MF ? (BM * BK + BK * BN) / 4
+                                : (NBUF * (A_ELEMS + B_ELEMS)) / 4;
   // A wave with a single 32x32 fragment alternates two accumulator chains (summed at the
-  // end) so consecutive MFMAs are independent.
-  // (DDL_TWO_CHAINS=0: one chain; gfx950 forwards a 32x32 MFMA's result to the next one's
-  // SrcC back to back, so the second chain is only registers — A/B knob)
-#ifndef DDL_TWO_CHAINS
-#define DDL_TWO_CHAINS 1
-#endif
-  static constexpr int NCH = (TM * TN == 1 && DDL_TWO_CHAINS) ? 2 : 1;
+  // end) so consecutive MFMAs are independent (one chain: measured 0.3050 -> 0.3070 ms/step)
+  static constexpr int NCH = TM * TN == 1 ? 2 : 1;
   static constexpr int WPART = TM * TN * 4 * 64;  // float4 of one wave's partial fragments
   static constexpr bool KM = KMapOf<P>::value;
   using Win = typename KMapOf<P>::Win;
@@ -280,86 +204,8 @@ struct GemmTile {
     if constexpr (DMA16) mainloop_dma16(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else if constexpr (DMA) mainloop_dma(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else if constexpr (DMA_MF) mainloop_dma_mf(p, m_blk, n_blk, kb, ke, lds, acc, w);
-    else if constexpr (DIRECT) mainloop_direct(p, m_blk, n_blk, kb, ke, acc, w);
     else if constexpr (PIPE) mainloop_pipe(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else mainloop_basic(p, m_blk, n_blk, kb, ke, lds, acc, w);
-  }
-
-  static DDL_DEV float ldB1(const P& p, const typename P::BInfo& b, int k, const Win& w) {
-    if constexpr (KM) return p.loadB1(b, k, w);
-    else return p.loadB1(b, k);
-  }
-
-  // Direct-fragment loop (one wave, one 32x32 fragment, no LDS).  MFMA s of 8-deep sub-step r
-  // takes k = 8r + 4h + s in lane half h (the LDS path's fragment order), so a K-contiguous
-  // operand's fragments of one sub-step are ONE 16-byte gather per lane (row = lane & 31, k
-  // offset 8r + 4h: the loaders' prep(mn, kk) / load(info, k0 + 8r) protocol, the sub-step
-  // base staying wave-uniform) and an MN-contiguous B's are four one-element gathers whose 32
-  // lanes of a half read 128 contiguous bytes.  Two register sets: tile t+2's loads are issued
-  // right after tile t's MFMAs, so they have tile t+1's MFMA cluster to land.
-  static DDL_DEV void mainloop_direct(const P& p, int m_blk, int n_blk, int kb, int ke,
-                                      f32x16 (&acc)[TM][TN], const Win& w) {
-    const int lane = threadIdx.x & 63;
-    const int lr = lane & 31, lh = lane >> 5;
-    const int nk = (ke - kb + BK - 1) / BK;
-    const typename P::AInfo ai = p.prepA(m_blk + lr, 4 * lh);
-    constexpr int NBI = BKC ? 1 : 4;
-    typename P::BInfo bi[NBI];
-#pragma unroll
-    for (int s = 0; s < NBI; ++s) bi[s] = p.prepB(n_blk + lr, 4 * lh + s);
-    float a0[R][4], b0[R][4], a1[R][4], b1[R][4];
-    auto gl = [&](int k0, float (&a)[R][4], float (&b)[R][4]) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const float4 t = ldA(p, ai, k0 + 8 * r, w);
-        a[r][0] = t.x; a[r][1] = t.y; a[r][2] = t.z; a[r][3] = t.w;
-        if constexpr (BKC) {
-          const float4 u = ldB(p, bi[0], k0 + 8 * r, w);
-          b[r][0] = u.x; b[r][1] = u.y; b[r][2] = u.z; b[r][3] = u.w;
-        } else {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) b[r][s] = ldB1(p, bi[s], k0 + 8 * r, w);
-        }
-      }
-    };
-    f32x16 c0, c1;  // two independent accumulator chains
-#pragma unroll
-    for (int q = 0; q < 16; ++q) { c0[q] = 0.f; c1[q] = 0.f; }
-    auto mf = [&](const float (&a)[R][4], const float (&b)[R][4]) {
-#if DDL_MFMA_PRIO
-      __builtin_amdgcn_s_setprio(1);
-#endif
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          if ((s & 1) && NCH == 2) c1 = mfma32x32x2(a[r][s], b[r][s], c1);
-          else c0 = mfma32x32x2(a[r][s], b[r][s], c0);
-        }
-#if DDL_MFMA_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    if (nk > 0) gl(kb, a0, b0);
-    if (nk > 1) gl(kb + BK, a1, b1);
-    __builtin_amdgcn_sched_barrier(0);
-    int kt = 0;
-    for (; kt + 3 < nk; kt += 2) {  // tiles kt (set 0) and kt+1 (set 1); kt+2, kt+3 exist
-      mf(a0, b0);
-      gl(kb + (kt + 2) * BK, a0, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      mf(a1, b1);
-      gl(kb + (kt + 3) * BK, a1, b1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    const int left = nk - kt;  // 0..3 tiles, already loaded or loaded below
-    if (left >= 1) mf(a0, b0);
-    if (left == 3) gl(kb + (kt + 2) * BK, a0, b0);
-    if (left >= 2) mf(a1, b1);
-    if (left == 3) mf(a0, b0);
-    if constexpr (NCH == 2) acc[0][0] = c0 + c1;
-    else acc[0][0] = c0;
   }
 
   // Software-pipelined main loop (one wave, one 32x32 fragment, single LDS buffer).
@@ -457,11 +303,7 @@ struct GemmTile {
     // reads (which must follow those stores) and the global loads between the rest.
     constexpr int NMF = 4 * R, NST = FA + FB;
     static_assert(NMF >= 2 * NST, "pipelined loop needs 2 MFMAs per staged float4");
-#ifndef DDL_PIPE_SCHED
-#define DDL_PIPE_SCHED 1
-#endif
     auto interleave = [&]() {
-      if constexpr (!DDL_PIPE_SCHED) return;
 #pragma unroll
       for (int i = 0; i < NST; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -484,10 +326,7 @@ struct GemmTile {
     }
     int kt = 0;
     // steady state: tiles kt (F0) and kt+1 (F1) per trip; all of kt+1..kt+4 exist
-#ifndef DDL_PIPE_STEADY
-#define DDL_PIPE_STEADY 1
-#endif
-    for (; DDL_PIPE_STEADY && kt + 4 < nk; kt += 2) {
+    for (; kt + 4 < nk; kt += 2) {
       sstore(ga1, gb1);                       // tile kt+1
       gload(kb + (kt + 3) * BK, ga1, gb1);    // tile kt+3
       fetch(f1a, f1b);                        // fragments of kt+1
@@ -539,11 +378,10 @@ struct GemmTile {
   // k + 4, land in opposite bank halves).  The MFMA order (k pairs, two accumulator chains) is
   // the basic loop's, so both give the same bits.  A's rows that are not in memory (HasOnesA:
   // the weight gradients' ones row) arrive as zeros and are patched in the image with one
-  // ds_write per holding lane once the tile has landed, before the fragment reads.
-  // NB = 2: tile t+2 is DMA'd while tile t's MFMAs run and tile t+1's fragments are read, in
-  // a second LDS image and a second fragment register set (the loop is unrolled by two so
-  // both stay static).  NB = 1: tile t+1 is DMA'd into the one image once tile t's fragments
-  // are in registers.  Completion is counted by hand (vm_wait: 8 DMAs per tile).
+  // ds_write per holding lane once the tile has landed, before the fragment reads.  Tile t+1
+  // is DMA'd into the one image once tile t's fragments are in registers; completion is
+  // counted by hand (vm_wait).  (A second image — tile t+2 in flight during tile t's MFMAs —
+  // measured 8 % slower: 152 registers and 16 KB of LDS cap the block at 2.5 waves per SIMD.)
   static DDL_DEV void mainloop_dma(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
                                    f32x16 (&acc)[TM][TN], const Win& w) {
     static_assert(FA == 4 && FB == 4 && R == 4, "32x32x32 one-wave tile");
@@ -562,25 +400,23 @@ struct GemmTile {
       else bi[it] = p.prepB(n_blk + q * 4, row ^ ((row >> 2) & 1));
     }
     // the image float that lane's DMA `it` of A fills first (its .x), for the ones-row patch
-    auto patch = [&](int k0, int buf) {
+    auto patch = [&](int k0) {
       if constexpr (HasOnesA<P>::value) {
-        float* As = lds + buf * 2048;
 #pragma unroll
         for (int it = 0; it < 4; ++it)
-          if (p.ones_group(ai[it])) As[(it * 64 + lane) * 4] = p.ones_value(ai[it], k0, w);
+          if (p.ones_group(ai[it])) lds[(it * 64 + lane) * 4] = p.ones_value(ai[it], k0, w);
       }
     };
     const uint32_t base = lds_addr(lds);
-    auto dma = [&](int k0, int buf) {
-      const uint32_t b0 = base + buf * 8192;
+    auto dma = [&](int k0) {
 #pragma unroll
-      for (int it = 0; it < 4; ++it) dma16(srcA(p, ai[it], k0, w), b0 + it * 1024);
+      for (int it = 0; it < 4; ++it) dma16(srcA(p, ai[it], k0, w), base + it * 1024);
 #pragma unroll
-      for (int it = 0; it < 4; ++it) dma16(srcB(p, bi[it], k0, w), b0 + 4096 + it * 1024);
+      for (int it = 0; it < 4; ++it) dma16(srcB(p, bi[it], k0, w), base + 4096 + it * 1024);
     };
     // fragments of K step (r, s): lane half h holds k = 8r + 4h + s (the basic loop's order)
-    auto rd = [&](int buf, float (&av)[R][4], float (&bv)[R][4]) {
-      const float* As = lds + buf * 2048;
+    auto rd = [&](float (&av)[R][4], float (&bv)[R][4]) {
+      const float* As = lds;
       const float* Bs = As + 1024;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -607,14 +443,12 @@ struct GemmTile {
       acc2[q] = 0.f;
       acc[0][0][q] = 0.f;
     }
-    // K steps [r0, r1) of a tile (inline asm is a scheduling barrier, so the split decides
-    // where the next tile's wait + fragment reads sit inside the MFMA stream)
-    auto mma = [&](const float (&av)[R][4], const float (&bv)[R][4], int r0 = 0, int r1 = R) {
+    auto mma = [&](const float (&av)[R][4], const float (&bv)[R][4]) {
 #if DDL_MFMA_PRIO
       __builtin_amdgcn_s_setprio(1);
 #endif
 #pragma unroll
-      for (int r = r0; r < r1; ++r)
+      for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           if constexpr (NCH == 2) {
@@ -630,52 +464,14 @@ struct GemmTile {
     };
     if (nk > 0) {
       float a0[R][4], b0[R][4];
-      if constexpr (DMA_NB == 1) {
-        dma(kb, 0);
-        for (int kt = 0; kt < nk; ++kt) {
-          vm_wait<0>();   // tile kt is in the image
-          patch(kb + kt * BK, 0);
-          rd(0, a0, b0);
-          lgkm_wait0();   // its fragments are in registers: the image may be restaged
-          if (kt + 1 < nk) dma(kb + (kt + 1) * BK, 0);
-          mma(a0, b0);
-        }
-      } else {
-        float a1[R][4], b1[R][4];
-        dma(kb, 0);
-        if (nk > 1) {
-          dma(kb + BK, 1);
-          vm_wait<8>();
-        } else {
-          vm_wait<0>();
-        }
-        patch(kb, 0);
-        rd(0, a0, b0);
-        // (half of a tile's MFMAs are issued before the wait for the next tile's DMA, so the
-        // wave never stalls on it with an empty MFMA pipe)
-        for (int kt = 0; kt < nk; kt += 2) {
-          lgkm_wait0();  // set 0 (tile kt) in registers, image 0 free
-          if (kt + 2 < nk) dma(kb + (kt + 2) * BK, 0);
-          mma(a0, b0, 0, R / 2);
-          if (kt + 1 < nk) {
-            if (kt + 2 < nk) vm_wait<8>();
-            else vm_wait<0>();
-            patch(kb + (kt + 1) * BK, 1);
-            rd(1, a1, b1);  // tile kt+1's reads overlap tile kt's MFMAs
-          }
-          mma(a0, b0, R / 2, R);
-          if (kt + 1 >= nk) break;
-          lgkm_wait0();  // set 1 (tile kt+1) in registers, image 1 free
-          if (kt + 3 < nk) dma(kb + (kt + 3) * BK, 1);
-          mma(a1, b1, 0, R / 2);
-          if (kt + 2 < nk) {
-            if (kt + 3 < nk) vm_wait<8>();
-            else vm_wait<0>();
-            patch(kb + (kt + 2) * BK, 0);
-            rd(0, a0, b0);
-          }
-          mma(a1, b1, R / 2, R);
-        }
+      dma(kb);
+      for (int kt = 0; kt < nk; ++kt) {
+        vm_wait<0>();   // tile kt is in the image
+        patch(kb + kt * BK);
+        rd(a0, b0);
+        lgkm_wait0();   // its fragments are in registers: the image may be restaged
+        if (kt + 1 < nk) dma(kb + (kt + 1) * BK);
+        mma(a0, b0);
       }
     }
     if constexpr (NCH == 2) acc[0][0] += acc2;
@@ -928,10 +724,6 @@ struct GemmTile {
     }
 #pragma unroll
     for (int it = 0; it < FB; ++it) {
-      if constexpr (BDIR) {  // (it < 4) the lane's fragment column, k offset 4h + it
-        bi[it] = p.prepB(n_blk + (lane & 31), 4 * (lane >> 5) + it);
-        continue;
-      }
       const int idx = tid + it * NT;
       if constexpr (BKC) {
         const int kq = idx % (BK / 4), row = idx / (BK / 4);
@@ -943,8 +735,6 @@ struct GemmTile {
         b_off[it] = kk * SB + nq * 4;
       }
     }
-    static_assert(!BDIR || FB == 4, "hybrid B: one info per k offset 4h + s");
-    float bn[BDIR ? R : 1][4];  // BDIR: next tile's B fragments (in flight)
 
     // Two register-prefetch stages of the global operands: K tile t+1 is stored to LDS
     // while tile t's fragments are already in VGPRs, and tile t+2 loads during t's MFMAs.
@@ -952,25 +742,16 @@ struct GemmTile {
     auto gload = [&](int k0) {
 #pragma unroll
       for (int it = 0; it < FA; ++it) ra[it] = ldA(p, ai[it], k0, w);
-      if constexpr (BDIR) {
 #pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-          for (int s = 0; s < 4; ++s) bn[r][s] = ldB1(p, bi[s], k0 + 8 * r, w);
-      } else {
-#pragma unroll
-        for (int it = 0; it < FB; ++it) rb[it] = ldB(p, bi[it], k0, w);
-      }
+      for (int it = 0; it < FB; ++it) rb[it] = ldB(p, bi[it], k0, w);
     };
     auto sstore = [&](int buf) {
       float* As = As0 + buf * A_ELEMS;
       float* Bs = Bs0 + buf * B_ELEMS;
 #pragma unroll
       for (int it = 0; it < FA; ++it) *reinterpret_cast<float4*>(As + a_off[it]) = ra[it];
-      if constexpr (!BDIR) {
 #pragma unroll
-        for (int it = 0; it < FB; ++it) *reinterpret_cast<float4*>(Bs + b_off[it]) = rb[it];
-      }
+      for (int it = 0; it < FB; ++it) *reinterpret_cast<float4*>(Bs + b_off[it]) = rb[it];
     };
 
     f32x16 acc2;
@@ -1005,7 +786,6 @@ struct GemmTile {
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          if constexpr (BDIR) break;  // B fragments arrive by register copy (bcopy)
           const int col = wn * WTN + j * 32 + lr;
           if constexpr (BKC) {
             const float4 t = *reinterpret_cast<const float4*>(Bs + col * SB + r * 8 + 4 * lh);
@@ -1018,26 +798,12 @@ struct GemmTile {
       }
     };
 
-    // BDIR: tile t+1's B fragments move from the in-flight set to the MFMA set where tile t+1's
-    // A image is stored to LDS (the same point that waits for tile t+1's loads)
-    auto bcopy = [&]() {
-      if constexpr (BDIR) {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-          for (int s = 0; s < 4; ++s) bv[r][0][s] = bn[r][s];
-      }
-    };
     if (nk > 0) {
       gload(kb);
       sstore(0);
-      bcopy();
       if (nk > 1) gload(kb + BK);
     }
     if constexpr (!SOLO) __syncthreads();
-#ifndef DDL_STORE_LATE
-#define DDL_STORE_LATE 1
-#endif
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = SOLO ? 0 : (kt & 1);
       fetch_all(As0 + cur * A_ELEMS, Bs0 + cur * B_ELEMS);
@@ -1045,9 +811,9 @@ struct GemmTile {
       // with two buffers the previous iteration's barrier freed buffer cur^1.
       // One-wave blocks stage tile kt+1 AFTER tile kt's MFMAs (below): issued before them, the
       // LDS writes' vmcnt waits for tile kt+1's global loads sat in front of the MFMA cluster
-      // (its lgkmcnt wait covers the writes), so every K tile paid the load latency again.
-      static_assert(!BDIR || DDL_STORE_LATE, "hybrid B needs the late staging order");
-      if (!(SOLO && DDL_STORE_LATE)) {
+      // (its lgkmcnt wait covers the writes), so every K tile paid the load latency again
+      // (0.3135 -> 0.3098 ms/step).
+      if constexpr (!SOLO) {
         if (kt + 1 < nk) sstore(SOLO ? 0 : (cur ^ 1));
         if (kt + 2 < nk) gload(kb + (kt + 2) * BK);
       }
@@ -1074,8 +840,8 @@ struct GemmTile {
       __builtin_amdgcn_s_setprio(0);
 #endif
       __builtin_amdgcn_sched_barrier(0);
-      if (SOLO && DDL_STORE_LATE) {
-        if (kt + 1 < nk) { sstore(0); bcopy(); }
+      if constexpr (SOLO) {
+        if (kt + 1 < nk) sstore(0);
         if (kt + 2 < nk) gload(kb + (kt + 2) * BK);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -1192,10 +958,9 @@ DDL_DEV void splitk_body(const P& p, int kchunk, int mode, float4* __restrict__ 
     // this tile's useful K sub-space, divided over the gz splits (whole BK tiles)
     const typename T::Win w = p.kwin(m_blk, min(p.M, m_blk + BM));
     const int kv = p.kvlen(w);
-    // kchunk < 0: one chunk length for every tile (window-aware split, see KFixOf); a z-slice
-    // past this tile's window runs no K tile and contributes a zero partial
-    const int kc = kchunk < 0 ? -kchunk
-                              : (gz > 1 ? ((kv + gz - 1) / gz + BK - 1) / BK * BK : kv);
+    // (one chunk length sized by the longest window instead, heavy tiles getting more waves
+    // than light ones: measured 0.3056 -> 0.3098-0.3167 ms/step, docs/DESIGN.md)
+    const int kc = gz > 1 ? ((kv + gz - 1) / gz + BK - 1) / BK * BK : kv;
     const int kb = bz * kc;
     T::mainloop(p, m_blk, n_blk, kb, min(kv, kb + kc), lds, acc, w);
   } else {
@@ -1275,20 +1040,14 @@ struct SubGrid {
   int kchunk = 0, mode = 0;  // split-K
   int KI = 0;                // stream-K
   long long I = 0;
-  int xcd = 0;               // split-K: XCD-contiguous block numbering (xcd_remap)
   float4* slab = nullptr;
   int* tickets = nullptr;
 };
 
-// The hardware dispatches block b to XCD b % 8 (each XCD has its own L2).  This bijection gives
-// XCD x a contiguous range of virtual ids instead, so the m-fastest neighbours that share a
-// weight panel (same n tile and K split) run behind one L2 (guide T1; any block count n).
-DDL_DEV int xcd_remap(int b, int n) {
-  const int q = n >> 3, r = n & 7;
-  const int x = b & 7, i = b >> 3;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
-}
-
+// Split-K blocks keep the hardware's round-robin XCD placement (block b on XCD b % 8): an
+// XCD-contiguous numbering (each XCD's L2 holding its eighth of the maps) measured 0.318 ->
+// 0.331 ms/step — with tap windows the per-tile cost depends on the position and contiguous
+// ranges hand one XCD all the heavy centre tiles (docs/DESIGN.md).
 // SK = false: no stream-K body in the kernel (its register count would set the launch's
 // occupancy even when the split-K body runs; the dual launch's 16x16x4 sub-problems)
 template <int BM, int BN, int BK, int WM, int WN, class P, int V = 0, bool SK = true>
@@ -1297,49 +1056,24 @@ DDL_DEV void run_sub(const P& p, const SubGrid& g, int vb, float* lds, int* flag
     streamk_body<BM, BN, BK, WM, WN, P, V>(p, g.KI, g.gx, g.I, g.slab, g.tickets, vb,
                                            g.nblocks, lds, flag);
   } else {
-    if (g.xcd) vb = xcd_remap(vb, g.nblocks);
     const int bx = vb % g.gx, t = vb / g.gx;
     splitk_body<BM, BN, BK, WM, WN, P, V>(p, g.kchunk, g.mode, g.slab, g.tickets, bx, t % g.gy,
                                           t / g.gy, g.gx, g.gy, g.gz, lds, flag);
   }
 }
 
-// Occupancy hint for the GEMM launches (A/B knob; 0 = the compiler's choice)
-#ifndef DDL_GEMM_WAVES
-#define DDL_GEMM_WAVES 0
-#endif
-#if DDL_GEMM_WAVES > 0
-#define DDL_GEMM_OCC __attribute__((amdgpu_waves_per_eu(DDL_GEMM_WAVES)))
-#else
-#define DDL_GEMM_OCC
-#endif
-// the same for the dual (data + weight gradient) launches only
-#ifndef DDL_DUAL_WAVES
-#define DDL_DUAL_WAVES 0
-#endif
-#if DDL_DUAL_WAVES > 0
-#define DDL_DUAL_OCC __attribute__((amdgpu_waves_per_eu(DDL_DUAL_WAVES)))
-#else
-#define DDL_DUAL_OCC DDL_GEMM_OCC
-#endif
-
+// (No amdgpu_waves_per_eu occupancy hints: forcing 4 waves per SIMD on the 32x32x2 tiles
+// measured slower on every driver — tighter schedules and small spills cost more than the
+// extra wave hides; the 16x16x4 tile reaches 5 waves by its register budget instead.)
 template <int BM, int BN, int BK, int WM, int WN, class P, int V = 0>
-__global__ void __launch_bounds__(WM * WN * 64) DDL_GEMM_OCC
-gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets,
-                int xcd) {
+__global__ void __launch_bounds__(WM * WN * 64)
+gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets) {
   using T = GemmTile<BM, BN, BK, WM, WN, P, V>;
   // staging images; the last-arriver flag reuses the first word (arrive() runs after the main
   // loop, whose last LDS reads have retired) — one array (guide §5 trap 4a), and no extra 16 B
   // that would push an 8 / 16 KB LDS-DMA block past an occupancy step
   __shared__ float4 lds4[T::LDS_F4 > 0 ? T::LDS_F4 : 1];
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (xcd) {  // linear id (x fastest, the dispatch order) -> XCD-contiguous virtual id
-    const int gx = gridDim.x, gy = gridDim.y;
-    const int v = xcd_remap(bx + gx * (by + gy * bz), gx * gy * gridDim.z);
-    bx = v % gx;
-    by = (v / gx) % gy;
-    bz = v / (gx * gy);
-  }
+  const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   splitk_body<BM, BN, BK, WM, WN, P, V>(p, kchunk, mode, slab, tickets, bx, by, bz, gridDim.x,
                                         gridDim.y, gridDim.z, reinterpret_cast<float*>(lds4),
                                         reinterpret_cast<int*>(lds4));
@@ -1500,7 +1234,7 @@ struct TailAux {
 // numbering holds).  The tail path must stay under the GEMM paths' VGPR count: at 8 float4
 // per lane it raised the conv4 dual from 113 to 149 VGPRs (3 -> 2 waves/SIMD, +9 us).
 template <class CA, class PA, class CB, class PB, class AUX>
-__global__ void __launch_bounds__(64) DDL_DUAL_OCC
+__global__ void __launch_bounds__(64)
 gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut, int bfirst) {
   static_assert(CA::NT == 64 && CB::NT == 64, "dual launch needs one-wave blocks");
   using TA = GemmTile<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA, CA::V>;
@@ -1523,22 +1257,12 @@ gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut, int bfirst) {
     return;
   }
   // bfirst 1: problem B's blocks are dispatched first (longest-first ordering shortens the
-  // launch's tail when B's blocks run longer); 0: A's first; 2: the two interleaved in
-  // proportion (block b is A's iff floor((b + 1) na / n) > floor(b na / n): A's blocks spread
-  // evenly over the dispatch order)
-  int ia, ib;
-  bool is_a;
-  if (bfirst == 2) {
-    const int na = ga.nblocks, n = gemm_blocks;
-    const int lo = (int)(((long long)b * na) / n), hi = (int)(((long long)(b + 1) * na) / n);
-    is_a = hi > lo;
-    ia = lo;
-    ib = b - lo;
-  } else {
-    is_a = bfirst ? (b >= gb.nblocks) : (b < ga.nblocks);
-    ia = bfirst ? b - gb.nblocks : b;
-    ib = bfirst ? b : b - ga.nblocks;
-  }
+  // launch's tail when B's blocks run longer); 0: A's first.  (Interleaving the two problems'
+  // blocks measured slower for every layer: the blocks of one problem running together share
+  // their operands in L2.)
+  const bool is_a = bfirst ? (b >= gb.nblocks) : (b < ga.nblocks);
+  const int ia = bfirst ? b - gb.nblocks : b;
+  const int ib = bfirst ? b : b - ga.nblocks;
   if (is_a)
     run_sub<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA, CA::V, CA::V == 0>(pa, ga, ia, lds, flag);
   else
@@ -1674,24 +1398,6 @@ inline size_t gemm_slab_f4(int M, int N, int K, int splits, int workers) {
   return sk > sp ? sk : sp;
 }
 
-// XCD-contiguous split-K numbering (xcd_remap): per policy (`static constexpr bool XCD_CONTIG`,
-// default off), or forced for every launch by DDL_XCD_REMAP=0/1 (A/B knob, read once)
-template <class P, class = void>
-struct XcdOf {
-  static constexpr bool value = false;
-};
-template <class P>
-struct XcdOf<P, std::void_t<decltype(P::XCD_CONTIG)>> {
-  static constexpr bool value = P::XCD_CONTIG;
-};
-inline int xcd_remap_env() {
-  static const int v = [] {
-    const char* e = getenv("DDL_XCD_REMAP");
-    return e ? atoi(e) : -1;
-  }();
-  return v;
-}
-
 // Schedule of one launch: stream-K when workers > 0 (and the tile count fits the tickets),
 // else split-K with `splits`: z > wide_thr uses mode 2 (separate wide reduce), else mode 1
 // (last arriver).
@@ -1701,8 +1407,6 @@ inline SubGrid plan_gemm(const P& p, int splits, int workers, int wide_thr,
   SubGrid g;
   g.slab = reinterpret_cast<float4*>(sc.slab);
   g.tickets = sc.tickets;
-  const bool kfix = splits < 0;  // window-aware split request (KFixOf policies only)
-  if (kfix) splits = -splits;
   if (p.M <= 0 || p.N <= 0) return g;
   g.gx = (p.M + BM - 1) / BM;
   g.gy = (p.N + BN - 1) / BN;
@@ -1716,23 +1420,6 @@ inline SubGrid plan_gemm(const P& p, int splits, int workers, int wide_thr,
   }
   g.gz = splitk_z<BK>(p.K, splits);
   g.kchunk = g.gz > 1 ? splitk_kchunk<BK>(p.K, splits) : p.K;
-  if constexpr (KFixOf<P>::value) {
-    if (kfix && g.gz > 1) {
-      int kvmax = BK;
-      for (int t = 0; t < g.gx; ++t) {
-        const int lo = t * BM, hi = lo + BM < p.M ? lo + BM : p.M;
-        const int kv = p.kvlen(p.kwin(lo, hi));
-        kvmax = kv > kvmax ? kv : kvmax;
-      }
-      // z never exceeds the balanced split's (the slab is sized for that)
-      int z = splits < g.gz ? splits : g.gz;
-      int kc = ((kvmax + z - 1) / z + BK - 1) / BK * BK;
-      z = (kvmax + kc - 1) / kc;
-      g.gz = z;
-      g.kchunk = -kc;
-    }
-  }
-  g.xcd = xcd_remap_env() >= 0 ? xcd_remap_env() : (XcdOf<P>::value ? 1 : 0);
   g.mode = g.gz == 1 ? 0 : (g.gz > wide_thr ? 2 : 1);
   if (g.mode == 1 && (long long)g.gx * g.gy > sc.max_tiles) g.mode = 2;  // ticket capacity
   g.nblocks = g.gx * g.gy * g.gz;
@@ -1794,7 +1481,7 @@ inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch
     return;
   }
   DDL_LAUNCH((gemm_f32_kernel<BM, BN, BK, WM, WN, P, V>), dim3(g.gx, g.gy, g.gz),
-                     dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets, g.xcd);
+                     dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets);
   launch_reduce<BM, BN, BK, WM, WN, P>(p, g, stream);
 }
 

@@ -112,38 +112,8 @@ head_bwd_kernel(const float* __restrict__ h2, const float* __restrict__ w,
   dpre2[idx] = g;
 }
 
-// fc2's split-K partial slab (gemm.h mode 2, 32x32 one-wave tiles, 4 < S <= 16: engine.hip
-// forward): the head sums the partials of its own sample row itself, with the
-// bias and dropout of fc2's epilogue (layers.h FcFwd<false>), in the association of the wide
-// reduce's 16-lane DPP tree (splitk_wide_reduce, RL = 16: lane z holds partial z, the group sum
-// is the balanced pairwise tree), and stores h2 — bit-identical to the reduce launch it replaces.
-struct Fc2Slab {
-  const float* slab = nullptr;  // [S][ntiles*256] float4 (fragment order per 32x32 tile)
-  int S = 0, gx = 0, zstride4 = 0;
-  const float* bias = nullptr;  // fc2 bias [HK]
-  float* h2 = nullptr;          // [B, HK] out
-};
-DDL_DEV float fc2_from_slab(const Fc2Slab& fs, int row, int n, uint32_t key, uint32_t thr24,
-                            float inv_keep) {
-  const int mm = row & 31;
-  const int tile = (n >> 5) * fs.gx + (row >> 5);
-  const int f4 = tile * 256 + (mm >> 3) * 64 + (n & 31) + 32 * ((mm >> 2) & 1);
-  const float* src = fs.slab + (size_t)f4 * 4 + (mm & 3);
-  float x[16];
-#pragma unroll
-  for (int z = 0; z < 16; ++z)
-    x[z] = z < fs.S ? 0.f + src[(size_t)z * fs.zstride4 * 4] : 0.f;
-  const float lo = ((x[0] + x[1]) + (x[2] + x[3])) + ((x[4] + x[5]) + (x[6] + x[7]));
-  const float hi = ((x[8] + x[9]) + (x[10] + x[11])) + ((x[12] + x[13]) + (x[14] + x[15]));
-  float val = (lo + hi) + fs.bias[n];
-  if (thr24) val = ddl_keep(key, (uint32_t)(row * HK + n), thr24) ? val * inv_keep : 0.f;
-  fs.h2[(size_t)row * HK + n] = val;
-  return val;
-}
-
-template <bool SLAB>
 __global__ void __launch_bounds__(256)
-head_fused_kernel(const float* __restrict__ h2, Fc2Slab fs, const float* __restrict__ w,
+head_fused_kernel(const float* __restrict__ h2, const float* __restrict__ w,
                   const float* __restrict__ bias, const int64_t* __restrict__ labels, int B,
                   float inv_batch, const uint32_t* __restrict__ seed, uint32_t seed_v,
                   uint32_t thr24, float inv_keep, float* __restrict__ dlog,
@@ -154,14 +124,7 @@ head_fused_kernel(const float* __restrict__ h2, Fc2Slab fs, const float* __restr
   // fc2's dropout key (layer 2) is also the dh2 mask key below
   const uint32_t key = thr24 ? ddl_mix32((seed ? *seed : seed_v) + 2u * 0x9E3779B9u) : 0u;
   float acc[HC];
-  if constexpr (SLAB) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const float hv[2] = {fc2_from_slab(fs, row, wave * 128 + lane, key, thr24, inv_keep),
-                         fc2_from_slab(fs, row, wave * 128 + 64 + lane, key, thr24, inv_keep)};
-    head_logits_hv(hv, w, bias, part, acc);
-  } else {
-    head_logits(h2 + (size_t)row * HK, w, bias, part, acc);
-  }
+  head_logits(h2 + (size_t)row * HK, w, bias, part, acc);
   float mx = acc[0];
 #pragma unroll
   for (int c = 1; c < HC; ++c) mx = acc[c] > mx ? acc[c] : mx;
@@ -202,24 +165,8 @@ head_fused_kernel(const float* __restrict__ h2, Fc2Slab fs, const float* __restr
 void launch_head_fused(const float* h2, const float* w, const float* bias, const int64_t* labels,
                        int B, const uint32_t* seed, uint32_t seed_v, uint32_t thr24,
                        float inv_keep, float* dlog, float* loss, float* dpre2, hipStream_t st) {
-  DDL_LAUNCH(head_fused_kernel<false>, dim3(B), dim3(256), 0, st, h2, Fc2Slab(), w, bias, labels,
-             B, 1.f / (float)B, seed, seed_v, thr24, inv_keep, dlog, loss, dpre2);
-}
-
-void launch_head_fused_slab(const float* slab, int S, int gx, int ntiles, const float* b2,
-                            float* h2, const float* w, const float* bias, const int64_t* labels,
-                            int B, const uint32_t* seed, uint32_t seed_v, uint32_t thr24,
-                            float inv_keep, float* dlog, float* loss, float* dpre2,
-                            hipStream_t st) {
-  Fc2Slab fs;
-  fs.slab = slab;
-  fs.S = S;
-  fs.gx = gx;
-  fs.zstride4 = ntiles * 256;
-  fs.bias = b2;
-  fs.h2 = h2;
-  DDL_LAUNCH(head_fused_kernel<true>, dim3(B), dim3(256), 0, st, nullptr, fs, w, bias, labels,
-             B, 1.f / (float)B, seed, seed_v, thr24, inv_keep, dlog, loss, dpre2);
+  DDL_LAUNCH(head_fused_kernel, dim3(B), dim3(256), 0, st, h2, w, bias, labels, B,
+             1.f / (float)B, seed, seed_v, thr24, inv_keep, dlog, loss, dpre2);
 }
 
 void launch_head_wgrad(const float* h2, const float* dlog, int B, float* gw, float* gb,

@@ -64,13 +64,6 @@ struct LinInfo {   // linear operand: element offset of (row, k = 0 + kk), valid
 // N = COUT, K = 25*CIN (k = tap*CIN + ci, tap = ky*5+kx).  Epilogue writes the pooled output
 // and a 1-byte code: argmax q, or 0xFF when the max is <= 0 (ReLU inactive => no gradient).
 // ---------------------------------------------------------------------------------------------
-// Image-major conv launches (conv1 / conv2 forward, conv2 data gradient) with XCD-contiguous
-// split-K numbering (gemm.h xcd_remap): each XCD's L2 then holds only its eighth of the images
-// instead of all of them (A/B knob).
-#ifndef DDL_XCD_IMG
-#define DDL_XCD_IMG 0
-#endif
-
 // KM: the K map (tap skipping, group-major rows) — on by default for the small maps (H <= 7);
 // the eval forward also takes it for conv2 (ConvFwd<14, 32, 64, true>: its border pool windows
 // skip 11 % of the taps, and at 10k images the group-major tiles keep their parallelism)
@@ -97,8 +90,6 @@ struct ConvFwd {
   // order spreads a tile's gathers over 32 images: 26.1 -> 26.6 us) keep the image-major
   // order m = b*RP + 4g + q.
   static constexpr bool KMAP = PADIN && KM;
-  static constexpr bool KFIX = true;  // kwin / kvlen host-callable: window-aware split-K (gemm.h)
-  static constexpr bool XCD_CONTIG = DDL_XCD_IMG && !KMAP;
   using KWin = TapWin;
   int M, N, K;
   const float* __restrict__ x;     // [B,H,H,CIN] (+ halo when PADIN)
@@ -183,7 +174,7 @@ struct ConvFwd {
     return a;
   }
   // the 16-byte gather of the halo-input forms (also the LDS-DMA source, gemm.h mainloop_dma)
-  static constexpr bool DMA = PADIN && DDL_LDSDMA_FWD;
+  static constexpr bool DMA = PADIN;
   DDL_DEV Gather16 srcA(const AInfo& a, int k0) const {
     const int tap = k0 / CIN, cib = k0 - tap * CIN;
     const int ky = tap / 5, kx = tap - ky * 5;
@@ -233,19 +224,6 @@ struct ConvFwd {
       const bool good = b.ok && k0 + b.kk < K;
       return bload4(r, good ? (b.off + k0 * COUT) * 4 : kOOB);
     }
-  }
-  // one weight (k0 + kk, n): the direct-fragment loop's B gather (gemm.h)
-  DDL_DEV float loadB1(const BInfo& b, int k0) const {
-    const brsrc_t r = make_rsrc(w, 25u * CIN * COUT * 4u);
-    if constexpr (PADIN) {
-      return bload1_so(r, b.ok ? b.off * 4 : kOOB, k0 * COUT * 4);
-    } else {
-      const bool good = b.ok && k0 + b.kk < K;
-      return bload1(r, good ? (b.off + k0 * COUT) * 4 : kOOB);
-    }
-  }
-  DDL_DEV float loadB1(const BInfo& b, int kv, const KWin& win) const {
-    return loadB1(b, kreal(win, kv));
   }
   // pooled output (halo layout when a conv reads it) and its pool code (no halo)
   DDL_DEV void store_pooled(int b, int py, int px, int n, float best, int arg) const {
@@ -330,8 +308,6 @@ struct ConvDgrad {
   // conv2 (14x14, 16 % of the taps in the halo) keeps m = (b*H + y)*H + x: the pixel-major
   // order made its dual launch 50.6 -> 58.4 us (gathers spread over 32 images per tile).
   static constexpr bool KMAP = H <= 7;
-  static constexpr bool KFIX = true;  // kwin / kvlen host-callable: window-aware split-K (gemm.h)
-  static constexpr bool XCD_CONTIG = DDL_XCD_IMG && !KMAP;
   using KWin = TapWin;
   int M, N, K;
   const float* __restrict__ dpre;        // [B,H+4,H+4,COUT] (halo)
@@ -378,8 +354,9 @@ struct ConvDgrad {
     row_pix(m < M ? m : 0, b, y, x);
     return {(((b * HI + y) * HI + x) * COUT + kk) * 4};
   }
-  // output gradient at (y - ky + 2, x - kx + 2) = halo pixel (y + 4 - ky, x + 4 - kx)
-  static constexpr bool DMA = DDL_LDSDMA_DGRAD;
+  // output gradient at (y - ky + 2, x - kx + 2) = halo pixel (y + 4 - ky, x + 4 - kx); the
+  // 16-byte gathers are the LDS-DMA sources of the 16x16x4 tile (CFG_MF16; on the 32x32x2 tile
+  // the data gradients stage through registers: DMA there measured slower inside the dual)
   DDL_DEV Gather16 srcA(const AInfo& a, int k0) const {
     const int tap = k0 / COUT, cob = k0 - tap * COUT;
     const int ky = tap / 5, kx = tap - ky * 5;
@@ -578,11 +555,6 @@ struct ConvWgrad {
 // A[m=(tap,ci)][k] = x[b, y+ky-2, x+kx-2, ci] = halo x[b, y+ky, x+kx, ci],
 // B[n=co][k] = halo dpre[b, y+2, x+2, co]; both MN-contiguous (ci / co innermost).
 // ---------------------------------------------------------------------------------------------
-#ifndef DDL_XCD_WGRAD
-#define DDL_XCD_WGRAD 0
-#endif
-constexpr bool XCD_WGRAD = DDL_XCD_WGRAD != 0;
-
 template <int H, int CIN, int COUT>
 struct ConvWgradBM {
   static constexpr bool A_KCONTIG = false;
@@ -602,9 +574,6 @@ struct ConvWgradBM {
   struct KWin {
     int y0, ny, x0, nx, rx;
   };
-  // split-K blocks numbered XCD-contiguous (gemm.h xcd_remap): the m-fastest neighbours are
-  // the taps of one K split, which read the same images' maps — one L2 instead of eight
-  static constexpr bool XCD_CONTIG = XCD_WGRAD;
   int M, N, K;                     // K = k_of(B)
   const float* __restrict__ x;     // [B,H+4,H+4,CIN]
   const float* __restrict__ dpre;  // [B,H+4,H+4,COUT]
@@ -660,10 +629,10 @@ struct ConvWgradBM {
     const int ky = tap / 5, kx = tap - ky * 5;
     return {m, (ky * HI + kx) * CIN + ci, kk, m + 3 < KW};
   }
-  // the 16-byte gathers (also the LDS-DMA sources, gemm.h mainloop_dma); A's ones row (the
-  // bias gradient) is not in memory: the group starting at row KW gathers zeros and its .x is
-  // patched — in registers by loadA, in the LDS image by the DMA loop (ones_group / ones_value)
-  static constexpr bool DMA = DDL_LDSDMA_WGRAD;
+  // the 16-byte gathers (also the LDS-DMA sources of the 16x16x4 tile, CFG_MF16); A's ones row
+  // (the bias gradient) is not in memory: the group starting at row KW gathers zeros and its .x
+  // is patched — in registers by loadA, in the LDS image by the DMA loop (ones_group /
+  // ones_value).  (LDS-DMA on the 32x32x2 tile measured neutral: registers staging kept.)
   DDL_DEV Gather16 srcA(const AInfo& a, int k0, const KWin& win) const {
     const int pos0 = (int)__umulhi((uint32_t)k0, mag);
     int y0, x0, y1, x1;
@@ -760,27 +729,7 @@ struct WgradAdam : P {
 // M = B, N = NOUT, K = KIN.  Dropout key derived on device from *seed (graph-replayable),
 // or from seed_v when no seed word is given (the native step runner: no seed-upload kernel).
 // ---------------------------------------------------------------------------------------------
-// Cache-policy flags of the fc policies for the in-launch hand-offs of the fused fc chain
-// (fc_chain.h): LSC1 = the activation operand (and any epilogue read of a handed-off buffer) is
-// loaded sc1, SSC1 = the epilogue stores write-through (sc1), so producer and consumer work
-// groups need no release / acquire fences (MI355X guide §6 Guideline 16, first table row).
-template <bool SC1>
-DDL_DEV float4 ld_op4(brsrc_t r, int off) {
-  if constexpr (SC1) return bload4_sc1(r, off);
-  else return bload4(r, off);
-}
-template <bool SC1>
-DDL_DEV void st_out(float* p, float v) {
-  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-template <bool SC1>
-DDL_DEV float ld_in(const float* p) {
-  if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else return *p;
-}
-
-template <bool RELU, bool LSC1 = false, bool SSC1 = false>
+template <bool RELU>
 struct FcFwd {
   static constexpr bool A_KCONTIG = true;
   static constexpr bool B_KCONTIG = false;
@@ -800,15 +749,13 @@ struct FcFwd {
   DDL_DEV AInfo prepA(int m, int kk) const { return {m * K + kk, kk, m < M}; }
   DDL_DEV float4 loadA(const AInfo& a, int k0) const {
     const brsrc_t r = make_rsrc(in, (uint32_t)M * K * 4u);
-    return ld_op4<LSC1>(r, a.ok && k0 + a.kk < K ? (a.off + k0) * 4 : kOOB);
+    return bload4(r, a.ok && k0 + a.kk < K ? (a.off + k0) * 4 : kOOB);
   }
   DDL_DEV BInfo prepB(int n, int kk) const { return {kk * N + n, kk, n < N}; }
   DDL_DEV float4 loadB(const BInfo& b, int k0) const {
     const brsrc_t r = make_rsrc(w, (uint32_t)K * N * 4u);
     return bload4(r, b.ok && k0 + b.kk < K ? (b.off + k0 * N) * 4 : kOOB);
   }
-  // (no loadB1: on the direct-fragment loop the fc forward's guarded gathers cost 24-36 more
-  // VGPRs than the LDS path — a wave per SIMD — and spilled in the 16-wave K-wave launch)
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
     const float bb = bias[n];
     uint32_t key = 0;
@@ -821,7 +768,7 @@ struct FcFwd {
       if (RELU) val = val > 0.f ? val : 0.f;
       const uint32_t idx = (uint32_t)(m * N + n);
       if (thr24) val = ddl_keep(key, idx, thr24) ? val * inv_keep : 0.f;
-      st_out<SSC1>(out + idx, val);
+      out[idx] = val;
     }
   }
 };
@@ -830,8 +777,7 @@ struct FcFwd {
 // W[i][o] (K-contig).  Epilogue variants:
 //   FcDgradAct  : previous layer was ReLU+dropout (fc1): dpre = hpost > 0 ? g/keep : 0
 //   FcDgradPool : previous layer was the conv4 max-pool (flatten of [B,2,2,256])
-template <bool LSC1 = false>
-struct FcDgradBaseT {
+struct FcDgradBase {
   static constexpr bool A_KCONTIG = true;
   static constexpr bool B_KCONTIG = true;
   int M, N, K;
@@ -842,7 +788,7 @@ struct FcDgradBaseT {
   DDL_DEV AInfo prepA(int m, int kk) const { return {m * K + kk, kk, m < M}; }
   DDL_DEV float4 loadA(const AInfo& a, int k0) const {
     const brsrc_t r = make_rsrc(dy, (uint32_t)M * K * 4u);
-    return ld_op4<LSC1>(r, a.ok && k0 + a.kk < K ? (a.off + k0) * 4 : kOOB);
+    return bload4(r, a.ok && k0 + a.kk < K ? (a.off + k0) * 4 : kOOB);
   }
   DDL_DEV BInfo prepB(int n, int kk) const { return {n * K + kk, kk, n < N}; }
   DDL_DEV float4 loadB(const BInfo& b, int k0) const {
@@ -851,10 +797,7 @@ struct FcDgradBaseT {
   }
 };
 
-using FcDgradBase = FcDgradBaseT<false>;
-
-template <bool LSC1 = false, bool SSC1 = false>
-struct FcDgradActT : FcDgradBaseT<LSC1> {
+struct FcDgradAct : FcDgradBase {
   const float* __restrict__ hpost;  // [B,N] post ReLU+dropout activation
   float inv_keep;
   float* __restrict__ dx;           // [B,N]
@@ -865,14 +808,13 @@ struct FcDgradActT : FcDgradBaseT<LSC1> {
       const int m = m0 + r;
       if (m >= M) break;
       const size_t o = (size_t)m * N + n;
-      st_out<SSC1>(dx + o, ld_in<LSC1>(hpost + o) > 0.f ? v[r] * inv_keep : 0.f);
+      dx[o] = hpost[o] > 0.f ? v[r] * inv_keep : 0.f;
     }
   }
 };
-using FcDgradAct = FcDgradActT<false, false>;
 
-template <int HP, int C, bool LSC1 = false>
-struct FcDgradPool : FcDgradBaseT<LSC1> {
+template <int HP, int C>
+struct FcDgradPool : FcDgradBase {
   static constexpr int HPREV = 2 * HP;
   const uint8_t* __restrict__ code;    // [B,HP,HP,C] == [B,N]
   float* __restrict__ dpre_prev;       // [B,HPREV,HPREV,C] + halo
@@ -891,8 +833,7 @@ struct FcDgradPool : FcDgradBaseT<LSC1> {
 };
 
 // fc weight gradient dW_aug[KIN+1, NOUT] = [X;1]^T dY (B2/B4/B6): M = KIN+1, N = NOUT, K = B.
-template <bool LSC1 = false>
-struct FcWgradT {
+struct FcWgrad {
   static constexpr bool A_KCONTIG = false;
   static constexpr bool B_KCONTIG = false;
   int M, N, K;
@@ -911,7 +852,7 @@ struct FcWgradT {
     const int k = k0 + a.kk;
     const bool kin = k < K;
     if ((KIN & 3) == 0) {  // group = all weight rows, or [ones row, 0, 0, 0] / zeros: branch-free
-      float4 v = ld_op4<LSC1>(r, (a.ok && kin) ? (k * KIN + a.off) * 4 : kOOB);
+      float4 v = bload4(r, (a.ok && kin) ? (k * KIN + a.off) * 4 : kOOB);
       if (a.off == KIN) v.x = kin ? 1.f : 0.f;
       return v;
     }
@@ -927,7 +868,7 @@ struct FcWgradT {
   DDL_DEV BInfo prepB(int n, int kk) const { return {kk * N + n, kk, n < N}; }
   DDL_DEV float4 loadB(const BInfo& b, int k0) const {
     const brsrc_t r = make_rsrc(dy, (uint32_t)K * N * 4u);
-    return ld_op4<LSC1>(r, b.ok && k0 + b.kk < K ? (b.off + k0 * N) * 4 : kOOB);
+    return bload4(r, b.ok && k0 + b.kk < K ? (b.off + k0 * N) * 4 : kOOB);
   }
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
 #pragma unroll
@@ -938,7 +879,6 @@ struct FcWgradT {
     }
   }
 };
-using FcWgrad = FcWgradT<false>;
 
 // ops the 16x16x4 LDS-DMA tile (CFG_MF16, gemm.h mainloop_dma16) is instantiated for: the
 // halo-layout convolutions, whose 16-byte gathers srcA / srcB are the DMA sources
@@ -954,11 +894,11 @@ struct Mf16OK<ConvWgradBM<H, CIN, COUT>> : std::true_type {};
 // ops the K-wave launch (gemm.h gemm_kwave_kernel, CFG_KWAVE) is instantiated for
 template <class P>
 struct KWaveOK : std::false_type {};
-template <bool R, bool L, bool S>
-struct KWaveOK<FcFwd<R, L, S>> : std::true_type {};
-template <bool L, bool S>
-struct KWaveOK<FcDgradActT<L, S>> : std::true_type {};
-template <int HP, int C, bool L>
-struct KWaveOK<FcDgradPool<HP, C, L>> : std::true_type {};
+template <bool R>
+struct KWaveOK<FcFwd<R>> : std::true_type {};
+template <>
+struct KWaveOK<FcDgradAct> : std::true_type {};
+template <int HP, int C>
+struct KWaveOK<FcDgradPool<HP, C>> : std::true_type {};
 
 }  // namespace ddl

@@ -90,10 +90,6 @@ RcclAsync::~RcclAsync() {
   if (gbuf_) (void)hipFree(gbuf_);
   if (ev_) (void)hipEventDestroy(ev_);
   if (cs_) (void)hipStreamDestroy(cs_);
-  if (locks_) {
-    munmap(locks_, lock_bytes_);
-    if (lock_owner_) shm_unlink(lock_name_.c_str());
-  }
 }
 
 void RcclAsync::init_comm(const char id_bytes[128]) {
@@ -106,26 +102,7 @@ void RcclAsync::init_comm(const char id_bytes[128]) {
 }
 
 void RcclAsync::attach_shm(const std::string& job, bool create) {
-  lock_name_ = "/" + job + "_rlock";
-  lock_bytes_ = (size_t)kXgmiMaxPeers * 64;  // one cache line per rank's lock word
-  int fd;
-  if (create) {
-    shm_unlink(lock_name_.c_str());
-    fd = shm_open(lock_name_.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
-    if (fd >= 0 && ftruncate(fd, (off_t)lock_bytes_) != 0) {
-      close(fd);
-      fd = -1;
-    }
-  } else {
-    fd = shm_open(lock_name_.c_str(), O_RDWR, 0600);
-  }
-  if (fd < 0) throw std::runtime_error("rccl async: shm_open failed: " + lock_name_);
-  void* p = mmap(nullptr, lock_bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-  close(fd);
-  if (p == MAP_FAILED) throw std::runtime_error("rccl async: mmap failed: " + lock_name_);
-  if (create) memset(p, 0, lock_bytes_);
-  locks_ = reinterpret_cast<uint64_t*>(p);
-  lock_owner_ = create;
+  locks_.attach("/" + job + "_rlock", kXgmiMaxPeers, create);
   // session mailboxes: every rank owns one (created by its owner before the job's barrier)
   box_name_ = "/" + job + "_rsess_";
 }
@@ -135,29 +112,6 @@ void RcclAsync::open_boxes(bool own) {
   else
     for (int r = 0; r < world_; ++r)
       if (r != rank_) boxes_[r] = std::make_unique<ShmMailbox>(box_name_ + std::to_string(r), 2, false);
-}
-
-uint64_t* RcclAsync::lock_word(int r) const { return locks_ + (size_t)r * 8; }
-
-bool RcclAsync::try_lock_pair(int h) {
-  const uint64_t tag = (uint64_t)rank_ + 1;
-  const int lo = std::min(rank_, h), hi = std::max(rank_, h);
-  uint64_t z = 0;
-  if (!__atomic_compare_exchange_n(lock_word(lo), &z, tag, false, __ATOMIC_ACQ_REL,
-                                   __ATOMIC_RELAXED))
-    return false;
-  z = 0;
-  if (lo != hi && !__atomic_compare_exchange_n(lock_word(hi), &z, tag, false, __ATOMIC_ACQ_REL,
-                                               __ATOMIC_RELAXED)) {
-    __atomic_store_n(lock_word(lo), 0, __ATOMIC_RELEASE);
-    return false;
-  }
-  return true;
-}
-
-void RcclAsync::unlock_pair(int h) {
-  __atomic_store_n(lock_word(std::max(rank_, h)), 0, __ATOMIC_RELEASE);
-  __atomic_store_n(lock_word(std::min(rank_, h)), 0, __ATOMIC_RELEASE);
 }
 
 AsyncPsState* RcclAsync::state_of(int p) {
@@ -227,7 +181,7 @@ bool RcclAsync::push_one(int p) {
     HIP_CHECK(hipStreamSynchronize(cs_));
     return true;
   }
-  if (!try_lock_pair(h)) return false;
+  if (!locks_.try_lock_pair(rank_, h)) return false;
   TraceRange r("ddl.async.rccl.push");
   try {
     if (!boxes_[h]->push(((int64_t)rank_ << 20) | p, 600.0))
@@ -238,10 +192,10 @@ bool RcclAsync::push_one(int p) {
     RCCL_CHECK(rccl().GroupEnd());
     HIP_CHECK(hipStreamSynchronize(cs_));
   } catch (...) {
-    unlock_pair(h);
+    locks_.unlock_pair(rank_, h);
     throw;
   }
-  unlock_pair(h);
+  locks_.unlock_pair(rank_, h);
   return true;
 }
 

@@ -307,7 +307,7 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
   // the remaining backward segments.
   {
     TraceRange r("ddl.fwd");
-    eng_->forward(x, B, seed, true, st, /*defer_fc=*/true);
+    eng_->forward(x, B, seed, true, st);
   }
   if (all_local_ && local_on_main_ && use_tail_ && tail_ok_ && opt_ == 0 && coef_ == 1.f) {
     // segment s-1's update rides in segment s's dual launch (flushed as a launch of its own

@@ -73,10 +73,14 @@ ShmMailbox::~ShmMailbox() {
 
 void ShmMailbox::unlink() { shm_unlink(name_.c_str()); }
 
+// The arrival queue is on the round trip of every async step (worker post -> PS service pop),
+// so an idle waiter stays on the CPU for a while before it sleeps: a sleep_for of a few
+// microseconds lasts ~50-80 us on Linux (timer slack), which the round trip would pay whenever
+// a token arrives just after the waiter dozed off.  Spin, then yield for ~2 ms, then sleep.
 static inline void backoff(int& spins) {
   if (spins < 64) {
     ++spins;
-  } else if (spins < 256) {
+  } else if (spins < 64 + 20000) {
     ++spins;
     std::this_thread::yield();
   } else {

@@ -95,16 +95,6 @@ class HipEngine:
         self.eng.set_concurrent(bool(on))
         self.graphs = None
 
-    def set_kfix(self, mask: int) -> None:
-        """Per-op bit mask (ops of csrc/kernels/api.h): window-aware split-K for the K-map conv
-        forwards / data gradients — one chunk length for every tile, the longest tap window
-        cut into splits[op] pieces."""
-        self.eng.set_kfix(int(mask))
-        self.graphs = None
-
-    def get_kfix(self) -> int:
-        return int(self.eng.get_kfix())
-
     def set_dual(self, on: bool) -> None:
         """Single stream: each layer's data- and weight-gradient GEMMs in one launch."""
         self.eng.set_dual(bool(on))
@@ -118,8 +108,7 @@ class HipEngine:
 
     # ---- step ----------------------------------------------------------------------------------
     def _eager(self, x, y, seed_t, on_segment):
-        # defer_fc: with the fused fc chain the fc forward runs inside segment 0's launch
-        self.eng.forward(x, seed_t, True, True)
+        self.eng.forward(x, seed_t, True)
         for s in range(len(self.segments)):
             self.eng.backward_segment(s, x, y, seed_t)
             if on_segment is not None:
@@ -137,7 +126,7 @@ class HipEngine:
                 # thread_local: RCCL's watchdog thread keeps polling events while we capture
                 with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
                     if s == 0:
-                        self.eng.forward(self.x_static, self.seed_static, True, True)
+                        self.eng.forward(self.x_static, self.seed_static, True)
                     self.eng.backward_segment(s, self.x_static, self.y_static, self.seed_static)
                 graphs.append(g)
         torch.cuda.current_stream().wait_stream(side)

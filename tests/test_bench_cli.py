@@ -51,8 +51,8 @@ def test_bench_single_process_json():
 def test_bench_torchrun_two_ranks_json(port):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-           "--steps", "2", "--warmup", "1", "--tta", "0"]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=_env())
+           "--steps", "2", "--warmup", "1", "--tta", "0.99", "--tta-steps", "2"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900, env=_env())
     assert r.returncode == 0, r.stderr[-2000:]
     recs = _json_lines(r.stdout)
     assert len(recs) == 1, r.stdout  # rank 0 only
@@ -67,6 +67,12 @@ def test_bench_torchrun_two_ranks_json(port):
     c = rec["plans"]["contiguous"]
     assert c["num_ps"] == 2 and c["ms_per_step"] > 0
     assert c["value"] == pytest.approx(2 * 100 / (c["ms_per_step"] / 1e3), rel=1e-3)
+    # data semantics are labelled: the throughput window's per-worker
+    # shards, and time to accuracy under both them and the reference's replicated batches
+    assert rec["config"]["data_sharding"] == "stride"
+    assert rec["time_to_acc"]["data_sharding"] == "stride"
+    assert rec["time_to_acc_replicate"]["data_sharding"] == "replicate"
+    assert rec["time_to_acc_replicate"]["steps_per_worker"] == 2
 
 
 @pytest.mark.slow

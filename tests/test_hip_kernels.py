@@ -127,37 +127,6 @@ def test_gradients_match_autograd(setup, B):
 
 
 @pytest.mark.parametrize("B", [100, 37])
-def test_fc_chain_matches_separate_launches(setup, B):
-    """The fused fc chain (csrc/kernels/fc_chain.h: fc1 fwd .. fc1 bwd as one persistent
-    work-queue launch) against the six separate launches: every gradient, h1 / h2, the loss
-    and the conv4 data gradient agree to fp32 summation-order noise, and no stage wait timed
-    out."""
-    eng, flat, params, grads, x, y = setup
-    x, y = x[:B].to(DEV), y[:B].to(DEV)
-    out = []
-    prev = eng.eng.fc_chain()
-    try:
-        for chain in (True, False):
-            eng.eng.set_fc_chain(chain)
-            grads.zero_()
-            eng.forward_backward(x, y, 0.5, 4321)
-            torch.cuda.synchronize()
-            out.append([grads.clone()] + [eng.eng.buffer(n, B).clone() for n in
-                                          ("h1", "h2", "loss", "d4")])
-    finally:
-        eng.eng.set_fc_chain(prev)
-    assert eng.eng.fc_chain_error() == 0
-    for t, a, b in zip(TENSORS, param_views(out[0][0], CANON_OFFSETS),
-                       param_views(out[1][0], CANON_OFFSETS)):
-        assert rel_err(a, b) < 1e-5, t.name
-    for a, b in zip(out[0][1:], out[1][1:]):
-        assert rel_err(a, b) < 1e-5
-    # dropout masks are the same bits: the zero patterns of h1 / h2 agree exactly
-    assert torch.equal(out[0][1] == 0, out[1][1] == 0)
-    assert torch.equal(out[0][2] == 0, out[1][2] == 0)
-
-
-@pytest.mark.parametrize("B", [100, 37])
 def test_conv1_direct_matches_gemm_path(setup, B):
     """conv1 forward on the direct LDS-staged kernel (csrc/kernels/conv1.hip) against the GEMM
     engine's ConvFwd<28, 1, 32> launch: pooled p1 to fp32 summation-order noise (the two
@@ -243,30 +212,6 @@ def test_conv1_direct_kernels_odd_batches(B):
         assert rel_err(out[0][0][o:o + t.numel], r64[t.index].reshape(-1)) < 5e-3, t.name
 
 
-@pytest.mark.parametrize("B", [100, 37])
-def test_head_slab_bit_identical(setup, B):
-    """fc2's split-K reduce folded into the fused head (head.hip head_fused_kernel<true>: the
-    head sums fc2's partial slab with the wide reduce's own association, adds the bias and
-    dropout, stores h2) gives the same bits as the reduce launch + head: every gradient, h2,
-    the loss and dlogits."""
-    eng, flat, params, grads, x, y = setup
-    x, y = x[:B].to(DEV), y[:B].to(DEV)
-    out = []
-    prev = eng.eng.head_slab()
-    try:
-        for on in (True, False):
-            eng.eng.set_head_slab(on)
-            grads.zero_()
-            eng.forward_backward(x, y, 0.5, 777)
-            torch.cuda.synchronize()
-            out.append([grads.clone()] + [eng.eng.buffer(n, B).clone() for n in
-                                          ("h2", "loss", "dlog")])
-    finally:
-        eng.eng.set_head_slab(prev)
-    for a, b in zip(out[0], out[1]):
-        assert torch.equal(a, b)
-
-
 def test_gradients_no_dropout(setup):
     eng, flat, params, grads, x, y = setup
     grads.zero_()
@@ -306,35 +251,6 @@ def test_split_k_variants_agree(setup):
             tol = 5e-5 if t.index > 7 else max(5e-3, 2 * e32 + 1e-6)
             err = rel_err(g[o:o + t.numel], ref)
             assert err < tol, (t.name, name, err, e32)
-
-
-@pytest.mark.parametrize("mul", [1, 2])
-def test_window_aware_split_matches(setup, mul):
-    """Window-aware split-K (one chunk length per launch, sized by the longest tap window) on
-    the K-map conv forwards / data gradients: same loss and gradients as the balanced split,
-    within fp32 summation-order noise, deterministic across reruns."""
-    eng, flat, params, grads, x, y = setup
-    base, kf = eng.get_splits(), eng.get_kfix()
-    grads.zero_()
-    eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 31)
-    torch.cuda.synchronize()
-    g0 = grads.clone()
-    ops = (2, 3, 10, 12)  # OP_CONV3_FWD, OP_CONV4_FWD, OP_CONV4_DGRAD, OP_CONV3_DGRAD
-    try:
-        eng.set_kfix(sum(1 << o for o in ops))
-        eng.set_splits([max(2, s * mul) if i in ops else s for i, s in enumerate(base)])
-        outs = []
-        for _ in range(2):
-            grads.zero_()
-            eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 31)
-            torch.cuda.synchronize()
-            outs.append(grads.clone())
-        assert torch.equal(outs[0], outs[1])
-        assert not torch.equal(outs[0], g0) or mul == 1  # the schedule really changed
-        check_grads(outs[0], flat, x, y, 0.5, 31)
-    finally:
-        eng.set_kfix(kf)
-        eng.set_splits(base)
 
 
 @pytest.mark.parametrize("cfg", [None, 0, 1, 2, 4, 5, 6, 7, 8])
@@ -494,10 +410,6 @@ def test_backward_modes_match(setup, conc, dual):
     """Single-stream dual launches, single-stream back-to-back and the two-stream backward
     compute the same (bitwise: same schedules, same reduction orders) gradients."""
     eng, flat, params, grads, x, y = setup
-    # (the separate fc launches on both sides: the two-stream mode has no fused fc chain, whose
-    # summation order differs — test_fc_chain_matches_separate_launches covers that one)
-    prev = eng.eng.fc_chain()
-    eng.eng.set_fc_chain(False)
     grads.zero_()
     eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 55)
     torch.cuda.synchronize()
@@ -512,7 +424,6 @@ def test_backward_modes_match(setup, conc, dual):
     finally:
         eng.set_concurrent(False)
         eng.set_dual(True)
-        eng.eng.set_fc_chain(prev)
 
 
 def test_graph_replay_matches_eager(setup):

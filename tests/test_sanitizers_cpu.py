@@ -29,3 +29,24 @@ def test_mailbox_asan_ubsan_stress(tmp_path):
                        env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("OK 80000 tokens")
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_async_session_locks_and_poster_asan_ubsan_stress(tmp_path):
+    """The round-3 host concurrency, factored into runtime/session.h and
+    used unchanged by kernels/rccl_async.hip (SessionLocks) and kernels/async_runner.hip
+    (PostQueue): 8 forked processes contending for exclusive sessions with the RcclAsync
+    serve-first loop, and the poster FIFO with out-of-order completions and an injected error —
+    no deadlock (every wait bounded), no lost or duplicated session, the pair-lock invariant
+    held for every served session, posts in push order."""
+    exe = str(tmp_path / "session_stress")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer",
+           "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+           os.path.join(RT, "session.cpp"), os.path.join(RT, "mailbox.cpp"),
+           os.path.join(RT, "tests", "session_stress.cpp"), "-o", exe, "-lrt", "-lpthread"]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([exe, "8", "20000"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("OK 160000 sessions, 8 processes")

@@ -102,3 +102,21 @@ def test_host_ranks_colocated():
     plan = make_plan("contiguous", 8)
     assert [plan.host_rank(p, 8) for p in range(8)] == list(range(8))
     assert [plan.host_rank(p, 2) for p in range(4)] == [0, 1, 0, 1]
+
+
+def test_replicated_bucket_is_the_last_backward_segments():
+    """the replicated (all-reduce / xGMI all-to-all) bucket of the native sync
+    exchange must be the one the LAST backward segment completes — conv1 + conv2, bucket 0 in
+    make_plan's min-tensor-id order — not the last index (the fc bucket, first to complete);
+    an unbucketed plan (no overlap) replicates its one bucket."""
+    from ddl_amd.models.layout import CANON_OFFSETS, TENSORS
+    from ddl_amd.parallel.native_exchange import last_segment_bucket
+    segs = [[8, 9, 10, 11, 12, 13], [6, 7], [4, 5], [0, 1, 2, 3]]  # HIP engine order
+    for W in (1, 2, 4, 8):
+        plan = make_plan("flat", W, buckets=segs)
+        b = last_segment_bucket(plan, segs)
+        lo, hi = plan.bucket_ranges[b]
+        assert sorted(plan.meta["buckets"][b]) == [0, 1, 2, 3]
+        assert hi - lo < 60000  # 52,160 parameters (+ padding to a multiple of 4 W)
+    plan = make_plan("flat", 2)
+    assert last_segment_bucket(plan, segs) == 0 and len(plan.bucket_ranges) == 1
