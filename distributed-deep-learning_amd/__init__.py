@@ -3,9 +3,11 @@
 Capabilities mirror epikjjh/DIstributed-Deep-Learning (six ``mnist_*`` variants:
 sync/async parameter servers, single/contiguous/greedy sharding), re-designed for
 MI355X: hand-written gfx950 HIP kernels for the CNN forward/backward and the fused
-TF1-Adam shard update, RCCL (``torch.distributed`` backend ``nccl``) over xGMI for
-gradient push / parameter pull, HIP graphs for the step, and a native shared-memory
-mailbox for the asynchronous control plane.
+TF1-Adam shard update, a C++ step runner that enqueues the whole training step on one
+stream (eager launches: replaying the step as a HIP graph measured slower, so graphs are
+opt-in), RCCL (``torch.distributed`` backend ``nccl``) or our own xGMI peer-memory kernels
+for gradient push / parameter pull, and a native shared-memory mailbox for the
+asynchronous control plane.
 
 Sub-packages:
   models/    layout table of the 14 tensors, the CNN (torch oracle + HIP engine)

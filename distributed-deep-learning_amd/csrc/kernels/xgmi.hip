@@ -113,8 +113,14 @@ DDL_DEV float4 scale4(float4 x, float a) {
 // what it reads from its inbox before it uses the slice and records error code 3 (and skips the
 // update) on a mismatch — a stale or torn inbox read is caught where it happens, per (bucket,
 // source, step), instead of as a parameter divergence steps later.
-DDL_DEV int ck_idx(int b, int src, int j) {
-  return 2 * kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices + arrive_idx(b, src, j);
+// The replicated bucket's checksum words carry the step parity like its inbox slots: a peer may
+// publish step e+1's checksum (its parity-(e+1) slot) while this rank still checks step e's —
+// with one word per (bucket, source, slice) the check of step e read step e+1's sum (error 3
+// in the W = 8 one-card test, where ranks drift a whole step apart).  Owner buckets need no
+// parity: a pusher writes an owner's inbox again only after that owner's DONE, i.e. after its
+// check.
+DDL_DEV int ck_idx(int b, int src, int j, int par = 0) {
+  return (2 + par) * kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices + arrive_idx(b, src, j);
 }
 DDL_DEV uint32_t bits4(float4 v) {
   return __float_as_uint(v.x) + __float_as_uint(v.y) + __float_as_uint(v.z) + __float_as_uint(v.w);
@@ -347,7 +353,7 @@ __global__ void __launch_bounds__(256) xgmi_repl_kernel(XgmiTable T, XgmiLaunch 
   if (a.check) {
     const uint32_t t = block_sum(cs, red);
     if (tid < W && tid != me)
-      __hip_atomic_store(T.flags[tid] + ck_idx(b, me, j), t, __ATOMIC_RELAXED,
+      __hip_atomic_store(T.flags[tid] + ck_idx(b, me, j, par), t, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
   }
   drain_vm();
@@ -365,7 +371,8 @@ __global__ void __launch_bounds__(256) xgmi_repl_kernel(XgmiTable T, XgmiLaunch 
   if (a.check && arrived) {
     bool ok = true;
     for (int q = 0; q < W; ++q)
-      if (q != me) ok &= check_piece(slot(me, q), 0, n4, myflags + ck_idx(b, q, j), a.err, red);
+      if (q != me)
+        ok &= check_piece(slot(me, q), 0, n4, myflags + ck_idx(b, q, j, par), a.err, red);
     if (!ok && tid == 0) arrived = 0;
     __syncthreads();
   }
@@ -447,8 +454,8 @@ PeerExchange::PeerExchange(float* params, const float* grads, int64_t total, int
   inbox_elems_ = inbox;
   X_CHECK(hipMalloc(&inbox_, inbox_elems_ * sizeof(float)));
   X_CHECK(hipMemset(inbox_, 0, inbox_elems_ * sizeof(float)));
-  // ARRIVE, DONE and (check mode) checksum words
-  flag_bytes_ = 3ull * kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices * sizeof(uint32_t);
+  // ARRIVE, DONE and (check mode) checksum words, the replicated bucket's in two parities
+  flag_bytes_ = 4ull * kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices * sizeof(uint32_t);
   X_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes_,
                                 hipDeviceMallocUncached));
   X_CHECK(hipMemset(flags_, 0, flag_bytes_));

@@ -14,6 +14,13 @@ from ddl_amd.utils.data import synthetic_mnist  # noqa: E402
 data = synthetic_mnist(n_train=5000, n_test=500)
 tr = Trainer(TrainConfig(mode="sync", shard="contiguous", steps=50, eval_every=0, engine="hip",
                          quiet=True), DistEnv(0, 1, 0, torch.device("cuda", 0)), dataset=data)
+if os.environ.get("DDL_PROBE_MF16") == "1":  # conv backward on CFG_MF16 (splits x2)
+    e = tr.engine.eng
+    cfg, spl = e.get_cfg(), e.get_splits()
+    for op in (10, 11, 12, 13, 14, 15):
+        cfg[op], spl[op] = 14, spl[op] * 2
+    e.set_cfg(cfg)
+    e.set_splits(spl)
 for i in range(int(os.environ.get("STEPS", "20"))):
     tr.train_step(i)
 torch.cuda.synchronize()
