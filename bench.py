@@ -151,6 +151,13 @@ def main(argv=None):
 
     def backend_of(t) -> str:
         ex = t.exchange
+        if getattr(t, "async_as_sync", False):
+            return "native-local (async W=1 as sync)"
+        if a.mode == "async":
+            if getattr(ex, "backend", "") != "xgmi":
+                return type(ex).__name__
+            return ("native-" if getattr(ex, "runner", None) is not None else "python-") + \
+                "xgmi-async"
         if not getattr(ex, "native", False):
             return "python"
         return "native-" + getattr(ex, "backend", "rccl")

@@ -356,7 +356,7 @@ class PyAsyncPeer {
 class PyAsyncService {
  public:
   // ps: list of (ps id, params, m, v | None, t)
-  PyAsyncService(PyAsyncPeer& peer, std::string mbox, int64_t world, py::list ps, int64_t opt,
+  PyAsyncService(PyAsyncPeer& peer, int64_t world, py::list ps, int64_t opt,
                  double lr, double b1, double b2, double eps, double mu, double scale,
                  int64_t epoch0, bool provenance) {
     std::vector<ddl::AsyncPsState> st;
@@ -381,7 +381,7 @@ class PyAsyncService {
       s.t = t[4].cast<int64_t>();
       st.push_back(s);
     }
-    svc_ = std::make_unique<ddl::AsyncService>(peer.raw(), mbox, (int)world, peer.device(), st,
+    svc_ = std::make_unique<ddl::AsyncService>(peer.raw(), (int)world, peer.device(), st,
                                                (int)opt, (float)lr, (float)b1, (float)b2,
                                                (float)eps, (float)mu, (float)scale,
                                                (uint32_t)epoch0, provenance);
@@ -487,13 +487,12 @@ class PyRcclAsync {
 class PyAsyncRunner {
  public:
   PyAsyncRunner(PyEngine& eng, PyAsyncPeer& peer, int64_t world, int64_t rank,
-                std::vector<int64_t> seg_of_ps, std::vector<int64_t> hosts,
-                std::vector<std::string> boxes, int64_t epoch0)
+                std::vector<int64_t> seg_of_ps, int64_t epoch0)
       : eng_(eng) {
-    std::vector<int> seg(seg_of_ps.begin(), seg_of_ps.end()), h(hosts.begin(), hosts.end());
+    std::vector<int> seg(seg_of_ps.begin(), seg_of_ps.end());
     c10::hip::HIPGuard guard(peer.device());
     r_ = std::make_unique<ddl::AsyncRunner>(eng.raw(), peer.raw(), (int)world, (int)rank,
-                                            peer.device(), seg, h, boxes, (uint32_t)epoch0);
+                                            peer.device(), seg, (uint32_t)epoch0);
   }
   void step(at::Tensor x, at::Tensor labels, int64_t seed, double timeout_s) {
     eng_.check_batch(x);
@@ -511,6 +510,7 @@ class PyAsyncRunner {
     r_->finish(timeout_s);
   }
   int64_t epoch() const { return r_->epoch(); }
+  void set_use_tail(bool on) { r_->set_use_tail(on); }
 
  private:
   PyEngine& eng_;
@@ -725,7 +725,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def(py::init<at::Tensor, at::Tensor, int64_t, int64_t, py::list, std::vector<int64_t>,
                     int64_t>(),
            py::arg("params"), py::arg("grads"), py::arg("world"), py::arg("rank"),
-           py::arg("ranges"), py::arg("hosts"), py::arg("max_slices") = 64)
+           py::arg("ranges"), py::arg("hosts"), py::arg("max_slices") = 512)
       .def("handle", &PyAsyncPeer::handle)
       .def("open", &PyAsyncPeer::open)
       .def("push_all", &PyAsyncPeer::push_all)
@@ -735,7 +735,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("error", &PyAsyncPeer::error);
 
   py::class_<PyAsyncService>(m, "AsyncService")
-      .def(py::init<PyAsyncPeer&, std::string, int64_t, py::list, int64_t, double, double, double,
+      .def(py::init<PyAsyncPeer&, int64_t, py::list, int64_t, double, double, double,
                     double, double, double, int64_t, bool>(),
            py::keep_alive<1, 2>())
       .def("start", &PyAsyncService::start)
@@ -763,14 +763,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("provenance", &PyRcclAsync::provenance);
 
   py::class_<PyAsyncRunner>(m, "AsyncRunner")
-      .def(py::init<PyEngine&, PyAsyncPeer&, int64_t, int64_t, std::vector<int64_t>,
-                    std::vector<int64_t>, std::vector<std::string>, int64_t>(),
+      .def(py::init<PyEngine&, PyAsyncPeer&, int64_t, int64_t, std::vector<int64_t>, int64_t>(),
            py::arg("engine"), py::arg("peer"), py::arg("world"), py::arg("rank"),
-           py::arg("seg_of_ps"), py::arg("hosts"), py::arg("boxes"), py::arg("epoch0"),
+           py::arg("seg_of_ps"), py::arg("epoch0"),
            py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
       .def("step", &PyAsyncRunner::step)
       .def("finish", &PyAsyncRunner::finish)
-      .def("epoch", &PyAsyncRunner::epoch);
+      .def("epoch", &PyAsyncRunner::epoch)
+      .def("set_use_tail", &PyAsyncRunner::set_use_tail);
 
   py::class_<PyPeer>(m, "PeerExchange")
       .def(py::init<at::Tensor, at::Tensor, int64_t, int64_t, py::list, int64_t, int64_t>(),

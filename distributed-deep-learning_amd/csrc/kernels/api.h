@@ -286,7 +286,7 @@ class PeerExchange {
 
 // ---- asynchronous PS over xGMI peer memory (xgmi_async.hip) ----------------------------------
 constexpr int kAsyncMaxPs = 64;
-constexpr int kAsyncMaxSlices = 64;
+constexpr int kAsyncMaxSlices = 512;
 struct AsyncShard {              // one PS's contiguous range of the flat buffer
   int64_t lo, n, slice, inbox_off;
   int host, nslice;
@@ -295,7 +295,8 @@ struct AsyncTable {
   float* params[kXgmiMaxPeers];  // every rank's worker parameter buffer (IPC-mapped)
   float* inbox[kXgmiMaxPeers];
   uint32_t* flags[kXgmiMaxPeers];
-  uint32_t* done;                // DONE[worker][ps] in host memory shared by all ranks
+  uint32_t* done;                // DONE[worker][ps][slice] in host memory shared by all ranks
+  uint32_t* posted;              // the arrival board POSTED[ps][worker][slice], same segment
   AsyncShard shard[kAsyncMaxPs];
 };
 
@@ -311,9 +312,16 @@ class AsyncPeer {
   void push_all(uint32_t epoch, float coef, hipStream_t st);
   // the same for the listed PS only (one launch)
   void push_set(const std::vector<int>& ps, uint32_t epoch, float coef, hipStream_t st);
-  // the DONE counters: a POSIX shm segment (created by one rank, attached by the others)
-  // registered with HIP, so every GPU bumps them and every host polls them directly
+  // the same push as tail blocks of another launch (tail.h kind 1, one block per arrival
+  // slice); false when the set does not fit a tail (more than kTailPieces shards)
+  bool push_tail(const std::vector<int>& ps, uint32_t epoch, UpdTail& out) const;
+  // the DONE counters and the arrival board: a POSIX shm segment (created by one rank,
+  // attached by the others) registered with HIP, so every GPU stores into them and every host
+  // polls them directly
   void attach_done(const std::string& name, bool create);
+  // PS host: has `worker` posted round `epoch` of PS `ps`?  next_slice: the caller's scan
+  // position (the first slice not yet seen posted; 0 for a new round)
+  bool posted(int ps, int worker, uint32_t epoch, int& next_slice) const;
   // worker host: wait until every PS has stored round `epoch`'s parameters here (false on
   // timeout or a recorded kernel error)
   bool wait_done(uint32_t epoch, double timeout_s);
@@ -325,10 +333,12 @@ class AsyncPeer {
   int num_ps() const { return nps_; }
 
  private:
+  void upload_table();           // table_ -> table_dev_ (set-up only: open, attach_done)
   float* params_;
   const float* grads_;
   int world_, rank_, nps_ = 0;
   AsyncTable table_;
+  AsyncTable* table_dev_ = nullptr;  // the kernels' copy
   float* inbox_ = nullptr;
   int64_t inbox_elems_ = 0;
   uint32_t* flags_ = nullptr;
@@ -337,6 +347,7 @@ class AsyncPeer {
   void* opened_[kXgmiMaxPeers][3] = {};
   bool opened_ok_ = false;
   uint32_t* done_host_ = nullptr;
+  uint32_t* posted_host_ = nullptr;
   size_t done_bytes_ = 0;
   std::string done_name_;
   bool done_owner_ = false;
@@ -352,11 +363,11 @@ struct AsyncPsState {            // one hosted PS as the service thread sees it
 
 class AsyncService {
  public:
-  AsyncService(AsyncPeer* peer, const std::string& mbox_name, int world, int device,
-               const std::vector<AsyncPsState>& ps, int opt, float lr, float b1, float b2,
-               float eps, float mu, float scale, uint32_t epoch0, bool provenance);
+  AsyncService(AsyncPeer* peer, int world, int device, const std::vector<AsyncPsState>& ps,
+               int opt, float lr, float b1, float b2, float eps, float mu, float scale,
+               uint32_t epoch0, bool provenance);
   ~AsyncService();
-  void start(int64_t expected);  // serve `expected` tokens on a native thread
+  void start(int64_t expected);  // serve `expected` pushes on a native thread
   void join();                   // rethrows the thread's error, if any
   // checkpoint hook: no apply is issued between pause() and resume(), and every issued one has
   // completed when pause() returns (the PS state is one consistent step); same caller thread
@@ -369,8 +380,8 @@ class AsyncService {
 
  private:
   void run();
+  void serve(AsyncPsState& st, int worker);
   AsyncPeer* peer_;
-  std::string mbox_name_;
   int world_, device_;
   std::vector<AsyncPsState> ps_;
   int opt_;
@@ -388,43 +399,30 @@ class AsyncService {
 
 // Native asynchronous worker step over the xGMI data plane (async_runner.hip): wait for the
 // previous round's parameters (host), forward, backward with each PS's gradient push launched
-// after the segment that completes its range, tokens posted by a poster thread once each push
-// has completed.
+// after the segment that completes its range (the push posts itself on the arrival board).
 class AsyncRunner {
  public:
   static constexpr int kSegments = 4;
-  // seg_of_ps[p]: backward segment after which PS p's range is complete; hosts[p]: its host
-  // rank; boxes[r]: arrival mailbox name of rank r ("" if it hosts no PS); epoch0: the round
+  // seg_of_ps[p]: backward segment after which PS p's range is complete; epoch0: the round
   // already completed (the set-up self-test)
   AsyncRunner(Engine* eng, AsyncPeer* peer, int world, int rank, int device,
-              const std::vector<int>& seg_of_ps, const std::vector<int>& hosts,
-              const std::vector<std::string>& boxes, uint32_t epoch0);
-  ~AsyncRunner();
+              const std::vector<int>& seg_of_ps, uint32_t epoch0);
   void step(const float* x, const int64_t* labels, int B, uint32_t seed, hipStream_t st,
             double timeout_s);
-  // the last round's parameters are back and every token has been posted
+  // the last round's parameters are back
   void finish(double timeout_s);
   uint32_t epoch() const { return epoch_; }
+  // pushes as tail blocks of the next segment's launch (default) or push kernels of their own
+  void set_use_tail(bool on) { use_tail_ = on; }
 
  private:
-  struct Posting {
-    hipEvent_t ev = nullptr;
-    std::vector<int> ps;
-  };
-  void wait_push(const Posting& job);   // poster thread: the push kernel has completed
-  void post_tokens(const Posting& job); // poster thread: its (worker, ps) tokens, PS order
   void wait_round(double timeout_s);
+  bool use_tail_ = true;
   Engine* eng_;
   AsyncPeer* peer_;
   int world_, rank_, device_;
   uint32_t epoch_, epoch0_;
   std::vector<int> seg_ps_[kSegments];
-  std::vector<int> hosts_;
-  std::unique_ptr<ShmMailbox> boxes_[kXgmiMaxPeers];
-  hipEvent_t ev_[kSegments] = {};
-  // the poster thread and its FIFO (runtime/session.h; CPU-stress-tested under ASan/UBSan);
-  // declared last: destroyed (joined) first, before the events it waits on
-  std::unique_ptr<PostQueue<Posting>> posts_;
 };
 
 // Asynchronous PS over point-to-point RCCL in exclusive sessions (rccl_async.hip): one

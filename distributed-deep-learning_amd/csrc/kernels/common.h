@@ -180,6 +180,20 @@ DDL_DEV float4 bload4_sc1(brsrc_t r, int byte_off) {
   return *reinterpret_cast<float4*>(&v);
 }
 
+// System-coherent (sc0 | sc1) 16-B store / load: data for another GPU (xGMI peer memory) or
+// the host.  A write-through store is counted complete (vmcnt) only once the memory side has
+// acknowledged it, so a drained wave's payload is globally visible before any flag it stores
+// next (guide G16 at system scope).
+DDL_DEV void bstore4_sys(brsrc_t r, int byte_off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
+                                         r, byte_off, 0, 1 | 16);
+}
+DDL_DEV float4 bload4_sys(brsrc_t r, int byte_off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 1 | 16);
+  return *reinterpret_cast<float4*>(&v);
+}
+DDL_DEV void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // 4-byte forms of the same pair (and plain 4-byte store / int load through a descriptor)
 DDL_DEV float bload1_sc1(brsrc_t r, int byte_off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 16));

@@ -207,7 +207,16 @@ void Engine::run_op(int op, const float* x, int B, const uint32_t* seed, bool tr
   }
 }
 
+// a push tail (tail.h kind 1) with no launch to ride in
+__global__ void __launch_bounds__(64) push_tail_kernel(UpdTail t) { tail_body(t, blockIdx.x); }
+
 void Engine::flush_tail(hipStream_t st) {
+  if (tail.kind == 1) {
+    if (tail.nblocks > 0)
+      hipLaunchKernelGGL(push_tail_kernel, dim3(tail.nblocks), dim3(64), 0, st, tail);
+    tail = UpdTail();
+    return;
+  }
   for (int i = 0; i < tail.npieces; ++i) {
     const UpdPiece& p = tail.p[i];
     launch_adam_c(p.w, p.g, p.m, p.v, p.n, p.lr_t, tail.c1, tail.c2, tail.eps, tail.scale, st);

@@ -51,6 +51,28 @@
 
 namespace ddl {
 
+// One push-tail block (tail.h kind 1): arrival slice j of piece P — the gradient slice into the
+// PS host's inbox (system write-through stores), then, once the wave's stores are
+// acknowledged, the slice's arrival flag at the host and its board word in host memory (the
+// protocol of xgmi_async.hip's push kernel; one wave, so vmcnt covers every lane's stores).
+DDL_DEV void push_tail_body(const UpdTail& t, const UpdPiece& P, int b) {
+  const int j = b - P.blk0;
+  if (j >= P.nslice) return;  // padding blocks of the last piece
+  const int lane = threadIdx.x & 63;
+  const int64_t n4 = P.n >> 2;
+  const int64_t s0 = (int64_t)j * P.slice4;
+  const int cnt = (int)((s0 + P.slice4 < n4 ? s0 + P.slice4 : n4) - s0);
+  const float4* src = reinterpret_cast<const float4*>(P.g) + s0;
+  const brsrc_t dst = make_rsrc(P.w + s0 * 4, (uint32_t)cnt * 16u);
+  for (int i = lane; i < cnt; i += 64) bstore4_sys(dst, i * 16, src[i]);
+  drain_vmem();
+  if (lane == 0) {
+    __hip_atomic_store(P.arrive + j, t.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    drain_vmem();
+    __hip_atomic_store(P.posted + j, t.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // One optimizer-tail block (tail.h): kTailF4PerLane float4 of one piece per lane, all loads
 // issued before any math (HBM-bound: memory-level parallelism is the whole game).
 DDL_DEV void tail_body(const UpdTail& t, int b) {
@@ -58,6 +80,10 @@ DDL_DEV void tail_body(const UpdTail& t, int b) {
 #pragma unroll
   for (int q = 1; q < kTailPieces; ++q)
     if (q < t.npieces && b >= t.p[q].blk0) i = q;
+  if (t.kind == 1) {
+    push_tail_body(t, t.p[i], b);
+    return;
+  }
   const UpdPiece& P = t.p[i];
   const int64_t n4 = P.n >> 2;
   const int64_t blk_base = (int64_t)(b - P.blk0) * t.f4_per_block + (threadIdx.x & 63);

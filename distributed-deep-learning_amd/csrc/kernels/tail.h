@@ -8,6 +8,11 @@
 // run as extra blocks of segment s+1's dual dgrad+wgrad launch: memory-bound blocks beside
 // MFMA-bound ones, hidden instead of serialised.  Only the last segment's (conv1 + conv2,
 // 52 k parameters) update remains a launch of its own.
+//
+// The asynchronous worker step (async_runner.hip) uses the same slot for its gradient PUSH
+// (kind 1): segment s's shards are stored into their PS hosts' inboxes and posted on the
+// arrival board by tail blocks of segment s+1's first launch instead of a push kernel of their
+// own on the compute stream (~5 us each, latency-bound).  One block per arrival slice.
 #pragma once
 #include <stdint.h>
 
@@ -18,18 +23,25 @@ constexpr int kTailF4PerLane = 2;  // float4 per lane per pass: keeps the tail p
 constexpr int kTailF4PerBlock = 64 * kTailF4PerLane;  // one-wave blocks
 
 struct UpdPiece {
-  float* w = nullptr;      // 16-B aligned, n % 4 == 0 (checked by the host)
-  const float* g = nullptr;
+  float* w = nullptr;      // 16-B aligned, n % 4 == 0 (checked by the host); push: the inbox slot
+  const float* g = nullptr;  // push: the gradient shard
   float* m = nullptr;
   float* v = nullptr;
   int64_t n = 0;           // elements
   float lr_t = 0.f;        // TF1 Adam step size of the owning PS
   int blk0 = 0;            // first tail block of this piece
+  // push (kind 1): slice j = block blk0 + j covers float4 [j * slice4, (j + 1) * slice4); its
+  // arrival flag arrive[j] (PS host's device flags) and board word posted[j] (host memory)
+  uint32_t* arrive = nullptr;
+  uint32_t* posted = nullptr;
+  int slice4 = 0, nslice = 0;
 };
 
 struct UpdTail {
   int nblocks = 0;         // tail blocks (multiple of 8: keeps the GEMM blocks' XCD mapping)
   int npieces = 0;
+  int kind = 0;            // 0: Adam update, 1: asynchronous gradient push (round `epoch`)
+  uint32_t epoch = 0;
   int first = 1;           // 1: tail blocks precede the GEMM blocks in the grid, 0: follow them
   int f4_per_block = kTailF4PerBlock;  // float4 per tail block (multiple of kTailF4PerBlock)
   UpdPiece p[kTailPieces];

@@ -7,24 +7,33 @@
 // parameters back to whoever sent.  Staleness is at most one step per worker.
 //
 // A worker round:
-//   push_all  (worker stream)  one kernel: every PS shard of the gradient -> that PS host's
-//             inbox slot [ps][worker] (system write-through stores), ARRIVE[ps][worker][slice] = e
-//             per workgroup at the host
-//   post      (worker host, after the push kernel completed) (worker, ps) tokens into each PS
-//             host's arrival mailbox
-//   apply     (PS host, its PS stream, issued by the host's service thread in arrival order)
-//             Adam on the PS's private parameter copy (one step of its counter t per arrival,
-//             atomic per shard: the reference's per-tag mixing race Q3 cannot happen), store
-//             the new shard into the WORKER's parameter buffer, then DONE[worker][ps][slice] = e
-//             per workgroup in host memory shared by all ranks (POSIX shm registered with HIP)
+//   push      (worker stream, after the backward segment that completes the listed PS ranges)
+//             one kernel: those PS shards of the gradient -> each PS host's inbox slot
+//             [ps][worker] (system write-through stores); per workgroup, once its payload is
+//             acknowledged: ARRIVE[ps][worker][slice] = e at the host (device flags, the apply's
+//             guard), then POSTED[ps][worker][slice] = e on the ARRIVAL BOARD in host memory
+//   serve     (PS host, a native service thread) scans the board of its hosted PS in host
+//             memory and issues one apply per (worker, ps) whose every slice is posted, in the
+//             order it observes them (the reference's MPI.ANY_SOURCE order)
+//   apply     (PS host, its PS stream) Adam on the PS's private parameter copy (one step of its
+//             counter t per arrival, atomic per shard: the reference's per-tag mixing race Q3
+//             cannot happen), store the new shard into the WORKER's parameter buffer, then
+//             DONE[worker][ps][slice] = e per workgroup in host memory
 //   wait      (worker host) polls DONE[me][*][*] >= e, then enqueues the next forward
+// Board and DONE words live in one POSIX shm segment registered with HIP by every rank (one
+// node: the xGMI hive).  The board replaced a token mailbox fed by a poster thread that waited
+// for each push's completion EVENT: a kernel with a completion signal ends with a system-scope
+// release (an L2 write-back) and left a ~4.6 us hole on the compute stream after every push,
+// plus two host hand-offs (poster -> mailbox -> service) on the critical path of the last push
+// (docs/DESIGN.md, round 4 async timeline).
 // NO kernel of this protocol waits for another kernel.  HIP multiplexes streams onto a few
 // hardware queues (GPU_MAX_HW_QUEUES), so a spinning kernel can sit in front of the very kernel
 // it waits for; with applies of many workers interleaving on every PS stream such a cycle is
-// reachable.  Here the apply is issued only after the push it reads has completed (the token is
-// posted after the push kernel's completion), and the worker's wait is on the host, so every
-// GPU queue only ever holds kernels that can run to completion.  The apply still checks the
-// arrival counter (bounded) as a guard, and records an error word instead of hanging.
+// reachable.  Here the apply is issued only after the host has seen the push it reads posted
+// (and the board word is stored after the ARRIVE flag is acknowledged), and the worker's wait
+// is on the host, so every GPU queue only ever holds kernels that can run to completion.  The
+// apply still checks the arrival flags (bounded) as a guard, and records an error word instead
+// of hanging.
 #include <fcntl.h>
 #include <stdlib.h>
 #include <string.h>
@@ -41,24 +50,12 @@
 #include "api.h"
 #include "trace.h"
 #include "common.h"
-#include "runtime/mailbox.h"
 
 namespace ddl {
 
 namespace {
 
-constexpr unsigned kSys = 1u | 16u;  // sc0 | sc1: system-coherent buffer op
-
-DDL_DEV void st4_sys(brsrc_t r, int byte_off, float4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(
-      __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), r, byte_off, 0,
-      kSys);
-}
-DDL_DEV float4 ld4_sys(brsrc_t r, int byte_off) {
-  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kSys);
-  return *reinterpret_cast<float4*>(&v);
-}
-DDL_DEV void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+DDL_DEV void drain_vm() { drain_vmem(); }
 
 DDL_DEV bool wait_ge(const uint32_t* f, uint32_t target, long long deadline, int* err, int code) {
   while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) <
@@ -93,10 +90,14 @@ DDL_DEV void flag_store(uint32_t* f, uint32_t v) {
 // arrival words of one rank: ARRIVE[ps][src][slice]; completion words DONE[worker][ps][slice]
 // in the shared host segment.  Every word has ONE writer and is only stored, never
 // read-modify-written (atomics through IPC / host mappings are not safe to combine)
-DDL_DEV int arrive_idx(int p, int src, int j) {
+__host__ __device__ inline int arrive_idx(int p, int src, int j) {
   return (p * kXgmiMaxPeers + src) * kAsyncMaxSlices + j;
 }
 DDL_DEV int done_word(int w, int p, int j) { return (w * kAsyncMaxPs + p) * kAsyncMaxSlices + j; }
+// arrival board POSTED[ps][worker][slice] (host memory, after the DONE words)
+__host__ __device__ inline size_t posted_word(int p, int w, int j) {
+  return ((size_t)p * kXgmiMaxPeers + w) * kAsyncMaxSlices + j;
+}
 
 struct PushArgs {
   int world, rank, nps;
@@ -108,7 +109,11 @@ struct PushArgs {
   float coef;
 };
 
-__global__ void __launch_bounds__(256) async_push_kernel(AsyncTable T, PushArgs a) {
+// The table (3 KB: 64 shard descriptors) is read from device memory, not passed by value: a
+// 3 KB kernel-argument block made every push / apply launch cost ~6-12 us of host time.
+__global__ void __launch_bounds__(256) async_push_kernel(const AsyncTable* __restrict__ Tp,
+                                                         PushArgs a) {
+  const AsyncTable& T = *Tp;
   const int blk = blockIdx.x, tid = threadIdx.x;
   int e = 0;
   while (e + 1 < a.nps && blk >= a.first_blk[e + 1]) ++e;
@@ -124,11 +129,16 @@ __global__ void __launch_bounds__(256) async_push_kernel(AsyncTable T, PushArgs 
   for (int i = tid; i < n4; i += 256) {
     float4 x = src[i];
     if (a.coef != 1.f) { x.x *= a.coef; x.y *= a.coef; x.z *= a.coef; x.w *= a.coef; }
-    st4_sys(dst, i * 16, x);
+    bstore4_sys(dst, i * 16, x);
   }
   drain_vm();
   __syncthreads();
-  if (tid == 0) flag_store(T.flags[S.host] + arrive_idx(p, a.rank, j), a.epoch);
+  if (tid == 0) {
+    flag_store(T.flags[S.host] + arrive_idx(p, a.rank, j), a.epoch);
+    drain_vm();  // the guard flag is acknowledged before the host can see the board word
+    __hip_atomic_store(T.posted + posted_word(p, a.rank, j), a.epoch, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 struct ApplyArgs {
@@ -143,7 +153,9 @@ struct ApplyArgs {
   long long timeout_ticks;
 };
 
-__global__ void __launch_bounds__(256) async_apply_kernel(AsyncTable T, ApplyArgs a) {
+__global__ void __launch_bounds__(256) async_apply_kernel(const AsyncTable* __restrict__ Tp,
+                                                          ApplyArgs a) {
+  const AsyncTable& T = *Tp;
   const long long deadline = wall_clock64() + a.timeout_ticks;
   const AsyncShard& S = T.shard[a.ps];
   const int j = blockIdx.x, tid = threadIdx.x;
@@ -165,7 +177,7 @@ __global__ void __launch_bounds__(256) async_apply_kernel(AsyncTable T, ApplyArg
   float4* m4 = reinterpret_cast<float4*>(a.m + s0);
   float4* v4 = a.v ? reinterpret_cast<float4*>(a.v + s0) : nullptr;
   for (int i = tid; i < n4; i += 256) {
-    const float4 g = ld4_sys(in, i * 16);
+    const float4 g = bload4_sys(in, i * 16);
     float4 w = w4[i];
     if (a.opt == 0) {
       float4 M = m4[i], V = v4[i];
@@ -185,7 +197,7 @@ __global__ void __launch_bounds__(256) async_apply_kernel(AsyncTable T, ApplyArg
       w = g;
     }
     w4[i] = w;
-    st4_sys(out, i * 16, w);
+    bstore4_sys(out, i * 16, w);
   }
   drain_vm();
   __syncthreads();
@@ -231,7 +243,10 @@ AsyncPeer::AsyncPeer(float* params, const float* grads, int64_t total, int world
     if (S.lo < 0 || S.n <= 0 || S.lo + S.n > total || S.n % 4 || S.lo % 4)
       throw std::invalid_argument("async xgmi: PS range must be a 4-aligned slice of the buffer");
     if (S.host < 0 || S.host >= world) throw std::invalid_argument("async xgmi: PS host");
-    int64_t ns = (S.n + 1023) / 1024;
+    // >= 2048 elements (8 KB) per workgroup, at most max_slices workgroups: a 1.6 M-element
+    // shard spreads over 512 workgroups (64 left the apply at ~2 TB/s, 41.6 us for the whole
+    // model at W = 1, profiles/r4_step_timeline_async_xgmi_w1.txt)
+    int64_t ns = (S.n + 2047) / 2048;
     if (ns > max_slices) ns = max_slices;
     S.slice = ((S.n + ns - 1) / ns + 3) & ~(int64_t)3;
     S.nslice = (int)((S.n + S.slice - 1) / S.slice);
@@ -255,6 +270,7 @@ AsyncPeer::AsyncPeer(float* params, const float* grads, int64_t total, int world
   X_CHECK(hipMemset(flags_, 0, flag_bytes));
   X_CHECK(hipHostMalloc(reinterpret_cast<void**>(&err_), 64, hipHostMallocDefault));
   memset(err_, 0, 64);
+  X_CHECK(hipMalloc(reinterpret_cast<void**>(&table_dev_), sizeof(AsyncTable)));
   X_CHECK(hipDeviceSynchronize());
   const char* t = getenv("DDL_XGMI_TIMEOUT_S");
   timeout_s_ = t ? atof(t) : 60.0;
@@ -269,6 +285,7 @@ AsyncPeer::~AsyncPeer() {
   if (inbox_) (void)hipFree(inbox_);
   if (flags_) (void)hipFree(flags_);
   if (err_) (void)hipHostFree(err_);
+  if (table_dev_) (void)hipFree(table_dev_);
   if (done_host_) {
     (void)hipHostUnregister(done_host_);
     munmap(done_host_, done_bytes_);
@@ -315,11 +332,17 @@ void AsyncPeer::open(const std::vector<std::string>& handles) {
     table_.inbox[q] = reinterpret_cast<float*>(ib);
     table_.flags[q] = reinterpret_cast<uint32_t*>(fl);
   }
+  upload_table();
   opened_ok_ = true;
 }
 
+void AsyncPeer::upload_table() {
+  X_CHECK(hipMemcpy(table_dev_, &table_, sizeof(AsyncTable), hipMemcpyHostToDevice));
+}
+
 void AsyncPeer::push_all(uint32_t epoch, float coef, hipStream_t st) {
-  if (!opened_ok_) throw std::runtime_error("async xgmi: open() first");
+  if (!opened_ok_ || !table_.posted)
+    throw std::runtime_error("async xgmi: open(), attach_done() first");
   PushArgs a;
   memset(&a, 0, sizeof(a));
   a.world = world_;
@@ -334,12 +357,13 @@ void AsyncPeer::push_all(uint32_t epoch, float coef, hipStream_t st) {
   a.first_blk[nps_] = blk;
   a.grads = grads_;
   a.coef = coef;
-  hipLaunchKernelGGL(async_push_kernel, dim3(blk), dim3(256), 0, st, table_, a);
+  hipLaunchKernelGGL(async_push_kernel, dim3(blk), dim3(256), 0, st, table_dev_, a);
   DDL_CHECK_LAUNCH();
 }
 
 void AsyncPeer::push_set(const std::vector<int>& ps, uint32_t epoch, float coef, hipStream_t st) {
-  if (!opened_ok_) throw std::runtime_error("async xgmi: open() first");
+  if (!opened_ok_ || !table_.posted)
+    throw std::runtime_error("async xgmi: open(), attach_done() first");
   if (ps.empty()) return;
   if ((int)ps.size() > kAsyncMaxPs) throw std::invalid_argument("async xgmi: PS list");
   PushArgs a;
@@ -359,12 +383,42 @@ void AsyncPeer::push_set(const std::vector<int>& ps, uint32_t epoch, float coef,
   a.grads = grads_;
   a.coef = coef;
   a.subset = 1;
-  DDL_LAUNCH(async_push_kernel, dim3(blk), dim3(256), 0, st, table_, a);
+  hipLaunchKernelGGL(async_push_kernel, dim3(blk), dim3(256), 0, st, table_dev_, a);
   DDL_CHECK_LAUNCH();
 }
 
+bool AsyncPeer::push_tail(const std::vector<int>& ps, uint32_t epoch, UpdTail& out) const {
+  if (!opened_ok_ || !table_.posted)
+    throw std::runtime_error("async xgmi: open(), attach_done() first");
+  if (ps.empty() || (int)ps.size() > kTailPieces) return false;
+  UpdTail t;
+  t.kind = 1;
+  t.epoch = epoch;
+  int blk = 0;
+  for (int p : ps) {
+    if (p < 0 || p >= nps_) throw std::invalid_argument("async xgmi: PS id");
+    const AsyncShard& S = table_.shard[p];
+    UpdPiece& q = t.p[t.npieces++];
+    q.g = grads_ + S.lo;
+    q.w = table_.inbox[S.host] + S.inbox_off + (int64_t)rank_ * S.n;
+    q.n = S.n;
+    q.arrive = table_.flags[S.host] + arrive_idx(p, rank_, 0);
+    q.posted = table_.posted + posted_word(p, rank_, 0);
+    q.slice4 = (int)(S.slice / 4);
+    q.nslice = S.nslice;
+    q.blk0 = blk;
+    blk += S.nslice;
+  }
+  t.nblocks = (blk + 7) & ~7;  // the GEMM blocks' XCD mapping (tail.h)
+  out = t;
+  return true;
+}
+
 void AsyncPeer::attach_done(const std::string& name, bool create) {
-  const size_t bytes = (size_t)world_ * kAsyncMaxPs * kAsyncMaxSlices * sizeof(uint32_t);
+  // DONE[worker][ps][slice] for every rank, then the board POSTED[ps][worker][slice]
+  const size_t done_words = (size_t)world_ * kAsyncMaxPs * kAsyncMaxSlices;
+  const size_t bytes =
+      (done_words + (size_t)kAsyncMaxPs * kXgmiMaxPeers * kAsyncMaxSlices) * sizeof(uint32_t);
   int fd = -1;
   if (create) {
     shm_unlink(name.c_str());  // stale segment of a crashed job
@@ -385,24 +439,43 @@ void AsyncPeer::attach_done(const std::string& name, bool create) {
   void* dp = nullptr;
   X_CHECK(hipHostGetDevicePointer(&dp, p, 0));
   done_host_ = reinterpret_cast<uint32_t*>(p);
+  posted_host_ = done_host_ + done_words;
   done_bytes_ = bytes;
   done_name_ = name;
   done_owner_ = create;
   table_.done = reinterpret_cast<uint32_t*>(dp);
+  table_.posted = table_.done + done_words;
+  upload_table();
+}
+
+bool AsyncPeer::posted(int ps, int worker, uint32_t epoch, int& next_slice) const {
+  const int n = table_.shard[ps].nslice;
+  while (next_slice < n) {
+    const uint32_t v = __atomic_load_n(posted_host_ + posted_word(ps, worker, next_slice),
+                                       __ATOMIC_ACQUIRE);
+    if ((int32_t)(v - epoch) < 0) return false;
+    ++next_slice;
+  }
+  return true;
 }
 
 bool AsyncPeer::wait_done(uint32_t epoch, double timeout_s) {
   if (!done_host_) throw std::runtime_error("async xgmi: attach_done() first");
   const auto t0 = std::chrono::steady_clock::now();
+  // the words complete roughly in PS order and never go back: resume the scan where the last
+  // poll stopped instead of re-reading every completed word (up to 64 x 512 of them)
+  int p = 0, j = 0;
   for (int spins = 0;; ++spins) {
-    bool all = true;
-    for (int p = 0; p < nps_ && all; ++p)
-      for (int j = 0; j < table_.shard[p].nslice && all; ++j) {
-        const uint32_t v = __atomic_load_n(
-            done_host_ + ((size_t)rank_ * kAsyncMaxPs + p) * kAsyncMaxSlices + j, __ATOMIC_ACQUIRE);
-        all = (int32_t)(v - epoch) >= 0;
+    while (p < nps_) {
+      const uint32_t v = __atomic_load_n(
+          done_host_ + ((size_t)rank_ * kAsyncMaxPs + p) * kAsyncMaxSlices + j, __ATOMIC_ACQUIRE);
+      if ((int32_t)(v - epoch) < 0) break;
+      if (++j == table_.shard[p].nslice) {
+        j = 0;
+        ++p;
       }
-    if (all) return true;
+    }
+    if (p == nps_) return true;
     if (error()) return false;
     if (spins > 256) {
       // (the worker's pull is on the step's critical path: yield for ~2 ms before sleeping —
@@ -443,25 +516,25 @@ void AsyncPeer::apply(int ps, int worker, uint32_t epoch, const XgmiUpdate& u, f
   a.scale = u.scale;
   a.err = err_;
   a.timeout_ticks = (long long)(timeout_s_ * 1e8);
-  hipLaunchKernelGGL(async_apply_kernel, dim3(table_.shard[ps].nslice), dim3(256), 0, st, table_,
-                     a);
+  hipLaunchKernelGGL(async_apply_kernel, dim3(table_.shard[ps].nslice), dim3(256), 0, st,
+                     table_dev_, a);
   DDL_CHECK_LAUNCH();
 }
 
 int AsyncPeer::error() const { return __atomic_load_n(err_, __ATOMIC_ACQUIRE); }
 
 // ---- the PS service loop in C++ -------------------------------------------------------------------
-// Pops (worker, ps) tokens from this host's arrival mailbox in order and enqueues one apply per
-// token on one PS stream; no Python, no GIL on the critical path of every remote worker's round.
-AsyncService::AsyncService(AsyncPeer* peer, const std::string& mbox_name, int world, int device,
+// Scans the arrival board of this host's PS and enqueues one apply per completed push on one PS
+// stream; no Python, no GIL, no hand-off thread on the critical path of any worker's round.
+AsyncService::AsyncService(AsyncPeer* peer, int world, int device,
                            const std::vector<AsyncPsState>& ps, int opt, float lr, float b1,
                            float b2, float eps, float mu, float scale, uint32_t epoch0,
                            bool provenance)
-    : peer_(peer), mbox_name_(mbox_name), world_(world), device_(device), ps_(ps), opt_(opt),
-      lr_(lr), b1_(b1), b2_(b2), eps_(eps), mu_(mu), scale_(scale), keep_prov_(provenance) {
+    : peer_(peer), world_(world), device_(device), ps_(ps), opt_(opt), lr_(lr), b1_(b1),
+      b2_(b2), eps_(eps), mu_(mu), scale_(scale), keep_prov_(provenance) {
   if (world < 1 || world > kXgmiMaxPeers) throw std::invalid_argument("async service: world");
   for (const auto& s : ps)
-    if (s.ps < 0 || s.ps >= kAsyncMaxPs || !s.params || !s.m || (opt == 0 && !s.v))
+    if (s.ps < 0 || s.ps >= peer->num_ps() || !s.params || !s.m || (opt == 0 && !s.v))
       throw std::invalid_argument("async service: PS state");
   epoch_.assign((size_t)world * kAsyncMaxPs, epoch0);
 }
@@ -479,46 +552,76 @@ void AsyncService::start(int64_t expected) {
   th_ = std::thread([this] { run(); });
 }
 
+void AsyncService::serve(AsyncPsState& st, int w) {
+  TraceRange apply_range("ddl.async.ps.apply");
+  const int p = st.ps;
+  std::lock_guard<std::mutex> hold(pause_mu_);  // pause(): no apply while a snapshot is taken
+  const uint32_t e = ++epoch_[(size_t)w * kAsyncMaxPs + p];
+  // one apply_gradients of this PS per arrival
+  const int64_t t = __atomic_add_fetch(&st.t, 1, __ATOMIC_ACQ_REL);
+  XgmiUpdate u;
+  u.opt = opt_;
+  u.m = st.m;
+  u.v = st.v;
+  // TF1 Adam: lr_t = lr * sqrt(1 - beta2^t) / (1 - beta1^t) (ops/adam.py adam_coeffs)
+  u.lr_t = (float)((double)lr_ * std::sqrt(1.0 - std::pow((double)b2_, (double)t)) /
+                   (1.0 - std::pow((double)b1_, (double)t)));
+  u.c1 = 1.f - b1_;
+  u.c2 = 1.f - b2_;
+  u.eps = eps_;
+  u.lr = lr_;
+  u.mu = mu_;
+  u.scale = scale_;
+  peer_->apply(p, w, e, u, st.params, stream_);
+  if (keep_prov_) prov_.push_back({(int64_t)w, (int64_t)p, (int64_t)e, t});
+  served_.fetch_add(1);
+}
+
 void AsyncService::run() {
   try {
     X_CHECK(hipSetDevice(device_));
-    ShmMailbox box(mbox_name_, 2, false);
-    for (int64_t k = 0; k < expected_; ++k) {
-      int64_t v;
-      {
-        TraceRange r("ddl.async.ps.wait_arrival");
-        v = box.pop(600.0);
+    const int np = (int)ps_.size();
+    const int pairs = np * world_;
+    // per (hosted PS, worker): the first slice of the next round not yet seen posted
+    std::vector<int> seen((size_t)pairs, 0);
+    int start = 0;  // round-robin: the scan resumes after the pair served last
+    int64_t k = 0;
+    auto idle_since = std::chrono::steady_clock::now();
+    TraceRange wait_range("ddl.async.ps.wait_arrival");
+    for (int spins = 0; k < expected_;) {
+      int hit = -1;
+      for (int i = 0; i < pairs && hit < 0; ++i) {
+        const int q = (start + i) % pairs;
+        AsyncPsState& st = ps_[q / world_];
+        const int w = q % world_;
+        const uint32_t next = epoch_[(size_t)w * kAsyncMaxPs + st.ps] + 1;
+        if (peer_->posted(st.ps, w, next, seen[q])) hit = q;
       }
-      if (v < 0) throw std::runtime_error("async PS: no arrival within 600 s");
-      TraceRange apply_range("ddl.async.ps.apply");
-      const int w = (int)(v >> 20), p = (int)(v & ((1 << 20) - 1));
-      AsyncPsState* st = nullptr;
-      for (auto& s : ps_)
-        if (s.ps == p) st = &s;
-      if (!st || w < 0 || w >= world_) throw std::runtime_error("async PS: bad token");
-      std::lock_guard<std::mutex> hold(pause_mu_);  // pause(): no apply while a snapshot is taken
-      const uint32_t e = ++epoch_[(size_t)w * kAsyncMaxPs + p];
-      // one apply_gradients of this PS per arrival
-      const int64_t t = __atomic_add_fetch(&st->t, 1, __ATOMIC_ACQ_REL);
-      XgmiUpdate u;
-      u.opt = opt_;
-      u.m = st->m;
-      u.v = st->v;
-      // TF1 Adam: lr_t = lr * sqrt(1 - beta2^t) / (1 - beta1^t) (ops/adam.py adam_coeffs)
-      u.lr_t = (float)((double)lr_ * std::sqrt(1.0 - std::pow((double)b2_, (double)t)) /
-                       (1.0 - std::pow((double)b1_, (double)t)));
-      u.c1 = 1.f - b1_;
-      u.c2 = 1.f - b2_;
-      u.eps = eps_;
-      u.lr = lr_;
-      u.mu = mu_;
-      u.scale = scale_;
-      peer_->apply(p, w, e, u, st->params, stream_);
-      if (keep_prov_) prov_.push_back({(int64_t)w, (int64_t)p, (int64_t)e, t});
-      served_.fetch_add(1);
-      if (const int err = peer_->error())
-        throw std::runtime_error("async PS: kernel wait timed out (code " + std::to_string(err) +
-                                 ")");
+      if (hit >= 0) {
+        serve(ps_[hit / world_], hit % world_);
+        seen[hit] = 0;
+        start = hit + 1;
+        ++k;
+        spins = 0;
+        idle_since = std::chrono::steady_clock::now();
+        if (const int err = peer_->error())
+          throw std::runtime_error("async PS: kernel wait timed out (code " +
+                                   std::to_string(err) + ")");
+        continue;
+      }
+      if (peer_->error())
+        throw std::runtime_error("async PS: kernel wait timed out (code " +
+                                 std::to_string(peer_->error()) + ")");
+      // an arrival is on some worker's critical path: yield (not sleep) for ~2 ms first
+      if (++spins < 20000) {
+        if (spins > 64) std::this_thread::yield();
+      } else {
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+      }
+      if ((spins & 255) == 0 &&
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - idle_since).count() >
+              600.0)
+        throw std::runtime_error("async PS: no arrival within 600 s");
     }
     X_CHECK(hipStreamSynchronize(stream_));
   } catch (const std::exception& ex) {

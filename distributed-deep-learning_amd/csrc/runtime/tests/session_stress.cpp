@@ -1,7 +1,7 @@
 // Host stress test of the async PS runtimes' concurrency (runtime/session.h), built with
 // -fsanitize=address,undefined by tests/test_sanitizers_cpu.py.
 //
-// 1. Exclusive sessions (kernels/rccl_async.hip protocol) between P forked processes: each runs
+// Exclusive sessions (kernels/rccl_async.hip protocol) between P forked processes: each runs
 //    the RcclAsync comm-thread loop shape — serve a pending request from its own mailbox first,
 //    else try to open a session to a random peer (all-or-nothing pair lock), post the request
 //    into the peer's mailbox and wait for the peer's acknowledgement, then release both locks.
@@ -9,9 +9,6 @@
 //    session.  Checks: every session is served exactly once by the right peer (per-pair counts),
 //    the lock invariant never breaks, and nobody waits past a deadline (a lock cycle or a lost
 //    request would show up as a timeout).
-// 2. PostQueue (kernels/async_runner.hip poster): jobs complete out of order on "device"
-//    threads, the poster posts them strictly in push order, finish() returns only when all are
-//    posted; an exception in a job's wait fails the following push() and finish().
 #include <sys/mman.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -113,71 +110,12 @@ int child(int r, int P, int N, const std::string& tag, Shared* sh) {
   }
 }
 
-int post_queue_test() {
-  struct Job {
-    int id = 0;
-    std::shared_ptr<std::atomic<int>> ready;
-  };
-  std::vector<int> posted;
-  std::mutex pm;
-  {
-    ddl::PostQueue<Job> q(
-        [](const Job& j) {
-          while (!j.ready->load(std::memory_order_acquire)) std::this_thread::yield();
-          if (j.ready->load() == 2) throw std::runtime_error("job failed");
-        },
-        [&](const Job& j) {
-          std::lock_guard<std::mutex> g(pm);
-          posted.push_back(j.id);
-        });
-    // device threads complete jobs in scrambled order
-    constexpr int K = 20000;
-    std::vector<Job> jobs(K);
-    for (int i = 0; i < K; ++i) jobs[i] = {i, std::make_shared<std::atomic<int>>(0)};
-    std::thread dev([&] {
-      std::mt19937 rng(7);
-      std::vector<int> order(K);
-      for (int i = 0; i < K; ++i) order[i] = i;
-      for (int i = 0; i < K; i += 64) std::shuffle(order.begin() + i, order.begin() + std::min(K, i + 64), rng);
-      for (int i : order) jobs[i].ready->store(1, std::memory_order_release);
-    });
-    for (int i = 0; i < K; ++i) q.push(jobs[i]);
-    q.finish();
-    dev.join();
-    if ((int)posted.size() != K) return 10;
-    for (int i = 0; i < K; ++i)
-      if (posted[i] != i) return 11;  // FIFO
-    // a failing job: the poster records it, later calls fail instead of hanging
-    Job bad{K, std::make_shared<std::atomic<int>>(2)};
-    q.push(bad);
-    bool threw = false;
-    try {
-      q.finish();
-    } catch (const std::exception&) {
-      threw = true;
-    }
-    if (!threw || q.error().empty()) return 12;
-    threw = false;
-    try {
-      q.push(Job{K + 1, std::make_shared<std::atomic<int>>(1)});
-    } catch (const std::exception&) {
-      threw = true;
-    }
-    if (!threw) return 13;
-  }
-  return 0;
-}
-
 }  // namespace
 
 int main(int argc, char** argv) {
   const int P = argc > 1 ? atoi(argv[1]) : 8;
   const int N = argc > 2 ? atoi(argv[2]) : 2000;
   if (P < 2 || P > kMaxP) return 2;
-  if (int rc = post_queue_test()) {
-    printf("FAIL post queue %d\n", rc);
-    return rc;
-  }
   const std::string tag = "ddl_sess_" + std::to_string(getpid());
   auto* sh = static_cast<Shared*>(mmap(nullptr, sizeof(Shared), PROT_READ | PROT_WRITE,
                                        MAP_SHARED | MAP_ANONYMOUS, -1, 0));
@@ -218,6 +156,6 @@ int main(int argc, char** argv) {
     printf("FAIL sessions %lld of %lld\n", (long long)total, (long long)P * N);
     return 1;
   }
-  printf("OK %lld sessions, %d processes, post queue FIFO\n", (long long)total, P);
+  printf("OK %lld sessions, %d processes\n", (long long)total, P);
   return 0;
 }

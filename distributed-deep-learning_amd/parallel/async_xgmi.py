@@ -7,16 +7,16 @@ applies Adam with its own step counter and Sends the parameters back to that wor
 
 MI355X design (no host staging, no RCCL pair communicators):
 
-* worker step: one ``push_all`` kernel stores every PS shard of the gradient into the PS
-  host's inbox slot for this worker (remote stores over xGMI); once it has completed the host
-  posts ``(worker, ps)`` tokens into each PS host's arrival mailbox (the ``ANY_SOURCE`` order,
-  ``parallel/mailbox.py``) and waits — like the reference's blocking Recv — until every PS
-  has stored the new parameters back (completion counters in host memory shared by all ranks);
-* PS host: a service thread pops tokens in arrival order and enqueues, on its PS stream, an
-  ``apply`` kernel: Adam on the PS's private copy (one step of its counter per arrival, atomic
-  per shard — fixing the reference's per-tag mixing race Q3), store the shard into the
-  worker's parameter buffer, bump the worker's completion counter.  The host never touches
-  the data.
+* worker step: push kernels store each PS shard of the gradient into the PS host's inbox
+  slot for this worker (remote stores over xGMI) and post every slice on the ARRIVAL BOARD in
+  host memory shared by all ranks; the worker then waits — like the reference's blocking
+  Recv — until every PS has stored the new parameters back (completion counters in the same
+  shared segment);
+* PS host: a native service thread scans the board and enqueues, on its PS stream, one
+  ``apply`` kernel per completed push in the order it sees them (the ``ANY_SOURCE`` order):
+  Adam on the PS's private copy (one step of its counter per arrival, atomic per shard —
+  fixing the reference's per-tag mixing race Q3), store the shard into the worker's parameter
+  buffer, bump the worker's completion counter.  The host never touches the data.
 
 No kernel waits for another kernel (the kernel file says why that matters: HIP multiplexes
 streams onto a few hardware queues), so no interleaving of workers and PS streams can
@@ -28,15 +28,12 @@ tested on a one-GPU box (``tests/test_xgmi_gpu.py``).
 from __future__ import annotations
 
 import contextlib
-import threading
 from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
 from ..ops import native
-from ..ops.adam import adam_coeffs
-from . import mailbox as mbox
 from .comm import DistEnv
 from .ps import ParameterServer
 from .sharding import ShardPlan
@@ -51,7 +48,7 @@ class AsyncPeerExchange:
 
     def __init__(self, plan: ShardPlan, env: DistEnv, params: torch.Tensor, grads: torch.Tensor,
                  servers: Dict[int, ParameterServer], steps_per_worker: int,
-                 grad_reduce: str = "sum", mailbox_kind: str = "auto", job_id: str = "ddl",
+                 grad_reduce: str = "sum", job_id: str = "ddl",
                  check_provenance: bool = False, optimizer: str = "adam"):
         if not params.is_cuda or not native.available():
             raise AsyncPeerUnavailable("async xGMI exchange needs the extension and a GPU")
@@ -117,22 +114,11 @@ class AsyncPeerExchange:
         self.peer = peer
         self._selftest(agree)
 
-        store = dist.distributed_c10d._get_default_store() if W > 1 else None
-        kind = mailbox_kind if W > 1 else "shm"
-        hosted = [p for p in range(P) if self.hosts[p] == r]
-        self.mailbox = (mbox.make_mailbox(kind, store, f"{job_id}_xmbox_{r}", owner=True)
-                        if hosted else None)
         if W > 1:
             dist.barrier()
-        self.boxes = {}
-        for h in set(self.hosts):
-            self.boxes[h] = self.mailbox if h == r else \
-                mbox.make_mailbox(kind, store, f"{job_id}_xmbox_{h}", owner=False)
         self.coef = 1.0
         self.timeout_s = 600.0
-        self._thread: Optional[threading.Thread] = None
         self._svc = None
-        self._error: Optional[BaseException] = None
         self.served = 0
         self.check_provenance = check_provenance
         self.provenance: List[Tuple[int, int, int, int]] = []
@@ -141,15 +127,13 @@ class AsyncPeerExchange:
     # -- the native worker step ----------------------------------------------------------------------
     def attach_runner(self, engine, segments) -> None:
         """Issue the worker step from C++ (csrc/kernels/async_runner.hip) — forward, the backward
-        segments with each PS's push launched as soon as its range is complete, tokens posted by
-        a native thread after each push completes, the previous round's pull as a host wait at
-        the start of the step — when the engine is the HIP one and every arrival mailbox is a
-        shared-memory ring (one host).  DDL_ASYNC_NATIVE=0 keeps the Python push_pull path."""
+        segments with each PS's push launched as soon as its range is complete (the push posts
+        itself on the arrival board), the previous round's pull as a host wait at the start of
+        the step — when the engine is the HIP one.  DDL_ASYNC_NATIVE=0 keeps the Python
+        push_pull path."""
         import os
         from ..models.layout import TENSORS
         if getattr(engine, "name", "") != "hip" or os.environ.get("DDL_ASYNC_NATIVE", "1") != "1":
-            return
-        if not all(isinstance(b, mbox.ShmMailbox) for b in self.boxes.values()):
             return
         seg_of = {t: s for s, ts in enumerate(segments) for t in ts}
         off = self.plan.tensor_offsets
@@ -157,10 +141,8 @@ class AsyncPeerExchange:
         for lo, hi in self.ranges:
             ts = [t.index for t in TENSORS if off[t.index] < hi and off[t.index] + t.numel > lo]
             seg_of_ps.append(max(seg_of[t] for t in ts))
-        W = self.env.world
-        boxes = [self.boxes[r].name if r in self.boxes else "" for r in range(W)]
-        self.runner = native.ops().AsyncRunner(engine.eng, self.peer, W, self.env.rank, seg_of_ps,
-                                               [int(h) for h in self.hosts], boxes, self.epoch)
+        self.runner = native.ops().AsyncRunner(engine.eng, self.peer, self.env.world,
+                                               self.env.rank, seg_of_ps, self.epoch)
 
     def native_step(self, engine, x, y, keep_prob: float, seed: int) -> None:
         engine._set_keep(keep_prob)
@@ -211,7 +193,6 @@ class AsyncPeerExchange:
         torch.cuda.synchronize(dev)
         agree(ok, why, "async xGMI self-test")
         self.epoch = 1                                   # worker rounds done
-        self.count = {(w, p): 1 for w in range(W) for p in range(len(self.ranges))}
 
     # -- PS service thread -------------------------------------------------------------------------
     def _expected(self) -> int:
@@ -219,53 +200,18 @@ class AsyncPeerExchange:
         return sum(1 for h in self.hosts if h == r) * W * self.steps
 
     def start(self) -> None:
+        """The service loop in C++ (xgmi_async.hip AsyncService): no Python and no GIL between
+        a remote worker's push and its apply kernel."""
         n = self._expected()
         if n == 0:
             return
-        if isinstance(self.mailbox, mbox.ShmMailbox):
-            # the service loop in C++ (xgmi_async.hip AsyncService): no Python and no GIL
-            # between a remote worker's token and its apply kernel
-            ps_list = [(p, ps.params, ps.m, ps.v, ps.t) for p, ps in self.servers.items()]
-            h = next(iter(self.servers.values())).h
-            mom = next(iter(self.servers.values())).momentum if self.mu is None else self.mu
-            self._svc = native.ops().AsyncService(
-                self.peer, self.mailbox.name, self.env.world, ps_list, self.opt, h.lr, h.beta1,
-                h.beta2, h.eps, mom, self.grad_scale, 1, self.check_provenance)
-            self._svc.start(n)
-            return
-        self._thread = threading.Thread(target=self._serve, name="ps-xgmi-service", daemon=True)
-        self._thread.start()
-
-    def _serve(self) -> None:
-        try:
-            dev = self.params.device
-            torch.cuda.set_device(dev)
-            for _ in range(self._expected()):
-                v = self.mailbox.pop(600.0)
-                if v is None:
-                    raise TimeoutError("async PS: no arrival within 600 s")
-                w, p = mbox.decode(v)
-                e = self.count[(w, p)] + 1
-                self.count[(w, p)] = e
-                ps = self.servers[p]
-                with ps.lock:  # paused(): no apply while a checkpoint snapshot is taken
-                    ps.begin()
-                    lr_t = adam_coeffs(ps.h, ps.t) if self.opt == 0 else 0.0
-                    with torch.cuda.stream(ps.stream):
-                        self.peer.apply(p, w, e, self.opt, ps.params, ps.m, ps.v, lr_t,
-                                        ps.h.beta1, ps.h.beta2, ps.h.eps, ps.h.lr,
-                                        ps.momentum if self.mu is None else self.mu,
-                                        self.grad_scale)
-                    t = ps.t
-                if self.check_provenance:
-                    self.provenance.append((w, p, e - 2, t))
-                self.served += 1
-                if self.peer.error():
-                    raise RuntimeError(f"async xGMI wait timed out (code {self.peer.error()})")
-            for p, ps in self.servers.items():
-                ps.stream.synchronize()
-        except BaseException as e:  # surfaced by join()
-            self._error = e
+        ps_list = [(p, ps.params, ps.m, ps.v, ps.t) for p, ps in self.servers.items()]
+        h = next(iter(self.servers.values())).h
+        mom = next(iter(self.servers.values())).momentum if self.mu is None else self.mu
+        self._svc = native.ops().AsyncService(
+            self.peer, self.env.world, ps_list, self.opt, h.lr, h.beta1, h.beta2, h.eps, mom,
+            self.grad_scale, 1, self.check_provenance)
+        self._svc.start(n)
 
     def _sync_counters(self, svc) -> None:
         """The native service advances each hosted PS's step counter; mirror it into the
@@ -280,20 +226,15 @@ class AsyncPeerExchange:
         """Checkpoint hook: no PS update is issued inside the block and every issued one has
         completed, so each hosted PS's parameters, m, v and t are one consistent step."""
         svc = self._svc
-        if svc is not None:
-            svc.pause()
-            try:
-                self._sync_counters(svc)
-                yield
-            finally:
-                svc.resume()
-            return
-        with contextlib.ExitStack() as held:
-            for ps in self.servers.values():
-                held.enter_context(ps.lock)
-                if ps._stream is not None:
-                    ps.stream.synchronize()
+        if svc is None:  # not started (or joined): no update in flight
             yield
+            return
+        svc.pause()
+        try:
+            self._sync_counters(svc)
+            yield
+        finally:
+            svc.resume()
 
     def join(self) -> None:
         self.drain_round()  # this worker's last round (the reference's final pull)
@@ -306,11 +247,6 @@ class AsyncPeerExchange:
                 self.served = svc.served()
                 if self.check_provenance:
                     self.provenance = [(w, p, e - 2, t) for (w, p, e, t) in svc.provenance()]
-        if self._thread is not None:
-            self._thread.join()
-            self._thread = None
-        if self._error is not None:
-            raise RuntimeError("async xGMI PS service failed") from self._error
         if self.peer.error():
             raise RuntimeError(f"async xGMI wait timed out (code {self.peer.error()})")
 
@@ -328,20 +264,13 @@ class AsyncPeerExchange:
 
     # -- worker side --------------------------------------------------------------------------------
     def push_pull(self) -> None:
-        """Push round e, post it once the push has completed, wait until every PS stored the
+        """Push round e (posted on the board by the kernel), wait until every PS stored the
         parameters back (host-side: the reference's blocking pull)."""
-        r = self.env.rank
         self.epoch += 1
         self.peer.push_all(self.epoch, self.coef)
-        ev = torch.cuda.Event()
-        ev.record()
-        ev.synchronize()
-        for p in range(len(self.ranges)):
-            self.boxes[self.hosts[p]].push(mbox.encode(r, p))
         if not self.peer.wait_done(self.epoch, self.timeout_s):
             raise RuntimeError(f"async xGMI: round {self.epoch} did not come back "
                                f"(kernel error code {self.peer.error()})")
 
     def close(self) -> None:
-        if self.mailbox is not None:
-            self.mailbox.close()
+        pass

@@ -34,7 +34,7 @@ from ..utils.tracing import trace_range
 from .comm import DistEnv, SyncExchange, AsyncExchange, init_distributed
 from .native_exchange import make_sync_exchange
 from .ps import ParameterServer
-from .sharding import make_plan
+from .sharding import make_plan, segment_aligned_num_ps
 
 
 def _job_id(env: DistEnv) -> str:
@@ -85,7 +85,17 @@ class Trainer:
         sync_step = cfg.mode == "sync" or self.async_as_sync
         buckets = segs if (cfg.shard == "flat" and cfg.overlap and sync_step) else None
         shard = "none" if cfg.mode == "single" else cfg.shard
-        self.plan = make_plan(shard, self.num_ps, buckets=buckets)
+        # Async flat plan: every PS range inside one backward segment, so each shard is pushed
+        # right after its segment and only the last segment's (52 K-element) shards remain on
+        # the step's critical path; needs a PS per segment (P a multiple of W with balanced
+        # hosts unless --num-ps sets it, sharding.segment_aligned_num_ps).
+        aligned = (asyncm and not self.async_as_sync and cfg.shard == "flat" and cfg.overlap
+                   and len(segs) > 1)
+        if aligned:
+            self.num_ps = cfg.num_ps or segment_aligned_num_ps(W, segs)
+            aligned = self.num_ps >= len(segs)
+            buckets = segs if aligned else None
+        self.plan = make_plan(shard, self.num_ps, buckets=buckets, segment_aligned=aligned)
         dev = env.device
         self.params = torch.zeros(self.plan.total, dtype=torch.float32, device=dev)
         self.grads = torch.zeros(self.plan.total, dtype=torch.float32, device=dev)

@@ -169,14 +169,99 @@ def _tensor_granular(policy: str, order: List[int], owner: List[int], num_ps: in
     return ShardPlan(policy, num_ps, seq, offsets, ranges, pos, owner=list(owner))
 
 
+def segment_ps_counts(sizes: Sequence[int], num_ps: int) -> List[int]:
+    """PS per group for a segment-aligned flat plan: at least one each, the rest by largest
+    remainder of the byte-proportional quota."""
+    g = len(sizes)
+    if num_ps < g:
+        raise ValueError(f"segment-aligned flat plan needs num_ps >= {g} groups, got {num_ps}")
+    tot = float(sum(sizes))
+    quota = [num_ps * s / tot for s in sizes]
+    k = [max(1, int(q)) for q in quota]
+    while sum(k) > num_ps:  # the minimum of one pushed the sum over: take from the largest
+        i = max((j for j in range(g) if k[j] > 1), key=lambda j: (k[j] - quota[j], k[j]))
+        k[i] -= 1
+    while sum(k) < num_ps:
+        i = max(range(g), key=lambda j: (quota[j] - k[j], sizes[j]))
+        k[i] += 1
+    return k
+
+
+def _segment_aligned_flat(num_ps: int, groups: Sequence[Sequence[int]]) -> ShardPlan:
+    """Flat plan whose every PS range lies inside ONE group of consecutive tensors (the
+    engine's backward segments): an asynchronous worker pushes a PS's shard as soon as its
+    segment's gradient exists, so no shard waits for the last segment unless it belongs to it.
+    Each group gets ``segment_ps_counts`` PS and is split into that many equal chunks."""
+    numel = [t.numel for t in TENSORS]
+    gs = [sorted(b) for b in sorted(groups, key=min)]
+    if sorted(i for b in gs for i in b) != list(range(NUM_TENSORS)):
+        raise ValueError("groups must partition the tensor ids")
+    sizes = [sum(padded(numel[i]) for i in b) for b in gs]
+    counts = segment_ps_counts(sizes, num_ps)
+    offsets = [0] * NUM_TENSORS
+    ranges: List[Tuple[int, int]] = []
+    pos = 0
+    for b, k in zip(gs, counts):
+        lo = pos
+        for i in b:
+            offsets[i] = pos
+            pos += padded(numel[i])
+        unit = k * FLAT_ALIGN
+        pos = lo + -(-(pos - lo) // unit) * unit
+        c = (pos - lo) // k
+        ranges += [(lo + j * c, lo + (j + 1) * c) for j in range(k)]
+    plan = ShardPlan("flat", num_ps, list(range(NUM_TENSORS)), offsets, ranges, pos)
+    plan.meta["segment_aligned"] = [len(b) for b in gs]
+    plan.meta["ps_per_group"] = counts
+    return plan
+
+
+def host_imbalance(plan: ShardPlan, world: int) -> float:
+    """max/mean elements per host process (PS p lives on rank p % world)."""
+    load = [0] * world
+    for p in range(plan.num_ps):
+        load[plan.host_rank(p, world)] += plan.shard_numel(p)
+    return max(load) / (sum(load) / world)
+
+
+def segment_aligned_num_ps(world: int, groups: Sequence[Sequence[int]],
+                           max_imbalance: float = 1.25) -> int:
+    """PS count of the async segment-aligned flat plan: the smallest multiple of ``world``
+    (every host serves the same number of PS) with a PS per group and per-host load within
+    ``max_imbalance`` (else the best of the first four multiples).  W=1: 4, W=2: 6, W=4: 8,
+    W=8: 8 with the HIP engine's four segments."""
+    best = None
+    for m in range(1, 5):
+        P = m * world
+        if P < len(groups):
+            continue
+        if P > 64:
+            break
+        imb = host_imbalance(_segment_aligned_flat(P, groups), world)
+        if imb <= max_imbalance:
+            return P
+        if best is None or imb < best[0]:
+            best = (imb, P)
+    if best is None:
+        raise ValueError(f"no PS count for {len(groups)} groups on {world} ranks")
+    return best[1]
+
+
 def make_plan(policy: str, num_ps: int,
-              buckets: Optional[Sequence[Sequence[int]]] = None) -> ShardPlan:
+              buckets: Optional[Sequence[Sequence[int]]] = None,
+              segment_aligned: bool = False) -> ShardPlan:
     """Build a plan.  ``buckets`` (flat policy only): groups of consecutive canonical
     tensor ids, each padded and split equally over the PSes, so that each bucket can be
-    reduce-scattered on its own as soon as backward has produced it."""
+    reduce-scattered on its own as soon as backward has produced it.  With
+    ``segment_aligned`` the groups are split over DIFFERENT PSes instead (one range per PS,
+    the asynchronous PS's layout, ``_segment_aligned_flat``)."""
     policy = policy.lower()
     if policy not in POLICIES:
         raise ValueError(f"unknown shard policy {policy!r}; choose from {POLICIES}")
+    if segment_aligned:
+        if policy != "flat" or buckets is None:
+            raise ValueError("segment_aligned applies to the flat policy with buckets")
+        return _segment_aligned_flat(num_ps, buckets)
     numel = [t.numel for t in TENSORS]
     if policy == "none":
         if num_ps != 1:

@@ -93,3 +93,29 @@ def test_async_eval_reports_the_same_accuracies(data):
         assert walls == sorted(walls)
     assert len(hist[0]) == 6
     assert hist[0] == hist[1]
+
+
+def test_async_xgmi_push_tails_match_push_kernels(data):
+    """W = 1 async over the xGMI data plane (segment-aligned flat plan: 4 PS): the gradient
+    pushes riding as tail blocks of the next segment's launch (default) and the stand-alone
+    push kernels deliver the same bytes, so the runs are bit-identical; and the async plane's
+    updates equal the local (sync-path) step's."""
+    runs = []
+    for tail in (True, False):
+        tr = _trainer(data, mode="async", shard="flat", steps=12, exchange_backend="xgmi")
+        assert tr.num_ps == 4 and tr.exchange.runner is not None
+        tr.exchange.runner.set_use_tail(tail)
+        s = tr.train()
+        assert s["steps"] == 12 and all(ps.t == 12 for ps in tr.servers.values())
+        torch.cuda.synchronize()
+        runs.append(tr)
+    assert torch.equal(runs[0].params, runs[1].params)
+    loc = _trainer(data, mode="async", shard="flat", steps=12)  # W = 1 local: the sync step
+    assert loc.async_as_sync
+    loc.train()
+    torch.cuda.synchronize()
+    for t in range(14):
+        lo, hi = runs[0].plan.tensor_extent(t)
+        lo2, hi2 = loc.plan.tensor_extent(t)
+        torch.testing.assert_close(runs[0].params[lo:hi], loc.params[lo2:hi2], rtol=1e-5,
+                                   atol=1e-6)

@@ -32,13 +32,13 @@ def test_mailbox_asan_ubsan_stress(tmp_path):
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
-def test_async_session_locks_and_poster_asan_ubsan_stress(tmp_path):
+def test_async_session_locks_asan_ubsan_stress(tmp_path):
     """The round-3 host concurrency, factored into runtime/session.h and
-    used unchanged by kernels/rccl_async.hip (SessionLocks) and kernels/async_runner.hip
-    (PostQueue): 8 forked processes contending for exclusive sessions with the RcclAsync
-    serve-first loop, and the poster FIFO with out-of-order completions and an injected error —
-    no deadlock (every wait bounded), no lost or duplicated session, the pair-lock invariant
-    held for every served session, posts in push order."""
+    used unchanged by kernels/rccl_async.hip (SessionLocks): 8 forked processes contending for
+    exclusive sessions with the RcclAsync serve-first loop — no deadlock (every wait bounded),
+    no lost or duplicated session, the pair-lock invariant held for every served session.
+    (The xGMI async runner's poster thread, also stressed here in round 4's first cut, was
+    replaced by the kernel-posted arrival board: kernels/xgmi_async.hip.)"""
     exe = str(tmp_path / "session_stress")
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer",
            "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",

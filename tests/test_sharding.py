@@ -3,7 +3,8 @@ import pytest
 
 from ddl_amd.models.layout import TENSORS, NUM_TENSORS, TOTAL_NUMEL, TOTAL_BYTES
 from ddl_amd.parallel.sharding import (make_plan, greedy_order, reference_route, balance_table,
-                                       contiguous_counts)
+                                       contiguous_counts, segment_aligned_num_ps, host_imbalance,
+                                       segment_ps_counts)
 
 
 def test_layout_constants():
@@ -120,3 +121,43 @@ def test_replicated_bucket_is_the_last_backward_segments():
         assert hi - lo < 60000  # 52,160 parameters (+ padding to a multiple of 4 W)
     plan = make_plan("flat", 2)
     assert last_segment_bucket(plan, segs) == 0 and len(plan.bucket_ranges) == 1
+
+
+SEGS = [list(range(8, 14)), [6, 7], [4, 5], [0, 1, 2, 3]]  # models.HIP_SEGMENTS
+
+
+@pytest.mark.parametrize("P", [4, 5, 6, 8, 16])
+def test_segment_aligned_flat_plan(P):
+    """Async flat plan: one range per PS, every range inside one backward segment, ranges
+    tile the buffer, 16-B aligned, every tensor inside its segment's ranges."""
+    plan = make_plan("flat", P, buckets=SEGS, segment_aligned=True)
+    assert plan.num_ps == P and len(plan.ps_ranges) == P
+    assert sum(plan.meta["ps_per_group"]) == P and min(plan.meta["ps_per_group"]) >= 1
+    pos = 0
+    for p in range(P):
+        lo, hi = plan.ps_segments(p)[0]
+        assert lo == pos and hi > lo and lo % 4 == 0 and (hi - lo) % 4 == 0
+        pos = hi
+        segs = {s for s, ts in enumerate(SEGS) for t in ts
+                if plan.tensor_offsets[t] < hi and plan.tensor_offsets[t] + TENSORS[t].numel > lo}
+        assert len(segs) == 1, (p, segs)
+    assert pos == plan.total
+    for t in TENSORS:
+        o = plan.tensor_offsets[t.index]
+        assert o % 64 == 0 and o + t.numel <= plan.total
+
+
+def test_segment_aligned_ps_counts():
+    """P is the smallest multiple of W with a PS per segment and per-host load within 1.25x
+    (the async critical path then carries only the last segment's 52 K-element shard)."""
+    got = {W: segment_aligned_num_ps(W, SEGS) for W in (1, 2, 3, 4, 8)}
+    assert got == {1: 4, 2: 6, 3: 9, 4: 8, 8: 8}
+    for W, P in got.items():
+        plan = make_plan("flat", P, buckets=SEGS, segment_aligned=True)
+        assert host_imbalance(plan, W) <= 1.25
+    assert segment_ps_counts([10, 10, 80], 3) == [1, 1, 1]
+    assert segment_ps_counts([10, 10, 80], 10) == [1, 1, 8]
+    with pytest.raises(ValueError):
+        make_plan("flat", 3, buckets=SEGS, segment_aligned=True)
+    with pytest.raises(ValueError):
+        make_plan("contiguous", 4, buckets=SEGS, segment_aligned=True)

@@ -74,6 +74,7 @@ def _rank(rank, world, port, outdir, kw):
         sys.path.insert(0, ROOT)
     kw = dict(kw)
     extra_env = kw.pop("_env", {})
+    kw.pop("_ps", None)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DDL_DIST_BACKEND="gloo",
                       DDL_XGMI_TIMEOUT_S="20")
@@ -179,6 +180,7 @@ def _async_rank(rank, world, port, outdir, kw):
         sys.path.insert(0, ROOT)
     kw = dict(kw)
     extra_env = kw.pop("_env", {})
+    kw.pop("_ps", None)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DDL_DIST_BACKEND="gloo",
                       DDL_XGMI_TIMEOUT_S="20")
@@ -220,6 +222,9 @@ def _async_rank(rank, world, port, outdir, kw):
     (4, dict(shard="greedy", num_ps=4)),         # mnist_async_sharding_greedy
     (3, dict(shard="contiguous", num_ps=5)),     # several PS per host
     (2, dict(shard="greedy", _env=dict(DDL_ASYNC_NATIVE="0"))),  # the Python push_pull path
+    # segment-aligned flat plans (sharding.segment_aligned_num_ps): 4 PS on one host, 6 on two
+    pytest.param(1, dict(shard="flat", _ps=4), id="1-flat"),
+    pytest.param(2, dict(shard="flat", _ps=6), id="2-flat"),
     pytest.param(8, dict(shard="contiguous", _env=dict(GPU_MAX_HW_QUEUES="1",
                                                        DDL_XGMI_TIMEOUT_S="60")), id="w8-contig"),
     pytest.param(8, dict(shard="greedy", _env=dict(GPU_MAX_HW_QUEUES="1",
@@ -234,7 +239,7 @@ def test_async_xgmi_serves_every_push(tmp_path, world, kw):
                  join=True)
     recs = [torch.load(os.path.join(tmp_path, f"rank{r}.pt")) for r in range(world)]
     n_ps = sum(len(rec["ps"]) for rec in recs)
-    assert n_ps == kw.get("num_ps", 1 if kw["shard"] == "none" else world)
+    assert n_ps == kw.get("_ps", kw.get("num_ps", 1 if kw["shard"] == "none" else world))
     for rec in recs:
         # every hosted PS applied exactly one update per push of every worker
         for p, (t, _) in rec["ps"].items():
