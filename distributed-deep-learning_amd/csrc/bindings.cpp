@@ -511,6 +511,7 @@ class PyAsyncRunner {
   }
   int64_t epoch() const { return r_->epoch(); }
   void set_use_tail(bool on) { r_->set_use_tail(on); }
+  void set_gate(bool on) { r_->set_gate(on); }
 
  private:
   PyEngine& eng_;
@@ -770,7 +771,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("step", &PyAsyncRunner::step)
       .def("finish", &PyAsyncRunner::finish)
       .def("epoch", &PyAsyncRunner::epoch)
-      .def("set_use_tail", &PyAsyncRunner::set_use_tail);
+      .def("set_use_tail", &PyAsyncRunner::set_use_tail)
+      .def("set_gate", &PyAsyncRunner::set_gate);
 
   py::class_<PyPeer>(m, "PeerExchange")
       .def(py::init<at::Tensor, at::Tensor, int64_t, int64_t, py::list, int64_t, int64_t>(),

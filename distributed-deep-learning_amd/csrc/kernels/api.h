@@ -325,6 +325,8 @@ class AsyncPeer {
   // worker host: wait until every PS has stored round `epoch`'s parameters here (false on
   // timeout or a recorded kernel error)
   bool wait_done(uint32_t epoch, double timeout_s);
+  // the same wait as one wave on stream `st` (the GPU-side pull gate, async_runner.hip)
+  void gate(uint32_t epoch, hipStream_t st);
   // PS host: apply worker `worker`'s round-`epoch` push to PS `ps` (private copy ps_params,
   // optimizer state in u) and store the new shard into that worker's parameter buffer
   void apply(int ps, int worker, uint32_t epoch, const XgmiUpdate& u, float* ps_params,
@@ -414,10 +416,15 @@ class AsyncRunner {
   uint32_t epoch() const { return epoch_; }
   // pushes as tail blocks of the next segment's launch (default) or push kernels of their own
   void set_use_tail(bool on) { use_tail_ = on; }
+  // the pull as a GPU-side gate before the next forward (default) or a host wait
+  void set_gate(bool on) { gate_ = on; }
 
  private:
   void wait_round(double timeout_s);
+  void check_round(uint32_t e, double timeout_s);
   bool use_tail_ = true;
+  bool gate_ = true;
+  uint32_t gated_ = 0;  // the round the last step's gate waits for (0: none)
   Engine* eng_;
   AsyncPeer* peer_;
   int world_, rank_, device_;

@@ -5,9 +5,19 @@
 // MPI Send per tensor to its PS, then a blocking Recv per tensor of the parameters that PS
 // sends back.  Here one C++ call per step:
 //
-//   1. wait (host, GIL released) until every PS has stored the PREVIOUS round's parameters
-//      into this worker's buffer — the reference's blocking pull, moved to just before the
-//      forward that reads them, so the Python loop never blocks between enqueues;
+//   1. the PREVIOUS round's parameters must be in this worker's buffer before the forward that
+//      reads them — the reference's blocking pull.  Default: a GPU-side gate, one wave enqueued
+//      on the compute stream after the round's last push, polling the round's DONE words; the
+//      forward behind it starts as soon as the last apply lands, with no host in between (the
+//      host wait + launch cost ~22 us of idle GPU per step, profiles/r4_async_host_latency.txt).
+//      The host only checks, bounded, the round before (failure detection).  set_gate(false):
+//      the host waits for the round itself before enqueuing the forward.
+//      Why the gate cannot deadlock: it blocks the compute stream's hardware queue until every
+//      PS has applied this worker's round.  Those applies run on other processes' queues or on
+//      this process's service stream, created with HIGH priority — HIP pools hardware queues
+//      per priority, so that stream never shares the gated queue — and each apply waits only
+//      for pushes that precede the gate in the compute queue (or come from other processes).
+//      No wait in the chain sits behind the gate.  And the gate is bounded (error word, no hang);
 //   2. forward, then the four backward segments; after segment s, one push kernel stores the
 //      gradient shards of every PS whose range is complete after s into their hosts' inboxes
 //      (the fc shards leave while the conv backward still computes) and posts each slice on
@@ -52,12 +62,25 @@ void AsyncRunner::wait_round(double timeout_s) {
                              std::to_string(peer_->error()) + ")");
 }
 
+void AsyncRunner::check_round(uint32_t e, double timeout_s) {
+  TraceRange r("ddl.async.worker.pull_check");
+  if (!peer_->wait_done(e, timeout_s))
+    throw std::runtime_error("async runner: round " + std::to_string(e) +
+                             " did not come back (kernel error code " +
+                             std::to_string(peer_->error()) + ")");
+}
+
 void AsyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t seed,
                        hipStream_t st, double timeout_s) {
   TraceRange step_range("ddl.async.step");
-  // (1) the previous round's parameters are in place (so every push of it has been applied:
-  // the gradient buffer is free to be overwritten)
-  wait_round(timeout_s);
+  // (1) the previous round's parameters are in place before the forward: the gate enqueued at
+  // the end of the previous step (the host checks the round before that: it ran before the
+  // previous forward, so in steady state this returns at once), or a host wait
+  if (gated_ != 0) {
+    if (gated_ - 1 != epoch0_) check_round(gated_ - 1, timeout_s);
+  } else {
+    wait_round(timeout_s);
+  }
   ++epoch_;
   eng_->seed_value = seed;
   {
@@ -84,6 +107,11 @@ void AsyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t se
     }
   }
   eng_->flush_tail(st);
+  gated_ = 0;
+  if (gate_) {
+    peer_->gate(epoch_, st);
+    gated_ = epoch_;
+  }
 }
 
 void AsyncRunner::finish(double timeout_s) { wait_round(timeout_s); }

@@ -94,6 +94,11 @@ __host__ __device__ inline int arrive_idx(int p, int src, int j) {
   return (p * kXgmiMaxPeers + src) * kAsyncMaxSlices + j;
 }
 DDL_DEV int done_word(int w, int p, int j) { return (w * kAsyncMaxPs + p) * kAsyncMaxSlices + j; }
+// the same completion words in the WORKER's uncached device flags (after its arrival words):
+// what the GPU-side pull gate polls.  A GPU polling the host-memory copy measured ~25 us late
+// (the registered host segment is not guaranteed to bypass the GPU's L2 for a system-scope load).
+constexpr int kArriveWords = kAsyncMaxPs * kXgmiMaxPeers * kAsyncMaxSlices;
+DDL_DEV int done_dev_idx(int p, int j) { return kArriveWords + p * kAsyncMaxSlices + j; }
 // arrival board POSTED[ps][worker][slice] (host memory, after the DONE words)
 __host__ __device__ inline size_t posted_word(int p, int w, int j) {
   return ((size_t)p * kXgmiMaxPeers + w) * kAsyncMaxSlices + j;
@@ -201,7 +206,35 @@ __global__ void __launch_bounds__(256) async_apply_kernel(const AsyncTable* __re
   }
   drain_vm();
   __syncthreads();
-  if (tid == 0) flag_store(T.done + done_word(a.worker, a.ps, j), a.epoch);
+  if (tid == 0) {
+    flag_store(T.flags[a.worker] + done_dev_idx(a.ps, j), a.epoch);  // the worker's gate
+    flag_store(T.done + done_word(a.worker, a.ps, j), a.epoch);       // the worker's host
+  }
+}
+
+// The worker's pull as a GPU-side gate (async_runner.hip): one wave on the compute stream,
+// enqueued after the round's last push and before the next forward, polls this worker's DONE
+// words of round `epoch` (every PS, every slice; the device copy in its own flags) and ends
+// when all have landed; the forward
+// behind it starts with no host round trip.  Bounded like every wait here: on timeout it records
+// error code 4 and ends (the host's lagged check raises).  Why this wait cannot deadlock is in
+// async_runner.hip (the applies it waits for run on other processes' queues or on this
+// process's high-priority service queue, never behind it).
+struct GateArgs {
+  int rank, nps;
+  uint32_t epoch;
+  int* err;
+  long long timeout_ticks;
+};
+
+__global__ void __launch_bounds__(64) async_gate_kernel(const AsyncTable* __restrict__ Tp,
+                                                        GateArgs a) {
+  const AsyncTable& T = *Tp;
+  const long long deadline = wall_clock64() + a.timeout_ticks;
+  const uint32_t* done = T.flags[a.rank];
+  for (int p = 0; p < a.nps; ++p)
+    for (int j = threadIdx.x; j < T.shard[p].nslice; j += 64)
+      if (!wait_ge(done + done_dev_idx(p, j), a.epoch, deadline, a.err, 4)) return;
 }
 
 #define X_CHECK(x)                                                                        \
@@ -264,7 +297,8 @@ AsyncPeer::AsyncPeer(float* params, const float* grads, int64_t total, int world
   inbox_elems_ = inbox > 0 ? inbox : 4;
   X_CHECK(hipMalloc(&inbox_, inbox_elems_ * sizeof(float)));
   X_CHECK(hipMemset(inbox_, 0, inbox_elems_ * sizeof(float)));
-  const size_t flag_bytes = (size_t)kAsyncMaxPs * kXgmiMaxPeers * kAsyncMaxSlices * sizeof(uint32_t);
+  const size_t flag_bytes =
+      ((size_t)kArriveWords + (size_t)kAsyncMaxPs * kAsyncMaxSlices) * sizeof(uint32_t);
   X_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes,
                                 hipDeviceMallocUncached));
   X_CHECK(hipMemset(flags_, 0, flag_bytes));
@@ -521,6 +555,18 @@ void AsyncPeer::apply(int ps, int worker, uint32_t epoch, const XgmiUpdate& u, f
   DDL_CHECK_LAUNCH();
 }
 
+void AsyncPeer::gate(uint32_t epoch, hipStream_t st) {
+  if (!opened_ok_ || !table_.done) throw std::runtime_error("async xgmi: open(), attach_done() first");
+  GateArgs a;
+  a.rank = rank_;
+  a.nps = nps_;
+  a.epoch = epoch;
+  a.err = err_;
+  a.timeout_ticks = (long long)(timeout_s_ * 1e8);
+  hipLaunchKernelGGL(async_gate_kernel, dim3(1), dim3(64), 0, st, table_dev_, a);
+  DDL_CHECK_LAUNCH();
+}
+
 int AsyncPeer::error() const { return __atomic_load_n(err_, __ATOMIC_ACQUIRE); }
 
 // ---- the PS service loop in C++ -------------------------------------------------------------------
@@ -547,7 +593,12 @@ AsyncService::~AsyncService() {
 void AsyncService::start(int64_t expected) {
   if (th_.joinable()) throw std::runtime_error("async service already running");
   X_CHECK(hipSetDevice(device_));
-  if (!stream_) X_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  // HIGH priority: HIP pools hardware queues per priority, so the applies never share a queue
+  // with the compute stream, where the worker's GPU-side pull gate may be waiting for them
+  // (async_runner.hip)
+  int lo = 0, hi = 0;
+  X_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  if (!stream_) X_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
   expected_ = expected;
   th_ = std::thread([this] { run(); });
 }
