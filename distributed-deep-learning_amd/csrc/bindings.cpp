@@ -605,6 +605,7 @@ class PyRunner {
   void set_scale(double grad_scale, double coef) { r_->set_scale((float)grad_scale, (float)coef); }
   void set_local_on_main(bool on) { r_->set_local_on_main(on); }
   void set_last_on_main(bool on) { r_->set_last_on_main(on); }
+  void set_ready_flags(int64_t mode) { r_->set_ready_flags((int)mode); }
   void set_use_tail(bool on) { r_->set_use_tail(on); }
   void set_final_in_reduce(bool on) { r_->set_final_in_reduce(on); }
   void set_tail_cfg(int64_t first, int64_t f4) { r_->set_tail_cfg((int)first, (int)f4); }
@@ -712,6 +713,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_local_on_main", &PyRunner::set_local_on_main)
       .def("set_last_on_main", &PyRunner::set_last_on_main)
       .def("set_use_tail", &PyRunner::set_use_tail)
+      .def("set_ready_flags", &PyRunner::set_ready_flags)
       .def("set_final_in_reduce", &PyRunner::set_final_in_reduce)
       .def("set_tail_cfg", &PyRunner::set_tail_cfg)
       .def("step", &PyRunner::step)

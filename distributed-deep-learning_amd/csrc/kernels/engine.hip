@@ -207,11 +207,11 @@ void Engine::run_op(int op, const float* x, int B, const uint32_t* seed, bool tr
   }
 }
 
-// a push tail (tail.h kind 1) with no launch to ride in
+// a push / ready-flag tail (tail.h kinds 1, 2) with no launch to ride in
 __global__ void __launch_bounds__(64) push_tail_kernel(UpdTail t) { tail_body(t, blockIdx.x); }
 
 void Engine::flush_tail(hipStream_t st) {
-  if (tail.kind == 1) {
+  if (tail.kind != 0) {
     if (tail.nblocks > 0)
       hipLaunchKernelGGL(push_tail_kernel, dim3(tail.nblocks), dim3(64), 0, st, tail);
     tail = UpdTail();

@@ -84,6 +84,11 @@ DDL_DEV void tail_body(const UpdTail& t, int b) {
     push_tail_body(t, t.p[i], b);
     return;
   }
+  if (t.kind == 2) {  // ready flag: the launch started, so every earlier launch has completed
+    if (b == 0 && (threadIdx.x & 63) == 0)
+      __hip_atomic_store(t.p[0].arrive, t.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   const UpdPiece& P = t.p[i];
   const int64_t n4 = P.n >> 2;
   const int64_t blk_base = (int64_t)(b - P.blk0) * t.f4_per_block + (threadIdx.x & 63);

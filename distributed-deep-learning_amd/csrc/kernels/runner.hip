@@ -364,10 +364,18 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
   for (int s = 0; s < kSegments; ++s) {
     const bool on_main = last_on_main_ && s == kSegments - 1;
     hipEvent_t ev = seg_xgmi_only_[s] ? seg_ev_dev_[s] : seg_ev_[s];
-    // the comm stream waits for this segment's gradients: bind the event to the segment's
-    // kernel launches themselves (the wait below is issued after the last one) rather than a
-    // marker packet behind them
-    const bool bind = ext_event_ && !on_main && seg_offstream_[s];
+    // xGMI-only segment followed by another: the hand-off to the comm stream is a READY flag
+    // stored by the next segment's first launch (tail.h kind 2) and a one-wave gate ahead of the
+    // bucket kernels on the comm stream — no event record / stream wait (each left ~5 us of
+    // idle compute stream: profiles/r4_step_timeline_forced_xgmi.txt).  The comm stream has
+    // high priority, so the gate never shares a hardware queue with the kernel it waits for;
+    // and it is bounded (error 5).
+    const bool flag = ready_flags_ > (s == 0 ? 1 : 0) && peer_ && !on_main &&
+                      seg_xgmi_only_[s] && s + 1 < kSegments;
+    // otherwise the comm stream waits for this segment's gradients by an event: bound to the
+    // segment's kernel launches themselves (the wait below is issued after the last one) rather
+    // than a marker packet behind them
+    const bool bind = ext_event_ && !on_main && seg_offstream_[s] && !flag;
     // bound to the segment's LAST launch (its count is learned from the previous step; a
     // wrong or unknown count falls back to a marker record below, which supersedes the binding)
     bool marker = !bind;
@@ -394,8 +402,21 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
         continue;
       }
       if (!waited) {
-        if (marker) HIP_CHECK(hipEventRecord(ev, st));
-        HIP_CHECK(hipStreamWaitEvent(cs_, ev, 0));
+        if (flag) {
+          eng_->flush_tail(st);  // (no update tail is pending at W > 1; keep the slot free)
+          UpdTail t;
+          t.kind = 2;
+          t.epoch = epoch_;
+          t.npieces = 1;
+          t.p[0].arrive = peer_->ready_flag(s);
+          t.nblocks = 8;
+          t.first = 1;
+          eng_->tail = t;
+          peer_->gate_ready(s, epoch_, cs_);
+        } else {
+          if (marker) HIP_CHECK(hipEventRecord(ev, st));
+          HIP_CHECK(hipStreamWaitEvent(cs_, ev, 0));
+        }
         waited = true;
       }
       if (u.kind == RunnerUnit::XGMI || u.kind == RunnerUnit::XGMI_REPL) {
@@ -412,6 +433,7 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
     }
     if (!reduces.empty()) issue_reduce_group(reduces, lr_t, xs);
   }
+  eng_->flush_tail(st);  // a READY flag no launch took (none in the tuned schedules)
   if (comm_used) {
     TraceRange r("ddl.exchange.join");
     // the next step's forward reads the updated parameters

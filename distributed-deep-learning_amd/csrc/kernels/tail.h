@@ -13,6 +13,12 @@
 // (kind 1): segment s's shards are stored into their PS hosts' inboxes and posted on the
 // arrival board by tail blocks of segment s+1's first launch instead of a push kernel of their
 // own on the compute stream (~5 us each, latency-bound).  One block per arrival slice.
+//
+// Kind 2 is a READY flag: the synchronous runner's xGMI bucket kernels on the comm stream wait
+// (behind a one-wave gate there) for segment s's gradients; block 0 of the tail stores
+// p[0].arrive[0] = epoch at the start of segment s+1's first launch, which the stream starts only
+// after every launch of segment s has completed.  It replaces an event record / stream wait
+// pair (~5 us of idle compute stream each, runner.hip).
 #pragma once
 #include <stdint.h>
 
@@ -40,7 +46,8 @@ struct UpdPiece {
 struct UpdTail {
   int nblocks = 0;         // tail blocks (multiple of 8: keeps the GEMM blocks' XCD mapping)
   int npieces = 0;
-  int kind = 0;            // 0: Adam update, 1: asynchronous gradient push (round `epoch`)
+  int kind = 0;            // 0: Adam update, 1: asynchronous gradient push (round `epoch`),
+                           // 2: ready flag (p[0].arrive[0] = epoch)
   uint32_t epoch = 0;
   int first = 1;           // 1: tail blocks precede the GEMM blocks in the grid, 0: follow them
   int f4_per_block = kTailF4PerBlock;  // float4 per tail block (multiple of kTailF4PerBlock)
