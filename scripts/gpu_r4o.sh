@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 R=$PWD
 timeout -k 10 700 python -u -m pytest tests/test_native_runner.py tests/test_xgmi_gpu.py -x -v -m gpu -p no:cacheprovider \
-    --timeout 240 --timeout-method thread -k "not async" > gpurun_out/r4o_tests.log 2>&1
+    --timeout 240 --timeout-method thread -k "not async or resume" > gpurun_out/r4o_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r4o_tests.log
 [ $rc -ne 0 ] && { grep -E "FAILED|Error" gpurun_out/r4o_tests.log | head; exit $rc; }
 timeout -k 10 300 python scripts/ready_ab.py > gpurun_out/r4o_ready_ab.log 2>&1 || { tail -20 gpurun_out/r4o_ready_ab.log; exit 1; }

@@ -167,3 +167,21 @@ def test_rccl_async_self_sessions_match_local(data):
     assert isinstance(rc.exchange, RcclAsyncExchange)
     assert torch.equal(loc.params, rc.params)
     assert rc.servers[0].t == loc.servers[0].t == 6
+
+
+@pytest.mark.parametrize("backend", ["rccl", "xgmi"])
+def test_async_resume_continues_exactly(tmp_path, data, backend):
+    """an async job (RCCL sessions / xGMI data plane, W = 1) checkpointed at
+    step 3 and resumed continues exactly: the native PS picks up the restored step counter
+    (RcclAsync.set_t / AsyncService built in start()), so parameters and t equal the
+    uninterrupted 6-step run's."""
+    full = _train_async(data, exchange_backend=backend)
+    ck = str(tmp_path / "ck")
+    part = _train_async(data, exchange_backend=backend, checkpoint_dir=ck, checkpoint_every=3,
+                        max_steps=3)
+    assert part.global_step == 3
+    res = _train_async(data, exchange_backend=backend, checkpoint_dir=ck, resume=True)
+    assert res.global_step == 6
+    assert all(s.t == 6 for s in res.servers.values())
+    assert all(s.t == f.t for s, f in zip(res.servers.values(), full.servers.values()))
+    assert torch.equal(res.params, full.params)
