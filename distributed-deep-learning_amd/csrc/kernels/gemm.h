@@ -53,8 +53,8 @@ namespace ddl {
 
 // One push-tail block (tail.h kind 1): arrival slice j of piece P — the gradient slice into the
 // PS host's inbox (system write-through stores), then, once the wave's stores are
-// acknowledged, the slice's arrival flag at the host and its board word in host memory (the
-// protocol of xgmi_async.hip's push kernel; one wave, so vmcnt covers every lane's stores).
+// acknowledged, the slice's word on the arrival board in host memory (the protocol of
+// xgmi_async.hip's push kernel; one wave, so vmcnt covers every lane's stores).
 DDL_DEV void push_tail_body(const UpdTail& t, const UpdPiece& P, int b) {
   const int j = b - P.blk0;
   if (j >= P.nslice) return;  // padding blocks of the last piece
@@ -66,11 +66,8 @@ DDL_DEV void push_tail_body(const UpdTail& t, const UpdPiece& P, int b) {
   const brsrc_t dst = make_rsrc(P.w + s0 * 4, (uint32_t)cnt * 16u);
   for (int i = lane; i < cnt; i += 64) bstore4_sys(dst, i * 16, src[i]);
   drain_vmem();
-  if (lane == 0) {
-    __hip_atomic_store(P.arrive + j, t.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    drain_vmem();
+  if (lane == 0)
     __hip_atomic_store(P.posted + j, t.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
 }
 
 // One optimizer-tail block (tail.h): kTailF4PerLane float4 of one piece per lane, all loads

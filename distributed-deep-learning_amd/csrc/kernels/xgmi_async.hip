@@ -7,18 +7,19 @@
 // parameters back to whoever sent.  Staleness is at most one step per worker.
 //
 // A worker round:
-//   push      (worker stream, after the backward segment that completes the listed PS ranges)
-//             one kernel: those PS shards of the gradient -> each PS host's inbox slot
-//             [ps][worker] (system write-through stores); per workgroup, once its payload is
-//             acknowledged: ARRIVE[ps][worker][slice] = e at the host (device flags, the apply's
-//             guard), then POSTED[ps][worker][slice] = e on the ARRIVAL BOARD in host memory
+//   push      (worker stream, after the backward segment that completes the listed PS ranges;
+//             tail blocks of the next segment's launch, async_runner.hip) those PS shards of the
+//             gradient -> each PS host's inbox slot [ps][worker] (system write-through stores);
+//             per workgroup, once its payload is acknowledged, POSTED[ps][worker][slice] = e on
+//             the ARRIVAL BOARD in host memory
 //   serve     (PS host, a native service thread) scans the board of its hosted PS in host
 //             memory and issues one apply per (worker, ps) whose every slice is posted, in the
 //             order it observes them (the reference's MPI.ANY_SOURCE order)
 //   apply     (PS host, its PS stream) Adam on the PS's private parameter copy (one step of its
 //             counter t per arrival, atomic per shard: the reference's per-tag mixing race Q3
 //             cannot happen), store the new shard into the WORKER's parameter buffer, then
-//             DONE[worker][ps][slice] = e per workgroup in host memory
+//             DONE[ps][slice] = e in the worker's device flags (its GPU-side pull gate) and
+//             DONE[worker][ps][slice] = e in host memory (its host's bounded check)
 //   wait      (worker host) polls DONE[me][*][*] >= e, then enqueues the next forward
 // Board and DONE words live in one POSIX shm segment registered with HIP by every rank (one
 // node: the xGMI hive).  The board replaced a token mailbox fed by a poster thread that waited
@@ -87,22 +88,17 @@ DDL_DEV void flag_store(uint32_t* f, uint32_t v) {
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// arrival words of one rank: ARRIVE[ps][src][slice]; completion words DONE[worker][ps][slice]
-// in the shared host segment.  Every word has ONE writer and is only stored, never
+// completion words DONE[worker][ps][slice] in the shared host segment, then the arrival board
+// POSTED[ps][worker][slice].  Every word has ONE writer and is only stored, never
 // read-modify-written (atomics through IPC / host mappings are not safe to combine)
-__host__ __device__ inline int arrive_idx(int p, int src, int j) {
-  return (p * kXgmiMaxPeers + src) * kAsyncMaxSlices + j;
-}
 DDL_DEV int done_word(int w, int p, int j) { return (w * kAsyncMaxPs + p) * kAsyncMaxSlices + j; }
-// the same completion words in the WORKER's uncached device flags (after its arrival words):
-// what the GPU-side pull gate polls.  A GPU polling the host-memory copy measured ~25 us late
-// (the registered host segment is not guaranteed to bypass the GPU's L2 for a system-scope load).
-constexpr int kArriveWords = kAsyncMaxPs * kXgmiMaxPeers * kAsyncMaxSlices;
-DDL_DEV int done_dev_idx(int p, int j) { return kArriveWords + p * kAsyncMaxSlices + j; }
-// arrival board POSTED[ps][worker][slice] (host memory, after the DONE words)
 __host__ __device__ inline size_t posted_word(int p, int w, int j) {
   return ((size_t)p * kXgmiMaxPeers + w) * kAsyncMaxSlices + j;
 }
+// the same completion words in the WORKER's uncached device flags DONE[ps][slice]: what its
+// GPU-side pull gate polls (a GPU polling the host-memory copy measured ~25 us late: the
+// registered host segment is not guaranteed to bypass the GPU's L2 for a system-scope load)
+DDL_DEV int done_dev_idx(int p, int j) { return p * kAsyncMaxSlices + j; }
 
 struct PushArgs {
   int world, rank, nps;
@@ -138,12 +134,9 @@ __global__ void __launch_bounds__(256) async_push_kernel(const AsyncTable* __res
   }
   drain_vm();
   __syncthreads();
-  if (tid == 0) {
-    flag_store(T.flags[S.host] + arrive_idx(p, a.rank, j), a.epoch);
-    drain_vm();  // the guard flag is acknowledged before the host can see the board word
+  if (tid == 0)
     __hip_atomic_store(T.posted + posted_word(p, a.rank, j), a.epoch, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
-  }
 }
 
 struct ApplyArgs {
@@ -154,27 +147,19 @@ struct ApplyArgs {
   float* v;
   int opt;
   float lr_t, c1, c2, eps, lr, mu, scale;
-  int* err;
-  long long timeout_ticks;
 };
 
 __global__ void __launch_bounds__(256) async_apply_kernel(const AsyncTable* __restrict__ Tp,
                                                           ApplyArgs a) {
   const AsyncTable& T = *Tp;
-  const long long deadline = wall_clock64() + a.timeout_ticks;
   const AsyncShard& S = T.shard[a.ps];
   const int j = blockIdx.x, tid = threadIdx.x;
-  // a failed wait (timeout / recorded error) leaves the PS state untouched: applying a stale
-  // inbox slot would advance m / v with the wrong gradient; DONE is still stored (the worker
-  // host then sees the error word instead of waiting out its own timeout)
-  __shared__ int arrived;
-  if (tid == 0)
-    arrived = wait_ge(T.flags[a.me] + arrive_idx(a.ps, a.worker, j), a.epoch, deadline, a.err, 1);
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // keep the loads below the poll
+  // no arrival poll: the service issues this apply only after it saw every slice of the push
+  // posted on the board, and a push block stores its board word only after its payload stores
+  // were acknowledged (the inbox loads below are system-coherent, so they see that payload)
   const int64_t s0 = (int64_t)j * S.slice;
   const int64_t s1 = s0 + S.slice < S.n ? s0 + S.slice : S.n;
-  const int n4 = (s0 < s1 && arrived) ? (int)((s1 - s0) >> 2) : 0;
+  const int n4 = s0 < s1 ? (int)((s1 - s0) >> 2) : 0;
   const brsrc_t in = make_rsrc(T.inbox[a.me] + S.inbox_off + (int64_t)a.worker * S.n + s0,
                                (uint32_t)n4 * 16u);
   const brsrc_t out = make_rsrc(T.params[a.worker] + S.lo + s0, (uint32_t)n4 * 16u);
@@ -297,8 +282,7 @@ AsyncPeer::AsyncPeer(float* params, const float* grads, int64_t total, int world
   inbox_elems_ = inbox > 0 ? inbox : 4;
   X_CHECK(hipMalloc(&inbox_, inbox_elems_ * sizeof(float)));
   X_CHECK(hipMemset(inbox_, 0, inbox_elems_ * sizeof(float)));
-  const size_t flag_bytes =
-      ((size_t)kArriveWords + (size_t)kAsyncMaxPs * kAsyncMaxSlices) * sizeof(uint32_t);
+  const size_t flag_bytes = (size_t)kAsyncMaxPs * kAsyncMaxSlices * sizeof(uint32_t);
   X_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes,
                                 hipDeviceMallocUncached));
   X_CHECK(hipMemset(flags_, 0, flag_bytes));
@@ -436,7 +420,6 @@ bool AsyncPeer::push_tail(const std::vector<int>& ps, uint32_t epoch, UpdTail& o
     q.g = grads_ + S.lo;
     q.w = table_.inbox[S.host] + S.inbox_off + (int64_t)rank_ * S.n;
     q.n = S.n;
-    q.arrive = table_.flags[S.host] + arrive_idx(p, rank_, 0);
     q.posted = table_.posted + posted_word(p, rank_, 0);
     q.slice4 = (int)(S.slice / 4);
     q.nslice = S.nslice;
@@ -548,8 +531,6 @@ void AsyncPeer::apply(int ps, int worker, uint32_t epoch, const XgmiUpdate& u, f
   a.lr = u.lr;
   a.mu = u.mu;
   a.scale = u.scale;
-  a.err = err_;
-  a.timeout_ticks = (long long)(timeout_s_ * 1e8);
   hipLaunchKernelGGL(async_apply_kernel, dim3(table_.shard[ps].nslice), dim3(256), 0, st,
                      table_dev_, a);
   DDL_CHECK_LAUNCH();
