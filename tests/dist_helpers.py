@@ -26,11 +26,17 @@ def train_rank(rank, world, port, cfg_kw, outdir, n_train=600):
         from ddl_amd.parallel.roles import Trainer
         from ddl_amd.utils.data import synthetic_mnist
         env = init_distributed(device="cpu")
+        cfg_kw = dict(cfg_kw)
+        segs = cfg_kw.pop("_segments", None)
+        if segs is not None:  # plan with another engine's backward segments (e.g. the HIP one's)
+            import ddl_amd.parallel.roles as roles
+            roles.engine_segments = lambda kind, device: segs
         cfg = TrainConfig(**cfg_kw)
         tr = Trainer(cfg, env, dataset=synthetic_mnist(n_train, 200, seed=7))
         summary = tr.train()
         torch.save({"params": tr.params.clone(), "plan_offsets": tr.plan.tensor_offsets,
                     "ps_t": {p: s.t for p, s in tr.servers.items()},
+                    "num_ps": tr.num_ps,
                     "served": getattr(tr.exchange, "served", None),
                     "provenance": list(getattr(tr.exchange, "provenance", []) or []),
                     "summary": summary},

@@ -126,6 +126,25 @@ def test_async_serves_every_push(tmp_path, world, shard):
         assert torch.isfinite(rec["params"]).all()
 
 
+@pytest.mark.parametrize("world,num_ps", [(2, 6), (3, 9)])
+def test_async_segment_aligned_flat_plan(tmp_path, world, num_ps):
+    """The async flat plan with the HIP engine's four backward segments (segment-aligned: every
+    PS range inside one segment, P the smallest balanced multiple of W): W = 2 -> 6 PS, W = 3 ->
+    9, three per host, uneven ranges — every push served once in order with checksummed bytes,
+    each PS at W x steps."""
+    from ddl_amd.models import HIP_SEGMENTS
+    recs, cfg = _run(tmp_path, world, mode="async", shard="flat", check_provenance=True,
+                     _segments=HIP_SEGMENTS)
+    ps_t = {}
+    for r, rec in enumerate(recs):
+        assert rec["num_ps"] == num_ps
+        ps_t.update(rec["ps_t"])
+        assert len(rec["provenance"]) == (num_ps // world) * (world - 1) * cfg["steps"]
+        assert torch.isfinite(rec["params"]).all()
+    assert sorted(ps_t) == list(range(num_ps))
+    assert all(t == world * cfg["steps"] for t in ps_t.values()), ps_t
+
+
 @pytest.mark.parametrize("world,kw", [(3, dict(shard="greedy")), (3, dict(shard="contiguous",
                                                                           num_ps=2))])
 def test_async_provenance_checked(tmp_path, world, kw):
