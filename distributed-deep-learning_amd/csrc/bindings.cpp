@@ -399,7 +399,6 @@ class PyAsyncService {
   }
   void resume() { svc_->resume(); }
   std::vector<std::array<int64_t, 4>> provenance() const { return svc_->provenance(); }
-  const ddl::AsyncService* raw() const { return svc_.get(); }
 
  private:
   std::vector<at::Tensor> keep_;
@@ -513,9 +512,6 @@ class PyAsyncRunner {
   int64_t epoch() const { return r_->epoch(); }
   void set_use_tail(bool on) { r_->set_use_tail(on); }
   void set_gate(bool on) { r_->set_gate(on); }
-  void set_local_service(py::object svc) {
-    r_->set_local_service(svc.is_none() ? nullptr : svc.cast<PyAsyncService&>().raw());
-  }
 
  private:
   PyEngine& eng_;
@@ -778,8 +774,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("finish", &PyAsyncRunner::finish)
       .def("epoch", &PyAsyncRunner::epoch)
       .def("set_use_tail", &PyAsyncRunner::set_use_tail)
-      .def("set_gate", &PyAsyncRunner::set_gate)
-      .def("set_local_service", &PyAsyncRunner::set_local_service);
+      .def("set_gate", &PyAsyncRunner::set_gate);
 
   py::class_<PyPeer>(m, "PeerExchange")
       .def(py::init<at::Tensor, at::Tensor, int64_t, int64_t, py::list, int64_t, int64_t>(),

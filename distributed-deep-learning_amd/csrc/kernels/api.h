@@ -339,7 +339,6 @@ class AsyncPeer {
              hipStream_t st);
   int error() const;
   int num_ps() const { return nps_; }
-  int host_of(int ps) const { return table_.shard[ps].host; }
 
  private:
   void upload_table();           // table_ -> table_dev_ (set-up only: open, attach_done)
@@ -384,10 +383,6 @@ class AsyncService {
   void resume();
   int64_t t(int ps) const;
   int64_t served() const { return served_.load(); }
-  // the round of worker w's push to PS p whose apply this thread has ISSUED (enqueued) last
-  uint32_t issued(int w, int p) const {
-    return issued_[(size_t)w * kAsyncMaxPs + p].load(std::memory_order_acquire);
-  }
   // (worker, ps, worker round, PS step) per apply, in service order
   const std::vector<std::array<int64_t, 4>>& provenance() const { return prov_; }
 
@@ -401,7 +396,6 @@ class AsyncService {
   float lr_, b1_, b2_, eps_, mu_, scale_;
   bool keep_prov_;
   std::vector<uint32_t> epoch_;
-  std::unique_ptr<std::atomic<uint32_t>[]> issued_;
   std::vector<std::array<int64_t, 4>> prov_;
   std::atomic<int64_t> served_{0};
   int64_t expected_ = 0;
@@ -430,9 +424,6 @@ class AsyncRunner {
   void set_use_tail(bool on) { use_tail_ = on; }
   // the pull as a GPU-side gate before the next forward (default) or a host wait
   void set_gate(bool on) { gate_ = on; }
-  // this process's PS service (nullptr: none): after the last push of a step to a PS hosted
-  // here, the step returns only once the service has issued that apply
-  void set_local_service(const AsyncService* s) { svc_ = s; }
 
  private:
   void wait_round(double timeout_s);
@@ -440,7 +431,6 @@ class AsyncRunner {
   bool use_tail_ = true;
   bool gate_ = true;
   uint32_t gated_ = 0;  // the round the last step's gate waits for (0: none)
-  const AsyncService* svc_ = nullptr;
   Engine* eng_;
   AsyncPeer* peer_;
   int world_, rank_, device_;

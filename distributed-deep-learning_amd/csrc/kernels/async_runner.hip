@@ -31,10 +31,8 @@
 // for another kernel (xgmi_async.hip explains the hardware-queue deadlock that rules it out):
 // an apply is issued only after the host has seen its push posted, and the only wait for
 // remote work is the host wait of step 1.  Staleness stays one round per worker.
-#include <chrono>
 #include <stdexcept>
 #include <string>
-#include <thread>
 
 #include "api.h"
 #include "common.h"
@@ -113,27 +111,6 @@ void AsyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t se
   if (gate_) {
     peer_->gate(epoch_, st);
     gated_ = epoch_;
-  }
-  // (3) the last segment's pushes to PS hosted by THIS process: let the service thread issue
-  // their applies before this thread enqueues the next step.  Both threads launch through one
-  // HIP runtime, and a launch issued while the other thread launches measured 10-20 us of host
-  // time (profiles/r4_async_host_latency.txt) — on the step's critical path for the apply,
-  // off it for the next step's launches, which only have to be queued before the gate opens.
-  // An optimisation only: bounded, never an error.
-  if (svc_) {
-    int last = kSegments - 1;
-    while (last > 0 && seg_ps_[last].empty()) --last;
-    const auto t0 = std::chrono::steady_clock::now();
-    for (int p : seg_ps_[last]) {
-      if (peer_->host_of(p) != rank_) continue;
-      TraceRange r("ddl.async.worker.yield_to_service");
-      for (int spins = 0; (int32_t)(svc_->issued(rank_, p) - epoch_) < 0; ++spins) {
-        if ((spins & 63) == 0 &&
-            std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5))
-          break;
-        if (spins > 256) std::this_thread::yield();
-      }
-    }
   }
 }
 

@@ -564,8 +564,6 @@ AsyncService::AsyncService(AsyncPeer* peer, int world, int device,
     if (s.ps < 0 || s.ps >= peer->num_ps() || !s.params || !s.m || (opt == 0 && !s.v))
       throw std::invalid_argument("async service: PS state");
   epoch_.assign((size_t)world * kAsyncMaxPs, epoch0);
-  issued_.reset(new std::atomic<uint32_t>[(size_t)world * kAsyncMaxPs]);
-  for (size_t i = 0; i < (size_t)world * kAsyncMaxPs; ++i) issued_[i].store(epoch0);
 }
 
 AsyncService::~AsyncService() {
@@ -607,7 +605,6 @@ void AsyncService::serve(AsyncPsState& st, int w) {
   u.mu = mu_;
   u.scale = scale_;
   peer_->apply(p, w, e, u, st.params, stream_);
-  issued_[(size_t)w * kAsyncMaxPs + p].store(e, std::memory_order_release);
   if (keep_prov_) prov_.push_back({(int64_t)w, (int64_t)p, (int64_t)e, t});
   served_.fetch_add(1);
 }

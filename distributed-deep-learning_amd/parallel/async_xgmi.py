@@ -212,8 +212,6 @@ class AsyncPeerExchange:
             self.peer, self.env.world, ps_list, self.opt, h.lr, h.beta1, h.beta2, h.eps, mom,
             self.grad_scale, 1, self.check_provenance)
         self._svc.start(n)
-        if self.runner is not None:  # the worker step yields the runtime to this service
-            self.runner.set_local_service(self._svc)
 
     def _sync_counters(self, svc) -> None:
         """The native service advances each hosted PS's step counter; mirror it into the
@@ -242,8 +240,6 @@ class AsyncPeerExchange:
         self.drain_round()  # this worker's last round (the reference's final pull)
         if self._svc is not None:
             svc, self._svc = self._svc, None
-            if self.runner is not None:
-                self.runner.set_local_service(None)
             try:
                 svc.join()
             finally:
