@@ -91,11 +91,15 @@ DDL_DEV int done_idx(int b, int src, int j) {
 // Bounded wait until *f >= target (wrap-safe).  false on timeout or when another workgroup
 // already reported an error (then the caller just runs to the end).
 DDL_DEV bool wait_ge(const uint32_t* f, uint32_t target, long long deadline, int* err, int code) {
-  while ((int32_t)(flag_load(f) - target) < 0) {
-    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return false;
-    if (wall_clock64() > deadline) {
-      __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return false;
+  // the error word lives in host memory (a PCIe round trip per load): look at it, and at the
+  // clock, only every 32nd poll, so a flag that lands is seen within one poll of local memory
+  for (int it = 0; (int32_t)(flag_load(f) - target) < 0; ++it) {
+    if ((it & 31) == 31) {
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return false;
+      if (wall_clock64() > deadline) {
+        __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+      }
     }
     __builtin_amdgcn_s_sleep(2);
   }

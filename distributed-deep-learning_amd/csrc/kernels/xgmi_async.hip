@@ -59,12 +59,15 @@ namespace {
 DDL_DEV void drain_vm() { drain_vmem(); }
 
 DDL_DEV bool wait_ge(const uint32_t* f, uint32_t target, long long deadline, int* err, int code) {
-  while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) <
-         0) {
-    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return false;
-    if (wall_clock64() > deadline) {
-      __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return false;
+  // the error word lives in host memory (a PCIe round trip per load): look at it, and at the
+  // clock, only every 32nd poll, so a flag that lands is seen within one poll of local memory
+  for (int it = 0; (int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0; ++it) {
+    if ((it & 31) == 31) {
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return false;
+      if (wall_clock64() > deadline) {
+        __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+      }
     }
     __builtin_amdgcn_s_sleep(2);
   }
