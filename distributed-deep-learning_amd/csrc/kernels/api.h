@@ -263,12 +263,6 @@ class PeerExchange {
   int64_t chunk(int b) const { return bk_[b].c; }
   int world() const { return world_; }
   int repl_bucket() const { return repl_; }
-  // READY word of backward segment s in this rank's uncached flags (written at the start of the
-  // next segment's first launch: tail.h kind 2) and the one-wave wait for it on stream `st`
-  // (bounded: error code 5), ahead of the segment's bucket kernels on the comm stream
-  static constexpr int kReadyWords = 8;
-  uint32_t* ready_flag(int s) const;
-  void gate_ready(int s, uint32_t epoch, hipStream_t st);
 
  private:
   struct Bucket { int64_t lo, c, inbox_off, slice; int nslice; };
@@ -557,15 +551,19 @@ class SyncRunner {
   hipEvent_t seg_ev_[kSegments] = {};
   hipEvent_t seg_ev_dev_[kSegments] = {};  // device-scope release (xGMI-only segments)
   bool seg_xgmi_only_[kSegments] = {};
-  // xGMI-only segments hand their gradients to the comm stream by a READY flag (tail.h kind 2)
-  // instead of an event: 0 never, 1 every segment but the first, 2 every segment (default:
-  // forced xGMI rehearsal 0.3156 / 0.3164 / 0.3058 ms/step, scripts/ready_ab.py)
+  // segments with exchange units on the comm stream (xGMI or RCCL) hand their gradients over
+  // by a READY flag (tail.h kind 2) instead of an event: 0 never, 1 every segment but the
+  // first, 2 every segment (default: forced xGMI rehearsal 0.3156 / 0.3164 / 0.3058 ms/step,
+  // scripts/ready_ab.py)
   int ready_flags_ = 2;
   bool seg_offstream_[kSegments] = {};     // the segment has units on the comm stream
   int seg_launches_[kSegments] = {};       // kernel launches of the segment in the last step
   // seg events recorded by the segment's own kernel packets (DDL_EXT_EVENT, default on)
   bool ext_event_ = true;
   hipEvent_t done_ev_ = nullptr;
+  uint32_t* ready_ = nullptr;     // READY[segment] (uncached device memory, tail.h kind 2)
+  int* ready_err_ = nullptr;      // a READY gate timed out (host memory)
+  uint32_t ready_epoch_ = 0;      // one per step
   std::vector<RunnerUnit> units_;
   int opt_ = 0;
   float lr_ = 1e-4f, b1_ = 0.9f, b2_ = 0.999f, eps_ = 1e-8f, mu_ = 0.9f;

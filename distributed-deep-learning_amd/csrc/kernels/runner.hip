@@ -34,6 +34,29 @@ namespace ddl {
 
 static ncclComm_t as_comm(void* c) { return reinterpret_cast<ncclComm_t>(c); }
 
+// One wave on the comm stream ahead of segment s's exchange units: returns once the compute
+// stream has started segment s+1 (READY[s] >= epoch, stored by that launch's first tail block,
+// tail.h kind 2), i.e. once every launch of segment s has completed — a kernel boundary writes
+// the producer's dirty L2 lines back, so the gradients are in memory for this GPU's exchange
+// kernels and for a peer's P2P reads alike.  The comm stream has high priority, so this wait
+// never shares a hardware queue with the kernel that releases it.  Bounded (error word).
+__global__ void __launch_bounds__(64) ready_gate_kernel(const uint32_t* flag, uint32_t epoch,
+                                                        int* err, long long timeout_ticks) {
+  if (threadIdx.x != 0) return;
+  const long long deadline = wall_clock64() + timeout_ticks;
+  // a long sleep between polls (~0.5 us): the first segment's gate of the next step is issued
+  // while that step's forward runs, and a tight poll slowed the forward GEMMs by ~20 %
+  for (int it = 0;
+       (int32_t)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0;
+       ++it) {
+    if ((it & 15) == 15 && wall_clock64() > deadline) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(16);
+  }
+}
+
 SyncRunner::SyncRunner(Engine* eng, float* params, float* grads, int world, int rank)
     : eng_(eng), w_(params), g_(grads), world_(world), rank_(rank) {
   int lo = 0, hi = 0;
@@ -61,6 +84,12 @@ SyncRunner::SyncRunner(Engine* eng, float* params, float* grads, int world, int 
                                       hipEventDisableTiming | hipEventDisableSystemFence));
   }
   HIP_CHECK(hipEventCreateWithFlags(&done_ev_, hipEventDisableTiming));
+  HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&ready_), kSegments * sizeof(uint32_t),
+                                  hipDeviceMallocUncached));
+  HIP_CHECK(hipMemset(ready_, 0, kSegments * sizeof(uint32_t)));
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ready_err_), 64, hipHostMallocDefault));
+  memset(ready_err_, 0, 64);
+  HIP_CHECK(hipDeviceSynchronize());
   const char* xe = getenv("DDL_EXT_EVENT");
   ext_event_ = xe ? xe[0] == '1' : true;
 }
@@ -72,6 +101,8 @@ SyncRunner::~SyncRunner() {
   for (int s = 0; s < kSegments; ++s)
     if (seg_ev_dev_[s]) (void)hipEventDestroy(seg_ev_dev_[s]);
   if (done_ev_) (void)hipEventDestroy(done_ev_);
+  if (ready_) (void)hipFree(ready_);
+  if (ready_err_) (void)hipHostFree(ready_err_);
   if (cs_) (void)hipStreamDestroy(cs_);
 }
 
@@ -354,6 +385,9 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
   // its exchange with: its collectives go in order on the compute stream (no event record /
   // stream wait between the final backward launch, the exchange and the next forward).
   bool comm_used = false;
+  if (__atomic_load_n(ready_err_, __ATOMIC_ACQUIRE))
+    throw std::runtime_error("sync runner: a READY gate timed out (a segment never completed)");
+  ++ready_epoch_;
   if (last_xgmi_ >= 0) {
     if (const int e = peer_->error())
       throw std::runtime_error("xGMI exchange timed out waiting for a peer (code " +
@@ -370,8 +404,8 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
     // idle compute stream: profiles/r4_step_timeline_forced_xgmi.txt).  The comm stream has
     // high priority, so the gate never shares a hardware queue with the kernel it waits for;
     // and it is bounded (error 5).
-    const bool flag = ready_flags_ > (s == 0 ? 1 : 0) && peer_ && !on_main &&
-                      seg_xgmi_only_[s] && s + 1 < kSegments;
+    const bool flag = ready_flags_ > (s == 0 ? 1 : 0) && !on_main && seg_offstream_[s] &&
+                      s + 1 < kSegments;
     // otherwise the comm stream waits for this segment's gradients by an event: bound to the
     // segment's kernel launches themselves (the wait below is issued after the last one) rather
     // than a marker packet behind them
@@ -406,13 +440,15 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
           eng_->flush_tail(st);  // (no update tail is pending at W > 1; keep the slot free)
           UpdTail t;
           t.kind = 2;
-          t.epoch = epoch_;
+          t.epoch = ready_epoch_;
           t.npieces = 1;
-          t.p[0].arrive = peer_->ready_flag(s);
+          t.p[0].arrive = ready_ + s;
           t.nblocks = 8;
           t.first = 1;
           eng_->tail = t;
-          peer_->gate_ready(s, epoch_, cs_);
+          hipLaunchKernelGGL(ready_gate_kernel, dim3(1), dim3(64), 0, cs_, ready_ + s,
+                             ready_epoch_, ready_err_, (long long)(20.0 * 1e8));
+          DDL_CHECK_LAUNCH();
         } else {
           if (marker) HIP_CHECK(hipEventRecord(ev, st));
           HIP_CHECK(hipStreamWaitEvent(cs_, ev, 0));

@@ -126,8 +126,7 @@ DDL_DEV float4 scale4(float4 x, float a) {
 DDL_DEV int ck_idx(int b, int src, int j, int par = 0) {
   return (2 + par) * kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices + arrive_idx(b, src, j);
 }
-// READY[s] (this rank's own words, after the four ARRIVE / DONE / checksum blocks)
-constexpr int kReadyBase = 4 * kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices;
+
 DDL_DEV uint32_t bits4(float4 v) {
   return __float_as_uint(v.x) + __float_as_uint(v.y) + __float_as_uint(v.z) + __float_as_uint(v.w);
 }
@@ -404,24 +403,6 @@ __global__ void __launch_bounds__(256) xgmi_repl_kernel(XgmiTable T, XgmiLaunch 
   if (a.final_wait) final_wait(a, myflags, W, deadline);
 }
 
-// One wave on the comm stream ahead of a segment's bucket kernels: returns when the compute
-// stream has started the next segment (READY[s] >= epoch, runner.hip).  The comm stream is a
-// high-priority stream, so this wait never shares a hardware queue with the compute stream whose
-// kernel writes the flag; bounded (error code 5).
-__global__ void __launch_bounds__(64) xgmi_ready_gate_kernel(const uint32_t* flag, uint32_t epoch,
-                                                             int* err, long long timeout_ticks) {
-  const long long deadline = wall_clock64() + timeout_ticks;
-  if (threadIdx.x != 0) return;
-  // a long sleep between polls (~0.5 us): this wave may wait through a whole forward pass
-  while ((int32_t)(flag_load(flag) - epoch) < 0) {
-    if (wall_clock64() > deadline) {
-      __hip_atomic_store(err, 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
-    }
-    __builtin_amdgcn_s_sleep(16);
-  }
-}
-
 #define X_CHECK(x)                                                                        \
   do {                                                                                    \
     hipError_t e_ = (x);                                                                  \
@@ -479,8 +460,7 @@ PeerExchange::PeerExchange(float* params, const float* grads, int64_t total, int
   X_CHECK(hipMalloc(&inbox_, inbox_elems_ * sizeof(float)));
   X_CHECK(hipMemset(inbox_, 0, inbox_elems_ * sizeof(float)));
   // ARRIVE, DONE and (check mode) checksum words, the replicated bucket's in two parities
-  flag_bytes_ = (4ull * kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices + kReadyWords) *
-                sizeof(uint32_t);
+  flag_bytes_ = 4ull * kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices * sizeof(uint32_t);
   X_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes_,
                                 hipDeviceMallocUncached));
   X_CHECK(hipMemset(flags_, 0, flag_bytes_));
@@ -600,17 +580,6 @@ void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool 
 #undef X_CASE
     default: DDL_LAUNCH(xgmi_ps_kernel<0>, dim3(B.nslice), dim3(256), 0, st, table_, a);
   }
-  DDL_CHECK_LAUNCH();
-}
-
-uint32_t* PeerExchange::ready_flag(int s) const {
-  if (s < 0 || s >= kReadyWords) throw std::invalid_argument("xgmi: ready flag index");
-  return flags_ + kReadyBase + s;
-}
-
-void PeerExchange::gate_ready(int s, uint32_t epoch, hipStream_t st) {
-  hipLaunchKernelGGL(xgmi_ready_gate_kernel, dim3(1), dim3(64), 0, st, ready_flag(s), epoch, err_,
-                     (long long)(timeout_s_ * 1e8));
   DDL_CHECK_LAUNCH();
 }
 

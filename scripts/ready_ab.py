@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of the sync runner's comm-stream hand-off on the one-GPU W > 1 rehearsal
-(--force-collectives --exchange xgmi): event record / wait (mode 0), READY flag + gate for
-every segment but the first (1, default), for every segment (2).
+(--force-collectives --exchange $EXCHANGE, xgmi or rccl): event record / wait (mode 0), READY
+flag + gate for every segment but the first (1), for every segment (2, default).
 Alternating timed windows on one box; prints ms/step per window and the medians."""
 import os
 import statistics
@@ -17,13 +17,14 @@ from ddl_amd.parallel.roles import Trainer  # noqa: E402
 from ddl_amd.utils.data import synthetic_mnist  # noqa: E402
 
 STEPS = int(os.environ.get("STEPS", "200"))
+EXCHANGE = os.environ.get("EXCHANGE", "xgmi")  # xgmi | rccl
 data = synthetic_mnist()
 
 
 def mk(flags):
     tr = Trainer(TrainConfig(mode="sync", shard="flat", steps=10000, eval_every=0, engine="hip",
                              quiet=True, data_sharding="stride", force_collectives=True,
-                             exchange_backend="xgmi"),
+                             exchange_backend=EXCHANGE),
                  DistEnv(0, 1, 0, torch.device("cuda", 0)), dataset=data)
     tr.exchange.runner.set_ready_flags(flags)
     return tr
