@@ -19,6 +19,7 @@ from op_bench import OPS  # noqa: E402
 
 STREAMK_OK = {1, 2, 3, 10, 11, 12, 13, 14}  # conv GEMMs (big enough for stream-K)
 KWAVE_OK = {4, 5, 6, 8}  # fc forward / data-gradient GEMMs (csrc/kernels/layers.h KWaveOK)
+MF16_OK = {1, 2, 3, 10, 11, 12, 13, 14, 15}  # conv GEMMs with 16-byte gathers (layers.h Mf16OK)
 
 
 def main():
@@ -87,6 +88,10 @@ def main():
         for c2 in (0, 3, 4, 5):  # the one-wave configs (dual launches instantiate these)
             if c2 != c:
                 out.append(mk(c2, s, w, wd))
+        if op in MF16_OK:  # CFG_MF16 (16x16x4 MFMA, LDS-DMA), at the split and twice it
+            for s2 in sorted({s, min(2048, s * 2)}):
+                if (c, s) != (14, s2):
+                    out.append(mk(14, s2, 0, wd))
         if a.multiwave and op in (0, 1, 2, 3):
             for c2 in (1, 2, 6, 7, 8):
                 for s2 in sorted({s, min(2048, s * 2), max(1, s // 2)}):
