@@ -290,6 +290,7 @@ constexpr int kAsyncMaxSlices = 512;
 struct AsyncShard {              // one PS's contiguous range of the flat buffer
   int64_t lo, n, slice, inbox_off;
   int host, nslice;
+  int slice0;                    // its first slice in the dense numbering of all PS' slices
 };
 struct AsyncTable {
   float* params[kXgmiMaxPeers];  // every rank's worker parameter buffer (IPC-mapped)

@@ -98,10 +98,11 @@ DDL_DEV int done_word(int w, int p, int j) { return (w * kAsyncMaxPs + p) * kAsy
 __host__ __device__ inline size_t posted_word(int p, int w, int j) {
   return ((size_t)p * kXgmiMaxPeers + w) * kAsyncMaxSlices + j;
 }
-// the same completion words in the WORKER's uncached device flags DONE[ps][slice]: what its
-// GPU-side pull gate polls (a GPU polling the host-memory copy measured ~25 us late: the
-// registered host segment is not guaranteed to bypass the GPU's L2 for a system-scope load)
-DDL_DEV int done_dev_idx(int p, int j) { return p * kAsyncMaxSlices + j; }
+// the same completion words in the WORKER's uncached device flags, densely numbered over all PS'
+// slices (AsyncShard::slice0): what its GPU-side pull gate polls (a GPU polling the host-memory
+// copy measured ~25 us late: the registered host segment is not guaranteed to bypass the GPU's
+// L2 for a system-scope load)
+DDL_DEV int done_dev_idx(const AsyncShard& S, int j) { return S.slice0 + j; }
 
 struct PushArgs {
   int world, rank, nps;
@@ -195,7 +196,7 @@ __global__ void __launch_bounds__(256) async_apply_kernel(const AsyncTable* __re
   drain_vm();
   __syncthreads();
   if (tid == 0) {
-    flag_store(T.flags[a.worker] + done_dev_idx(a.ps, j), a.epoch);  // the worker's gate
+    flag_store(T.flags[a.worker] + done_dev_idx(S, j), a.epoch);  // the worker's gate
     flag_store(T.done + done_word(a.worker, a.ps, j), a.epoch);       // the worker's host
   }
 }
@@ -209,20 +210,51 @@ __global__ void __launch_bounds__(256) async_apply_kernel(const AsyncTable* __re
 // async_runner.hip (the applies it waits for run on other processes' queues or on this
 // process's high-priority service queue, never behind it).
 struct GateArgs {
-  int rank, nps;
+  int total;  // slices of all PS (the dense DONE words 0 .. total-1)
   uint32_t epoch;
   int* err;
   long long timeout_ticks;
+  int rank;
 };
 
+// Each sweep issues eight independent loads per lane before comparing (one round of latency for
+// 512 words, instead of one per word), and skips the leading batches already seen complete
+// (the early segments' PS finish first).
 __global__ void __launch_bounds__(64) async_gate_kernel(const AsyncTable* __restrict__ Tp,
                                                         GateArgs a) {
   const AsyncTable& T = *Tp;
   const long long deadline = wall_clock64() + a.timeout_ticks;
   const uint32_t* done = T.flags[a.rank];
-  for (int p = 0; p < a.nps; ++p)
-    for (int j = threadIdx.x; j < T.shard[p].nslice; j += 64)
-      if (!wait_ge(done + done_dev_idx(p, j), a.epoch, deadline, a.err, 4)) return;
+  const int lane = threadIdx.x;
+  int start = 0;  // wave-uniform: batches below it are complete
+  for (int it = 0;; ++it) {
+    bool all = true;
+    for (int k0 = start; k0 < a.total; k0 += 512) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u * 64 + lane;
+        v[u] = k < a.total ? __hip_atomic_load(done + k, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM)
+                           : a.epoch;
+      }
+      bool ok = true;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) ok &= (int32_t)(v[u] - a.epoch) >= 0;
+      const bool batch = __all(ok);
+      if (batch && k0 == start) start += 512;
+      all &= batch;
+    }
+    if (all) return;
+    if ((it & 31) == 31) {
+      if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
+      if (wall_clock64() > deadline) {
+        if (lane == 0) __hip_atomic_store(a.err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+      }
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
 }
 
 #define X_CHECK(x)                                                                        \
@@ -271,6 +303,7 @@ AsyncPeer::AsyncPeer(float* params, const float* grads, int64_t total, int world
     if (ns > max_slices) ns = max_slices;
     S.slice = ((S.n + ns - 1) / ns + 3) & ~(int64_t)3;
     S.nslice = (int)((S.n + S.slice - 1) / S.slice);
+    S.slice0 = p == 0 ? 0 : table_.shard[p - 1].slice0 + table_.shard[p - 1].nslice;
     if (S.n * 4 * world > 0x7fffffffLL) throw std::invalid_argument("async xgmi: shard too large");
   }
   // inbox of a host: one [W][n] slot block per hosted PS, in PS order (every rank computes
@@ -542,11 +575,11 @@ void AsyncPeer::apply(int ps, int worker, uint32_t epoch, const XgmiUpdate& u, f
 void AsyncPeer::gate(uint32_t epoch, hipStream_t st) {
   if (!opened_ok_ || !table_.done) throw std::runtime_error("async xgmi: open(), attach_done() first");
   GateArgs a;
-  a.rank = rank_;
-  a.nps = nps_;
+  a.total = table_.shard[nps_ - 1].slice0 + table_.shard[nps_ - 1].nslice;
   a.epoch = epoch;
   a.err = err_;
   a.timeout_ticks = (long long)(timeout_s_ * 1e8);
+  a.rank = rank_;
   hipLaunchKernelGGL(async_gate_kernel, dim3(1), dim3(64), 0, st, table_dev_, a);
   DDL_CHECK_LAUNCH();
 }
