@@ -562,6 +562,9 @@ class SyncRunner {
   // seg events recorded by the segment's own kernel packets (DDL_EXT_EVENT, default on)
   bool ext_event_ = true;
   hipEvent_t done_ev_ = nullptr;
+  bool gate_safe(hipStream_t st);  // `st` is not a high-priority stream (runner.hip)
+  hipStream_t gate_checked_stream_ = nullptr;
+  bool gate_checked_ = false, gate_checked_ok_ = false;
   uint32_t* ready_ = nullptr;     // READY[segment] (uncached device memory, tail.h kind 2)
   int* ready_err_ = nullptr;      // a READY gate timed out (host memory)
   uint32_t ready_epoch_ = 0;      // one per step

@@ -108,7 +108,13 @@ void AsyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t se
   }
   eng_->flush_tail(st);
   gated_ = 0;
-  if (gate_) {
+  // (the gate sits on `st` and waits for applies on the high-priority service stream: only when
+  // `st` is not itself high priority can the two never share a hardware queue; else host wait)
+  int lo = 0, hi = 0, pr = 0;  // (the null stream is a normal-priority stream)
+  const bool safe = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+                    (st == nullptr || hipStreamGetPriority(st, &pr) == hipSuccess) &&
+                    hi != lo && pr != hi;
+  if (gate_ && safe) {
     peer_->gate(epoch_, st);
     gated_ = epoch_;
   }

@@ -405,7 +405,7 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
     // high priority, so the gate never shares a hardware queue with the kernel it waits for;
     // and it is bounded (error 5).
     const bool flag = ready_flags_ > (s == 0 ? 1 : 0) && !on_main && seg_offstream_[s] &&
-                      s + 1 < kSegments;
+                      s + 1 < kSegments && gate_safe(st);
     // otherwise the comm stream waits for this segment's gradients by an event: bound to the
     // segment's kernel launches themselves (the wait below is issued after the last one) rather
     // than a marker packet behind them
@@ -476,6 +476,20 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
     HIP_CHECK(hipEventRecord(done_ev_, cs_));
     HIP_CHECK(hipStreamWaitEvent(st, done_ev_, 0));
   }
+}
+
+// The READY gate waits on the comm stream for a kernel of `st`: only safe when `st` cannot share
+// a hardware queue with the comm stream, i.e. when it is not itself a high-priority stream (HIP
+// pools hardware queues per priority).  Otherwise the segment falls back to the event hand-off.
+bool SyncRunner::gate_safe(hipStream_t st) {
+  if (gate_checked_ && st == gate_checked_stream_) return gate_checked_ok_;
+  int lo = 0, hi = 0, p = 0;  // (the null stream is a normal-priority stream)
+  gate_checked_ok_ = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+                     (st == nullptr || hipStreamGetPriority(st, &p) == hipSuccess) && hi != lo &&
+                     p != hi;
+  gate_checked_stream_ = st;
+  gate_checked_ = true;
+  return gate_checked_ok_;
 }
 
 void SyncRunner::issue_xgmi(const RunnerUnit& u, const float* lr_t, bool final_wait,

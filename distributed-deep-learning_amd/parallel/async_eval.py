@@ -47,9 +47,14 @@ class AsyncEvaluator:
         # the target eval delays it).  Measured the same time to 95 % either way (0.1404-0.1417
         # vs 0.1415-0.1422 s, profiles/r3_ab_evalprio.log): the queues' priority barely moves
         # the dispatcher once both streams have work
+        # The training stream itself is NORMAL priority either way, the eval stream low (or
+        # high with =eval): the native runners' GPU-side gates rely on the training (compute)
+        # stream never sharing a hardware queue with their high-priority comm / PS-service
+        # streams, and HIP pools hardware queues per priority (runner.hip, async_runner.hip;
+        # a high-priority training stream stalled the W = 2 one-card time-to-accuracy run).
         eval_first = os.environ.get("DDL_EVAL_PRIORITY", "train") == "eval"
-        self.stream = torch.cuda.Stream(device=dev, priority=-1 if eval_first else 0)
-        self.train_stream = torch.cuda.Stream(device=dev, priority=0 if eval_first else -1)
+        self.stream = torch.cuda.Stream(device=dev, priority=-1 if eval_first else 1)
+        self.train_stream = torch.cuda.Stream(device=dev, priority=0)
         self.snap = torch.empty_like(tr.params)
         chunk = int(os.environ.get("DDL_EVAL_CHUNK", "10000"))
         self.engine = HipEngine(self.snap, torch.zeros_like(tr.params), tr.plan.tensor_offsets,

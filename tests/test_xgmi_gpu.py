@@ -318,3 +318,43 @@ def test_xgmi_job_survivor_exits_when_a_peer_fails(tmp_path, fault):
     codes = wait_survivors(procs, 1, 4.0 + 12.0 + 5.0 + 90.0)  # + import torch / HIP init
     assert 0 in codes, ("rank 0 still running", logs(tmp_path, 2))
     assert codes[0][0] != 0, logs(tmp_path, 2)
+
+
+def _eval_rank(rank, world, port, outdir):
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DDL_DIST_BACKEND="gloo",
+                      DDL_XGMI_TIMEOUT_S="20")
+    try:
+        import torch.distributed as dist
+        from ddl_amd.config import TrainConfig
+        from ddl_amd.parallel.comm import init_distributed
+        from ddl_amd.parallel.roles import Trainer
+        from ddl_amd.utils.data import synthetic_mnist
+        env = init_distributed()
+        cfg = TrainConfig(mode="sync", shard="flat", steps=30, batch_size=100, eval_every=10,
+                          engine="hip", quiet=True, data_sharding="stride",
+                          exchange_backend="xgmi", eval_async=True, watchdog_s=120.0)
+        tr = Trainer(cfg, env, dataset=synthetic_mnist(3000, 500, seed=5))
+        s = tr.train()
+        torch.save({"acc": s["final_acc"], "evals": len(tr.history)},
+                   os.path.join(outdir, f"eval{rank}.pt"))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
+def test_xgmi_sync_with_side_stream_eval_completes(tmp_path):
+    """W = 2 sync over xGMI with the periodic eval on a side stream (the bench's time-to-
+    accuracy configuration at W > 1): the training stream must not be a high-priority stream,
+    or the comm stream's READY gate can share its hardware queue and wait behind the very launch
+    that releases it (this job stalled before the AsyncEvaluator's training stream went to
+    normal priority)."""
+    import torch.multiprocessing as mp
+    mp.spawn(_eval_rank, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        rec = torch.load(os.path.join(tmp_path, f"eval{r}.pt"))
+        assert rec["evals"] >= 3 and rec["acc"] > 0.1
