@@ -426,6 +426,8 @@ class AsyncRunner {
   bool use_tail_ = true;
   bool gate_ = true;
   uint32_t gated_ = 0;  // the round the last step's gate waits for (0: none)
+  hipStream_t safe_stream_ = nullptr;  // the compute stream whose priority was checked
+  bool safe_checked_ = false, safe_ = false;
   Engine* eng_;
   AsyncPeer* peer_;
   int world_, rank_, device_;

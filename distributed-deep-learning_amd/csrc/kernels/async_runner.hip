@@ -110,11 +110,17 @@ void AsyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t se
   gated_ = 0;
   // (the gate sits on `st` and waits for applies on the high-priority service stream: only when
   // `st` is not itself high priority can the two never share a hardware queue; else host wait)
-  int lo = 0, hi = 0, pr = 0;  // (the null stream is a normal-priority stream)
-  const bool safe = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
-                    (st == nullptr || hipStreamGetPriority(st, &pr) == hipSuccess) &&
-                    hi != lo && pr != hi;
-  if (gate_ && safe) {
+  // (queried once per stream: a runtime call here sits in the window where this process's
+  // service thread launches the round's last apply)
+  if (!safe_checked_ || st != safe_stream_) {
+    int lo = 0, hi = 0, pr = 0;  // (the null stream is a normal-priority stream)
+    safe_ = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+            (st == nullptr || hipStreamGetPriority(st, &pr) == hipSuccess) && hi != lo &&
+            pr != hi;
+    safe_stream_ = st;
+    safe_checked_ = true;
+  }
+  if (gate_ && safe_) {
     peer_->gate(epoch_, st);
     gated_ = epoch_;
   }
