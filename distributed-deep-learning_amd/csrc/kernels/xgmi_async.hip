@@ -20,21 +20,22 @@
 //             cannot happen), store the new shard into the WORKER's parameter buffer, then
 //             DONE[ps][slice] = e in the worker's device flags (its GPU-side pull gate) and
 //             DONE[worker][ps][slice] = e in host memory (its host's bounded check)
-//   wait      (worker host) polls DONE[me][*][*] >= e, then enqueues the next forward
+//   wait      (worker) a one-wave gate on its compute stream polls DONE[ps][slice] >= e
+//             before the next forward (async_runner.hip; the host wait of set_gate(false) and
+//             of the Python push_pull path polls the host copy)
 // Board and DONE words live in one POSIX shm segment registered with HIP by every rank (one
 // node: the xGMI hive).  The board replaced a token mailbox fed by a poster thread that waited
 // for each push's completion EVENT: a kernel with a completion signal ends with a system-scope
 // release (an L2 write-back) and left a ~4.6 us hole on the compute stream after every push,
 // plus two host hand-offs (poster -> mailbox -> service) on the critical path of the last push
 // (docs/DESIGN.md, round 4 async timeline).
-// NO kernel of this protocol waits for another kernel.  HIP multiplexes streams onto a few
-// hardware queues (GPU_MAX_HW_QUEUES), so a spinning kernel can sit in front of the very kernel
-// it waits for; with applies of many workers interleaving on every PS stream such a cycle is
-// reachable.  Here the apply is issued only after the host has seen the push it reads posted
-// (and the board word is stored after the ARRIVE flag is acknowledged), and the worker's wait
-// is on the host, so every GPU queue only ever holds kernels that can run to completion.  The
-// apply still checks the arrival flags (bounded) as a guard, and records an error word instead
-// of hanging.
+// Only one kernel of this protocol waits for another: the worker's gate, for applies that run
+// on other processes' queues or on this process's HIGH-priority service stream — HIP pools
+// hardware queues per priority and the compute stream is not high priority (checked), so no
+// apply is ever queued behind the gate (async_runner.hip).  The applies wait for nothing: the
+// service issues one only after it has seen every slice of the push posted, and a push block
+// posts its word only after its payload stores were acknowledged.  The gate is bounded and
+// records an error word instead of hanging.
 #include <fcntl.h>
 #include <stdlib.h>
 #include <string.h>
