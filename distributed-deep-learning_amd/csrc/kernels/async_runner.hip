@@ -15,22 +15,22 @@
 //      Why the gate cannot deadlock: it blocks the compute stream's hardware queue until every
 //      PS has applied this worker's round.  Those applies run on other processes' queues or on
 //      this process's service stream, created with HIGH priority — HIP pools hardware queues
-//      per priority, so that stream never shares the gated queue — and each apply waits only
-//      for pushes that precede the gate in the compute queue (or come from other processes).
-//      No wait in the chain sits behind the gate.  And the gate is bounded (error word, no hang);
-//   2. forward, then the four backward segments; after segment s, one push kernel stores the
-//      gradient shards of every PS whose range is complete after s into their hosts' inboxes
-//      (the fc shards leave while the conv backward still computes) and posts each slice on
-//      the arrival board in host memory once its payload is acknowledged.  The push is a plain
-//      launch: no completion event (whose system-scope release cost ~4.6 us of idle compute
-//      stream per push), no host thread between the push and its PS host's service.
+//      per priority, so that stream never shares the gated queue as long as the compute stream
+//      is not high priority itself (checked once per stream; a high-priority compute stream gets
+//      the host wait instead) — and each apply waits for nothing on the GPU (the service issues
+//      it after seeing the push posted).  No wait in the chain sits behind the gate, and the
+//      gate is bounded (error word, no hang);
+//   2. forward, then the four backward segments; segment s's PS shards are pushed by tail blocks
+//      of segment s+1's first launch (tail.h kind 1; the last segment's by a push kernel), each
+//      block posting its slice on the arrival board in host memory once its payload is
+//      acknowledged: no push kernels on the compute stream, no completion events (whose
+//      system-scope release cost ~4.6 us of idle compute stream per push), no host thread
+//      between a push and its PS host's service.
 //
 // The PS side: each host's AsyncService scans the board in host memory and issues one apply
 // per completed push (Adam on the PS's private copy, the new shard stored into the worker's
-// buffer, DONE in shared host memory).  As in the rest of the async protocol NO kernel waits
-// for another kernel (xgmi_async.hip explains the hardware-queue deadlock that rules it out):
-// an apply is issued only after the host has seen its push posted, and the only wait for
-// remote work is the host wait of step 1.  Staleness stays one round per worker.
+// buffer, DONE words in the worker's device flags and in shared host memory).  Staleness stays
+// one round per worker.
 #include <stdexcept>
 #include <string>
 
