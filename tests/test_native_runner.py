@@ -21,11 +21,13 @@ def data():
     return synthetic_mnist(n_train=2000, n_test=500, seed=5)
 
 
-def _run(data, native, steps=6, **kw):
+def _run(data, native, steps=6, ready=None, **kw):
     env = DistEnv(0, 1, 0, torch.device("cuda", 0))
     cfg = TrainConfig(mode="sync", steps=steps, batch_size=100, eval_every=0, engine="hip",
                       quiet=True, native_exchange=native, **kw)
     tr = Trainer(cfg, env, dataset=data)
+    if ready is not None:
+        tr.exchange.runner.set_ready_flags(ready)
     assert getattr(tr.exchange, "native", False) == native
     if kw.get("force_collectives"):
         if kw.get("exchange_backend") == "xgmi":
@@ -185,3 +187,21 @@ def test_async_resume_continues_exactly(tmp_path, data, backend):
     assert all(s.t == 6 for s in res.servers.values())
     assert all(s.t == f.t for s, f in zip(res.servers.values(), full.servers.values()))
     assert torch.equal(res.params, full.params)
+
+
+@pytest.mark.parametrize("backend", ["rccl", "xgmi"])
+def test_ready_flag_handoff_matches_events(data, backend):
+    """The comm stream's hand-off: READY flags for every segment (default), only after the first
+    segment, events, and — on a HIGH-priority compute stream, where a gate could share the comm
+    stream's hardware queue — the automatic fallback to events.  Same kernels in the same order
+    on both streams, so all four are bit-identical."""
+    kw = dict(shard="flat", force_collectives=True, exchange_backend=backend)
+    ref = _run(data, True, **kw)
+    runs = [_run(data, True, ready=1, **kw), _run(data, True, ready=0, **kw)]
+    with torch.cuda.stream(torch.cuda.Stream(priority=-1)):
+        runs.append(_run(data, True, **kw))
+    torch.cuda.synchronize()
+    for p, st in runs:
+        assert torch.equal(ref[0], p)
+        for q in ref[1]:
+            assert torch.equal(ref[1][q][1], st[q][1])
