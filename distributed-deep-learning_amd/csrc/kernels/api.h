@@ -311,8 +311,10 @@ class AsyncPeer {
   void open(const std::vector<std::string>& handles);
   // worker: every PS shard of the gradient (x coef) into its host's inbox slot, round `epoch`
   void push_all(uint32_t epoch, float coef, hipStream_t st);
-  // the same for the listed PS only (one launch)
-  void push_set(const std::vector<int>& ps, uint32_t epoch, float coef, hipStream_t st);
+  // the same for the listed PS only (one launch); with_gate: plus the pull gate of round
+  // `epoch` as the launch's last block (the round's last push, async_runner.hip)
+  void push_set(const std::vector<int>& ps, uint32_t epoch, float coef, hipStream_t st,
+                bool with_gate = false);
   // the same push as tail blocks of another launch (tail.h kind 1, one block per arrival
   // slice); false when the set does not fit a tail (more than kTailPieces shards)
   bool push_tail(const std::vector<int>& ps, uint32_t epoch, UpdTail& out) const;

@@ -87,6 +87,21 @@ void AsyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t se
     TraceRange r("ddl.fwd");
     eng_->forward(x, B, nullptr, true, st);
   }
+  // the gate may only sit on a stream that is not high priority (queried once per stream: a
+  // runtime call at the end of the step would sit in the window where this process's service
+  // thread launches the round's last apply)
+  if (!safe_checked_ || st != safe_stream_) {
+    int lo = 0, hi = 0, pr = 0;  // (the null stream is a normal-priority stream)
+    safe_ = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+            (st == nullptr || hipStreamGetPriority(st, &pr) == hipSuccess) && hi != lo &&
+            pr != hi;
+    safe_stream_ = st;
+    safe_checked_ = true;
+  }
+  const bool gate = gate_ && safe_;
+  int last = kSegments - 1;
+  while (last > 0 && seg_ps_[last].empty()) --last;
+  gated_ = 0;
   for (int s = 0; s < kSegments; ++s) {
     {
       TraceRange r("ddl.bwd");
@@ -103,24 +118,14 @@ void AsyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t se
       eng_->tail = t;
     } else {
       eng_->flush_tail(st);
-      peer_->push_set(seg_ps_[s], epoch_, 1.f, st);
+      // the round's last push carries the pull gate as its launch's last block
+      const bool with_gate = gate && s == last;
+      peer_->push_set(seg_ps_[s], epoch_, 1.f, st, with_gate);
+      if (with_gate) gated_ = epoch_;
     }
   }
   eng_->flush_tail(st);
-  gated_ = 0;
-  // (the gate sits on `st` and waits for applies on the high-priority service stream: only when
-  // `st` is not itself high priority can the two never share a hardware queue; else host wait)
-  // (queried once per stream: a runtime call here sits in the window where this process's
-  // service thread launches the round's last apply)
-  if (!safe_checked_ || st != safe_stream_) {
-    int lo = 0, hi = 0, pr = 0;  // (the null stream is a normal-priority stream)
-    safe_ = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
-            (st == nullptr || hipStreamGetPriority(st, &pr) == hipSuccess) && hi != lo &&
-            pr != hi;
-    safe_stream_ = st;
-    safe_checked_ = true;
-  }
-  if (gate_ && safe_) {
+  if (gate && gated_ == 0) {  // (the last push rode as tail blocks: a gate launch of its own)
     peer_->gate(epoch_, st);
     gated_ = epoch_;
   }

@@ -113,7 +113,14 @@ struct PushArgs {
   int subset;
   const float* grads;
   float coef;
+  // the pull gate as the launch's last block (async_runner.hip: the round's last push)
+  int gate, gate_total;
+  int* err;
+  long long timeout_ticks;
 };
+
+DDL_DEV void gate_body(const AsyncTable& T, int rank, int total, uint32_t epoch, int* err,
+                       long long timeout_ticks);
 
 // The table (3 KB: 64 shard descriptors) is read from device memory, not passed by value: a
 // 3 KB kernel-argument block made every push / apply launch cost ~6-12 us of host time.
@@ -121,6 +128,10 @@ __global__ void __launch_bounds__(256) async_push_kernel(const AsyncTable* __res
                                                          PushArgs a) {
   const AsyncTable& T = *Tp;
   const int blk = blockIdx.x, tid = threadIdx.x;
+  if (a.gate && blk == (int)gridDim.x - 1) {  // dispatched after every push block of the launch
+    if (tid < 64) gate_body(T, a.rank, a.gate_total, a.epoch, a.err, a.timeout_ticks);
+    return;
+  }
   int e = 0;
   while (e + 1 < a.nps && blk >= a.first_blk[e + 1]) ++e;
   const int p = a.subset ? a.ps[e] : e;
@@ -221,41 +232,44 @@ struct GateArgs {
 // Each sweep issues eight independent loads per lane before comparing (one round of latency for
 // 512 words, instead of one per word), and skips the leading batches already seen complete
 // (the early segments' PS finish first).
-__global__ void __launch_bounds__(64) async_gate_kernel(const AsyncTable* __restrict__ Tp,
-                                                        GateArgs a) {
-  const AsyncTable& T = *Tp;
-  const long long deadline = wall_clock64() + a.timeout_ticks;
-  const uint32_t* done = T.flags[a.rank];
-  const int lane = threadIdx.x;
+DDL_DEV void gate_body(const AsyncTable& T, int rank, int total, uint32_t epoch, int* err,
+                       long long timeout_ticks) {
+  const long long deadline = wall_clock64() + timeout_ticks;
+  const uint32_t* done = T.flags[rank];
+  const int lane = threadIdx.x & 63;
   int start = 0;  // wave-uniform: batches below it are complete
   for (int it = 0;; ++it) {
     bool all = true;
-    for (int k0 = start; k0 < a.total; k0 += 512) {
+    for (int k0 = start; k0 < total; k0 += 512) {
       uint32_t v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int k = k0 + u * 64 + lane;
-        v[u] = k < a.total ? __hip_atomic_load(done + k, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM)
-                           : a.epoch;
+        v[u] = k < total ? __hip_atomic_load(done + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                         : epoch;
       }
       bool ok = true;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) ok &= (int32_t)(v[u] - a.epoch) >= 0;
+      for (int u = 0; u < 8; ++u) ok &= (int32_t)(v[u] - epoch) >= 0;
       const bool batch = __all(ok);
       if (batch && k0 == start) start += 512;
       all &= batch;
     }
     if (all) return;
     if ((it & 31) == 31) {
-      if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
       if (wall_clock64() > deadline) {
-        if (lane == 0) __hip_atomic_store(a.err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane == 0) __hip_atomic_store(err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
       }
     }
     __builtin_amdgcn_s_sleep(2);
   }
+}
+
+__global__ void __launch_bounds__(64) async_gate_kernel(const AsyncTable* __restrict__ Tp,
+                                                        GateArgs a) {
+  gate_body(*Tp, a.rank, a.total, a.epoch, a.err, a.timeout_ticks);
 }
 
 #define X_CHECK(x)                                                                        \
@@ -416,7 +430,8 @@ void AsyncPeer::push_all(uint32_t epoch, float coef, hipStream_t st) {
   DDL_CHECK_LAUNCH();
 }
 
-void AsyncPeer::push_set(const std::vector<int>& ps, uint32_t epoch, float coef, hipStream_t st) {
+void AsyncPeer::push_set(const std::vector<int>& ps, uint32_t epoch, float coef, hipStream_t st,
+                         bool with_gate) {
   if (!opened_ok_ || !table_.posted)
     throw std::runtime_error("async xgmi: open(), attach_done() first");
   if (ps.empty()) return;
@@ -438,6 +453,14 @@ void AsyncPeer::push_set(const std::vector<int>& ps, uint32_t epoch, float coef,
   a.grads = grads_;
   a.coef = coef;
   a.subset = 1;
+  if (with_gate) {  // one more block: the pull gate of round `epoch`
+    if (!table_.done) throw std::runtime_error("async xgmi: attach_done() first");
+    a.gate = 1;
+    a.gate_total = table_.shard[nps_ - 1].slice0 + table_.shard[nps_ - 1].nslice;
+    a.err = err_;
+    a.timeout_ticks = (long long)(timeout_s_ * 1e8);
+    ++blk;
+  }
   hipLaunchKernelGGL(async_push_kernel, dim3(blk), dim3(256), 0, st, table_dev_, a);
   DDL_CHECK_LAUNCH();
 }
