@@ -104,6 +104,11 @@ class NativeSyncExchange(SyncExchange):
             z = lambda: torch.zeros(hi - lo, dtype=torch.float32, device=params.device)  # noqa: E731
             self.repl = (b, int(lo), int(hi), z(), z() if optimizer == "adam" else None)
         self.runner = ops.SyncRunner(engine.eng, params, grads, env.world, env.rank)
+        # DDL_READY_FLAGS: the comm stream's hand-off (2: READY flags for every segment, the
+        # default; 1: all but the first; 0: events) — runner.hip SyncRunner::set_ready_flags
+        rf = os.environ.get("DDL_READY_FLAGS")
+        if rf is not None:
+            self.runner.set_ready_flags(int(rf))
         self.backend = "local" if env.world == 1 and not force_collectives else backend
         self.peer = None
         if backend == "xgmi" and (env.world > 1 or force_collectives):
