@@ -293,6 +293,29 @@ def main(argv=None):
             except RuntimeError as e:
                 plans[p] = {"error": str(e)[:200]}
 
+    # the record's facts about the benchmarked trainer, taken before any release below
+    engine_name = getattr(tr.engine, "name", a.engine)
+    num_ps, policy, exchange_name = tr.num_ps, tr.plan.policy, backend_of(tr)
+    # W > 1 sync: close and drop every trainer built so far (collectively, between barriers,
+    # nothing in flight) before each time-to-accuracy run.  Kept alive, their streams and peer
+    # mappings add hardware queues per process; with several processes on ONE card that
+    # stalled the time-to-accuracy runs (docs/DESIGN.md, "W = 4 on one card").
+    # DDL_BENCH_RELEASE=0 keeps them to the end as before.
+    release = (world > 1 and a.mode == "sync"
+               and os.environ.get("DDL_BENCH_RELEASE", "1") == "1")
+
+    def release_all():
+        import gc
+        from ddl_amd.parallel.roles import close_trainers
+        close_trainers(keep, env)
+        keep.clear()
+        gc.collect()
+        sync()
+
+    if release:
+        t = best = tr = None  # noqa: F841 - drop the last references before the collect
+        release_all()
+
     def time_to_acc(sharding):
         cfg2 = TrainConfig(mode=a.mode, shard=a.shard, batch_size=a.batch_size, eval_every=10,
                            steps=a.tta_steps,
@@ -303,6 +326,8 @@ def main(argv=None):
         tr2 = Trainer(cfg2, env, dataset=data)
         keep.append(tr2)
         s = tr2.train()
+        if release:
+            release_all()
         return {"target_acc": a.tta, "time_to_target_s": s["time_to_target"],
                 "final_acc": round(s["final_acc"], 4), "epoch_wall_s": round(s["wall_time"], 4),
                 "steps_per_worker": s["steps"], "eval_every": 10, "data_sharding": sharding,
@@ -320,7 +345,6 @@ def main(argv=None):
 
     if env.rank == 0:
         base = BASELINE_IMG_PER_S_PER_GPU
-        engine_name = getattr(tr.engine, "name", a.engine)
         rec = {
             "metric": METRIC,
             "value": round(imgs, 1),
@@ -338,13 +362,13 @@ def main(argv=None):
                 "model": "mnist_cnn 4conv+3fc (2,656,010 params)",
                 "global_batch": world * a.batch_size,
                 "seq_len": None,
-                "parallelism": f"dp{world}-ps{tr.num_ps}-{a.mode}-{tr.plan.policy}",
-                "variant": variant_of(a.mode, tr.plan.policy),
-                "plan": tr.plan.policy,
+                "parallelism": f"dp{world}-ps{num_ps}-{a.mode}-{policy}",
+                "variant": variant_of(a.mode, policy),
+                "plan": policy,
                 "engine": engine_name,
                 "hip_graph": bool(a.graph and not a.no_graph),
                 "overlap": not a.no_overlap,
-                "exchange": backend_of(tr),
+                "exchange": exchange_name,
                 "forced_1rank_collectives": bool(a.force_collectives),
                 "optimizer": "adam(1e-4) on PS shards",
                 # the throughput window's batches: worker r reads batch r, r + W, ... (per-step
