@@ -311,6 +311,11 @@ def main(argv=None):
         keep.clear()
         gc.collect()
         sync()
+        if os.environ.get("DDL_BENCH_DEBUG"):
+            from ddl_amd.parallel.roles import Trainer as _T
+            alive = sum(isinstance(o, _T) for o in gc.get_objects())
+            print(f"[bench] rank {env.rank}: {alive} trainer(s) alive after release",
+                  file=sys.stderr, flush=True)
 
     if release:
         t = best = tr = None  # noqa: F841 - drop the last references before the collect
@@ -327,6 +332,7 @@ def main(argv=None):
         keep.append(tr2)
         s = tr2.train()
         if release:
+            tr2 = None  # noqa: F841 - the frame's own reference, before the collect
             release_all()
         return {"target_acc": a.tta, "time_to_target_s": s["time_to_target"],
                 "final_acc": round(s["final_acc"], 4), "epoch_wall_s": round(s["wall_time"], 4),
