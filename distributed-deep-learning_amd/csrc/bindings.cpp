@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "kernels/api.h"
+#include "kernels/stamps.h"
 #include "runtime/mailbox.h"
 
 namespace py = pybind11;
@@ -71,7 +72,7 @@ class PyEngine {
     TORCH_CHECK((int)c.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " tile configs");
     for (int i = 0; i < ddl::OP_COUNT; ++i) {
       TORCH_CHECK((c[i] >= 0 && c[i] < ddl::NUM_TILE_CFGS) || c[i] == ddl::CFG_KWAVE ||
-                      c[i] == ddl::CFG_MF16,
+                      c[i] == ddl::CFG_MF16 || ddl::dma_cfg((int)c[i]),
                   "tile config out of range");
       e_.cfg[i] = (int)c[i];
     }
@@ -118,6 +119,17 @@ class PyEngine {
   }
   std::vector<int64_t> get_wide() const {
     return std::vector<int64_t>(e_.wide, e_.wide + ddl::OP_COUNT);
+  }
+  // per-op split-K block order (gemm.h split_coords; 0..3)
+  void set_order(std::vector<int64_t> o) {
+    TORCH_CHECK((int)o.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " orders");
+    for (int i = 0; i < ddl::OP_COUNT; ++i) {
+      TORCH_CHECK(o[i] >= 0 && o[i] <= 3, "block order must be 0..3");
+      e_.order[i] = (int)o[i];
+    }
+  }
+  std::vector<int64_t> get_order() const {
+    return std::vector<int64_t>(e_.order, e_.order + ddl::OP_COUNT);
   }
 
   void set_keep_prob(double keep) {
@@ -260,10 +272,23 @@ class PyPeer {
     check_f32_cuda(params, "params");
     check_f32_cuda(grads, "grads");
     TORCH_CHECK(params.numel() == grads.numel(), "params/grads size mismatch");
-    std::vector<std::pair<int64_t, int64_t>> bk;
+    // each bucket: (lo, hi) — an equal-chunk bucket — or (runs, state_offs, owner) — an owner
+    // bucket of a tensor-granular plan (kernels/api.h XgmiBucketSpec)
+    std::vector<ddl::XgmiBucketSpec> bk;
     for (auto b : buckets) {
       auto t = b.cast<py::tuple>();
-      bk.emplace_back(t[0].cast<int64_t>(), t[1].cast<int64_t>());
+      ddl::XgmiBucketSpec sp;
+      if (t.size() == 3) {
+        for (auto r : t[0].cast<py::list>()) {
+          auto rr = r.cast<py::tuple>();
+          sp.runs.emplace_back(rr[0].cast<int64_t>(), rr[1].cast<int64_t>());
+        }
+        sp.state_offs = t[1].cast<std::vector<int64_t>>();
+        sp.owner = t[2].cast<int>();
+      } else {
+        sp.runs.emplace_back(t[0].cast<int64_t>(), t[1].cast<int64_t>());
+      }
+      bk.push_back(sp);
     }
     c10::hip::HIPGuard guard(params.device().index());
     p_ = std::make_unique<ddl::PeerExchange>(params.data_ptr<float>(), grads.data_ptr<float>(),
@@ -652,6 +677,35 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("w"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr_t"), py::arg("b1"),
         py::arg("b2"), py::arg("eps"), py::arg("scale") = 1.0);
   m.def("momentum_flat", &momentum_flat, "Fused momentum SGD on a flat shard");
+  // per-block timestamps of the split-K dual launches (kernels/stamps.h; a build with
+  // DDL_STAMPS=1 records them, the default build records nothing)
+  m.def("stamps_enabled", []() { return (bool)DDL_STAMPS; });
+  m.def("stamps_begin", [](int64_t cap) {
+    ddl::StampState& s = ddl::stamp_state();
+    if (s.buf) (void)hipFree(s.buf);
+    s.buf = nullptr;
+    s.cap = s.next = 0;
+    s.log.clear();
+    if (cap <= 0) return;
+    TORCH_CHECK(hipMalloc(&s.buf, (size_t)cap * 64) == hipSuccess, "stamp buffer");
+    TORCH_CHECK(hipMemset(s.buf, 0, (size_t)cap * 64) == hipSuccess, "stamp buffer");
+    s.cap = cap;
+  });
+  m.def("stamps_end", []() {
+    ddl::StampState& s = ddl::stamp_state();
+    TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "stamps: device sync");
+    at::Tensor out = at::empty({(int64_t)s.next, 8}, at::kLong);
+    if (s.next)
+      TORCH_CHECK(hipMemcpy(out.data_ptr(), s.buf, (size_t)s.next * 64, hipMemcpyDeviceToHost) ==
+                      hipSuccess, "stamps: copy");
+    std::vector<std::vector<int64_t>> log;
+    for (const auto& r : s.log) log.push_back({r.off, r.nblocks, r.sub, r.gx, r.gy, r.gz});
+    if (s.buf) (void)hipFree(s.buf);
+    s.buf = nullptr;
+    s.cap = s.next = 0;
+    s.log.clear();
+    return std::make_pair(out, log);
+  });
   m.def("mfma_peak", [](at::Tensor out, int64_t blocks, int64_t iters, int64_t kind) {
     check_f32_cuda(out, "out");
     TORCH_CHECK(out.numel() >= blocks * 64, "out too small");
@@ -687,6 +741,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("conv1_wgrad_direct", [](PyEngine& e) { return e.raw()->conv1_wgrad_direct; })
       .def("set_wide_thr", &PyEngine::set_wide_thr)
       .def("set_wide", &PyEngine::set_wide)
+      .def("set_order", &PyEngine::set_order)
+      .def("get_order", &PyEngine::get_order)
       .def("get_wide", &PyEngine::get_wide)
       .def("forward", &PyEngine::forward, py::arg("x"), py::arg("seed"), py::arg("train"))
       .def("backward_segment", &PyEngine::backward_segment)

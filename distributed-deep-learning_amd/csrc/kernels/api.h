@@ -93,6 +93,19 @@ constexpr int CFG_KWAVE = 13;
 // (gemm.h GemmTile::mainloop_dma16); conv2-4 forward / data gradient / weight gradient only
 // (other ops fall back to config 3)
 constexpr int CFG_MF16 = 14;
+// training: one-wave multi-fragment tiles on the generic LDS-DMA main loop (gemm.h
+// GemmTile::mainloop_dma_g: any operand contiguity, no staging registers); conv2-4 forward /
+// data gradient / weight gradient only (other ops fall back to config 3).  64x32, 32x64, 64x64.
+constexpr int CFG_DMA_64x32 = 16;
+constexpr int CFG_DMA_32x64 = 17;
+constexpr int CFG_DMA_64x64 = 18;
+inline bool dma_g_cfg(int c) { return c >= CFG_DMA_64x32 && c <= CFG_DMA_64x64; }
+// training: the one-wave 32x32 tile on a ring of 3 / 2 LDS-DMA images with the next tiles' DMAs
+// interleaved into the MFMA cluster (gemm.h GemmTile::mainloop_ring); conv2-4 GEMMs only
+constexpr int CFG_RING3 = 19;
+constexpr int CFG_RING2 = 20;
+inline bool ring_cfg(int c) { return c == CFG_RING3 || c == CFG_RING2; }
+inline bool dma_cfg(int c) { return dma_g_cfg(c) || ring_cfg(c); }
 
 struct Engine {
   const float* P[14] = {};   // parameter tensors v0..v13 (any flat layout)
@@ -103,6 +116,8 @@ struct Engine {
   int cfg[OP_COUNT];
   int eval_cfg[OP_COUNT];    // tile configs of the no-split eval forward (train = false)
   int workers[OP_COUNT];     // > 0: stream-K with this many workers (overrides splits)
+  int order[OP_COUNT];       // split-K block order (gemm.h split_coords: 0 round-robin, 1-3
+                             // XCD-contiguous with K splits / M rows / N tiles grouped)
   int wide_thr = 1;          // default split count above which the separate wide reduce is used
   int wide[OP_COUNT];        // per op: z > wide[op] -> separate wide reduce (mode 2), else the
                              // in-launch last-arriver reduction (mode 1)
@@ -211,7 +226,10 @@ struct RunnerUnit {
 
 // ---- parameter-server exchange over xGMI peer memory (xgmi.hip) ------------------------------
 constexpr int kXgmiMaxPeers = 16;
-constexpr int kXgmiMaxBuckets = 8;
+// flat plans: one bucket per backward segment (<= 8); tensor-granular plans: one OWNER bucket per
+// (PS, segment) exchange unit (<= 8 PS x 4 segments)
+constexpr int kXgmiMaxBuckets = 32;
+constexpr int kXgmiMaxRuns = 8;   // plan-buffer ranges of one owner bucket
 #ifndef DDL_XGMI_MAX_SLICES
 #define DDL_XGMI_MAX_SLICES 512
 #endif
@@ -234,6 +252,23 @@ struct XgmiLaunch {              // one bucket's kernel arguments
   long long timeout_ticks;
   int check;                     // DDL_XGMI_CHECK: per-(bucket, source, slice) inbox checksums
   int repl_bucket;               // the replicated bucket (-1: none)
+  int owners[kXgmiMaxBuckets];   // -1: chunk r of the bucket on rank r; >= 0: single owner rank
+  // owner buckets: the launched bucket's runs (plan-buffer range, element offset in the owner
+  // PS's optimizer state, offset in the bucket's concatenation, slice size, first slice)
+  int owner, nruns;
+  int64_t run_lo[kXgmiMaxRuns], run_n[kXgmiMaxRuns], run_soff[kXgmiMaxRuns];
+  int64_t run_voff[kXgmiMaxRuns], run_slice[kXgmiMaxRuns];
+  int run_sl0[kXgmiMaxRuns + 1];
+};
+// One bucket of a PeerExchange.  owner < 0: a single plan-buffer range split into W equal chunks,
+// chunk r owned by rank r (the flat plan: reduce-scatter form).  owner >= 0: one PS's exchange
+// unit of a tensor-granular plan (reference none / contiguous / greedy, lpt; or a flat plan with
+// fewer PS than ranks) — every rank pushes the whole unit to its owner, which sums, updates with
+// that PS's optimizer state (run r at state_offs[r]) and pushes the parameters to every rank.
+struct XgmiBucketSpec {
+  std::vector<std::pair<int64_t, int64_t>> runs;
+  std::vector<int64_t> state_offs;
+  int owner = -1;
 };
 struct XgmiUpdate {              // owner-side update of one bucket chunk
   int opt = 0;                   // 0 Adam (TF1), 1 momentum, 2 self-test (w := summed g)
@@ -252,6 +287,9 @@ class PeerExchange {
   PeerExchange(float* params, const float* grads, int64_t total, int world, int rank,
                const std::vector<std::pair<int64_t, int64_t>>& buckets, int max_slices,
                int repl_bucket = -1);
+  // general form: equal-chunk and owner buckets (XgmiBucketSpec)
+  PeerExchange(float* params, const float* grads, int64_t total, int world, int rank,
+               const std::vector<XgmiBucketSpec>& buckets, int max_slices, int repl_bucket = -1);
   ~PeerExchange();
   std::string handle() const;                         // this rank's IPC handles, as bytes
   void open(const std::vector<std::string>& handles);  // every rank's, in rank order
@@ -261,11 +299,19 @@ class PeerExchange {
   int num_buckets() const { return (int)bk_.size(); }
   int nslices(int b) const { return bk_[b].nslice; }
   int64_t chunk(int b) const { return bk_[b].c; }
+  int owner(int b) const { return bk_[b].owner; }
   int world() const { return world_; }
   int repl_bucket() const { return repl_; }
 
  private:
-  struct Bucket { int64_t lo, c, inbox_off, slice; int nslice; };
+  struct Bucket {
+    int64_t lo, c, inbox_off, slice;
+    int nslice;
+    int owner = -1;
+    std::vector<int64_t> run_lo, run_n, run_soff, run_voff, run_slice;
+    std::vector<int> run_sl0;
+  };
+  void init(const std::vector<XgmiBucketSpec>& buckets, int max_slices);
   int repl_ = -1;
   bool check_ = false;
   float* params_;

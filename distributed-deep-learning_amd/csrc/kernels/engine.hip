@@ -63,6 +63,7 @@ Engine::Engine() {
   eval_cfg[OP_CONV4_FWD] = 0;
   memcpy(splits, defs, sizeof(defs));
   memcpy(workers, defw, sizeof(defw));
+  memset(order, 0, sizeof(order));
   for (int op = 0; op < OP_COUNT; ++op) wide[op] = inl[op] ? (1 << 20) : 1;
 }
 
@@ -120,6 +121,11 @@ static size_t slab_need(int c, int M, int N, int K, int s, int w) {
     // launch with the same split factor (engine_impl.h launch_cfg), so size for that
     case CFG_KWAVE: return gemm_slab_f4<TILE_3>(M, N, K, s, w);
     case CFG_MF16: return gemm_slab_f4<TILE_3>(M, N, K, s, w);  // same 32x32 partial layout
+    // the generic LDS-DMA tiles: the partial layouts of the one-wave tiles of their size
+    case CFG_DMA_64x32: return gemm_slab_f4<TILE_2>(M, N, K, s, w);
+    case CFG_DMA_32x64: return gemm_slab_f4<TILE_4>(M, N, K, s, w);
+    case CFG_DMA_64x64: return gemm_slab_f4<TILE_0>(M, N, K, s, w);
+    case CFG_RING3: case CFG_RING2: return gemm_slab_f4<TILE_3>(M, N, K, s, w);
     case 0: return gemm_slab_f4<TILE_0>(M, N, K, s, w);
     case 1: return gemm_slab_f4<TILE_1>(M, N, K, s, w);
     case 2: return gemm_slab_f4<TILE_2>(M, N, K, s, w);

@@ -31,10 +31,17 @@ namespace ddl {
 #define TILE_12 128, 128, 32, 4, 1
 // training: one-wave 32x32x32 on 16x16x4 MFMAs with LDS-DMA staging (CFG_MF16)
 #define TILE_14 32, 32, 32, 1, 1, 1
+// training: one-wave multi-fragment tiles on the generic LDS-DMA loop (CFG_DMA_*)
+#define TILE_16 64, 32, 32, 1, 1, 2
+#define TILE_17 32, 64, 32, 1, 1, 2
+#define TILE_18 64, 64, 32, 1, 1, 2
+// training: one-wave 32x32 on a ring of 3 / 2 LDS-DMA images (CFG_RING3 / CFG_RING2)
+#define TILE_19 32, 32, 32, 1, 1, 3
+#define TILE_20 32, 32, 32, 1, 1, 4
 
 template <class P>
 inline void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const SplitScratch& sc,
-                       hipStream_t st) {
+                       hipStream_t st, int o = 0) {
   if (c == CFG_KWAVE) {
     if constexpr (KWaveOK<P>::value) {
       launch_gemm_kwave<32>(p, s < 0 ? -s : s, st);
@@ -44,21 +51,38 @@ inline void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const Spli
   }
   if (c == CFG_MF16) {
     if constexpr (Mf16OK<P>::value) {
-      launch_gemm<TILE_14>(p, s, wide_thr, sc, st, w);
+      launch_gemm<TILE_14>(p, s, wide_thr, sc, st, w, o);
+      return;
+    }
+    c = 3;
+  }
+  if (ring_cfg(c)) {
+    if constexpr (DmaOK<P>::value) {
+      if (c == CFG_RING3) launch_gemm<TILE_19>(p, s, wide_thr, sc, st, w, o);
+      else launch_gemm<TILE_20>(p, s, wide_thr, sc, st, w, o);
+      return;
+    }
+    c = 3;
+  }
+  if (dma_g_cfg(c)) {
+    if constexpr (DmaOK<P>::value) {
+      if (c == CFG_DMA_64x32) launch_gemm<TILE_16>(p, s, wide_thr, sc, st, w, o);
+      else if (c == CFG_DMA_32x64) launch_gemm<TILE_17>(p, s, wide_thr, sc, st, w, o);
+      else launch_gemm<TILE_18>(p, s, wide_thr, sc, st, w, o);
       return;
     }
     c = 3;
   }
   switch (c) {
-    case 0: launch_gemm<TILE_0>(p, s, wide_thr, sc, st, w); break;
-    case 1: launch_gemm<TILE_1>(p, s, wide_thr, sc, st, w); break;
-    case 2: launch_gemm<TILE_2>(p, s, wide_thr, sc, st, w); break;
-    case 3: launch_gemm<TILE_3>(p, s, wide_thr, sc, st, w); break;
-    case 4: launch_gemm<TILE_4>(p, s, wide_thr, sc, st, w); break;
-    case 5: launch_gemm<TILE_5>(p, s, wide_thr, sc, st, w); break;
-    case 6: launch_gemm<TILE_6>(p, s, wide_thr, sc, st, w); break;
-    case 7: launch_gemm<TILE_7>(p, s, wide_thr, sc, st, w); break;
-    default: launch_gemm<TILE_8>(p, s, wide_thr, sc, st, w); break;
+    case 0: launch_gemm<TILE_0>(p, s, wide_thr, sc, st, w, o); break;
+    case 1: launch_gemm<TILE_1>(p, s, wide_thr, sc, st, w, o); break;
+    case 2: launch_gemm<TILE_2>(p, s, wide_thr, sc, st, w, o); break;
+    case 3: launch_gemm<TILE_3>(p, s, wide_thr, sc, st, w, o); break;
+    case 4: launch_gemm<TILE_4>(p, s, wide_thr, sc, st, w, o); break;
+    case 5: launch_gemm<TILE_5>(p, s, wide_thr, sc, st, w, o); break;
+    case 6: launch_gemm<TILE_6>(p, s, wide_thr, sc, st, w, o); break;
+    case 7: launch_gemm<TILE_7>(p, s, wide_thr, sc, st, w, o); break;
+    default: launch_gemm<TILE_8>(p, s, wide_thr, sc, st, w, o); break;
   }
 }
 
@@ -142,13 +166,56 @@ void run_op_inst(Engine& e, const float* x, int B, const uint32_t* seed, bool tr
   }
   launch_cfg(train ? e.cfg[OP] : e.eval_cfg[OP], p, train ? e.splits[OP] : 1,
              train ? e.workers[OP] : 0, e.wide[OP],
-             e.scratch[si], st);
+             e.scratch[si], st, train ? e.order[OP] : 0);
 }
 
 // ---- dual launches: data- and weight-gradient GEMM of one layer in one kernel -----------------
-// dual launches are instantiated for the one-wave 32x32 configs (others run back to back: the
+// dual launches are instantiated for the one-wave configs: 32x32 (3), 32x32 BK 16 pipelined (5),
+// the 16x16x4 tile (CFG_MF16) and the generic LDS-DMA tiles (CFG_DMA_*; the register-staged
 // one-wave 64x64 / 32x64 tiles, 180-230 VGPRs, never won a dual launch in the real-step tuner)
-inline bool one_wave_cfg(int c) { return c == 3 || c == 5 || c == CFG_MF16; }
+inline bool one_wave_cfg(int c) { return c == 3 || c == 5 || c == CFG_MF16 || dma_cfg(c); }
+
+template <int C> struct CfgOf;
+template <> struct CfgOf<3> { using T = TileCfg<TILE_3>; };
+template <> struct CfgOf<5> { using T = TileCfg<TILE_5>; };
+template <> struct CfgOf<CFG_MF16> { using T = TileCfg<TILE_14>; };
+template <> struct CfgOf<CFG_DMA_64x32> { using T = TileCfg<TILE_16>; };
+template <> struct CfgOf<CFG_DMA_32x64> { using T = TileCfg<TILE_17>; };
+template <> struct CfgOf<CFG_DMA_64x64> { using T = TileCfg<TILE_18>; };
+template <> struct CfgOf<CFG_RING3> { using T = TileCfg<TILE_19>; };
+template <> struct CfgOf<CFG_RING2> { using T = TileCfg<TILE_20>; };
+template <int C> using IC = std::integral_constant<int, C>;
+
+// f(IC<c'>) for the one-wave config c' that op policy P runs for run-time config c (configs P
+// has no instantiation for fall back to 3; anything but 5 / MF16 / DMA likewise)
+template <class P, class F>
+inline void with_one_wave_cfg(int c, F&& f) {
+  if constexpr (Mf16OK<P>::value) {
+    if (c == CFG_MF16) return f(IC<CFG_MF16>{});
+  }
+  if constexpr (DmaOK<P>::value) {
+    if (c == CFG_DMA_64x32) return f(IC<CFG_DMA_64x32>{});
+    if (c == CFG_DMA_32x64) return f(IC<CFG_DMA_32x64>{});
+    if (c == CFG_DMA_64x64) return f(IC<CFG_DMA_64x64>{});
+    if (c == CFG_RING3) return f(IC<CFG_RING3>{});
+    if (c == CFG_RING2) return f(IC<CFG_RING2>{});
+  }
+  if (c == 5) return f(IC<5>{});
+  f(IC<3>{});
+}
+// the dual pairings that are instantiated: every pairing of the register-staged / 16x16x4
+// configs, every pairing of the DMA tiles with each other and with 3 / 5 (not DMA x MF16)
+constexpr bool dual_pair_ok(int a, int b) {
+  // the ring tiles pair with each other and with 3 / 5; the multi-fragment DMA tiles likewise;
+  // the two families do not mix
+  const bool ra = a == CFG_RING3 || a == CFG_RING2, rb = b == CFG_RING3 || b == CFG_RING2;
+  const bool ga = a >= CFG_DMA_64x32 && a <= CFG_DMA_64x64;
+  const bool gb = b >= CFG_DMA_64x32 && b <= CFG_DMA_64x64;
+  if ((ra && gb) || (ga && rb)) return false;
+  if ((ra || ga) && b == CFG_MF16) return false;
+  if ((rb || gb) && (a == CFG_MF16 || a == 5)) return false;
+  return true;
+}
 
 // fc3's weight gradient as aux blocks (head.h), pending after the fused head kernel
 inline HeadWgradAux head_aux(Engine& e, int B) {
@@ -165,33 +232,31 @@ inline HeadWgradAux head_aux(Engine& e, int B) {
   return a;
 }
 
-template <class CA, int OA, int OB, class PA, class PB>
+template <int OA, int OB>
+inline void run_back_to_back(Engine& e, const float* x, int B, const uint32_t* seed,
+                             hipStream_t st) {
+  e.flush_tail(st);
+  if constexpr (OA == OP_FC2_DGRAD) e.flush_head_wgrad(B, st);
+  run_op_inst<OA>(e, x, B, seed, true, st, 0);
+  run_op_inst<OB>(e, x, B, seed, true, st, 0);
+}
+
+template <class CA, class CB, int OA, int OB, class PA, class PB>
 inline void dual_b(Engine& e, const PA& pa, const PB& pb, int B, hipStream_t st) {
-#define DDL_DUAL_B(CB, AUXV) \
-  launch_gemm_dual<CA, PA, TileCfg<CB>, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], \
-                                            e.wide[OA], pb, e.splits[OB], e.workers[OB], \
-                                            e.scratch[1], e.wide[OB], st, AUXV, nullptr, \
-                                            e.dual_order(OA))
+  auto go = [&](const auto& aux) {
+    launch_gemm_dual<CA, PA, CB, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA],
+                                     pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB],
+                                     st, aux, nullptr, e.dual_order(OA), e.order[OA],
+                                     e.order[OB]);
+  };
   // the fc2 dual carries fc3's weight gradient; the others a pending optimizer tail
-#define DDL_DUAL_SW(AUXV)                                                       \
-  switch (e.cfg[OB]) {                                                          \
-    case CFG_MF16:                                                              \
-      if constexpr (Mf16OK<PB>::value) { DDL_DUAL_B(TILE_14, AUXV); break; }    \
-      [[fallthrough]];                                                          \
-    case 3: DDL_DUAL_B(TILE_3, AUXV); break;                                    \
-    default: DDL_DUAL_B(TILE_5, AUXV); break;                                   \
-  }
   if constexpr (OA == OP_FC2_DGRAD) {
     e.flush_tail(st);
-    const HeadWgradAux aux = head_aux(e, B);
-    DDL_DUAL_SW(aux)
+    go(head_aux(e, B));
   } else {
-    const TailAux aux(e.tail);
-    DDL_DUAL_SW(aux)
+    go(TailAux(e.tail));
     e.tail = UpdTail();
   }
-#undef DDL_DUAL_SW
-#undef DDL_DUAL_B
 }
 
 // Ops OA and OB (independent) in one launch if both use one-wave tiles, else back to back.
@@ -214,26 +279,22 @@ void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipSt
     }
   }
   if (!e.dual || !one_wave_cfg(e.cfg[OA]) || !one_wave_cfg(e.cfg[OB])) {
-    e.flush_tail(st);
-    if constexpr (OA == OP_FC2_DGRAD) e.flush_head_wgrad(B, st);
-    run_op_inst<OA>(e, x, B, seed, true, st, 0);
-    run_op_inst<OB>(e, x, B, seed, true, st, 0);
+    run_back_to_back<OA, OB>(e, x, B, seed, st);
     return;
   }
   const auto pa = make_policy<OA>(e, B, x, seed, true);
   const auto pb = make_policy<OB>(e, B, x, seed, true);
   using PA = std::decay_t<decltype(pa)>;
   using PB = std::decay_t<decltype(pb)>;
-  switch (e.cfg[OA]) {
-    case CFG_MF16:
-      if constexpr (Mf16OK<PA>::value) {
-        dual_b<TileCfg<TILE_14>, OA, OB, PA, PB>(e, pa, pb, B, st);
-        break;
-      }
-      [[fallthrough]];
-    case 3: dual_b<TileCfg<TILE_3>, OA, OB, PA, PB>(e, pa, pb, B, st); break;
-    default: dual_b<TileCfg<TILE_5>, OA, OB, PA, PB>(e, pa, pb, B, st); break;
-  }
+  with_one_wave_cfg<PA>(e.cfg[OA], [&](auto ca) {
+    with_one_wave_cfg<PB>(e.cfg[OB], [&](auto cb) {
+      constexpr int A = decltype(ca)::value, Bc = decltype(cb)::value;
+      if constexpr (dual_pair_ok(A, Bc))
+        dual_b<typename CfgOf<A>::T, typename CfgOf<Bc>::T, OA, OB>(e, pa, pb, B, st);
+      else
+        run_back_to_back<OA, OB>(e, x, B, seed, st);
+    });
+  });
 }
 
 // Split the last segment's update `in` into conv1's weight / bias spans (applied by the
@@ -372,7 +433,8 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
   SubGrid gb;
   launch_gemm_dual<CA, PA, CB, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb,
                                    e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st,
-                                   TailAux(e.tail), &gb, e.dual_order(OA));
+                                   TailAux(e.tail), &gb, e.dual_order(OA), e.order[OA],
+                                   e.order[OB]);
   e.tail = UpdTail();
   constexpr bool kFinal = ON == OP_CONV1_WGRAD;
   if constexpr (kFinal) {
@@ -422,29 +484,31 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
   }
 }
 
-// Instantiated for OA on 32x32 tiles, OB on 32x32 (BK 32 or pipelined BK 16), ON on 32x32
-// split-K; any other schedule takes the unfused sequence.
+// Instantiated for OA / OB on the one-wave configs (dual_pair_ok), ON on 32x32 split-K; any
+// other schedule takes the unfused sequence.
 template <int OA, int OB, int ON>
 void run_dual_then_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
   const int ca = e.cfg[OA], cb = e.cfg[OB];
-  if (!e.dual || (ca != 3 && ca != CFG_MF16) || (cb != 3 && cb != 5 && cb != CFG_MF16) ||
-      e.cfg[ON] != 3 || e.workers[ON] > 0) {
+  if (!e.dual || (ca != 3 && ca != CFG_MF16 && !dma_cfg(ca)) ||
+      (cb != 3 && cb != 5 && cb != CFG_MF16 && !dma_cfg(cb)) || e.cfg[ON] != 3 ||
+      e.workers[ON] > 0) {
     run_dual_inst<OA, OB>(e, x, B, seed, st);
     e.run_op(ON, x, B, seed, true, st, 0);
     return;
   }
-  using C3 = TileCfg<TILE_3>;
-  using C5 = TileCfg<TILE_5>;
-  using C14 = TileCfg<TILE_14>;
-  if (ca == CFG_MF16) {
-    if (cb == CFG_MF16) dual_then_b<OA, OB, ON, C14, C14>(e, x, B, seed, st);
-    else if (cb == 3) dual_then_b<OA, OB, ON, C14, C3>(e, x, B, seed, st);
-    else dual_then_b<OA, OB, ON, C14, C5>(e, x, B, seed, st);
-  } else {
-    if (cb == CFG_MF16) dual_then_b<OA, OB, ON, C3, C14>(e, x, B, seed, st);
-    else if (cb == 3) dual_then_b<OA, OB, ON, C3, C3>(e, x, B, seed, st);
-    else dual_then_b<OA, OB, ON, C3, C5>(e, x, B, seed, st);
-  }
+  using PA = decltype(make_policy<OA>(e, B, x, seed, true));
+  using PB = decltype(make_policy<OB>(e, B, x, seed, true));
+  with_one_wave_cfg<PA>(ca, [&](auto ia) {
+    with_one_wave_cfg<PB>(cb, [&](auto ib) {
+      constexpr int A = decltype(ia)::value, Bc = decltype(ib)::value;
+      if constexpr (A != 5 && dual_pair_ok(A, Bc)) {
+        dual_then_b<OA, OB, ON, typename CfgOf<A>::T, typename CfgOf<Bc>::T>(e, x, B, seed, st);
+      } else {
+        run_dual_inst<OA, OB>(e, x, B, seed, st);
+        e.run_op(ON, x, B, seed, true, st, 0);
+      }
+    });
+  });
 }
 
 }  // namespace ddl

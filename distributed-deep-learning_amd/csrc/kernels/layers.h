@@ -594,12 +594,12 @@ struct ConvWgradBM {
     int kk;
     bool ok;
   };
-  static DDL_DEV KWin pos_win(int y0, int y1, int x0, int x1) {  // inclusive bounds
+  static DDL_HD KWin pos_win(int y0, int y1, int x0, int x1) {  // inclusive bounds
     const int nx = x1 - x0 + 1;
     return {y0, y1 - y0 + 1, x0, nx, (65536 + nx - 1) / nx};
   }
-  DDL_DEV KWin kfull() const { return pos_win(0, H - 1, 0, H - 1); }
-  DDL_DEV KWin kwin(int m_lo, int m_hi) const {
+  DDL_HD KWin kfull() const { return pos_win(0, H - 1, 0, H - 1); }
+  DDL_HD KWin kwin(int m_lo, int m_hi) const {
     if (m_hi > KW) return kfull();  // the ones row (bias gradient) sums every position
     const int t0 = m_lo / CIN, t1 = (m_hi - 1) / CIN;
     const int kylo = t0 / 5, kyhi = t1 / 5;
@@ -608,7 +608,7 @@ struct ConvWgradBM {
     return pos_win(max(0, 2 - kyhi), min(H - 1, H + 1 - kylo), max(0, 2 - kxhi),
                    min(H - 1, H + 1 - kxlo));
   }
-  DDL_DEV int kvlen(const KWin& w) const { return w.ny * w.nx * NB; }
+  DDL_HD int kvlen(const KWin& w) const { return w.ny * w.nx * NB; }
   static DDL_DEV void vpos(const KWin& w, int v, int& y, int& xx) {
     const int r = (v * w.rx) >> 16;
     y = w.y0 + r;
@@ -890,6 +890,11 @@ template <int H, int CIN, int COUT, int HPREV>
 struct Mf16OK<ConvDgrad<H, CIN, COUT, HPREV>> : std::true_type {};
 template <int H, int CIN, int COUT>
 struct Mf16OK<ConvWgradBM<H, CIN, COUT>> : std::true_type {};
+
+// ops the generic LDS-DMA tiles (CFG_DMA_*, gemm.h mainloop_dma_g) are instantiated for: the
+// same 16-byte-gather set
+template <class P>
+using DmaOK = Mf16OK<P>;
 
 // ops the K-wave launch (gemm.h gemm_kwave_kernel, CFG_KWAVE) is instantiated for
 template <class P>

@@ -154,7 +154,11 @@ void SyncRunner::set_units(const std::vector<RunnerUnit>& units) {
       // the last backward segment makes both safe
       if (u.kind == RunnerUnit::XGMI_REPL && u.seg != kSegments - 1)
         throw std::invalid_argument("the replicated xGMI bucket must be the last segment's");
-      if (opt_ == 0 && !u.v) throw std::invalid_argument("xGMI unit without Adam state");
+      // (an owner bucket's optimizer state exists only on its owner rank)
+      const bool owns = peer_->owner(u.bucket) < 0 || peer_->owner(u.bucket) == rank_;
+      if (owns && opt_ == 0 && !u.v) throw std::invalid_argument("xGMI unit without Adam state");
+      if (peer_->owner(u.bucket) >= 0 && peer_->owner(u.bucket) != u.host)
+        throw std::invalid_argument("xGMI owner bucket hosted on another rank than its unit");
     }
   }
   units_ = units;
@@ -497,8 +501,10 @@ void SyncRunner::issue_xgmi(const RunnerUnit& u, const float* lr_t, bool final_w
   XgmiUpdate up;
   const auto& r = u.ranges[0];
   up.opt = opt_;
-  up.m = u.m ? u.m + r.state_off : nullptr;
-  up.v = u.v ? u.v + r.state_off : nullptr;
+  // an owner bucket addresses its runs' state offsets itself (PeerExchange bucket spec)
+  const bool own = peer_->owner(u.bucket) >= 0;
+  up.m = u.m ? u.m + (own ? 0 : r.state_off) : nullptr;
+  up.v = u.v ? u.v + (own ? 0 : r.state_off) : nullptr;
   up.lr_t = lr_t[u.ps];
   up.c1 = 1.f - b1_;
   up.c2 = 1.f - b2_;

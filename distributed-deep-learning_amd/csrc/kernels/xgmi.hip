@@ -156,20 +156,24 @@ DDL_DEV bool check_piece(brsrc_t in, int off, int n4, const uint32_t* ck, int* e
 
 // The final wait of a step: every (bucket, owner, slice) DONE word of the step, except the
 // replicated bucket's (it has none), spread over all threads of the launch and polled at once.
+// An owner bucket's DONE words come from its one owner, an equal-chunk bucket's from every rank.
 DDL_DEV void final_wait(const XgmiLaunch& a, const uint32_t* myflags, int W, long long deadline) {
+  auto words = [&](int bb) {
+    return bb == a.repl_bucket ? 0 : (a.owners[bb] >= 0 ? 1 : W) * a.nslices[bb];
+  };
   int total = 0;
-  for (int bb = 0; bb < a.nbuckets; ++bb)
-    if (bb != a.repl_bucket) total += W * a.nslices[bb];
+  for (int bb = 0; bb < a.nbuckets; ++bb) total += words(bb);
   for (int k = blockIdx.x * 256 + threadIdx.x; k < total; k += gridDim.x * 256) {
     int bb = 0, x = k;
     for (;;) {
-      const int nb = bb == a.repl_bucket ? 0 : W * a.nslices[bb];
+      const int nb = words(bb);
       if (x < nb) break;
       x -= nb;
       ++bb;
     }
     const int q = x / a.nslices[bb], jj = x - q * a.nslices[bb];
-    wait_ge(myflags + done_idx(bb, q, jj), a.epoch, deadline, a.err, 2);
+    wait_ge(myflags + done_idx(bb, a.owners[bb] >= 0 ? a.owners[bb] : q, jj), a.epoch, deadline,
+            a.err, 2);
   }
 }
 
@@ -403,6 +407,93 @@ __global__ void __launch_bounds__(256) xgmi_repl_kernel(XgmiTable T, XgmiLaunch 
   if (a.final_wait) final_wait(a, myflags, W, deadline);
 }
 
+// One OWNER bucket: a tensor-granular plan's exchange unit — the ranges of
+// one PS's tensors that backward segment s completes — with a single owner, the rank hosting
+// that PS (reference: every worker Sends the PS's tensors to it, the PS sums the W arrivals,
+// applies Adam and Sends the parameters back, mnist_sync/parameter_server.py:52-69,
+// mnist_sync_sharding/parameter_server.py:108-126).  Workgroup j owns slice j of the unit; a
+// slice lies inside one run (plan-buffer range), so its gradient, parameters and optimizer state
+// are each one contiguous span.
+//   every rank but the owner: push my slice to the owner's inbox slot [me], drain, ARRIVE = e;
+//   the owner: wait for every peer's ARRIVE, sum the W contributions in rank order, update with
+//   the PS's state, store the parameters to EVERY rank (write-through), drain, DONE_q[owner] = e.
+// A non-owner's workgroups end after their push (unless they carry the step's final wait), so an
+// unbalanced plan (contiguous at W = 8: PS 7 owns 59 % of the bytes) loads only its owner's CUs
+// and links.  Same flags, bounds, error words and reuse argument as xgmi_ps_kernel: a rank
+// rewrites the owner's inbox slot only after its next forward, i.e. after its final wait saw the
+// owner's DONE, which the owner sets after reading that slot.
+template <int WT>
+__global__ void __launch_bounds__(256) xgmi_owner_kernel(XgmiTable T, XgmiLaunch a) {
+  constexpr int NQ = WT ? WT : kXgmiMaxPeers;
+  const int j = blockIdx.x, tid = threadIdx.x;
+  const int W = WT ? WT : a.world, me = a.rank, b = a.bucket, own = a.owner;
+  const long long deadline = wall_clock64() + a.timeout_ticks;
+  int r = 0;
+#pragma unroll
+  for (int k = 1; k < kXgmiMaxRuns; ++k)
+    if (k < a.nruns && j >= a.run_sl0[k]) r = k;
+  const int64_t s0 = (int64_t)(j - a.run_sl0[r]) * a.run_slice[r];
+  const int64_t s1 = s0 + a.run_slice[r] < a.run_n[r] ? s0 + a.run_slice[r] : a.run_n[r];
+  const int n4 = s0 < s1 ? (int)((s1 - s0) >> 2) : 0;
+  const int64_t lo = a.run_lo[r] + s0;    // plan-buffer offset of the slice
+  const int64_t vo = a.run_voff[r] + s0;  // its offset in the unit's inbox slot
+  uint32_t* myflags = T.flags[me];
+  __shared__ int arrived;
+  const float4* mine = reinterpret_cast<const float4*>(a.grads + lo);
+
+  if (me != own) {
+    const brsrc_t dst = make_rsrc(T.inbox[own] + a.inbox_off + (int64_t)me * a.c + vo,
+                                  (uint32_t)n4 * 16u);
+    for (int i = tid; i < n4; i += 256) {
+      const float4 x = mine[i];
+      st4_sys(dst, i * 16, a.coef != 1.f ? scale4(x, a.coef) : x);
+    }
+    drain_vm();
+    __syncthreads();
+    if (tid == 0) flag_store(T.flags[own] + arrive_idx(b, me, j), a.epoch);
+    if (a.final_wait) final_wait(a, myflags, W, deadline);
+    return;
+  }
+
+  if (tid == 0) arrived = 1;
+  __syncthreads();
+  if (tid < W && tid != me &&
+      !wait_ge(myflags + arrive_idx(b, tid, j), a.epoch, deadline, a.err, 1))
+    arrived = 0;  // (no update on a failed wait: see xgmi_ps_kernel)
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const int n4u = arrived ? n4 : 0;
+  const brsrc_t inbox = make_rsrc(T.inbox[me] + a.inbox_off, (uint32_t)(W * a.c * 4));
+  float4* m4 = a.m ? reinterpret_cast<float4*>(a.m + a.run_soff[r] + s0) : nullptr;
+  float4* v4 = a.v ? reinterpret_cast<float4*>(a.v + a.run_soff[r] + s0) : nullptr;
+  float4* w4 = reinterpret_cast<float4*>(T.params[me] + lo);
+  for (int i = tid; i < n4u; i += 256) {
+    float4 x[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      if (q < W)
+        x[q] = q == me ? (a.coef != 1.f ? scale4(mine[i], a.coef) : mine[i])
+                       : ld4_sys(inbox, (int)(((int64_t)q * a.c + vo) * 4) + i * 16);
+    float4 w = w4[i];
+    float4 g = f4zero();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)  // rank order, as the RCCL reduce and xgmi_ps_kernel
+      if (q < W) { g.x += x[q].x; g.y += x[q].y; g.z += x[q].z; g.w += x[q].w; }
+    update4(a, w, g, m4, v4, i);
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      if (k < W) {
+        const int q = (me + k + j) % W;
+        st4_sys(make_rsrc(T.params[q] + lo, (uint32_t)n4 * 16u), i * 16, w);
+      }
+    }
+  }
+  drain_vm();
+  __syncthreads();
+  if (tid < W) flag_store(T.flags[tid] + done_idx(b, me, j), a.epoch);
+  if (a.final_wait) final_wait(a, myflags, W, deadline);
+}
+
 #define X_CHECK(x)                                                                        \
   do {                                                                                    \
     hipError_t e_ = (x);                                                                  \
@@ -418,33 +509,100 @@ struct HandleBlob {  // what one rank publishes (exchanged as bytes over the def
 
 }  // namespace
 
+static std::vector<XgmiBucketSpec> equal_specs(
+    const std::vector<std::pair<int64_t, int64_t>>& buckets) {
+  std::vector<XgmiBucketSpec> v;
+  for (const auto& b : buckets) {
+    XgmiBucketSpec s;
+    s.runs.push_back(b);
+    v.push_back(s);
+  }
+  return v;
+}
+
 PeerExchange::PeerExchange(float* params, const float* grads, int64_t total, int world, int rank,
                            const std::vector<std::pair<int64_t, int64_t>>& buckets, int max_slices,
+                           int repl_bucket)
+    : PeerExchange(params, grads, total, world, rank, equal_specs(buckets), max_slices,
+                   repl_bucket) {}
+
+PeerExchange::PeerExchange(float* params, const float* grads, int64_t total, int world, int rank,
+                           const std::vector<XgmiBucketSpec>& buckets, int max_slices,
                            int repl_bucket)
     : params_(params), grads_(grads), total_(total), world_(world), rank_(rank),
       repl_(repl_bucket) {
   if (world < 1 || world > kXgmiMaxPeers) throw std::invalid_argument("xgmi: world out of range");
   if (rank < 0 || rank >= world) throw std::invalid_argument("xgmi: rank out of range");
   if (buckets.empty() || (int)buckets.size() > kXgmiMaxBuckets)
-    throw std::invalid_argument("xgmi: 1..8 buckets");
+    throw std::invalid_argument("xgmi: 1..32 buckets");
   if (max_slices < 1 || max_slices > kXgmiMaxSlices)
     throw std::invalid_argument("xgmi: max_slices out of range");
   if (reinterpret_cast<uintptr_t>(params) % 16 || reinterpret_cast<uintptr_t>(grads) % 16)
     throw std::invalid_argument("xgmi: buffers must be 16-B aligned");
   if (repl_bucket >= (int)buckets.size()) throw std::invalid_argument("xgmi: replicated bucket");
+  init(buckets, max_slices);
+}
+
+void PeerExchange::init(const std::vector<XgmiBucketSpec>& buckets, int max_slices) {
+  const int world = world_;
   int64_t inbox = 0;
   for (size_t bi = 0; bi < buckets.size(); ++bi) {
-    const auto& bk = buckets[bi];
-    const int64_t lo = bk.first, hi = bk.second;
-    const bool repl = (int)bi == repl_bucket;
-    if (lo < 0 || hi > total || hi <= lo) throw std::invalid_argument("xgmi: bucket out of range");
+    const XgmiBucketSpec& sp = buckets[bi];
+    const bool repl = (int)bi == repl_;
+    Bucket B;
+    B.owner = sp.owner;
+    B.inbox_off = inbox;
+    if (sp.owner >= 0) {
+      // owner bucket: the runs concatenated; each run sliced on its own (a slice never crosses
+      // a run), >= 1024 elements per slice, at most max_slices slices over the whole unit
+      if (sp.owner >= world) throw std::invalid_argument("xgmi: bucket owner out of range");
+      if (repl) throw std::invalid_argument("xgmi: an owner bucket cannot be replicated");
+      if (sp.runs.empty() || (int)sp.runs.size() > kXgmiMaxRuns ||
+          sp.state_offs.size() != sp.runs.size())
+        throw std::invalid_argument("xgmi: owner bucket needs 1..8 runs with state offsets");
+      int64_t n = 0;
+      for (size_t r = 0; r < sp.runs.size(); ++r) {
+        const int64_t lo = sp.runs[r].first, hi = sp.runs[r].second;
+        if (lo < 0 || hi > total_ || hi <= lo || (hi - lo) % 4 || lo % 4 || sp.state_offs[r] % 4)
+          throw std::invalid_argument("xgmi: owner-bucket run out of range or not 16-B shaped");
+        n += hi - lo;
+      }
+      int64_t ns = (n + 1023) / 1024;
+      if (ns > max_slices) ns = max_slices;
+      if (ns < (int64_t)sp.runs.size()) ns = (int64_t)sp.runs.size();
+      const int64_t per = ((n + ns - 1) / ns + 3) & ~(int64_t)3;
+      int sl = 0;
+      int64_t voff = 0;
+      for (size_t r = 0; r < sp.runs.size(); ++r) {
+        const int64_t rn = sp.runs[r].second - sp.runs[r].first;
+        B.run_lo.push_back(sp.runs[r].first);
+        B.run_n.push_back(rn);
+        B.run_soff.push_back(sp.state_offs[r]);
+        B.run_voff.push_back(voff);
+        B.run_slice.push_back(per);
+        B.run_sl0.push_back(sl);
+        sl += (int)((rn + per - 1) / per);
+        voff += rn;
+      }
+      B.run_sl0.push_back(sl);
+      if (sl > kXgmiMaxSlices) throw std::invalid_argument("xgmi: owner bucket has too many slices");
+      B.lo = sp.runs[0].first;
+      B.c = n;
+      B.slice = per;
+      B.nslice = sl;
+      if (n * 4 * world > 0x7fffffffLL) throw std::invalid_argument("xgmi: bucket too large");
+      inbox += n * world;
+      bk_.push_back(B);
+      continue;
+    }
+    if (sp.runs.size() != 1) throw std::invalid_argument("xgmi: equal-chunk bucket needs one range");
+    const int64_t lo = sp.runs[0].first, hi = sp.runs[0].second;
+    if (lo < 0 || hi > total_ || hi <= lo) throw std::invalid_argument("xgmi: bucket out of range");
     if ((hi - lo) % (repl ? 4 : 4 * world))
       throw std::invalid_argument("xgmi: bucket not divisible by 4W (replicated: by 4)");
-    Bucket B;
     B.lo = lo;
     // owner buckets: this rank's chunk; the replicated bucket: all of it
     B.c = repl ? hi - lo : (hi - lo) / world;
-    B.inbox_off = inbox;
     // >= 1024 elements (4 KB) per workgroup slice, at most max_slices workgroups
     int64_t ns = (B.c + 1023) / 1024;
     if (ns > max_slices) ns = max_slices;
@@ -531,8 +689,9 @@ void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool 
   if (!opened_ok_) throw std::runtime_error("xgmi: open() the peer handles first");
   if (bucket < 0 || bucket >= (int)bk_.size()) throw std::invalid_argument("xgmi: bucket index");
   const Bucket& B = bk_[bucket];
-  if (u.opt != 2 && !u.m) throw std::invalid_argument("xgmi: optimizer state missing");
-  if (u.opt == 0 && !u.v) throw std::invalid_argument("xgmi: Adam needs v");
+  const bool owns = B.owner < 0 || B.owner == rank_;  // runs the update of (part of) the bucket
+  if (owns && u.opt != 2 && !u.m) throw std::invalid_argument("xgmi: optimizer state missing");
+  if (owns && u.opt == 0 && !u.v) throw std::invalid_argument("xgmi: Adam needs v");
   XgmiLaunch a;
   memset(&a, 0, sizeof(a));
   a.world = world_;
@@ -562,6 +721,30 @@ void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool 
   a.timeout_ticks = (long long)(timeout_s_ * 1e8);  // wall_clock64: 100 MHz
   a.check = check_ ? 1 : 0;
   a.repl_bucket = repl_;
+  for (size_t i = 0; i < bk_.size(); ++i) a.owners[i] = bk_[i].owner;
+  for (int i = (int)bk_.size(); i < kXgmiMaxBuckets; ++i) a.owners[i] = -1;
+  if (B.owner >= 0) {
+    a.owner = B.owner;
+    a.nruns = (int)B.run_lo.size();
+    for (int r = 0; r < a.nruns; ++r) {
+      a.run_lo[r] = B.run_lo[r];
+      a.run_n[r] = B.run_n[r];
+      a.run_soff[r] = B.run_soff[r];
+      a.run_voff[r] = B.run_voff[r];
+      a.run_slice[r] = B.run_slice[r];
+      a.run_sl0[r] = B.run_sl0[r];
+    }
+    a.run_sl0[a.nruns] = B.run_sl0[a.nruns];
+    switch (world_) {
+#define X_CASE(N) \
+  case N: DDL_LAUNCH(xgmi_owner_kernel<N>, dim3(B.nslice), dim3(256), 0, st, table_, a); break;
+      X_CASE(1) X_CASE(2) X_CASE(3) X_CASE(4) X_CASE(5) X_CASE(6) X_CASE(7) X_CASE(8)
+#undef X_CASE
+      default: DDL_LAUNCH(xgmi_owner_kernel<0>, dim3(B.nslice), dim3(256), 0, st, table_, a);
+    }
+    DDL_CHECK_LAUNCH();
+    return;
+  }
   if (bucket == repl_) {
     switch (world_) {
 #define X_CASE(N) \

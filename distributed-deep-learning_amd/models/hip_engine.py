@@ -90,6 +90,15 @@ class HipEngine:
     def get_wide(self) -> List[int]:
         return list(self.eng.get_wide())
 
+    def set_order(self, order: List[int]) -> None:
+        """Per-op split-K block order: 0 round-robin over the XCDs, 1-3 XCD-contiguous with the
+        K splits / M rows / N tiles grouped on one XCD (csrc/kernels/gemm.h split_coords)."""
+        self.eng.set_order(list(order))
+        self.graphs = None
+
+    def get_order(self) -> List[int]:
+        return list(self.eng.get_order())
+
     def set_concurrent(self, on: bool) -> None:
         """Weight-gradient GEMMs on a second stream (fork/join per backward segment)."""
         self.eng.set_concurrent(bool(on))

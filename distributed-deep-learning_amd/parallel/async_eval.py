@@ -40,20 +40,20 @@ class AsyncEvaluator:
         self.tr = tr
         self.on_result = on_result
         dev = tr.params.device
-        # DDL_EVAL_PRIORITY=train (default): training on the high-priority stream, so when a CU
-        # frees up the dispatcher prefers the latency-bound training blocks and the eval's large
-        # GEMMs fill the rest.  =eval: the reverse (the evals are the time-to-accuracy critical
-        # path: training is far ahead of the eval queue, and every training kernel run before
-        # the target eval delays it).  Measured the same time to 95 % either way (0.1404-0.1417
-        # vs 0.1415-0.1422 s, profiles/r3_ab_evalprio.log): the queues' priority barely moves
-        # the dispatcher once both streams have work
-        # The training stream itself is NORMAL priority either way, the eval stream low (or
-        # high with =eval): the native runners' GPU-side gates rely on the training (compute)
-        # stream never sharing a hardware queue with their high-priority comm / PS-service
-        # streams, and HIP pools hardware queues per priority (runner.hip, async_runner.hip;
-        # a high-priority training stream stalled the W = 2 one-card time-to-accuracy run).
+        # Stream priorities.  torch's HIP stream pool offers priorities <= 0 only (a positive
+        # request maps to 0), so "low" does not exist here: by default (DDL_EVAL_PRIORITY=train)
+        # the eval stream and the training stream are both NORMAL priority (0) and share the
+        # normal hardware-queue pool; with =eval the eval stream is HIGH priority (-1), so when a
+        # CU frees up the dispatcher prefers the eval's GEMMs (the evals are the time-to-accuracy
+        # critical path).  Measured the same time to 95 % either way (0.1404-0.1417 vs
+        # 0.1415-0.1422 s, profiles/r3_ab_evalprio.log).
+        # The training stream is NORMAL priority in both modes: the native runners' GPU-side
+        # gates rely on the training (compute) stream never sharing a hardware queue with their
+        # high-priority comm / PS-service streams, and HIP pools hardware queues per priority
+        # (runner.hip, async_runner.hip; a high-priority training stream stalled the W = 2
+        # one-card time-to-accuracy run).
         eval_first = os.environ.get("DDL_EVAL_PRIORITY", "train") == "eval"
-        self.stream = torch.cuda.Stream(device=dev, priority=-1 if eval_first else 1)
+        self.stream = torch.cuda.Stream(device=dev, priority=-1 if eval_first else 0)
         self.train_stream = torch.cuda.Stream(device=dev, priority=0)
         self.snap = torch.empty_like(tr.params)
         chunk = int(os.environ.get("DDL_EVAL_CHUNK", "10000"))

@@ -292,7 +292,8 @@ class Trainer:
             aeval = AsyncEvaluator(self, on_result=on_eval)
             torch.cuda.synchronize()
             clock = metrics.Clock()
-        # with the side-stream eval, training runs on the evaluator's high-priority stream
+        # with the side-stream eval, training runs on the evaluator's training stream (NORMAL
+        # priority: the native runners' gates need it off the high-priority queue pool)
         train_ctx = (torch.cuda.stream(aeval.train_stream) if aeval is not None
                      else contextlib.nullcontext())
         with train_ctx:

@@ -89,19 +89,53 @@ def synthetic_mnist(n_train: int = TRAIN_SIZE, n_test: int = TEST_SIZE,
     return Dataset(xtr, ytr, xte, yte, "synthetic")
 
 
+# The only globals a pickle of numpy arrays needs (numpy 1.x and 2.x module paths): the array
+# reconstructor, the ndarray / dtype types and the buffer constructor of newer protocols, plus
+# _codecs.encode, which protocol-2 pickles written by python 3 use to rebuild a bytes object
+# (it only encodes a string).
+_NUMPY_GLOBALS = {
+    ("_codecs", "encode"),
+    ("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct"),
+    ("numpy", "ndarray"), ("numpy", "dtype"),
+    ("numpy.core.multiarray", "scalar"), ("numpy._core.multiarray", "scalar"),
+    ("numpy.core.numeric", "_frombuffer"), ("numpy._core.numeric", "_frombuffer"),
+}
+
+
+class _ArrayOnlyUnpickler:
+    """``pickle.Unpickler`` that reconstructs numpy arrays, tuples, lists and scalars and
+    refuses every other global: a crafted ``mnist.pkl`` cannot run code (the reference
+    unpickles without restriction, ``mnist_sync/model/model.py:8-9``)."""
+
+    def __new__(cls, f):
+        import pickle
+
+        class _U(pickle.Unpickler):
+            def find_class(self, module, name):
+                if (module, name) in _NUMPY_GLOBALS:
+                    return super().find_class(module, name)
+                raise pickle.UnpicklingError(
+                    f"refusing global {module}.{name} in a dataset pickle (numpy arrays only)")
+        return _U(f, encoding="latin1")
+
+
+def load_pickle_arrays(f):
+    """Unpickle a dataset file that may hold only numpy arrays (tuples / lists of them)."""
+    return _ArrayOnlyUnpickler(f).load()
+
+
 def load_file(path: str) -> Dataset:
     """Load ``.npz`` (x_train, y_train, x_test, y_test) or the reference ``mnist.pkl[.gz]``.
 
-    The pickle format is only read from a user-supplied path (the reference tree ships
-    no data); prefer converting it once to ``.npz``."""
+    The pickle format is read only from a user-supplied path (the reference tree ships no
+    data) and only through an unpickler that admits numpy arrays (load_pickle_arrays)."""
     if path.endswith(".npz"):
         d = np.load(path, allow_pickle=False)
         xtr, ytr, xte, yte = d["x_train"], d["y_train"], d["x_test"], d["y_test"]
     else:
-        import pickle  # user-provided dataset in the reference's format
         opener = gzip.open if path.endswith(".gz") else open
         with opener(path, "rb") as f:
-            (xtr, ytr), _, (xte, yte) = pickle.load(f, encoding="latin1")
+            (xtr, ytr), _, (xte, yte) = load_pickle_arrays(f)
     t = lambda a, dt: torch.as_tensor(np.asarray(a), dtype=dt)  # noqa: E731
     return Dataset(t(xtr, torch.float32).reshape(-1, INPUT_DIM), t(ytr, torch.int64),
                    t(xte, torch.float32).reshape(-1, INPUT_DIM), t(yte, torch.int64),

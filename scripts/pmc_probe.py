@@ -21,6 +21,14 @@ if os.environ.get("DDL_PROBE_MF16") == "1":  # conv backward on CFG_MF16 (splits
         cfg[op], spl[op] = 14, spl[op] * 2
     e.set_cfg(cfg)
     e.set_splits(spl)
+if os.environ.get("DDL_PROBE_SCHED"):  # a runner_tune.py / sched JSON (cfg, splits, ...)
+    import json
+    sc = json.load(open(os.environ["DDL_PROBE_SCHED"]))
+    e = tr.engine.eng
+    e.set_cfg(sc["cfg"])
+    e.set_splits(sc["splits"])
+    e.set_workers(sc["workers"])
+    e.set_wide(sc["wide"])
 for i in range(int(os.environ.get("STEPS", "20"))):
     tr.train_step(i)
 torch.cuda.synchronize()

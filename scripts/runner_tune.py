@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from op_bench import OPS  # noqa: E402
 
-STREAMK_OK = {1, 2, 3, 10, 11, 12, 13, 14}  # conv GEMMs (big enough for stream-K)
+STREAMK_OK = {1, 2, 3, 10, 11, 12, 13, 14, 15}  # conv GEMMs (K-mapped stream-K on the tap windows)
 KWAVE_OK = {4, 5, 6, 8}  # fc forward / data-gradient GEMMs (csrc/kernels/layers.h KWaveOK)
 MF16_OK = {1, 2, 3, 10, 11, 12, 13, 14, 15}  # conv GEMMs with 16-byte gathers (layers.h Mf16OK)
 
@@ -32,6 +32,10 @@ def main():
     ap.add_argument("--multiwave", action="store_true",
                     help="also try the multi-wave block tiles (configs 1, 2, 6, 7, 8) on the "
                          "forward convolutions (not dual-launched, so any tile config runs)")
+    ap.add_argument("--verbose", action="store_true", help="print every candidate's time")
+    ap.add_argument("--dma", action="store_true",
+                    help="also try the generic LDS-DMA multi-fragment tiles (configs 16-18) on "
+                         "the conv GEMMs, at 0.5x / 1x / 2x / 4x the split")
     a = ap.parse_args()
     import torch
     from ddl_amd.config import TrainConfig
@@ -80,7 +84,7 @@ def main():
             out.append(mk(c, s2, 0, wd))
         out.append(mk(c, s, w, 1 if wd > 1 else W))            # toggle the reduce mode
         if op in STREAMK_OK:
-            for w2 in (1024, 2048, 3072):
+            for w2 in (512, 1024, 1536, 2048, 3072):
                 if w2 != w:
                     out.append(mk(c, 1, w2, wd))
             if w:
@@ -92,6 +96,11 @@ def main():
             for s2 in sorted({s, min(2048, s * 2)}):
                 if (c, s) != (14, s2):
                     out.append(mk(14, s2, 0, wd))
+        if op in MF16_OK and a.dma:  # generic LDS-DMA tiles 64x32 / 32x64 / 64x64 (16 / 17 / 18)
+            for c2 in (16, 17, 18, 19, 20):
+                for s2 in sorted({s, min(2048, s * 2), min(2048, s * 4), max(1, s // 2)}):
+                    if (c, s) != (c2, s2):
+                        out.append(mk(c2, s2, 0, wd))
         if a.multiwave and op in (0, 1, 2, 3):
             for c2 in (1, 2, 6, 7, 8):
                 for s2 in sorted({s, min(2048, s * 2), max(1, s // 2)}):
@@ -111,6 +120,10 @@ def main():
             best, best_t = None, None
             for cand in cands(op):
                 t = timed(cand)
+                if a.verbose:
+                    print(f"    {name:12s} c{cand['cfg'][op]} s{cand['splits'][op]} "
+                          f"w{cand['workers'][op]} {'inl' if cand['wide'][op] > 1 else 'wide'} "
+                          f"{t:.1f}", flush=True)
                 if best_t is None or t < best_t:
                     best, best_t = cand, t
             # head-to-head re-measure of the incumbent vs the best candidate

@@ -20,6 +20,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--splits-variants", default="",
                     help="';'-separated split overrides of the defaults, each 'op=s,op=s'")
+    ap.add_argument("--cfg-variants", default="",
+                    help="';'-separated tile-config overrides 'op=cfg[:split],...' (name=... first "
+                         "to label it)")
+    ap.add_argument("--order-variants", default="",
+                    help="';'-separated block-order overrides (gemm.h split_coords), 'op=o,op=o'")
     a = ap.parse_args()
     import torch
     from ddl_amd.config import TrainConfig
@@ -33,7 +38,8 @@ def main():
     tr = Trainer(cfg, env, dataset=synthetic_mnist())
     e = tr.engine.eng
     scheds = {"default": {"cfg": e.get_cfg(), "splits": e.get_splits(),
-                          "workers": e.get_workers(), "wide": e.get_wide()}}
+                          "workers": e.get_workers(), "wide": e.get_wide(),
+                          "order": e.get_order()}}
     for p in a.tuned:
         scheds[os.path.basename(p)] = json.load(open(p))
     for v in filter(None, a.splits_variants.split(";")):
@@ -42,6 +48,26 @@ def main():
             op, val = kv.split("=")
             sp[int(op)] = int(val)
         scheds["splits[" + v + "]"] = dict(scheds["default"], splits=sp)
+    for v in filter(None, a.cfg_variants.split(";")):
+        cf = list(scheds["default"]["cfg"])
+        sp = list(scheds["default"]["splits"])
+        label = v
+        for kv in v.split(","):
+            if kv.startswith("name="):
+                label = kv[5:]
+                continue
+            op, val = kv.split("=")
+            c, _, spl = val.partition(":")
+            cf[int(op)] = int(c)
+            if spl:
+                sp[int(op)] = int(spl)
+        scheds["cfg[" + label + "]"] = dict(scheds["default"], cfg=cf, splits=sp)
+    for v in filter(None, a.order_variants.split(";")):
+        od = list(scheds["default"]["order"])
+        for kv in v.split(","):
+            op, val = kv.split("=")
+            od[int(op)] = int(val)
+        scheds["order[" + v + "]"] = dict(scheds["default"], order=od)
     res = {k: [] for k in scheds}
     step = 0
     for _ in range(a.rounds):
@@ -50,6 +76,7 @@ def main():
             e.set_splits(s["splits"])
             e.set_workers(s["workers"])
             e.set_wide(s["wide"])
+            e.set_order(s.get("order", scheds["default"]["order"]))
             for _ in range(20):
                 tr.train_step(step)
                 step += 1
@@ -61,7 +88,7 @@ def main():
             torch.cuda.synchronize()
             res[name].append(1e6 * (time.perf_counter() - t0) / a.steps)
     for name, ts in res.items():
-        print(f"{name:24s} us/step min {min(ts):7.1f}  all {' '.join(f'{t:.1f}' for t in ts)}")
+        print(f"{name:48s} us/step min {min(ts):7.1f}  all {' '.join(f'{t:.1f}' for t in ts)}")
 
 
 if __name__ == "__main__":

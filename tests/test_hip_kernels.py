@@ -253,6 +253,29 @@ def test_split_k_variants_agree(setup):
             assert err < tol, (t.name, name, err, e32)
 
 
+@pytest.mark.parametrize("order", [1, 2, 3])
+def test_block_orders_are_bit_identical(setup, order):
+    """Every split-K block order (gemm.h split_coords: XCD-contiguous renumbering with the K
+    splits, M rows or N tiles grouped) on every op — forward convs on the 3-D split-K grid,
+    the backward dual launches, in-launch and wide reduces — gives the default order's bits:
+    the partial slab and tickets are indexed by (tile, split), not by block id."""
+    eng, flat, params, grads, x, y = setup
+    base = eng.get_order()
+    grads.zero_()
+    eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 41)
+    torch.cuda.synchronize()
+    ref = grads.clone()
+    try:
+        eng.set_order([order] * len(base))
+        for _ in range(2):
+            grads.zero_()
+            eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 41)
+            torch.cuda.synchronize()
+            assert torch.equal(grads, ref), f"order {order}"
+    finally:
+        eng.set_order(base)
+
+
 @pytest.mark.parametrize("cfg", [None, 0, 1, 2, 4, 5, 6, 7, 8])
 def test_stream_k_matches_reference(setup, cfg):
     """Stream-K schedules (several worker counts, every tile config) give the fp64-reference
@@ -394,6 +417,55 @@ def test_mf16_config_matches_reference(setup, mode):
         check_grads(outs[0], flat, x, y, 0.5, 66)
         pv = param_views(flat, CANON_OFFSETS)
         pooled, _, _ = ref_intermediates(pv, x, 0.5, 66)
+        for name, ref in zip(["p1", "p2", "p3", "p4"], pooled):
+            got = eng.eng.buffer(name, x.shape[0])
+            assert rel_err(got.reshape(ref.shape), ref) < 2e-5, name
+    finally:
+        eng.set_dual(True)
+        eng.set_cfg(base[0])
+        eng.set_splits(base[1])
+        eng.set_workers(base[2])
+        eng.set_wide(base[3])
+
+
+@pytest.mark.parametrize("tile", [16, 17, 18, 19, 20])
+@pytest.mark.parametrize("mode", ["default", "split1", "wide", "nodual"])
+def test_dma_g_configs_match_reference(setup, tile, mode):
+    """The LDS-DMA tiles — one-wave multi-fragment (CFG_DMA_64x32 / 32x64 / 64x64 = 16 / 17 / 18,
+    gemm.h mainloop_dma_g: K- and MN-contiguous images, the ones-row patch of the weight
+    gradients) and the 32x32 ring tiles (CFG_RING3 / CFG_RING2 = 19 / 20, mainloop_ring: 3 / 2
+    LDS images, next tiles' DMAs inside the MFMA cluster, split-K 1 = long K loops) — on
+    every conv GEMM, under every schedule that consumes their 2- and 4-fragment accumulators —
+    fused epilogue (split 1), in-launch reduce, wide reduce, dual and back-to-back launches (and
+    the conv2 dual fused with conv1's weight gradient): fp32 / fp64 autograd gradients,
+    bit-deterministic across reruns, forward activations within fp32 noise."""
+    eng, flat, params, grads, x, y = setup
+    base = (eng.get_cfg(), eng.get_splits(), eng.get_workers(), eng.get_wide())
+    cfg, spl, wrk, wide = (list(v) for v in base)
+    for op in MF16_OPS:
+        cfg[op], wrk[op] = tile, 0
+        if mode == "split1":
+            spl[op] = 1
+        elif mode == "wide":
+            spl[op], wide[op] = max(2, spl[op]), 1
+        else:
+            spl[op] = max(1, spl[op])
+    try:
+        eng.set_cfg(cfg)
+        eng.set_splits(spl)
+        eng.set_workers(wrk)
+        eng.set_wide(wide)
+        eng.set_dual(mode != "nodual")
+        outs = []
+        for _ in range(2):
+            grads.zero_()
+            eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 67)
+            torch.cuda.synchronize()
+            outs.append(grads.clone())
+        assert torch.equal(outs[0], outs[1])
+        check_grads(outs[0], flat, x, y, 0.5, 67)
+        pv = param_views(flat, CANON_OFFSETS)
+        pooled, _, _ = ref_intermediates(pv, x, 0.5, 67)
         for name, ref in zip(["p1", "p2", "p3", "p4"], pooled):
             got = eng.eng.buffer(name, x.shape[0])
             assert rel_err(got.reshape(ref.shape), ref) < 2e-5, name

@@ -134,6 +134,43 @@ def test_npz_loader(tmp_path):
     assert d.x_train.shape == (10, 784) and int(d.y_test[3]) == 3
 
 
+@pytest.mark.parametrize("gz", [False, True])
+def test_reference_pickle_loads_arrays(tmp_path, gz):
+    """The reference's mnist.pkl layout ((train, valid, test) tuples of numpy arrays, protocol 2
+    as written by python 2 and the current protocol) loads through the array-only unpickler."""
+    import gzip
+    import pickle
+    rng = np.random.default_rng(0)
+    tr = (rng.random((6, 784), dtype=np.float32), np.arange(6, dtype=np.int64))
+    va = (np.zeros((2, 784), np.float32), np.zeros(2, np.int64))
+    te = (rng.random((3, 784), dtype=np.float32), np.array([7, 8, 9]))
+    for proto in (2, pickle.HIGHEST_PROTOCOL):
+        f = tmp_path / f"m{proto}.pkl{'.gz' if gz else ''}"
+        with (gzip.open if gz else open)(f, "wb") as h:
+            pickle.dump((tr, va, te), h, protocol=proto)
+        d = load_file(str(f))
+        assert torch.equal(d.x_train, torch.from_numpy(tr[0]))
+        assert d.y_test.tolist() == [7, 8, 9]
+
+
+class _Evil:
+    def __reduce__(self):
+        import os
+        return (os.system, ("echo pwned",))
+
+
+def test_reference_pickle_refuses_other_globals(tmp_path):
+    """A pickle carrying any global but the numpy array reconstructors is refused before
+    anything it names is called."""
+    import pickle
+    arr = (np.zeros((1, 784), np.float32), np.zeros(1, np.int64))
+    for payload in [(arr, arr, (_Evil(), arr[1])), (arr, arr, (arr[0], [print]))]:
+        f = tmp_path / "evil.pkl"
+        f.write_bytes(pickle.dumps(payload))
+        with pytest.raises(pickle.UnpicklingError, match="refusing global"):
+            load_file(str(f))
+
+
 def test_batch_indices_semantics():
     # reference: every worker walks the same slices (Q5)
     assert batch_indices(3, 100, 50000, rank=2, world=4) == (300, 400)
