@@ -253,6 +253,13 @@ def main(argv=None):
         tr = make_trainer(chosen)
     keep.append(tr)
     cfg = tr.cfg
+    # W > 1 (or the forced 1-rank rehearsal), sync, native runner: prove the READY-flag hand-off
+    # on this job before the timed run (bit-identical to the event hand-off on every rank, else
+    # every rank falls back to the events); the verdict goes into the JSON config
+    handoff = None
+    if (a.mode == "sync" and hasattr(tr.exchange, "handoff_check")
+            and (world > 1 or a.force_collectives)):
+        handoff = tr.exchange.handoff_check(tr)
 
     def timed_run(t):
         """prewarm + warmup (untimed), then exactly a.steps steps between barrier+sync pairs;
@@ -282,27 +289,31 @@ def main(argv=None):
     plans = {}
     extra = [p for p in a.extra_plans.split(",") if p and p != a.shard]
     if world > 1 and a.mode == "sync" and extra:
+        # each plan over RCCL (grouped reduce / broadcast) and over the xGMI owner buckets (one
+        # push / owner update / pull kernel per unit); a shared-GPU rehearsal has no RCCL
         for p in extra:
-            try:
-                t = make_trainer("rccl", shard=p)
-                keep.append(t)
-                el = timed_run(t)
-                plans[p] = {"ms_per_step": round(1e3 * el / a.steps, 4),
-                            "value": round(world * a.batch_size * a.steps / el, 1),
-                            "exchange": backend_of(t), "num_ps": t.num_ps}
-            except RuntimeError as e:
-                plans[p] = {"error": str(e)[:200]}
+            for be in (["xgmi"] if shared_gpu else ["rccl", "xgmi"]):
+                key = p if be == "rccl" or shared_gpu else f"{p}/xgmi"
+                try:
+                    t = make_trainer(be, shard=p)
+                    keep.append(t)
+                    el = timed_run(t)
+                    plans[key] = {"ms_per_step": round(1e3 * el / a.steps, 4),
+                                  "value": round(world * a.batch_size * a.steps / el, 1),
+                                  "exchange": backend_of(t), "num_ps": t.num_ps}
+                except RuntimeError as e:
+                    plans[key] = {"error": str(e)[:200]}
 
     # the record's facts about the benchmarked trainer, taken before any release below
     engine_name = getattr(tr.engine, "name", a.engine)
     num_ps, policy, exchange_name = tr.num_ps, tr.plan.policy, backend_of(tr)
-    # W > 1 sync: close and drop every trainer built so far (collectively, between barriers,
-    # nothing in flight) before each time-to-accuracy run.  Kept alive, their streams and peer
-    # mappings add hardware queues per process; with several processes on ONE card that
-    # stalled the time-to-accuracy runs (docs/DESIGN.md, "W = 4 on one card").
-    # DDL_BENCH_RELEASE=0 keeps them to the end as before.
-    release = (world > 1 and a.mode == "sync"
-               and os.environ.get("DDL_BENCH_RELEASE", "1") == "1")
+    # W > 1 (sync, and async after its exchange joined): close and drop every trainer built so
+    # far (collectively, between barriers, nothing in flight) before each time-to-accuracy run —
+    # close() releases each runner's comm stream, events, flags and peer mappings, the side-
+    # stream evaluator its own streams.  Kept alive, they add hardware queues per process; with
+    # several processes on ONE card that stalled the time-to-accuracy runs (docs/DESIGN.md,
+    # "W = 4 on one card").  DDL_BENCH_RELEASE=0 keeps them to the end as before.
+    release = world > 1 and os.environ.get("DDL_BENCH_RELEASE", "1") == "1"
 
     def release_all():
         import gc
@@ -380,12 +391,17 @@ def main(argv=None):
                 # the throughput window's batches: worker r reads batch r, r + W, ... (per-step
                 # work and traffic are the same under the reference's replicate protocol)
                 "data_sharding": "stride",
+                "handoff": (handoff["handoff"] if handoff
+                            else "n/a (W = 1, local updates)" if world == 1
+                            else "n/a (no native runner)"),
             },
             "test_acc_after_run": round(acc, 4),
             "prewarm": {"steps": n_pre, "note": "untimed steps before the warmup steps: the "
                         "GPU is still ramping up after a few steps (20-step window after 5 "
                         "warmup steps: 0.322 vs 0.308 ms/step after 100)"},
         }
+        if handoff:
+            rec["handoff_check"] = handoff
         if ab:
             rec["exchange_ab"] = ab
         if plans:

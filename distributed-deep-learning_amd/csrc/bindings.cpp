@@ -309,6 +309,16 @@ class PyPeer {
     for (int b = 0; b < p_->num_buckets(); ++b) v.push_back(p_->nslices(b));
     return v;
   }
+  void close() {
+    c10::hip::HIPGuard guard(params_.device().index());
+    py::gil_scoped_release nogil;
+    p_->close();
+  }
+  // -1: equal-chunk bucket; else the rank hosting the owner bucket's PS
+  int owner(int64_t b) const {
+    TORCH_CHECK(b >= 0 && b < p_->num_buckets(), "bucket out of range");
+    return p_->owner((int)b);
+  }
   ddl::PeerExchange* raw() { return p_.get(); }
 
  private:
@@ -367,6 +377,11 @@ class PyAsyncPeer {
     u.mu = (float)mu;
     u.scale = (float)scale;
     p_->apply((int)ps, (int)worker, (uint32_t)epoch, u, ps_params.data_ptr<float>(), cur_stream());
+  }
+  void close() {
+    c10::hip::HIPGuard guard(params_.device().index());
+    py::gil_scoped_release nogil;
+    p_->close();
   }
   int error() const { return p_->error(); }
   ddl::AsyncPeer* raw() { return p_.get(); }
@@ -599,12 +614,18 @@ class PyRunner {
         return x.data_ptr<float>();
       };
       int64_t need_state = 0, need_shard = 0;
+      if (t.size() == 9) u.bucket = t[8].cast<int>();
+      // an xGMI OWNER bucket (tensor-granular plan): its owner updates the whole unit
+      const bool owner_bucket = u.kind == ddl::RunnerUnit::XGMI && r_->peer() &&
+                                u.bucket >= 0 && u.bucket < r_->peer()->num_buckets() &&
+                                r_->peer()->owner(u.bucket) >= 0;
       for (auto r : t[4].cast<py::list>()) {
         auto rr = r.cast<py::tuple>();
         ddl::RunnerRange range{rr[0].cast<int64_t>(), rr[1].cast<int64_t>(), rr[2].cast<int64_t>()};
         TORCH_CHECK(0 <= range.lo && range.lo <= range.hi && range.hi <= n, "range out of bounds");
         int64_t len = range.hi - range.lo;
-        if (u.kind == ddl::RunnerUnit::RS || u.kind == ddl::RunnerUnit::XGMI) {  // (AR and
+        if (u.kind == ddl::RunnerUnit::RS ||
+            (u.kind == ddl::RunnerUnit::XGMI && !owner_bucket)) {  // (AR and
           // XGMI_REPL update the whole range on every rank: state for all of it)
           // reduce-scatter: this rank updates (and needs state / a shard buffer for) 1/W of it;
           // a remainder would silently get no exchange and no update
@@ -619,7 +640,6 @@ class PyRunner {
       u.m = opt_ptr(t[5], need_state, "m");
       u.v = opt_ptr(t[6], need_state, "v");
       u.shard = opt_ptr(t[7], need_shard, "shard");
-      if (t.size() == 9) u.bucket = t[8].cast<int>();
       out.push_back(std::move(u));
     }
     r_->set_units(out);
@@ -791,6 +811,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("attach_done", &PyAsyncPeer::attach_done)
       .def("wait_done", &PyAsyncPeer::wait_done)
       .def("apply", &PyAsyncPeer::apply)
+      .def("close", &PyAsyncPeer::close)
       .def("error", &PyAsyncPeer::error);
 
   py::class_<PyAsyncService>(m, "AsyncService")
@@ -839,7 +860,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("handle", &PyPeer::handle)
       .def("open", &PyPeer::open)
       .def("error", &PyPeer::error)
-      .def("nslices", &PyPeer::nslices);
+      .def("nslices", &PyPeer::nslices)
+      .def("owner", &PyPeer::owner)
+      .def("close", &PyPeer::close);
 
   py::class_<ddl::ShmMailbox>(m, "ShmMailbox")
       .def(py::init<const std::string&, int64_t, bool>(), py::arg("name"), py::arg("capacity"),

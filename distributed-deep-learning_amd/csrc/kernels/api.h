@@ -253,6 +253,10 @@ struct XgmiLaunch {              // one bucket's kernel arguments
   int check;                     // DDL_XGMI_CHECK: per-(bucket, source, slice) inbox checksums
   int repl_bucket;               // the replicated bucket (-1: none)
   int owners[kXgmiMaxBuckets];   // -1: chunk r of the bucket on rank r; >= 0: single owner rank
+  // the READY gate ahead of this kernel on the comm stream timed out (host word, or null): the
+  // segment's gradients may be incomplete, so the kernel publishes nothing (no pushes, no
+  // ARRIVE / DONE words); the peers then time out too and every host raises
+  const int* gate_err;
   // owner buckets: the launched bucket's runs (plan-buffer range, element offset in the owner
   // PS's optimizer state, offset in the bucket's concatenation, slice size, first slice)
   int owner, nruns;
@@ -294,8 +298,16 @@ class PeerExchange {
   std::string handle() const;                         // this rank's IPC handles, as bytes
   void open(const std::vector<std::string>& handles);  // every rank's, in rank order
   // the fused push / owner update / pull of one bucket at step `epoch` (same on all ranks)
-  void launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool final_wait, hipStream_t st);
+  // gated: the launch sits behind the runner's READY gate on the comm stream (checks its error
+  // word before publishing anything)
+  void launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool final_wait, hipStream_t st,
+              bool gated = false);
   int error() const;             // nonzero once a wait timed out (1 arrive, 2 done)
+  // the runner's READY-gate error word, checked by every bucket kernel before it publishes
+  void set_gate_error(const int* w) { gate_err_ = w; }
+  // unmap the peers' buffers and free this rank's (after the device has drained); idempotent
+  void close();
+  double timeout_s() const { return timeout_s_; }
   int num_buckets() const { return (int)bk_.size(); }
   int nslices(int b) const { return bk_[b].nslice; }
   int64_t chunk(int b) const { return bk_[b].c; }
@@ -324,6 +336,7 @@ class PeerExchange {
   uint32_t* flags_ = nullptr;
   size_t flag_bytes_ = 0;
   int* err_ = nullptr;
+  const int* gate_err_ = nullptr;
   double timeout_s_ = 60.0;
   XgmiTable table_{};
   void* opened_[kXgmiMaxPeers][3] = {};
@@ -355,6 +368,7 @@ class AsyncPeer {
   ~AsyncPeer();
   std::string handle() const;
   void open(const std::vector<std::string>& handles);
+  void close();  // unmap peers, free buffers and the shm board (after a device drain); idempotent
   // worker: every PS shard of the gradient (x coef) into its host's inbox slot, round `epoch`
   void push_all(uint32_t epoch, float coef, hipStream_t st);
   // the same for the listed PS only (one launch); with_gate: plus the pull gate of round
@@ -573,12 +587,17 @@ class SyncRunner {
   void set_last_on_main(bool on) { last_on_main_ = on; }
   std::string async_error();  // "" while the communicator is healthy (RCCL and xGMI)
   // XGMI units exchange through this (owned by the caller; outlives the runner's use)
-  void set_peer(PeerExchange* p) { peer_ = p; }
+  PeerExchange* peer() const { return peer_; }
+  void set_peer(PeerExchange* p) {
+    peer_ = p;
+    if (p) p->set_gate_error(ready_err_);
+  }
   // one full exchange of every bucket with w := sum over ranks of g (no optimizer) at the
   // next epoch; the caller fills g, checks w
   void peer_selftest_step(hipStream_t st);
   void abort();               // ncclCommAbort: unblocks this rank's pending collectives
-  void close();               // orderly ncclCommDestroy (call on every rank at the same point)
+  // orderly ncclCommDestroy (call on every rank at the same point), then release()
+  void close();
   hipStream_t comm_stream() const { return cs_; }
 
  private:
@@ -589,8 +608,11 @@ class SyncRunner {
                           hipStream_t st);
   void update(float* w, const float* g, float* m, float* v, int64_t n, float lr_t,
               hipStream_t st);
-  void issue_xgmi(const RunnerUnit& u, const float* lr_t, bool final_wait, hipStream_t st);
+  void issue_xgmi(const RunnerUnit& u, const float* lr_t, bool final_wait, hipStream_t st,
+                  bool gated = false);
   int last_xgmi_ = -1;     // index of the step's last XGMI unit (carries the final wait)
+  void release();          // destroy the comm stream, events and flags (idempotent)
+  bool closed_ = false;
   Engine* eng_;
   float* w_;
   float* g_;
@@ -617,6 +639,7 @@ class SyncRunner {
   bool gate_checked_ = false, gate_checked_ok_ = false;
   uint32_t* ready_ = nullptr;     // READY[segment] (uncached device memory, tail.h kind 2)
   int* ready_err_ = nullptr;      // a READY gate timed out (host memory)
+  double gate_timeout_s_ = 20.0;  // DDL_XGMI_TIMEOUT_S
   uint32_t ready_epoch_ = 0;      // one per step
   std::vector<RunnerUnit> units_;
   int opt_ = 0;

@@ -92,18 +92,36 @@ SyncRunner::SyncRunner(Engine* eng, float* params, float* grads, int world, int 
   HIP_CHECK(hipDeviceSynchronize());
   const char* xe = getenv("DDL_EXT_EVENT");
   ext_event_ = xe ? xe[0] == '1' : true;
+  // the READY gate is bounded like the xGMI waits (the same setting and default)
+  const char* to = getenv("DDL_XGMI_TIMEOUT_S");
+  gate_timeout_s_ = to ? atof(to) : 20.0;
 }
 
 SyncRunner::~SyncRunner() {
   if (comm_) (void)rccl().CommDestroy(as_comm(comm_));
-  for (int s = 0; s < kSegments; ++s)
+  comm_ = nullptr;
+  release();
+}
+
+// Every HIP object the runner owns: the comm stream (a hardware queue of its own priority), the
+// events, the READY flags.  Idempotent; after it the runner refuses to step.
+void SyncRunner::release() {
+  if (cs_) (void)hipStreamSynchronize(cs_);
+  if (peer_) peer_->set_gate_error(nullptr);
+  for (int s = 0; s < kSegments; ++s) {
     if (seg_ev_[s]) (void)hipEventDestroy(seg_ev_[s]);
-  for (int s = 0; s < kSegments; ++s)
     if (seg_ev_dev_[s]) (void)hipEventDestroy(seg_ev_dev_[s]);
+    seg_ev_[s] = seg_ev_dev_[s] = nullptr;
+  }
   if (done_ev_) (void)hipEventDestroy(done_ev_);
+  done_ev_ = nullptr;
   if (ready_) (void)hipFree(ready_);
+  ready_ = nullptr;
   if (ready_err_) (void)hipHostFree(ready_err_);
+  ready_err_ = nullptr;
   if (cs_) (void)hipStreamDestroy(cs_);
+  cs_ = nullptr;
+  closed_ = true;
 }
 
 void SyncRunner::unique_id(char out[128]) {
@@ -333,6 +351,7 @@ static const char* const kExRange[SyncRunner::kSegments] = {
 
 void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t seed_value,
                       const float* lr_t, hipStream_t st) {
+  if (closed_) throw std::runtime_error("sync runner: step() after close()");
   TraceRange step_range("ddl.step");
   eng_->seed_value = seed_value;  // dropout seed by kernel argument: no seed-upload kernel
   const uint32_t* seed = nullptr;
@@ -451,7 +470,7 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
           t.first = 1;
           eng_->tail = t;
           hipLaunchKernelGGL(ready_gate_kernel, dim3(1), dim3(64), 0, cs_, ready_ + s,
-                             ready_epoch_, ready_err_, (long long)(20.0 * 1e8));
+                             ready_epoch_, ready_err_, (long long)(gate_timeout_s_ * 1e8));
           DDL_CHECK_LAUNCH();
         } else {
           if (marker) HIP_CHECK(hipEventRecord(ev, st));
@@ -464,7 +483,7 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
         // on the comm stream does the compute stream need the end-of-exchange event
         const bool fin = (int)i == last_xgmi_;
         comm_used |= fin && !on_main;
-        issue_xgmi(u, lr_t, fin, xs);
+        issue_xgmi(u, lr_t, fin, xs, flag);
         continue;
       }
       comm_used |= !on_main;
@@ -497,7 +516,7 @@ bool SyncRunner::gate_safe(hipStream_t st) {
 }
 
 void SyncRunner::issue_xgmi(const RunnerUnit& u, const float* lr_t, bool final_wait,
-                            hipStream_t st) {
+                            hipStream_t st, bool gated) {
   XgmiUpdate up;
   const auto& r = u.ranges[0];
   up.opt = opt_;
@@ -513,7 +532,7 @@ void SyncRunner::issue_xgmi(const RunnerUnit& u, const float* lr_t, bool final_w
   up.mu = mu_;
   up.scale = grad_scale_;
   up.coef = coef_;
-  peer_->launch(u.bucket, epoch_, up, final_wait, st);
+  peer_->launch(u.bucket, epoch_, up, final_wait, st, gated);
 }
 
 void SyncRunner::peer_selftest_step(hipStream_t st) {
@@ -543,10 +562,14 @@ std::string SyncRunner::async_error() {
 // so a communicator finalisation that synchronises with the peers cannot hang on a rank that
 // has not reached it yet; afterwards the destructor has nothing collective left to do.
 void SyncRunner::close() {
-  if (!comm_) return;
-  HIP_CHECK(hipStreamSynchronize(cs_));
-  (void)rccl().CommDestroy(as_comm(comm_));
-  comm_ = nullptr;
+  if (comm_) {
+    HIP_CHECK(hipStreamSynchronize(cs_));
+    (void)rccl().CommDestroy(as_comm(comm_));
+    comm_ = nullptr;
+  }
+  // and every stream / event / flag with it: a closed runner holds no hardware queue (the
+  // one-card W = 4 rehearsal kept four processes' released runners' queues until GC)
+  release();
 }
 
 void SyncRunner::abort() {

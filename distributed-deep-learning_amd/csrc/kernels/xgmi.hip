@@ -106,6 +106,15 @@ DDL_DEV bool wait_ge(const uint32_t* f, uint32_t target, long long deadline, int
   return true;
 }
 
+// The READY gate ahead of this kernel timed out (its gradients may be incomplete): publish
+// nothing, record error 6 (the peers' waits then time out as well and every host raises).
+DDL_DEV bool gate_failed(const XgmiLaunch& a) {
+  if (!a.gate_err || __hip_atomic_load(a.gate_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0)
+    return false;
+  if (threadIdx.x == 0) __hip_atomic_store(a.err, 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return true;
+}
+
 DDL_DEV float4 scale4(float4 x, float a) {
   x.x *= a; x.y *= a; x.z *= a; x.w *= a;
   return x;
@@ -203,6 +212,7 @@ DDL_DEV void update4(const XgmiLaunch& a, float4& w, float4 g, float4* m4, float
 // element's remote loads / stores are in flight together), 0 = any world size.
 template <int WT>
 __global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a) {
+  if (gate_failed(a)) return;
   constexpr int NQ = WT ? WT : kXgmiMaxPeers;
   const int j = blockIdx.x, tid = threadIdx.x;
   const int W = WT ? WT : a.world, me = a.rank, b = a.bucket;
@@ -330,6 +340,7 @@ __global__ void __launch_bounds__(256) xgmi_ps_kernel(XgmiTable T, XgmiLaunch a)
 // conv2, launched on the compute stream): parallel/native_exchange.py last_segment_bucket.
 template <int WT>
 __global__ void __launch_bounds__(256) xgmi_repl_kernel(XgmiTable T, XgmiLaunch a) {
+  if (gate_failed(a)) return;
   constexpr int NQ = WT ? WT : kXgmiMaxPeers;
   const int j = blockIdx.x, tid = threadIdx.x;
   const int W = WT ? WT : a.world, me = a.rank, b = a.bucket;
@@ -424,6 +435,7 @@ __global__ void __launch_bounds__(256) xgmi_repl_kernel(XgmiTable T, XgmiLaunch 
 // owner's DONE, which the owner sets after reading that slot.
 template <int WT>
 __global__ void __launch_bounds__(256) xgmi_owner_kernel(XgmiTable T, XgmiLaunch a) {
+  if (gate_failed(a)) return;
   constexpr int NQ = WT ? WT : kXgmiMaxPeers;
   const int j = blockIdx.x, tid = threadIdx.x;
   const int W = WT ? WT : a.world, me = a.rank, b = a.bucket, own = a.owner;
@@ -631,15 +643,24 @@ void PeerExchange::init(const std::vector<XgmiBucketSpec>& buckets, int max_slic
   check_ = ck && ck[0] == '1';
 }
 
-PeerExchange::~PeerExchange() {
+PeerExchange::~PeerExchange() { close(); }
+
+void PeerExchange::close() {
+  if (inbox_ || flags_ || opened_ok_) (void)hipDeviceSynchronize();
   for (int q = 0; q < world_; ++q) {
     if (q == rank_) continue;
-    for (void* p : opened_[q])
+    for (void*& p : opened_[q]) {
       if (p) (void)hipIpcCloseMemHandle(p);
+      p = nullptr;
+    }
   }
+  opened_ok_ = false;
   if (inbox_) (void)hipFree(inbox_);
   if (flags_) (void)hipFree(flags_);
   if (err_) (void)hipHostFree(err_);
+  inbox_ = nullptr;
+  flags_ = nullptr;
+  err_ = nullptr;
 }
 
 std::string PeerExchange::handle() const {
@@ -685,7 +706,7 @@ void PeerExchange::open(const std::vector<std::string>& handles) {
 }
 
 void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool final_wait,
-                          hipStream_t st) {
+                          hipStream_t st, bool gated) {
   if (!opened_ok_) throw std::runtime_error("xgmi: open() the peer handles first");
   if (bucket < 0 || bucket >= (int)bk_.size()) throw std::invalid_argument("xgmi: bucket index");
   const Bucket& B = bk_[bucket];
@@ -721,6 +742,7 @@ void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool 
   a.timeout_ticks = (long long)(timeout_s_ * 1e8);  // wall_clock64: 100 MHz
   a.check = check_ ? 1 : 0;
   a.repl_bucket = repl_;
+  a.gate_err = gated ? gate_err_ : nullptr;
   for (size_t i = 0; i < bk_.size(); ++i) a.owners[i] = bk_[i].owner;
   for (int i = (int)bk_.size(); i < kXgmiMaxBuckets; ++i) a.owners[i] = -1;
   if (B.owner >= 0) {
@@ -767,7 +789,7 @@ void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool 
 }
 
 int PeerExchange::error() const {
-  return __atomic_load_n(err_, __ATOMIC_ACQUIRE);
+  return err_ ? __atomic_load_n(err_, __ATOMIC_ACQUIRE) : 0;
 }
 
 }  // namespace ddl

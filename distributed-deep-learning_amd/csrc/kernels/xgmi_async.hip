@@ -345,21 +345,33 @@ AsyncPeer::AsyncPeer(float* params, const float* grads, int64_t total, int world
   timeout_s_ = t ? atof(t) : 60.0;
 }
 
-AsyncPeer::~AsyncPeer() {
+AsyncPeer::~AsyncPeer() { close(); }
+
+void AsyncPeer::close() {
+  if (inbox_ || flags_ || opened_ok_) (void)hipDeviceSynchronize();
   for (int q = 0; q < world_; ++q) {
     if (q == rank_) continue;
-    for (void* p : opened_[q])
+    for (void*& p : opened_[q]) {
       if (p) (void)hipIpcCloseMemHandle(p);
+      p = nullptr;
+    }
   }
+  opened_ok_ = false;
   if (inbox_) (void)hipFree(inbox_);
   if (flags_) (void)hipFree(flags_);
   if (err_) (void)hipHostFree(err_);
   if (table_dev_) (void)hipFree(table_dev_);
+  inbox_ = nullptr;
+  flags_ = nullptr;
+  err_ = nullptr;
+  table_dev_ = nullptr;
   if (done_host_) {
     (void)hipHostUnregister(done_host_);
     munmap(done_host_, done_bytes_);
     if (done_owner_) shm_unlink(done_name_.c_str());
   }
+  done_host_ = nullptr;
+  posted_host_ = nullptr;
 }
 
 std::string AsyncPeer::handle() const {
@@ -501,7 +513,7 @@ void AsyncPeer::attach_done(const std::string& name, bool create) {
     shm_unlink(name.c_str());  // stale segment of a crashed job
     fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
     if (fd >= 0 && ftruncate(fd, (off_t)bytes) != 0) {
-      close(fd);
+      ::close(fd);
       fd = -1;
     }
   } else {
@@ -509,7 +521,7 @@ void AsyncPeer::attach_done(const std::string& name, bool create) {
   }
   if (fd < 0) throw std::runtime_error("async xgmi: shm_open failed: " + name);
   void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-  close(fd);
+  ::close(fd);
   if (p == MAP_FAILED) throw std::runtime_error("async xgmi: mmap failed: " + name);
   if (create) memset(p, 0, bytes);
   X_CHECK(hipHostRegister(p, bytes, hipHostRegisterMapped));
@@ -608,7 +620,7 @@ void AsyncPeer::gate(uint32_t epoch, hipStream_t st) {
   DDL_CHECK_LAUNCH();
 }
 
-int AsyncPeer::error() const { return __atomic_load_n(err_, __ATOMIC_ACQUIRE); }
+int AsyncPeer::error() const { return err_ ? __atomic_load_n(err_, __ATOMIC_ACQUIRE) : 0; }
 
 // ---- the PS service loop in C++ -------------------------------------------------------------------
 // Scans the arrival board of this host's PS and enqueues one apply per completed push on one PS

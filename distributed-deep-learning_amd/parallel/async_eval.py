@@ -29,7 +29,6 @@ from typing import Callable, List, Optional
 import torch
 import torch.distributed as dist
 
-
 Result = Callable[[dict, float, float], None]  # (meta, accuracy, seconds since start)
 
 
@@ -52,6 +51,9 @@ class AsyncEvaluator:
         # high-priority comm / PS-service streams, and HIP pools hardware queues per priority
         # (runner.hip, async_runner.hip; a high-priority training stream stalled the W = 2
         # one-card time-to-accuracy run).
+        # (torch's pooled streams: the pool is fixed per device and priority, so evaluators
+        # built one after another reuse the same streams and hardware queues; destroying an
+        # external stream instead left the caching allocator's blocks tied to a dead stream)
         eval_first = os.environ.get("DDL_EVAL_PRIORITY", "train") == "eval"
         self.stream = torch.cuda.Stream(device=dev, priority=-1 if eval_first else 0)
         self.train_stream = torch.cuda.Stream(device=dev, priority=0)
@@ -77,6 +79,18 @@ class AsyncEvaluator:
         self.done_records: List[dict] = []  # finished (meta, count, ms) in submit order
         self.t0 = torch.cuda.Event(enable_timing=True)
         self.n = 0
+
+    def close(self) -> None:
+        """Drop the eval engine (its 10k-row workspace, ~2.6 GB) and the snapshot ring now,
+        after the last eval, instead of whenever garbage collection gets to them."""
+        if self.engine is None:
+            return
+        self.drain()
+        torch.cuda.current_stream().wait_stream(self.train_stream)
+        torch.cuda.synchronize()
+        self.engine = None
+        self.ring = [None] * self.slots
+        self.snap = None
 
     def start(self) -> None:
         """Time origin: recorded on the training stream when the training clock starts."""

@@ -273,4 +273,11 @@ class AsyncPeerExchange:
                                f"(kernel error code {self.peer.error()})")
 
     def close(self) -> None:
-        pass
+        """Release the data plane deterministically (every rank, same program point, after
+        join()): the service's stream, the peer mappings, inbox / flags and the shm board."""
+        if self._svc is not None:  # a run that never joined (error path)
+            svc, self._svc = self._svc, None
+            svc.join()
+        self.runner = None
+        if self.peer is not None:
+            self.peer.close()

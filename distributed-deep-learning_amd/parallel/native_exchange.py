@@ -15,12 +15,17 @@ known pattern) runs on every rank and the decision to use it is agreed by all ra
 PS state (``m``/``v``/step counter ``t``) stays in the Python ``ParameterServer`` objects, so
 checkpointing and inspection are unchanged.
 
-``backend="xgmi"`` (flat plan, one PS per GPU): instead of RCCL, each bucket is ONE fused kernel
-over IPC-mapped peer memory (``csrc/kernels/xgmi.hip``): push gradient chunks to their owners,
-owner sum + Adam, push the parameters back.  Set up collectively (IPC handles all-gathered over
-the default group) and verified by a self-test on a known pattern whose result all ranks vote
-on; it needs no RCCL communicator, so it also runs with several ranks on ONE GPU (gloo default
-group) — the multi-process rehearsal of the W > 1 step on a one-GPU box.
+``backend="xgmi"``: instead of RCCL, each bucket is ONE fused kernel over IPC-mapped peer memory
+(``csrc/kernels/xgmi.hip``): push the gradients to their owners, owner sum + optimizer, push the
+parameters back.  Flat plan with one PS per GPU: equal-chunk buckets (rank r owns chunk r, the
+reduce-scatter form).  Every other plan — the reference's tensor-granular ``none`` (1 PS + W
+workers, ``mnist_sync/``), ``contiguous`` and ``greedy`` (``mnist_sync_sharding*/``), ``lpt``, or
+a flat plan with fewer PS than GPUs — gets one OWNER bucket per exchange unit (one PS's tensors
+completed by one backward segment): every rank pushes the unit to the rank hosting that PS, which
+sums, updates with the PS's state and pushes the parameters to every rank.  Set up collectively
+(IPC handles all-gathered over the default group) and verified by a self-test on a known pattern
+whose result all ranks vote on; it needs no RCCL communicator, so it also runs with several ranks
+on ONE GPU (gloo default group) — the multi-process rehearsal of the W > 1 step on a one-GPU box.
 """
 from __future__ import annotations
 
@@ -111,12 +116,14 @@ class NativeSyncExchange(SyncExchange):
             self.runner.set_ready_flags(int(rf))
         self.backend = "local" if env.world == 1 and not force_collectives else backend
         self.peer = None
+        self._xbucket = {}  # id(unit) -> its xGMI owner bucket (tensor-granular plans)
         if backend == "xgmi" and (env.world > 1 or force_collectives):
             # (W = 1 with force_collectives: the whole W > 1 step structure — comm stream,
             # events, fused bucket kernels, final wait — on one GPU, every push to itself)
+            specs = None
             if plan.bucket_ranges is None or plan.num_ps != env.world:
-                raise NativeUnavailable("xgmi exchange needs the flat plan with one PS per GPU")
-            self._init_peer_collectively(ops, env, plan, params, grads)
+                specs = self._owner_specs()
+            self._init_peer_collectively(ops, env, plan, params, grads, specs)
         elif env.world > 1:
             self._init_comm_collectively(ops, env)
         elif force_collectives:
@@ -153,16 +160,17 @@ class NativeSyncExchange(SyncExchange):
             srv = servers.get(ps)
             offs = u.state_offs or [0] * len(u.ranges)
             ranges = [(int(lo), int(hi), int(off)) for (lo, hi), off in zip(u.ranges, offs)]
-            kind = "xgmi" if (self.peer is not None and u.kind == "rs") else u.kind
+            kind = "xgmi" if (self.peer is not None and u.kind in ("rs", "reduce")) else u.kind
             m = srv.m if srv is not None else None
             v = srv.v if srv is not None else None
             shard = None if kind == "xgmi" else u.shard_buf
+            bucket = self._xbucket.get(id(u), u.bucket)
             if self.repl is not None and u.kind == "rs" and u.bucket == self.repl[0]:
                 kind = "xgmi_repl" if self.peer is not None else "ar"
                 _, lo, hi, m, v = self.repl
                 ranges, shard = [(lo, hi, 0)], None
             units.append((seg_of(u.tensors), _KIND[kind], int(u.host), int(ps), ranges,
-                          m, v, shard, int(u.bucket)))
+                          m, v, shard, int(bucket)))
         h = hyper if hyper is not None else next(iter(servers.values())).h
         # (before set_units: it checks each unit's optimizer state against the update kind)
         self.runner.set_optimizer(0 if optimizer == "adam" else 1, h.lr, h.beta1, h.beta2, h.eps,
@@ -201,8 +209,25 @@ class NativeSyncExchange(SyncExchange):
         ok, why = self.runner.selftest()
         agree(ok, why, "RCCL self-test")
 
+    def _owner_specs(self):
+        """One xGMI owner bucket per exchange unit of a plan without one equal chunk per rank:
+        (runs, the runs' offsets in the owning PS's optimizer state, the hosting rank)."""
+        specs = []
+        for u in self.units:
+            if u.kind != "reduce":
+                raise NativeUnavailable(f"xgmi exchange: unexpected unit kind {u.kind}")
+            if len(u.ranges) > 8:
+                raise NativeUnavailable("xgmi exchange: a unit with more than 8 runs")
+            offs = u.state_offs or [0] * len(u.ranges)
+            self._xbucket[id(u)] = len(specs)
+            specs.append(([(int(lo), int(hi)) for lo, hi in u.ranges], [int(o) for o in offs],
+                          int(u.host)))
+        if len(specs) > 32:
+            raise NativeUnavailable(f"xgmi exchange: {len(specs)} units (at most 32)")
+        return specs
+
     def _init_peer_collectively(self, ops, env: DistEnv, plan: ShardPlan, params: torch.Tensor,
-                                grads: torch.Tensor) -> None:
+                                grads: torch.Tensor, specs=None) -> None:
         """IPC handles out and in, then a self-test: every rank fills its gradients with
         (rank + 1) * (i % 13 + 1), one exchange with w := sum of g must give
         W (W + 1) / 2 * (i % 13 + 1) everywhere (exact in fp32).  Every stage is voted on, so
@@ -227,8 +252,9 @@ class NativeSyncExchange(SyncExchange):
             # spinning bucket kernels must all find room on the one card.
             shared_gpu = env.world > max(1, torch.cuda.device_count())
             slices = int(os.environ.get("DDL_XGMI_SLICES", "128" if shared_gpu else "384"))
-            peer = ops.PeerExchange(params, grads, env.world, env.rank,
-                                    [tuple(map(int, b)) for b in plan.bucket_ranges], slices,
+            buckets = (specs if specs is not None
+                       else [tuple(map(int, b)) for b in plan.bucket_ranges])
+            peer = ops.PeerExchange(params, grads, env.world, env.rank, buckets, slices,
                                     self.repl[0] if self.repl is not None else -1)
             mine = peer.handle()
         except RuntimeError as e:
@@ -258,7 +284,9 @@ class NativeSyncExchange(SyncExchange):
         if peer.error():
             ok, why = False, f"timed out (code {peer.error()})"
         else:
-            for lo, hi in plan.bucket_ranges:
+            spans = ([r for runs, _, _ in specs for r in runs] if specs is not None
+                     else plan.bucket_ranges)
+            for lo, hi in spans:
                 if not torch.equal(params[lo:hi], want[lo:hi]):
                     bad = int((params[lo:hi] != want[lo:hi]).nonzero()[0]) + lo
                     ok, why = False, f"mismatch at {bad}: {float(params[bad])} != {float(want[bad])}"
@@ -282,6 +310,78 @@ class NativeSyncExchange(SyncExchange):
         self._n += 1
         if self.env.world > 1 and self._n % 64 == 0:
             self.check()
+
+    # -- the READY-flag hand-off, proven per job ------------------------------
+    def _snapshot(self):
+        srv = {p: (ps.m.clone(), None if ps.v is None else ps.v.clone(), ps.t, ps.updates)
+               for p, ps in self.servers.items()}
+        repl = None if self.repl is None else tuple(
+            None if x is None else x.clone() for x in self.repl[3:])
+        return self.params.clone(), srv, repl
+
+    def _restore(self, snap) -> None:
+        params, srv, repl = snap
+        self.params.copy_(params)
+        for p, (m, v, t, n) in srv.items():
+            ps = self.servers[p]
+            ps.m.copy_(m)
+            if v is not None:
+                ps.v.copy_(v)
+            ps.t, ps.updates = t, n
+        if repl is not None:
+            for dst, src in zip(self.repl[3:], repl):
+                if dst is not None:
+                    dst.copy_(src)
+        torch.cuda.synchronize(self.params.device)
+
+    def handoff_check(self, trainer, steps: int = 6) -> dict:
+        """Prove the READY-flag hand-off on THIS job before trusting it.
+
+        The comm stream's exchange of segment s starts behind a READY flag that the next
+        segment's first launch stores (runner.hip), not behind an event with a system-scope
+        release; that peers read the gradients and parameters coherently then rests on the
+        kernel-boundary L2 write-back, which no single-card test can exercise.  So: from the same
+        state, ``steps`` steps with the event hand-off (system fence) and ``steps`` steps with
+        the READY flags, a SHA-256 of the resulting parameters on every rank; the flags are kept
+        only if both modes give the same bits and every rank agrees, otherwise every rank falls
+        back to the events.  The state (parameters, PS m / v / t, replicated state) is restored
+        afterwards — with the trainer's global step (its dropout seeds) — so the caller's run
+        starts where it would have."""
+        import hashlib
+        if self.backend == "local":
+            return {"handoff": "none (every update local)"}
+        snap = self._snapshot()
+        g0 = trainer.global_step
+        digests = {}
+        try:
+            for mode, rf in (("events", 0), ("ready_flags", 2)):
+                self._restore(snap)
+                trainer.global_step = g0
+                self.runner.set_ready_flags(rf)
+                for i in range(steps):
+                    trainer.train_step(i)
+                torch.cuda.synchronize(self.params.device)
+                self.check()
+                digests[mode] = hashlib.sha256(
+                    self.params.detach().cpu().numpy().tobytes()).hexdigest()
+        finally:
+            self._restore(snap)
+            trainer.global_step = g0
+        same = digests["events"] == digests["ready_flags"]
+        votes = [(same, digests["ready_flags"])]
+        if self.env.world > 1:
+            votes = [None] * self.env.world
+            dist.all_gather_object(votes, (same, digests["ready_flags"]))
+        modes_agree = all(v[0] for v in votes)
+        ranks_agree = len({v[1] for v in votes}) == 1
+        ok = modes_agree and ranks_agree
+        forced = os.environ.get("DDL_READY_FLAGS")  # an explicit choice stays in force
+        self.runner.set_ready_flags(int(forced) if forced is not None else (2 if ok else 0))
+        return {"handoff": ("ready_flags" if ok else "events (READY flags failed the check)")
+                + (f" (DDL_READY_FLAGS={forced} in force)" if forced is not None else ""),
+                "check_steps": steps, "modes_bit_identical": modes_agree,
+                "ranks_bit_identical": ranks_agree,
+                "params_sha256": digests["ready_flags"][:16]}
 
     # -- replicated last bucket <-> the PS objects (checkpoint / resume) ---------------------------
     def _repl_chunk(self):
@@ -327,8 +427,12 @@ class NativeSyncExchange(SyncExchange):
         self.runner.abort()
 
     def close(self) -> None:
-        """Orderly teardown of the runner's communicator (every rank, same program point)."""
+        """Orderly teardown (every rank, same program point): the runner's communicator, comm
+        stream, events and READY flags, then the xGMI peer mappings and buffers — nothing of a
+        closed exchange keeps a hardware queue or an IPC mapping until garbage collection."""
         self.runner.close()
+        if self.peer is not None:
+            self.peer.close()
 
 
 def make_sync_exchange(plan, env, params, grads, segments, servers, engine, cfg, hyper):

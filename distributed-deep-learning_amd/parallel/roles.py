@@ -15,6 +15,7 @@ final accuracy and ``Time``.
 from __future__ import annotations
 
 import contextlib
+import sys
 import time
 from typing import Dict, List, Optional
 
@@ -94,6 +95,9 @@ class Trainer:
         if aligned:
             self.num_ps = cfg.num_ps or segment_aligned_num_ps(W, segs)
             aligned = self.num_ps >= len(segs)
+            if not cfg.num_ps and env.rank == 0 and not cfg.quiet:
+                print(f"[ddl_amd] async flat plan: {self.num_ps} segment-aligned PS "
+                      f"(--num-ps not given)", file=sys.stderr)
             buckets = segs if aligned else None
         self.plan = make_plan(shard, self.num_ps, buckets=buckets, segment_aligned=aligned)
         dev = env.device
@@ -332,6 +336,7 @@ class Trainer:
         if aeval is not None:
             torch.cuda.current_stream().wait_stream(aeval.train_stream)
             aeval.drain()
+            aeval.close()  # its streams and its eval engine's workspace, now
         if asyncx:
             self.exchange.join()
             if cfg.check_provenance:
@@ -371,8 +376,11 @@ def close_trainers(trainers, env: DistEnv) -> None:
             torch.cuda.synchronize()
         dist.barrier()
     for t in trainers:
+        # native sync runners and the asynchronous data planes (xGMI / RCCL); the Python sync
+        # exchange has nothing native to release
         close = getattr(t.exchange, "close", None)
-        if close is not None and getattr(t.exchange, "native", False):
+        if close is not None and (getattr(t.exchange, "native", False)
+                                  or t.cfg.mode == "async"):
             close()
     if env.world > 1:
         dist.barrier()

@@ -92,8 +92,13 @@ def save(trainer, path: str) -> None:
         ps_t = {}
         for d in all_t:
             ps_t.update({str(k): v for k, v in d.items()})
+        # the PS ranges themselves: two plans with one policy and PS count can
+        # still differ (flat vs segment-aligned flat), and a PS step counter is only valid on
+        # the ranges it counted
         man = dict(policy=plan.policy, num_ps=plan.num_ps, world=env.world, mode=trainer.cfg.mode,
-                   global_step=trainer.global_step, ps_t=ps_t)
+                   global_step=trainer.global_step, ps_t=ps_t,
+                   ps_segments=[[list(map(int, r)) for r in plan.ps_segments(p)]
+                                for p in range(plan.num_ps)])
         with open(os.path.join(path, "manifest.json"), "w") as f:
             json.dump(man, f, indent=1)
     if env.world > 1:
@@ -169,7 +174,9 @@ def load(trainer, path: str) -> None:
                     ps.v[s0:s0 + (b - a)].copy_(full[i]["v"][a:b])
                 if ps.params is not None:
                     ps.params[s0:s0 + (b - a)].copy_(full[i]["w"][a:b])
-        same_plan = (man["policy"] == plan.policy and man["num_ps"] == plan.num_ps)
+        same_plan = (man["policy"] == plan.policy and man["num_ps"] == plan.num_ps
+                     and man.get("ps_segments") == [[list(map(int, r)) for r in plan.ps_segments(q)]
+                                                    for q in range(plan.num_ps)])
         ps.t = int(man["ps_t"].get(str(p)) or t_resume) if same_plan else t_resume
     trainer.global_step = int(man["global_step"])
     load_state = getattr(trainer.exchange, "load_ps_state", None)

@@ -86,6 +86,12 @@ def test_native_runner_trains(data):
     dict(shard="flat", exchange_backend="xgmi", overlap=False),
     dict(shard="flat", exchange_backend="xgmi", optimizer="sgd"),
     dict(shard="flat", exchange_backend="xgmi", optimizer="momentum"),
+    # tensor-granular plans on xGMI OWNER buckets (one push / owner update / pull kernel per
+    # unit; at W = 1 every unit is owned here): reference none / contiguous / greedy
+    dict(shard="none", exchange_backend="xgmi"),
+    dict(shard="contiguous", exchange_backend="xgmi"),
+    dict(shard="greedy", num_ps=3, exchange_backend="xgmi"),
+    dict(shard="lpt", num_ps=4, exchange_backend="xgmi", optimizer="momentum"),
 ])
 def test_forced_collectives_on_one_rank_match_local(data, kw):
     """The multi-GPU exchange path on one GPU: torch's librccl resolved by dlsym, a 1-rank
@@ -205,3 +211,29 @@ def test_ready_flag_handoff_matches_events(data, backend):
         assert torch.equal(ref[0], p)
         for q in ref[1]:
             assert torch.equal(ref[1][q][1], st[q][1])
+
+
+@pytest.mark.parametrize("kw", [dict(shard="flat"), dict(shard="contiguous"),
+                                dict(shard="flat", exchange_backend="xgmi"),
+                                dict(shard="greedy", num_ps=3, exchange_backend="xgmi")])
+def test_handoff_check_proves_ready_flags(data, kw):
+    """the forced 1-rank rehearsal runs the bench's hand-off check — K steps
+    with the event hand-off and K with the READY flags from the same state, bit-identical —
+    keeps the flags, and leaves the trainer's state exactly as before the check."""
+    env = DistEnv(0, 1, 0, torch.device("cuda", 0))
+    cfg = TrainConfig(mode="sync", steps=20, batch_size=100, eval_every=0, engine="hip",
+                      quiet=True, force_collectives=True, **kw)
+    tr = Trainer(cfg, env, dataset=data)
+    before = tr.params.clone()
+    t_before = {p: s.t for p, s in tr.servers.items()}
+    res = tr.exchange.handoff_check(tr, steps=4)
+    assert res["handoff"] == "ready_flags", res
+    assert res["modes_bit_identical"] and res["ranks_bit_identical"]
+    assert torch.equal(tr.params, before)
+    assert {p: s.t for p, s in tr.servers.items()} == t_before
+    # and training continues from the restored state exactly like a fresh trainer
+    for i in range(3):
+        tr.train_step(i)
+    torch.cuda.synchronize()
+    p_fresh, _ = _run(data, True, steps=3, force_collectives=True, **kw)
+    assert torch.equal(tr.params, p_fresh)

@@ -87,12 +87,17 @@ def _rank(rank, world, port, outdir, kw):
         from ddl_amd.utils.data import synthetic_mnist
         env = init_distributed()
         assert env.device.index == 0
-        cfg = TrainConfig(mode="sync", shard="flat", steps=STEPS, batch_size=100, eval_every=0,
+        shard = kw.pop("shard", "flat")
+        cfg = TrainConfig(mode="sync", shard=shard, steps=STEPS, batch_size=100, eval_every=0,
                           engine="hip", quiet=True, data_sharding="stride",
                           exchange_backend="xgmi", **kw)
         tr = Trainer(cfg, env, dataset=synthetic_mnist(2000, 500, seed=5))
         ex = tr.exchange
         assert getattr(ex, "native", False) and ex.peer is not None, "xgmi path not taken"
+        # tensor-granular plans: one xGMI OWNER bucket per exchange unit, hosted where its PS is
+        owner = shard != "flat" or tr.plan.num_ps != world
+        assert all((ex.peer.owner(b) >= 0) == owner for b in range(len(ex.peer.nslices()))), \
+            "wrong xGMI bucket kind for the plan"
         sums = []
         for i in range(STEPS):
             tr.train_step(i)
@@ -152,6 +157,15 @@ def _simulate(world, kw):
     (2, dict(_env=dict(DDL_REPL_LAST="0"))),     # last bucket by its chunk owners
     (4, dict(_env=dict(DDL_XGMI_CHECK="1"))),
     pytest.param(8, dict(_env=W8_ENV), id="w8"),  # the 8-worker size of BASELINE configs 3-5
+    # tensor-granular plans on owner buckets (every rank pushes a unit to the rank hosting its
+    # PS, which sums, updates and pushes the parameters back):
+    pytest.param(2, dict(shard="none"), id="2-none"),              # BASELINE config 2: 1 PS + 2
+    pytest.param(2, dict(shard="contiguous"), id="2-contig"),      # mnist_sync_sharding
+    pytest.param(4, dict(shard="contiguous"), id="4-contig"),
+    pytest.param(3, dict(shard="contiguous", num_ps=5), id="3-contig-5ps"),  # 2 PS on some hosts
+    pytest.param(4, dict(shard="greedy", grad_reduce="mean"), id="4-greedy"),
+    pytest.param(8, dict(shard="contiguous", _env=W8_ENV), id="w8-contig"),  # BASELINE config 3
+    pytest.param(8, dict(shard="greedy", _env=W8_ENV), id="w8-greedy"),
 ])
 def test_xgmi_exchange_matches_simulation(tmp_path, world, kw):
     import torch.multiprocessing as mp
@@ -164,7 +178,8 @@ def test_xgmi_exchange_matches_simulation(tmp_path, world, kw):
         assert torch.equal(rec["params"], recs[0]["params"])
         assert rec["acc"] == recs[0]["acc"]
     assert all(t == STEPS for rec in recs for t in rec["t"].values())
-    ref, ref_sums = _simulate(world, {k: v for k, v in kw.items() if k not in ("overlap", "_env")})
+    ref, ref_sums = _simulate(world, {k: v for k, v in kw.items()
+                                      if k not in ("overlap", "_env", "shard", "num_ps")})
     got = recs[0]["params"]
     diff = float((got - ref).abs().max())
     # per-step parameter checksums localise a divergence (which step, which rank)
