@@ -156,8 +156,9 @@ def main(argv=None):
         if a.mode == "async":
             if getattr(ex, "backend", "") != "xgmi":
                 return type(ex).__name__
+            svc = getattr(ex, "service_mode", None)  # PS side: device-claim / host service
             return ("native-" if getattr(ex, "runner", None) is not None else "python-") + \
-                "xgmi-async"
+                "xgmi-async" + (f" ({svc} service)" if svc else "")
         if not getattr(ex, "native", False):
             return "python"
         return "native-" + getattr(ex, "backend", "rccl")
@@ -408,7 +409,9 @@ def main(argv=None):
             rec["plans"] = plans
         if shared_gpu and world > 1:
             rec["note"] = (f"{world} ranks share ONE GPU (DDL_DIST_BACKEND=gloo rehearsal): "
-                           "functional check of the W > 1 path, not a multi-GPU measurement")
+                           "functional check of the W > 1 path, not a multi-GPU measurement; "
+                           f"GPU_MAX_HW_QUEUES={os.environ.get('GPU_MAX_HW_QUEUES', 'default')} "
+                           "per process")
         if tta is not None:
             rec["time_to_acc"] = tta
         if tta_rep is not None:

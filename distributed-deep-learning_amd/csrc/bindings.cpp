@@ -439,6 +439,7 @@ class PyAsyncService {
   }
   void resume() { svc_->resume(); }
   std::vector<std::array<int64_t, 4>> provenance() const { return svc_->provenance(); }
+  std::string mode() const { return svc_->mode(); }
 
  private:
   std::vector<at::Tensor> keep_;
@@ -824,7 +825,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("pause", &PyAsyncService::pause)
       .def("resume", &PyAsyncService::resume)
       .def("served", &PyAsyncService::served)
-      .def("provenance", &PyAsyncService::provenance);
+      .def("provenance", &PyAsyncService::provenance)
+      .def("mode", &PyAsyncService::mode);
 
   py::class_<PyRcclAsync>(m, "RcclAsync")
       .def(py::init<at::Tensor, at::Tensor, int64_t, int64_t, py::list, std::vector<int64_t>,

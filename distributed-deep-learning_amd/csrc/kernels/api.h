@@ -346,6 +346,10 @@ class PeerExchange {
 // ---- asynchronous PS over xGMI peer memory (xgmi_async.hip) ----------------------------------
 constexpr int kAsyncMaxPs = 64;
 constexpr int kAsyncMaxSlices = 512;
+// a rank's uncached device flags: [0, kAsyncDense) its DONE words as a worker (dense over all
+// PS' slices), then POSTED[worker][dense slice] as a PS host (what its claim kernel polls)
+constexpr int kAsyncDense = kAsyncMaxPs * kAsyncMaxSlices;
+constexpr size_t kAsyncFlagWords = (size_t)kAsyncDense * (1 + kXgmiMaxPeers);
 struct AsyncShard {              // one PS's contiguous range of the flat buffer
   int64_t lo, n, slice, inbox_off;
   int host, nslice;
@@ -398,6 +402,7 @@ class AsyncPeer {
   int num_ps() const { return nps_; }
 
  private:
+  friend class AsyncService;     // its claim kernels read the table, flags and error word
   void upload_table();           // table_ -> table_dev_ (set-up only: open, attach_done)
   float* params_;
   const float* grads_;
@@ -426,6 +431,8 @@ struct AsyncPsState {            // one hosted PS as the service thread sees it
   int64_t t;                     // its step counter (advanced once per arrival)
 };
 
+struct ClaimState;               // the device-side service's state (xgmi_async.hip)
+
 class AsyncService {
  public:
   AsyncService(AsyncPeer* peer, int world, int device, const std::vector<AsyncPsState>& ps,
@@ -439,13 +446,26 @@ class AsyncService {
   void pause();
   void resume();
   int64_t t(int ps) const;
-  int64_t served() const { return served_.load(); }
+  int64_t served() const;
   // (worker, ps, worker round, PS step) per apply, in service order
   const std::vector<std::array<int64_t, 4>>& provenance() const { return prov_; }
+  // "device-claim": pre-enqueued claim + apply kernel pairs pop arrivals on the GPU (default);
+  // "host": the thread scans the board and launches each apply (DDL_ASYNC_CLAIM=0)
+  const char* mode() const { return claim_ ? "device-claim" : "host"; }
 
  private:
   void run();
+  void run_claim();
   void serve(AsyncPsState& st, int worker);
+  void free_claim();
+  bool claim_ = true;
+  int depth_ = 3;                // claim pairs in flight on the PS stream
+  double idle_us_ = 500.0;       // a claim kernel with no arrival for this long ends empty
+  ClaimState* cs_dev_ = nullptr;
+  float* lr_tab_ = nullptr;
+  int32_t* prov_dev_ = nullptr;
+  int64_t* host_words_ = nullptr;  // pinned: [0] claim kernels ended, [1] claims, [2] hold,
+                                   // [8 + i] hosted PS i's step counter
   AsyncPeer* peer_;
   int world_, device_;
   std::vector<AsyncPsState> ps_;

@@ -31,8 +31,11 @@ Engine::Engine() {
   // of the one-wave dual launch + wide reduce: 308.7 -> 304.4 us (profiles/r2_runner_tune_pack.log)
   // (round 3, after the direct conv1 kernels: fc2 data gradient on the K-wave half of a packed
   // launch with its weight gradient, like fc1's: 292.8 -> 291.5 us, profiles/r3_runner_tune.log)
+  // (round 5, scripts/sched_ab.py on one MI355X, 5 alternating rounds of 300 steps: conv4
+  // weight gradient and conv2 data gradient on the 16x16x4 MFMA tile (config 14), conv4 weight
+  // gradient split 8: 295.3 -> 293.0 us, profiles/r5_sched_ab_mf16.log)
   static const int defc[OP_COUNT] = {3, 3, 3, 3, CFG_KWAVE, 3, CFG_KWAVE, 5, CFG_KWAVE, 5,
-                                     3, 3, 3, 3, 3, 3, 3};
+                                     3, CFG_MF16, 3, 3, CFG_MF16, 3, 3};
   // (re-tuned in the real step with scripts/sched_ab.py after the compact 52-row conv3
   // enumeration and the wgrad row decode: conv3 forward split 4 + in-launch reduce instead of
   // stream-K 3072 workers, 372.4 -> 369.5 us; conv4 weight gradient split 4 instead of 8,
@@ -44,7 +47,7 @@ Engine::Engine() {
   // (round 3, conv forwards on the LDS-DMA main loop: conv2 / conv3 / conv4 forward split-K
   // 3 / 3 / 6 instead of 2 / 4 / 8, 302.5 -> 299.0 us fwd+bwd, scripts/sched_ab.py
   // --splits-variants, profiles/r3_sched_ab_ldsdma.log)
-  static const int defs[OP_COUNT] = {1, 3, 3, 6, 8, 16, 4, 1, 4, 1, 4, 4, 8, 12, 4, 32, 1024};
+  static const int defs[OP_COUNT] = {1, 3, 3, 6, 8, 16, 4, 1, 4, 1, 4, 8, 8, 12, 4, 32, 1024};
   static const int defw[OP_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
   static const bool inl[OP_COUNT] = {0, 1, 1, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0};

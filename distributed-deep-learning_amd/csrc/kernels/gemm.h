@@ -67,8 +67,11 @@ DDL_DEV void push_tail_body(const UpdTail& t, const UpdPiece& P, int b) {
   const brsrc_t dst = make_rsrc(P.w + s0 * 4, (uint32_t)cnt * 16u);
   for (int i = lane; i < cnt; i += 64) bstore4_sys(dst, i * 16, src[i]);
   drain_vmem();
-  if (lane == 0)
+  if (lane == 0) {
     __hip_atomic_store(P.posted + j, t.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // the PS host's device copy of the word: what its claim kernel polls (xgmi_async.hip)
+    __hip_atomic_store(P.arrive + j, t.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // One optimizer-tail block (tail.h): kTailF4PerLane float4 of one piece per lane, all loads

@@ -11,10 +11,13 @@
 //             tail blocks of the next segment's launch, async_runner.hip) those PS shards of the
 //             gradient -> each PS host's inbox slot [ps][worker] (system write-through stores);
 //             per workgroup, once its payload is acknowledged, POSTED[ps][worker][slice] = e on
-//             the ARRIVAL BOARD in host memory
-//   serve     (PS host, a native service thread) scans the board of its hosted PS in host
-//             memory and issues one apply per (worker, ps) whose every slice is posted, in the
-//             order it observes them (the reference's MPI.ANY_SOURCE order)
+//             the ARRIVAL BOARD in host memory and in the PS host's uncached device flags
+//   serve     (PS host) default: pre-enqueued claim kernels on the PS stream poll the device
+//             copy and pop the next (worker, ps) whose every slice is posted, in the order they
+//             observe them (the reference's MPI.ANY_SOURCE order), each followed by a generic
+//             apply kernel of that claim; the native service thread only keeps that queue
+//             topped up (AsyncService::run_claim).  DDL_ASYNC_CLAIM=0: the thread scans the
+//             host board and launches each apply itself (AsyncService::run)
 //   apply     (PS host, its PS stream) Adam on the PS's private parameter copy (one step of its
 //             counter t per arrival, atomic per shard: the reference's per-tag mixing race Q3
 //             cannot happen), store the new shard into the WORKER's parameter buffer, then
@@ -29,20 +32,31 @@
 // release (an L2 write-back) and left a ~4.6 us hole on the compute stream after every push,
 // plus two host hand-offs (poster -> mailbox -> service) on the critical path of the last push
 // (docs/DESIGN.md, round 4 async timeline).
-// Only one kernel of this protocol waits for another: the worker's gate, for applies that run
-// on other processes' queues or on this process's HIGH-priority service stream — HIP pools
-// hardware queues per priority and the compute stream is not high priority (checked), so no
-// apply is ever queued behind the gate (async_runner.hip).  The applies wait for nothing: the
-// service issues one only after it has seen every slice of the push posted, and a push block
-// posts its word only after its payload stores were acknowledged.  The gate is bounded and
-// records an error word instead of hanging.
+// The hardware-queue argument (why no wait here can deadlock).  Two kinds of kernel wait:
+//   * the worker's pull gate (compute stream) waits for applies;
+//   * a claim kernel (PS stream) waits for pushes.
+// HIP maps a process's streams onto hardware queues pooled PER PRIORITY; the PS stream is HIGH
+// priority and the compute stream is not (async_runner.hip checks it and falls back to a host
+// wait), so no apply or claim kernel is ever queued behind a gate, and no push behind a claim.
+// A gate waits for applies that sit on PS queues (this process's or a peer's); an apply waits for
+// nothing but the claim kernel in front of it; a claim kernel waits for pushes, which are GEMM
+// tail blocks or push kernels on compute queues that never wait except at the gate of the NEXT
+// round — issued after those pushes in the same queue.  Every chain ends at a kernel that waits
+// for nothing, so there is no cycle under any stream -> queue mapping that keeps the two
+// priorities apart.  The one remaining hazard is time slicing of oversubscribed hardware
+// queues (several ranks on one card): a waiter then spins until the queue holding what it waits
+// for is mapped in again (milliseconds), which parallel/comm.py share_gpu_queue_cap avoids with
+// one hardware queue per process.  Every wait is bounded: the gate records an error word
+// instead of hanging, and a claim kernel ends empty after `idle_us` (the host re-enqueues it).
 #include <fcntl.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -104,6 +118,11 @@ __host__ __device__ inline size_t posted_word(int p, int w, int j) {
 // copy measured ~25 us late: the registered host segment is not guaranteed to bypass the GPU's
 // L2 for a system-scope load)
 DDL_DEV int done_dev_idx(const AsyncShard& S, int j) { return S.slice0 + j; }
+// the arrival words in the PS HOST's uncached device flags (what its claim kernel polls; the
+// host board copy serves the host-scan service, DDL_ASYNC_CLAIM=0)
+__host__ __device__ inline size_t posted_dev_idx(const AsyncShard& S, int w, int j) {
+  return (size_t)kAsyncDense * (1 + w) + S.slice0 + j;
+}
 
 struct PushArgs {
   int world, rank, nps;
@@ -150,9 +169,11 @@ __global__ void __launch_bounds__(256) async_push_kernel(const AsyncTable* __res
   }
   drain_vm();
   __syncthreads();
-  if (tid == 0)
+  if (tid == 0) {
     __hip_atomic_store(T.posted + posted_word(p, a.rank, j), a.epoch, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
+    flag_store(T.flags[S.host] + posted_dev_idx(S, a.rank, j), a.epoch);
+  }
 }
 
 struct ApplyArgs {
@@ -165,14 +186,13 @@ struct ApplyArgs {
   float lr_t, c1, c2, eps, lr, mu, scale;
 };
 
-__global__ void __launch_bounds__(256) async_apply_kernel(const AsyncTable* __restrict__ Tp,
-                                                          ApplyArgs a) {
-  const AsyncTable& T = *Tp;
+// Slice j of one apply.  No arrival poll: the apply runs only after every slice of the push was
+// seen posted (by the claim kernel in front of it, or by the host service), and a push block
+// posts only after its payload stores were acknowledged (the inbox loads below are
+// system-coherent, so they see that payload).
+DDL_DEV void apply_body(const AsyncTable& T, const ApplyArgs& a, int j) {
   const AsyncShard& S = T.shard[a.ps];
-  const int j = blockIdx.x, tid = threadIdx.x;
-  // no arrival poll: the service issues this apply only after it saw every slice of the push
-  // posted on the board, and a push block stores its board word only after its payload stores
-  // were acknowledged (the inbox loads below are system-coherent, so they see that payload)
+  const int tid = threadIdx.x;
   const int64_t s0 = (int64_t)j * S.slice;
   const int64_t s1 = s0 + S.slice < S.n ? s0 + S.slice : S.n;
   const int n4 = s0 < s1 ? (int)((s1 - s0) >> 2) : 0;
@@ -211,6 +231,155 @@ __global__ void __launch_bounds__(256) async_apply_kernel(const AsyncTable* __re
     flag_store(T.flags[a.worker] + done_dev_idx(S, j), a.epoch);  // the worker's gate
     flag_store(T.done + done_word(a.worker, a.ps, j), a.epoch);       // the worker's host
   }
+}
+
+__global__ void __launch_bounds__(256) async_apply_kernel(const AsyncTable* __restrict__ Tp,
+                                                          ApplyArgs a) {
+  apply_body(*Tp, a, blockIdx.x);
+}
+
+}  // namespace
+
+// ---- the on-GPU ANY_SOURCE pop (the default service) ------------------------------------------
+// The service keeps `depth` (claim, apply) kernel pairs enqueued on its high-priority PS stream.
+// The claim kernel (one wave) polls this host's arrival words in its own uncached device flags,
+// round-robin over (hosted PS, worker) from where the last claim stopped, takes the first push
+// whose every slice is posted — the reference's MPI.ANY_SOURCE receive in arrival order
+// (mnist_async_sharding/parameter_server.py:94-111) — advances that PS's step counter, looks up
+// its TF1 Adam step size in a table the host filled with the host formula (bit-identical to the
+// host service), and leaves the claim for the apply kernel behind it (grid = the largest hosted
+// shard's slices; blocks beyond the claimed shard's return).  No host thread and no host launch
+// sits between a push's last slice and its apply: the thread only tops the queue up.
+// The claim kernel waits `idle_us` at most and then ends without a claim (the host re-enqueues):
+// a pair queued for a push that this very process issues only after a device-wide synchronize
+// (torch.cuda.synchronize() before the bench's timed window, a checkpoint, an in-line eval)
+// must not hold that synchronize forever.  It also ends at once when pause() raises `hold`.
+struct ClaimState {
+  int me, world, nh, per_ps, opt;
+  int ps[kAsyncMaxPs];             // hosted PS ids
+  float* params[kAsyncMaxPs];      // their private parameter copies and optimizer state
+  float* m[kAsyncMaxPs];
+  float* v[kAsyncMaxPs];
+  int64_t t0[kAsyncMaxPs];         // step counters at start (the lr table's origin)
+  int64_t t[kAsyncMaxPs];          // step counters (claim kernels only)
+  uint32_t last[kXgmiMaxPeers * kAsyncMaxPs];  // last claimed round per (worker, hosted PS)
+  int start;                       // round-robin position of the next scan
+  int64_t claims, ended;
+  // the current claim: written by a claim kernel, read by the apply kernel behind it
+  int cur_valid, cur_pl, cur_w;
+  uint32_t cur_e;
+  float cur_lr_t;
+  const float* lr_tab;             // [nh][per_ps]: lr_t of step t0 + 1 + i
+  int32_t* prov;                   // [claims][4] (worker, ps, round, t) or null
+  int64_t* host;                   // pinned host words (api.h AsyncService::host_words_)
+  int* err;
+  float c1, c2, eps, lr, mu, scale;
+  long long idle_ticks;
+};
+
+namespace {
+
+__global__ void __launch_bounds__(64) async_claim_kernel(const AsyncTable* __restrict__ Tp,
+                                                         ClaimState* __restrict__ C) {
+  const AsyncTable& T = *Tp;
+  const int lane = threadIdx.x;
+  const int world = C->world, pairs = C->nh * C->world;
+  const uint32_t* posted = T.flags[C->me];
+  const long long deadline = wall_clock64() + C->idle_ticks;
+  int hit = -1;
+  uint32_t hit_e = 0;
+  for (int it = 0; hit < 0; ++it) {
+    for (int i = 0; i < pairs && hit < 0; ++i) {
+      int q = C->start + i;
+      if (q >= pairs) q -= pairs;
+      const int pl = q / world, w = q - pl * world;
+      const AsyncShard& S = T.shard[C->ps[pl]];
+      const uint32_t e = C->last[w * kAsyncMaxPs + pl] + 1;
+      bool all = true;
+      for (int k0 = 0; k0 < S.nslice && all; k0 += 512) {
+        uint32_t f[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int j = k0 + u * 64 + lane;
+          f[u] = j < S.nslice ? __hip_atomic_load(posted + posted_dev_idx(S, w, j),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                              : e;
+        }
+        bool ok = true;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ok &= (int32_t)(f[u] - e) >= 0;
+        all = __all(ok);
+      }
+      if (all) {
+        hit = q;
+        hit_e = e;
+      }
+    }
+    if (hit >= 0) break;
+    if ((it & 15) == 15) {
+      if (__hip_atomic_load(C->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
+      if (__hip_atomic_load(C->host + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
+      if (wall_clock64() > deadline) break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (lane != 0) return;
+  int valid = 0;
+  if (hit >= 0) {
+    const int pl = hit / world, w = hit - pl * world;
+    const int64_t t = C->t[pl] + 1;
+    const int64_t idx = t - C->t0[pl] - 1;
+    if (idx < 0 || idx >= C->per_ps) {
+      // more arrivals than the service was started for: a protocol error, not an update
+      __hip_atomic_store(C->err, 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      valid = 1;
+      C->t[pl] = t;
+      C->last[w * kAsyncMaxPs + pl] = hit_e;
+      C->start = hit + 1 < pairs ? hit + 1 : 0;
+      C->cur_pl = pl;
+      C->cur_w = w;
+      C->cur_e = hit_e;
+      C->cur_lr_t = C->lr_tab[(int64_t)pl * C->per_ps + idx];
+      if (C->prov) {
+        int32_t* r = C->prov + C->claims * 4;
+        r[0] = w;
+        r[1] = C->ps[pl];
+        r[2] = (int32_t)hit_e;
+        r[3] = (int32_t)t;
+      }
+      C->claims += 1;
+      __hip_atomic_store(C->host + 8 + pl, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(C->host + 1, C->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  C->cur_valid = valid;
+  C->ended += 1;
+  __hip_atomic_store(C->host + 0, C->ended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(256) async_claimed_apply_kernel(const AsyncTable* __restrict__ Tp,
+                                                                  const ClaimState* __restrict__ C) {
+  if (!C->cur_valid) return;  // the claim kernel in front ended empty
+  const int pl = C->cur_pl;
+  ApplyArgs a;
+  a.me = C->me;
+  a.ps = C->ps[pl];
+  a.worker = C->cur_w;
+  a.epoch = C->cur_e;
+  a.ps_params = C->params[pl];
+  a.m = C->m[pl];
+  a.v = C->v[pl];
+  a.opt = C->opt;
+  a.lr_t = C->cur_lr_t;
+  a.c1 = C->c1;
+  a.c2 = C->c2;
+  a.eps = C->eps;
+  a.lr = C->lr;
+  a.mu = C->mu;
+  a.scale = C->scale;
+  if ((int)blockIdx.x >= Tp->shard[a.ps].nslice) return;
+  apply_body(*Tp, a, blockIdx.x);
 }
 
 // The worker's pull as a GPU-side gate (async_runner.hip): one wave on the compute stream,
@@ -333,7 +502,7 @@ AsyncPeer::AsyncPeer(float* params, const float* grads, int64_t total, int world
   inbox_elems_ = inbox > 0 ? inbox : 4;
   X_CHECK(hipMalloc(&inbox_, inbox_elems_ * sizeof(float)));
   X_CHECK(hipMemset(inbox_, 0, inbox_elems_ * sizeof(float)));
-  const size_t flag_bytes = (size_t)kAsyncMaxPs * kAsyncMaxSlices * sizeof(uint32_t);
+  const size_t flag_bytes = kAsyncFlagWords * sizeof(uint32_t);  // DONE, then POSTED[worker]
   X_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes,
                                 hipDeviceMallocUncached));
   X_CHECK(hipMemset(flags_, 0, flag_bytes));
@@ -493,6 +662,7 @@ bool AsyncPeer::push_tail(const std::vector<int>& ps, uint32_t epoch, UpdTail& o
     q.w = table_.inbox[S.host] + S.inbox_off + (int64_t)rank_ * S.n;
     q.n = S.n;
     q.posted = table_.posted + posted_word(p, rank_, 0);
+    q.arrive = table_.flags[S.host] + posted_dev_idx(S, rank_, 0);  // the host's device copy
     q.slice4 = (int)(S.slice / 4);
     q.nslice = S.nslice;
     q.blk0 = blk;
@@ -636,24 +806,155 @@ AsyncService::AsyncService(AsyncPeer* peer, int world, int device,
     if (s.ps < 0 || s.ps >= peer->num_ps() || !s.params || !s.m || (opt == 0 && !s.v))
       throw std::invalid_argument("async service: PS state");
   epoch_.assign((size_t)world * kAsyncMaxPs, epoch0);
+  if (const char* c = getenv("DDL_ASYNC_CLAIM")) claim_ = atoi(c) != 0;
+  if (const char* d = getenv("DDL_ASYNC_CLAIM_DEPTH")) depth_ = std::max(1, atoi(d));
+  if (const char* u = getenv("DDL_ASYNC_CLAIM_IDLE_US")) idle_us_ = std::max(10.0, atof(u));
+  if ((int)ps.size() > kAsyncMaxPs) throw std::invalid_argument("async service: too many PS");
 }
 
 AsyncService::~AsyncService() {
   if (th_.joinable()) th_.join();
-  if (stream_) (void)hipStreamDestroy(stream_);
+  if (stream_) {
+    (void)hipStreamSynchronize(stream_);
+    (void)hipStreamDestroy(stream_);
+  }
+  free_claim();
+}
+
+void AsyncService::free_claim() {
+  if (cs_dev_) (void)hipFree(cs_dev_);
+  if (lr_tab_) (void)hipFree(lr_tab_);
+  if (prov_dev_) (void)hipFree(prov_dev_);
+  if (host_words_) (void)hipHostFree(host_words_);
+  cs_dev_ = nullptr;
+  lr_tab_ = nullptr;
+  prov_dev_ = nullptr;
+  host_words_ = nullptr;
 }
 
 void AsyncService::start(int64_t expected) {
   if (th_.joinable()) throw std::runtime_error("async service already running");
   X_CHECK(hipSetDevice(device_));
-  // HIGH priority: HIP pools hardware queues per priority, so the applies never share a queue
-  // with the compute stream, where the worker's GPU-side pull gate may be waiting for them
-  // (async_runner.hip)
+  // HIGH priority: HIP pools hardware queues per priority, so the applies (and the claim
+  // kernels in front of them) never share a queue with the compute stream, where the worker's
+  // GPU-side pull gate may be waiting for them (async_runner.hip)
   int lo = 0, hi = 0;
   X_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   if (!stream_) X_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
   expected_ = expected;
+  const int nh = (int)ps_.size();
+  if (claim_ && nh > 0 && expected % nh == 0) {
+    // every hosted PS serves the same number of arrivals (W x steps): one step-size table row
+    // each, filled with the host service's formula (double precision, rounded once)
+    free_claim();
+    const int64_t per_ps = expected / nh;
+    std::vector<float> tab((size_t)nh * per_ps);
+    for (int i = 0; i < nh; ++i)
+      for (int64_t k = 0; k < per_ps; ++k) {
+        const double t = (double)(ps_[i].t + 1 + k);
+        tab[(size_t)i * per_ps + k] =
+            (float)((double)lr_ * std::sqrt(1.0 - std::pow((double)b2_, t)) /
+                    (1.0 - std::pow((double)b1_, t)));
+      }
+    X_CHECK(hipMalloc(reinterpret_cast<void**>(&lr_tab_), tab.size() * sizeof(float)));
+    X_CHECK(hipMemcpy(lr_tab_, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice));
+    if (keep_prov_)
+      X_CHECK(hipMalloc(reinterpret_cast<void**>(&prov_dev_), (size_t)expected * 16));
+    X_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_words_), (8 + kAsyncMaxPs) * 8,
+                          hipHostMallocDefault));
+    memset(host_words_, 0, (8 + kAsyncMaxPs) * 8);
+    auto cs = std::make_unique<ClaimState>();
+    memset(cs.get(), 0, sizeof(ClaimState));
+    cs->me = peer_->rank_;
+    cs->world = world_;
+    cs->nh = nh;
+    cs->per_ps = (int)std::min<int64_t>(per_ps, 0x7fffffff);
+    cs->opt = opt_;
+    for (int i = 0; i < nh; ++i) {
+      cs->ps[i] = ps_[i].ps;
+      cs->params[i] = ps_[i].params;
+      cs->m[i] = ps_[i].m;
+      cs->v[i] = ps_[i].v;
+      cs->t0[i] = cs->t[i] = ps_[i].t;
+      host_words_[8 + i] = ps_[i].t;
+      for (int w = 0; w < world_; ++w) cs->last[w * kAsyncMaxPs + i] = epoch_[(size_t)w * kAsyncMaxPs + ps_[i].ps];
+    }
+    cs->lr_tab = lr_tab_;
+    cs->prov = prov_dev_;
+    void* hd = nullptr;
+    X_CHECK(hipHostGetDevicePointer(&hd, host_words_, 0));
+    cs->host = reinterpret_cast<int64_t*>(hd);
+    X_CHECK(hipHostGetDevicePointer(&hd, peer_->err_, 0));
+    cs->err = reinterpret_cast<int*>(hd);
+    cs->c1 = 1.f - b1_;
+    cs->c2 = 1.f - b2_;
+    cs->eps = eps_;
+    cs->lr = lr_;
+    cs->mu = mu_;
+    cs->scale = scale_;
+    cs->idle_ticks = (long long)(idle_us_ * 100.0);  // wall_clock64: 100 MHz
+    X_CHECK(hipMalloc(reinterpret_cast<void**>(&cs_dev_), sizeof(ClaimState)));
+    X_CHECK(hipMemcpy(cs_dev_, cs.get(), sizeof(ClaimState), hipMemcpyHostToDevice));
+    th_ = std::thread([this] { run_claim(); });
+    return;
+  }
+  claim_ = false;
   th_ = std::thread([this] { run(); });
+}
+
+// The thread of the device-side service: keep `depth_` claim + apply pairs in flight, never more
+// than the arrivals still to come (each pair claims at most one), and report errors.  It polls
+// two pinned words every ~20 us: nothing it does is on a worker's critical path any more.
+void AsyncService::run_claim() {
+  try {
+    X_CHECK(hipSetDevice(device_));
+    const AsyncTable* T = peer_->table_dev_;
+    int maxs = 1;
+    for (const auto& s : ps_) maxs = std::max(maxs, peer_->table_.shard[s.ps].nslice);
+    int64_t enq = 0, last_claims = 0;
+    auto idle_since = std::chrono::steady_clock::now();
+    TraceRange wait_range("ddl.async.ps.claim_service");
+    for (;;) {
+      // ended first, then claims: a pair that ends between the two reads is counted as
+      // outstanding AND its claim as done (conservative: never one pair too many)
+      const int64_t ended = __atomic_load_n(host_words_ + 0, __ATOMIC_ACQUIRE);
+      const int64_t claims = __atomic_load_n(host_words_ + 1, __ATOMIC_ACQUIRE);
+      if (claims >= expected_) break;
+      if (const int err = peer_->error())
+        throw std::runtime_error("async PS: kernel error (code " + std::to_string(err) + ")");
+      {
+        std::lock_guard<std::mutex> hold(pause_mu_);  // pause(): nothing enqueued while paused
+        while (enq - ended < depth_ && enq - ended < expected_ - claims) {
+          hipLaunchKernelGGL(async_claim_kernel, dim3(1), dim3(64), 0, stream_, T, cs_dev_);
+          DDL_CHECK_LAUNCH();
+          hipLaunchKernelGGL(async_claimed_apply_kernel, dim3(maxs), dim3(256), 0, stream_, T,
+                             cs_dev_);
+          DDL_CHECK_LAUNCH();
+          ++enq;
+        }
+      }
+      const auto now = std::chrono::steady_clock::now();
+      if (claims != last_claims) {
+        last_claims = claims;
+        idle_since = now;
+      } else if (std::chrono::duration<double>(now - idle_since).count() > 600.0) {
+        throw std::runtime_error("async PS: no arrival within 600 s");
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    X_CHECK(hipStreamSynchronize(stream_));
+    if (prov_dev_ && keep_prov_) {
+      std::vector<int32_t> r((size_t)expected_ * 4);
+      X_CHECK(hipMemcpy(r.data(), prov_dev_, r.size() * 4, hipMemcpyDeviceToHost));
+      for (int64_t k = 0; k < expected_; ++k)
+        prov_.push_back({r[k * 4], r[k * 4 + 1], r[k * 4 + 2], r[k * 4 + 3]});
+    }
+    if (const int err = peer_->error())
+      throw std::runtime_error("async PS: kernel error (code " + std::to_string(err) + ")");
+  } catch (const std::exception& ex) {
+    error_ = ex.what();
+    if (stream_) (void)hipStreamSynchronize(stream_);  // no pair left running on an error path
+  }
 }
 
 void AsyncService::serve(AsyncPsState& st, int w) {
@@ -740,6 +1041,9 @@ void AsyncService::join() {
 
 void AsyncService::pause() {
   pause_mu_.lock();
+  // device-side service: `hold` ends every queued claim kernel without a claim (a claim already
+  // taken still applies before the stream drains), and the thread enqueues nothing until resume
+  if (host_words_) __atomic_store_n(host_words_ + 2, (int64_t)1, __ATOMIC_RELEASE);
   if (stream_) {
     const hipError_t e = hipStreamSynchronize(stream_);
     if (e != hipSuccess) {
@@ -749,12 +1053,22 @@ void AsyncService::pause() {
   }
 }
 
-void AsyncService::resume() { pause_mu_.unlock(); }
+void AsyncService::resume() {
+  if (host_words_) __atomic_store_n(host_words_ + 2, (int64_t)0, __ATOMIC_RELEASE);
+  pause_mu_.unlock();
+}
 
 int64_t AsyncService::t(int ps) const {
-  for (const auto& s : ps_)  // lock-free: also read while paused
-    if (s.ps == ps) return __atomic_load_n(&s.t, __ATOMIC_ACQUIRE);
+  for (size_t i = 0; i < ps_.size(); ++i)  // lock-free: also read while paused
+    if (ps_[i].ps == ps)
+      return claim_ && host_words_ ? __atomic_load_n(host_words_ + 8 + i, __ATOMIC_ACQUIRE)
+                                   : __atomic_load_n(&ps_[i].t, __ATOMIC_ACQUIRE);
   throw std::invalid_argument("async service: PS not hosted here");
+}
+
+int64_t AsyncService::served() const {
+  return claim_ && host_words_ ? __atomic_load_n(host_words_ + 1, __ATOMIC_ACQUIRE)
+                               : served_.load();
 }
 
 }  // namespace ddl

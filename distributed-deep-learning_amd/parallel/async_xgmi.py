@@ -123,6 +123,7 @@ class AsyncPeerExchange:
         self.check_provenance = check_provenance
         self.provenance: List[Tuple[int, int, int, int]] = []
         self.runner = None
+        self.service_mode = None
 
     # -- the native worker step ----------------------------------------------------------------------
     def attach_runner(self, engine, segments) -> None:
@@ -212,6 +213,7 @@ class AsyncPeerExchange:
             self.peer, self.env.world, ps_list, self.opt, h.lr, h.beta1, h.beta2, h.eps, mom,
             self.grad_scale, 1, self.check_provenance)
         self._svc.start(n)
+        self.service_mode = self._svc.mode()  # "device-claim" (default) or "host"
 
     def _sync_counters(self, svc) -> None:
         """The native service advances each hosted PS's step counter; mirror it into the

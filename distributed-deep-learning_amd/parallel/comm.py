@@ -55,6 +55,31 @@ class DistEnv:
         return self.world > 1
 
 
+def share_gpu_queue_cap(local_world: int) -> Optional[str]:
+    """Ranks sharing one GPU (the one-box rehearsal): one hardware queue per process.
+
+    HIP gives every process ``GPU_MAX_HW_QUEUES`` (4) hardware queues per priority it uses.  Four
+    processes with the compute, PS comm (high priority) and side-stream eval (low priority)
+    streams map more user queues than the command processor's hardware queue slots, so it
+    time-slices them: a kernel spinning on a peer's flag (the xGMI pull gate, an owner bucket's
+    arrival wait) then waits for the queue that holds the peer's kernel to be mapped in again —
+    a runlist rotation, milliseconds.  Measured on one MI355X, W = 4 one-card time-to-accuracy
+    with side-stream eval: epoch 14.87 s with the default queues, 0.98 s with one queue per
+    process (`profiles/r5_w4_one_card_queues.txt`).  Must run before anything initialises HIP
+    (``torch.cuda.is_available()`` does; ``device_count()`` does not).  The GPU boxes export
+    ``GPU_MAX_HW_QUEUES=4`` (HIP's default) for every job, so a shared-GPU job overrides it;
+    ``DDL_SHARED_GPU_HW_QUEUES`` picks another value (``keep``: leave the environment alone).
+    Returns the value set."""
+    want = os.environ.get("DDL_SHARED_GPU_HW_QUEUES", "1")
+    if local_world <= 1 or want == "keep":
+        return None
+    ndev = torch.cuda.device_count()
+    if ndev == 0 or local_world <= ndev:
+        return None  # one process per GPU: HIP's default queues
+    os.environ["GPU_MAX_HW_QUEUES"] = want
+    return want
+
+
 def init_distributed(device: str = "auto") -> DistEnv:
     """One process per GPU.  Reads RANK/WORLD_SIZE/LOCAL_RANK (torchrun); backend
     ``nccl`` (= RCCL on ROCm) on GPU, ``gloo`` on CPU.
@@ -66,6 +91,7 @@ def init_distributed(device: str = "auto") -> DistEnv:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    share_gpu_queue_cap(int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
     use_gpu = (device == "cuda") or (device == "auto" and torch.cuda.is_available())
     backend = None
     if world > 1:

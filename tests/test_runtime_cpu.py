@@ -171,6 +171,28 @@ def test_reference_pickle_refuses_other_globals(tmp_path):
             load_file(str(f))
 
 
+def test_shared_gpu_ranks_get_one_hw_queue(monkeypatch):
+    from ddl_amd.parallel import comm
+    monkeypatch.delenv("DDL_SHARED_GPU_HW_QUEUES", raising=False)
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")          # what the GPU boxes export
+    monkeypatch.setattr(comm.torch.cuda, "device_count", lambda: 1)
+    assert comm.share_gpu_queue_cap(1) is None           # one process: HIP's default
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "4"
+    assert comm.share_gpu_queue_cap(4) == "1"             # four ranks on one card
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "1"
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    monkeypatch.setenv("DDL_SHARED_GPU_HW_QUEUES", "keep")
+    assert comm.share_gpu_queue_cap(4) is None and os.environ["GPU_MAX_HW_QUEUES"] == "4"
+    monkeypatch.setenv("DDL_SHARED_GPU_HW_QUEUES", "2")
+    assert comm.share_gpu_queue_cap(4) == "2" and os.environ["GPU_MAX_HW_QUEUES"] == "2"
+    monkeypatch.delenv("DDL_SHARED_GPU_HW_QUEUES")
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    monkeypatch.setattr(comm.torch.cuda, "device_count", lambda: 8)
+    assert comm.share_gpu_queue_cap(8) is None            # one process per GPU
+    monkeypatch.setattr(comm.torch.cuda, "device_count", lambda: 0)
+    assert comm.share_gpu_queue_cap(4) is None            # CPU ranks
+
+
 def test_batch_indices_semantics():
     # reference: every worker walks the same slices (Q5)
     assert batch_indices(3, 100, 50000, rank=2, world=4) == (300, 400)

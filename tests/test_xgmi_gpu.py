@@ -218,6 +218,9 @@ def _async_rank(rank, world, port, outdir, kw):
         assert (tr.exchange.runner is not None) == want_native, "native async step not taken"
         s = tr.train()  # verify_provenance runs inside (check_provenance=True)
         torch.cuda.synchronize()
+        if tr.servers:  # the PS service this host ran: claim kernels unless DDL_ASYNC_CLAIM=0
+            want = "host" if extra_env.get("DDL_ASYNC_CLAIM") == "0" else "device-claim"
+            assert tr.exchange.service_mode == want, tr.exchange.service_mode
         torch.save({"params": tr.params.cpu(), "served": tr.exchange.served,
                     "ps": {p: (sv.t, sv.params.cpu()) for p, sv in tr.servers.items()},
                     "ranges": {p: tr.plan.ps_segments(p)[0] for p in tr.servers},
@@ -240,6 +243,10 @@ def _async_rank(rank, world, port, outdir, kw):
     # segment-aligned flat plans (sharding.segment_aligned_num_ps): 4 PS on one host, 6 on two
     pytest.param(1, dict(shard="flat", _ps=4), id="1-flat"),
     pytest.param(2, dict(shard="flat", _ps=6), id="2-flat"),
+    # the host-scan PS service (the default pops arrivals with claim kernels on the GPU)
+    pytest.param(2, dict(shard="contiguous", _env=dict(DDL_ASYNC_CLAIM="0")), id="2-host-service"),
+    pytest.param(4, dict(shard="greedy", num_ps=4, _env=dict(DDL_ASYNC_CLAIM="0")),
+                 id="4-host-service"),
     pytest.param(8, dict(shard="contiguous", _env=dict(GPU_MAX_HW_QUEUES="1",
                                                        DDL_XGMI_TIMEOUT_S="60")), id="w8-contig"),
     pytest.param(8, dict(shard="greedy", _env=dict(GPU_MAX_HW_QUEUES="1",
