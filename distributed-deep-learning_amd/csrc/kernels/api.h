@@ -361,6 +361,11 @@ struct AsyncTable {
   uint32_t* flags[kXgmiMaxPeers];
   uint32_t* done;                // DONE[worker][ps][slice] in host memory shared by all ranks
   uint32_t* posted;              // the arrival board POSTED[ps][worker][slice], same segment
+  // this rank's gradient buffer: with `elide` set, a push to a PS this rank hosts itself only
+  // posts its words, and the apply of this worker's push reads the gradient here instead of an
+  // inbox copy (the worker overwrites it only after its pull gate, i.e. after that apply)
+  const float* grads;
+  int elide;
   AsyncShard shard[kAsyncMaxPs];
 };
 

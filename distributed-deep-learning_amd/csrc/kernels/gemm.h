@@ -64,9 +64,11 @@ DDL_DEV void push_tail_body(const UpdTail& t, const UpdPiece& P, int b) {
   const int64_t s0 = (int64_t)j * P.slice4;
   const int cnt = (int)((s0 + P.slice4 < n4 ? s0 + P.slice4 : n4) - s0);
   const float4* src = reinterpret_cast<const float4*>(P.g) + s0;
-  const brsrc_t dst = make_rsrc(P.w + s0 * 4, (uint32_t)cnt * 16u);
-  for (int i = lane; i < cnt; i += 64) bstore4_sys(dst, i * 16, src[i]);
-  drain_vmem();
+  if (P.w) {  // (null: a shard this rank hosts, posted only — xgmi_async.hip AsyncTable::elide)
+    const brsrc_t dst = make_rsrc(P.w + s0 * 4, (uint32_t)cnt * 16u);
+    for (int i = lane; i < cnt; i += 64) bstore4_sys(dst, i * 16, src[i]);
+    drain_vmem();
+  }
   if (lane == 0) {
     __hip_atomic_store(P.posted + j, t.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // the PS host's device copy of the word: what its claim kernel polls (xgmi_async.hip)

@@ -162,7 +162,8 @@ __global__ void __launch_bounds__(256) async_push_kernel(const AsyncTable* __res
   const float4* src = reinterpret_cast<const float4*>(a.grads + S.lo + s0);
   const brsrc_t dst = make_rsrc(T.inbox[S.host] + S.inbox_off + (int64_t)a.rank * S.n + s0,
                                 (uint32_t)n4 * 16u);
-  for (int i = tid; i < n4; i += 256) {
+  const bool local = T.elide && S.host == a.rank;  // the apply reads T.grads itself
+  for (int i = local ? n4 : tid; i < n4; i += 256) {
     float4 x = src[i];
     if (a.coef != 1.f) { x.x *= a.coef; x.y *= a.coef; x.z *= a.coef; x.w *= a.coef; }
     bstore4_sys(dst, i * 16, x);
@@ -196,8 +197,10 @@ DDL_DEV void apply_body(const AsyncTable& T, const ApplyArgs& a, int j) {
   const int64_t s0 = (int64_t)j * S.slice;
   const int64_t s1 = s0 + S.slice < S.n ? s0 + S.slice : S.n;
   const int n4 = s0 < s1 ? (int)((s1 - s0) >> 2) : 0;
-  const brsrc_t in = make_rsrc(T.inbox[a.me] + S.inbox_off + (int64_t)a.worker * S.n + s0,
-                               (uint32_t)n4 * 16u);
+  const float* src = T.elide && a.worker == a.me
+                        ? T.grads + S.lo + s0  // this rank's own push: no inbox copy
+                        : T.inbox[a.me] + S.inbox_off + (int64_t)a.worker * S.n + s0;
+  const brsrc_t in = make_rsrc(src, (uint32_t)n4 * 16u);
   const brsrc_t out = make_rsrc(T.params[a.worker] + S.lo + s0, (uint32_t)n4 * 16u);
   float4* w4 = reinterpret_cast<float4*>(a.ps_params + s0);
   float4* m4 = reinterpret_cast<float4*>(a.m + s0);
@@ -275,9 +278,22 @@ struct ClaimState {
   int* err;
   float c1, c2, eps, lr, mu, scale;
   long long idle_ticks;
+  int publish_in_claim;            // DDL_ASYNC_PUBLISH=claim (A/B)
 };
 
 namespace {
+
+// The service thread's view of the claim in front (pinned host words).  Stored by block 0 AFTER
+// its slice's DONE flags: a wave's drain before its flag store would otherwise wait out these
+// stores' PCIe round trip, and the worker's gate waits for that flag.
+DDL_DEV void publish_claim(const ClaimState* C) {
+  if (C->cur_valid)
+    __hip_atomic_store(C->host + 8 + C->cur_pl, C->t[C->cur_pl], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(C->host + 1, C->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // (release: a host that sees this `ended` sees the `claims` stored before it)
+  __hip_atomic_store(C->host + 0, C->ended, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __global__ void __launch_bounds__(64) async_claim_kernel(const AsyncTable* __restrict__ Tp,
                                                          ClaimState* __restrict__ C) {
@@ -286,33 +302,63 @@ __global__ void __launch_bounds__(64) async_claim_kernel(const AsyncTable* __res
   const int world = C->world, pairs = C->nh * C->world;
   const uint32_t* posted = T.flags[C->me];
   const long long deadline = wall_clock64() + C->idle_ticks;
+  // per pair, the first slice of its next round not yet seen posted (LDS, this wave only).  A
+  // sweep issues one load per lane for up to 8 pairs at once (64 slices each, one round of
+  // uncached-load latency for all of them) and only follows a pair further, 512 slices per
+  // batch, once its first 64 landed: the pair whose push just completed is found within about
+  // one load latency, whatever the number of pairs
+  __shared__ int seen[kAsyncMaxPs * kXgmiMaxPeers];
+  for (int q = lane; q < pairs; q += 64) seen[q] = 0;
+  __builtin_amdgcn_wave_barrier();
   int hit = -1;
   uint32_t hit_e = 0;
   for (int it = 0; hit < 0; ++it) {
-    for (int i = 0; i < pairs && hit < 0; ++i) {
-      int q = C->start + i;
-      if (q >= pairs) q -= pairs;
-      const int pl = q / world, w = q - pl * world;
-      const AsyncShard& S = T.shard[C->ps[pl]];
-      const uint32_t e = C->last[w * kAsyncMaxPs + pl] + 1;
-      bool all = true;
-      for (int k0 = 0; k0 < S.nslice && all; k0 += 512) {
-        uint32_t f[8];
+    for (int g = 0; g < pairs && hit < 0; g += 8) {
+      uint32_t f[8], e[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int j = k0 + u * 64 + lane;
-          f[u] = j < S.nslice ? __hip_atomic_load(posted + posted_dev_idx(S, w, j),
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                              : e;
-        }
-        bool ok = true;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) ok &= (int32_t)(f[u] - e) >= 0;
-        all = __all(ok);
+      for (int u = 0; u < 8; ++u) {
+        f[u] = e[u] = 0;
+        if (g + u >= pairs) continue;
+        int q = C->start + g + u;
+        if (q >= pairs) q -= pairs;
+        const int pl = q / world, w = q - pl * world;
+        const AsyncShard& S = T.shard[C->ps[pl]];
+        e[u] = C->last[w * kAsyncMaxPs + pl] + 1;
+        const int j = seen[q] + lane;
+        f[u] = j < S.nslice ? __hip_atomic_load(posted + posted_dev_idx(S, w, j),
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                            : e[u];
       }
-      if (all) {
-        hit = q;
-        hit_e = e;
+      for (int u = 0; u < 8 && g + u < pairs && hit < 0; ++u) {
+        if (!__all((int32_t)(f[u] - e[u]) >= 0)) continue;
+        int q = C->start + g + u;
+        if (q >= pairs) q -= pairs;
+        const int pl = q / world, w = q - pl * world;
+        const AsyncShard& S = T.shard[C->ps[pl]];
+        int k0 = seen[q] + 64;
+        bool all = true;
+        while (all && k0 < S.nslice) {  // the rest of this pair, 512 slices per batch
+          uint32_t v[8];
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            const int j = k0 + b * 64 + lane;
+            v[b] = j < S.nslice ? __hip_atomic_load(posted + posted_dev_idx(S, w, j),
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                : e[u];
+          }
+          bool ok = true;
+#pragma unroll
+          for (int b = 0; b < 8; ++b) ok &= (int32_t)(v[b] - e[u]) >= 0;
+          all = __all(ok);
+          if (all) k0 += 512;
+        }
+        if (all) {
+          hit = q;
+          hit_e = e[u];
+        } else if (lane == 0) {
+          seen[q] = k0;  // (a batch that failed is re-read from its start next sweep)
+        }
+        __builtin_amdgcn_wave_barrier();
       }
     }
     if (hit >= 0) break;
@@ -321,7 +367,9 @@ __global__ void __launch_bounds__(64) async_claim_kernel(const AsyncTable* __res
       if (__hip_atomic_load(C->host + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
       if (wall_clock64() > deadline) break;
     }
-    __builtin_amdgcn_s_sleep(1);
+    // ~0.45 us between sweeps: the claim wave polls while the backward's GEMMs run, and a
+    // tighter poll loop measurably slows them (the READY gate's lesson, runner.hip)
+    __builtin_amdgcn_s_sleep(16);
   }
   if (lane != 0) return;
   int valid = 0;
@@ -349,18 +397,22 @@ __global__ void __launch_bounds__(64) async_claim_kernel(const AsyncTable* __res
         r[3] = (int32_t)t;
       }
       C->claims += 1;
-      __hip_atomic_store(C->host + 8 + pl, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(C->host + 1, C->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   C->cur_valid = valid;
   C->ended += 1;
-  __hip_atomic_store(C->host + 0, C->ended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // the host-visible copies of these counters: stored by the apply kernel behind (default), or
+  // here (DDL_ASYNC_PUBLISH=claim: holds this kernel's end, and so the apply's start, for a
+  // PCIe round trip)
+  if (C->publish_in_claim) publish_claim(C);
 }
 
 __global__ void __launch_bounds__(256) async_claimed_apply_kernel(const AsyncTable* __restrict__ Tp,
                                                                   const ClaimState* __restrict__ C) {
-  if (!C->cur_valid) return;  // the claim kernel in front ended empty
+  if (!C->cur_valid) {  // the claim kernel in front ended empty
+    if (blockIdx.x == 0 && threadIdx.x == 0 && !C->publish_in_claim) publish_claim(C);
+    return;
+  }
   const int pl = C->cur_pl;
   ApplyArgs a;
   a.me = C->me;
@@ -380,6 +432,7 @@ __global__ void __launch_bounds__(256) async_claimed_apply_kernel(const AsyncTab
   a.scale = C->scale;
   if ((int)blockIdx.x >= Tp->shard[a.ps].nslice) return;
   apply_body(*Tp, a, blockIdx.x);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && !C->publish_in_claim) publish_claim(C);
 }
 
 // The worker's pull as a GPU-side gate (async_runner.hip): one wave on the compute stream,
@@ -512,6 +565,9 @@ AsyncPeer::AsyncPeer(float* params, const float* grads, int64_t total, int world
   X_CHECK(hipDeviceSynchronize());
   const char* t = getenv("DDL_XGMI_TIMEOUT_S");
   timeout_s_ = t ? atof(t) : 60.0;
+  const char* el = getenv("DDL_ASYNC_ELIDE_LOCAL");
+  table_.grads = grads;
+  table_.elide = el ? atoi(el) != 0 : 1;
 }
 
 AsyncPeer::~AsyncPeer() { close(); }
@@ -607,6 +663,8 @@ void AsyncPeer::push_all(uint32_t epoch, float coef, hipStream_t st) {
   a.first_blk[nps_] = blk;
   a.grads = grads_;
   a.coef = coef;
+  if (coef != 1.f && table_.elide)
+    throw std::invalid_argument("async xgmi: a scaled push needs DDL_ASYNC_ELIDE_LOCAL=0");
   hipLaunchKernelGGL(async_push_kernel, dim3(blk), dim3(256), 0, st, table_dev_, a);
   DDL_CHECK_LAUNCH();
 }
@@ -633,6 +691,8 @@ void AsyncPeer::push_set(const std::vector<int>& ps, uint32_t epoch, float coef,
   a.first_blk[ps.size()] = blk;
   a.grads = grads_;
   a.coef = coef;
+  if (coef != 1.f && table_.elide)
+    throw std::invalid_argument("async xgmi: a scaled push needs DDL_ASYNC_ELIDE_LOCAL=0");
   a.subset = 1;
   if (with_gate) {  // one more block: the pull gate of round `epoch`
     if (!table_.done) throw std::runtime_error("async xgmi: attach_done() first");
@@ -659,7 +719,9 @@ bool AsyncPeer::push_tail(const std::vector<int>& ps, uint32_t epoch, UpdTail& o
     const AsyncShard& S = table_.shard[p];
     UpdPiece& q = t.p[t.npieces++];
     q.g = grads_ + S.lo;
-    q.w = table_.inbox[S.host] + S.inbox_off + (int64_t)rank_ * S.n;
+    // a shard this rank hosts itself: post only (the apply reads the gradient in place)
+    q.w = table_.elide && S.host == rank_ ? nullptr
+                                          : table_.inbox[S.host] + S.inbox_off + (int64_t)rank_ * S.n;
     q.n = S.n;
     q.posted = table_.posted + posted_word(p, rank_, 0);
     q.arrive = table_.flags[S.host] + posted_dev_idx(S, rank_, 0);  // the host's device copy
@@ -893,6 +955,8 @@ void AsyncService::start(int64_t expected) {
     cs->mu = mu_;
     cs->scale = scale_;
     cs->idle_ticks = (long long)(idle_us_ * 100.0);  // wall_clock64: 100 MHz
+    const char* pub = getenv("DDL_ASYNC_PUBLISH");
+    cs->publish_in_claim = pub && std::string(pub) == "claim";
     X_CHECK(hipMalloc(reinterpret_cast<void**>(&cs_dev_), sizeof(ClaimState)));
     X_CHECK(hipMemcpy(cs_dev_, cs.get(), sizeof(ClaimState), hipMemcpyHostToDevice));
     th_ = std::thread([this] { run_claim(); });
