@@ -97,9 +97,11 @@ def main(argv=None):
                          "(default on GPU: side-stream eval from parameter snapshots)")
     ap.add_argument("--prewarm-steps", type=int, default=-1,
                     help="untimed training steps BEFORE the --warmup steps (reported in the "
-                         "JSON; default 100 on a GPU, 0 on CPU).  Measured on MI355X: after 5 warmup steps a 20-step window "
+                         "JSON; default 1000 on a GPU, 0 on CPU).  Measured on MI355X: after 5 warmup steps a 20-step window "
                          "runs 0.321-0.323 ms/step, after 100 0.308-0.312 (the GPU is still "
-                         "ramping up); --steps 200 --warmup 5 amortises it to 0.307")
+                         "ramping up); round 5, the driver's --steps 20 --warmup 5 on one box, 4 "
+                         "alternating rounds: prewarm 100 0.2967-0.2979, 300 0.2958-0.3012, 1000 "
+                         "0.2955-0.2965 ms/step (profiles/r5_driver_window_prewarm.txt)")
     ap.add_argument("--extra-plans", default="contiguous",
                     help="W > 1 sync: comma-separated shard plans also timed after the headline "
                          "plan (same steps), reported under 'plans' (BASELINE config 3 names "
@@ -120,7 +122,7 @@ def main(argv=None):
         if env.rank == 0:
             print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     cuda = env.device.type == "cuda"
-    n_pre = a.prewarm_steps if a.prewarm_steps >= 0 else (100 if cuda else 0)
+    n_pre = a.prewarm_steps if a.prewarm_steps >= 0 else (1000 if cuda else 0)
     total_steps = n_pre + a.warmup + a.steps
     data = synthetic_mnist()
 
@@ -399,7 +401,8 @@ def main(argv=None):
             "test_acc_after_run": round(acc, 4),
             "prewarm": {"steps": n_pre, "note": "untimed steps before the warmup steps: the "
                         "GPU is still ramping up after a few steps (20-step window after 5 "
-                        "warmup steps: 0.322 vs 0.308 ms/step after 100)"},
+                        "warmup steps: 0.322 vs 0.308 ms/step after 100; after 1000 the "
+                        "20-step window spreads 1 us instead of 1-5 us)"},
         }
         if handoff:
             rec["handoff_check"] = handoff

@@ -33,9 +33,11 @@ Engine::Engine() {
   // launch with its weight gradient, like fc1's: 292.8 -> 291.5 us, profiles/r3_runner_tune.log)
   // (round 5, scripts/sched_ab.py on one MI355X, 5 alternating rounds of 300 steps: conv4
   // weight gradient and conv2 data gradient on the 16x16x4 MFMA tile (config 14), conv4 weight
-  // gradient split 8: 295.3 -> 293.0 us, profiles/r5_sched_ab_mf16.log)
+  // gradient split 8: 295.3 -> 293.0 us, profiles/r5_sched_ab_mf16.log; then conv3 weight
+  // gradient on config 14 too: 293.5 -> 292.7 us, profiles/r5_sched_ab_conv3w.log — conv2's
+  // weight gradient on it loses 6 us)
   static const int defc[OP_COUNT] = {3, 3, 3, 3, CFG_KWAVE, 3, CFG_KWAVE, 5, CFG_KWAVE, 5,
-                                     3, CFG_MF16, 3, 3, CFG_MF16, 3, 3};
+                                     3, CFG_MF16, 3, CFG_MF16, CFG_MF16, 3, 3};
   // (re-tuned in the real step with scripts/sched_ab.py after the compact 52-row conv3
   // enumeration and the wgrad row decode: conv3 forward split 4 + in-launch reduce instead of
   // stream-K 3072 workers, 372.4 -> 369.5 us; conv4 weight gradient split 4 instead of 8,

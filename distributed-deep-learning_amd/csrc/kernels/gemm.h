@@ -1197,6 +1197,48 @@ struct GemmTile {
           acc[i][j][4 * g + 2] += t.z; acc[i][j][4 * g + 3] += t.w;
         }
   }
+  // The last arriver's sum of the gz partials at base0 + z * zstride, in z order (bit-identical
+  // to zero() + one add_partial per z) with the loads of ZB partials in flight per round: one
+  // add_partial per z waits a full sc1-load latency per partial, so a 12-way split's last
+  // arriver spent ~12 load round trips in its epilogue — the longest block of the launch.
+#ifndef DDL_SPLITK_ZB
+#define DDL_SPLITK_ZB 4  // partials in flight per round for a one-fragment tile (1: the old chain)
+#endif
+  static constexpr int ZB = TM * TN >= DDL_SPLITK_ZB ? 1 : DDL_SPLITK_ZB / (TM * TN);
+  static DDL_DEV void sum_partials(brsrc_t slab, size_t base0, size_t zstride, int gz,
+                                   f32x16 (&acc)[TM][TN]) {
+    zero(acc);
+    const int lane_off = ((threadIdx.x & (NT - 1)) >> 6) * WPART + (threadIdx.x & 63);
+    int z = 0;
+    if constexpr (ZB > 1) {
+      for (; z + ZB <= gz; z += ZB) {
+        float4 t[ZB][TM][TN][4];
+#pragma unroll
+        for (int b = 0; b < ZB; ++b) {
+          const int src = (int)(base0 + (size_t)(z + b) * zstride) + lane_off;
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+              for (int g = 0; g < 4; ++g)
+                t[b][i][j][g] = bload4_sc1(slab, (src + ((i * TN + j) * 4 + g) * 64) * 16);
+        }
+#pragma unroll
+        for (int b = 0; b < ZB; ++b)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+              for (int g = 0; g < 4; ++g) {
+                acc[i][j][4 * g] += t[b][i][j][g].x; acc[i][j][4 * g + 1] += t[b][i][j][g].y;
+                acc[i][j][4 * g + 2] += t[b][i][j][g].z; acc[i][j][4 * g + 3] += t[b][i][j][g].w;
+              }
+      }
+    }
+    for (; z < gz; ++z) add_partial(slab, base0 + (size_t)z * zstride, acc);
+  }
   static DDL_DEV void zero(f32x16 (&acc)[TM][TN]) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -1274,8 +1316,7 @@ DDL_DEV int splitk_body(const P& p, int kchunk, int mode, float4* __restrict__ s
     T::store_partial(sr, ((size_t)bz * ntiles + tile) * G::PART4, acc);
     if (mode == 2) return nkt;
     if (!T::arrive(&tickets[tile], gz, flag)) return nkt;
-    T::zero(acc);
-    for (int z = 0; z < gz; ++z) T::add_partial(sr, ((size_t)z * ntiles + tile) * G::PART4, acc);
+    T::sum_partials(sr, (size_t)tile * G::PART4, (size_t)ntiles * G::PART4, gz, acc);
   }
   T::epilogue(p, m_blk, n_blk, acc);
   return nkt;
