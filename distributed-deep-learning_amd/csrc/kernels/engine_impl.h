@@ -262,12 +262,15 @@ inline void dual_b(Engine& e, const PA& pa, const PB& pb, int B, hipStream_t st)
 // Ops OA and OB (independent) in one launch if both use one-wave tiles, else back to back.
 // OA on the K-wave config (fc data gradients) with OB on a one-wave 32x32 config: one packed
 // launch (gemm.h gemm_pack_kernel; OB's tiles run BK 32 there).
+// (fc only: the packed launch runs OB's tiles unsplit over the raw K range, which the conv weight
+// gradients' tap-window K maps do not support; a conv pair with a K-wave op runs back to back)
 template <int OA, int OB>
 void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
-  if (e.dual && e.cfg[OA] == CFG_KWAVE && (e.cfg[OB] == 3 || e.cfg[OB] == 5)) {
+  constexpr bool fc_pair = OA == OP_FC2_DGRAD || OA == OP_FC1_DGRAD;
+  if (fc_pair && e.dual && e.cfg[OA] == CFG_KWAVE && (e.cfg[OB] == 3 || e.cfg[OB] == 5)) {
     const auto pa = make_policy<OA>(e, B, x, seed, true);
     const auto pb = make_policy<OB>(e, B, x, seed, true);
-    if constexpr (KWaveOK<std::decay_t<decltype(pa)>>::value) {
+    if constexpr (fc_pair && KWaveOK<std::decay_t<decltype(pa)>>::value) {
       if constexpr (OA == OP_FC2_DGRAD) {
         e.flush_tail(st);
         launch_gemm_pack(pa, e.splits[OA], pb, head_aux(e, B), st);

@@ -905,5 +905,11 @@ template <>
 struct KWaveOK<FcDgradAct> : std::true_type {};
 template <int HP, int C>
 struct KWaveOK<FcDgradPool<HP, C>> : std::true_type {};
+// conv backward as K-wave tiles (round 5 experiment: the split-K partial slab, tickets and
+// last-arriver sums replaced by an LDS reduction inside the workgroup; not dual-launched)
+template <int H, int CIN, int COUT>
+struct KWaveOK<ConvWgradBM<H, CIN, COUT>> : std::true_type {};
+template <int H, int CIN, int COUT, int HPREV>
+struct KWaveOK<ConvDgrad<H, CIN, COUT, HPREV>> : std::true_type {};
 
 }  // namespace ddl

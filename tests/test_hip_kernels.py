@@ -340,20 +340,28 @@ def test_inlaunch_splitk_reduce_matches_reference(setup, cfg, wide):
 
 
 @pytest.mark.parametrize("waves", [4, 8, 16])
-@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("packed", [False, True, "conv"])  # "conv": back to back (no pack)
 def test_kwave_config_matches_reference(setup, waves, packed):
-    """The fc GEMMs on the K-wave launch (CFG_KWAVE = 13: K split over the waves of one
+    """The GEMMs on the K-wave launch (CFG_KWAVE = 13: K split over the waves of one
     workgroup, LDS reduction, fused epilogue): fp64-reference gradients, bit-deterministic
-    across runs.  packed=False: every op set to 13 (non-fc ops fall back to one-wave 32x32,
-    the fc duals run back to back); packed=True: only the fc data gradients on 13, so each fc
-    backward is one packed launch with its weight gradient and the fc3 aux blocks."""
+    across runs.  packed=False: every op set to 13 (the forward convs fall back to one-wave
+    32x32, the fc and conv backward pairs run back to back as K-wave launches); packed=True:
+    only the fc data gradients on 13, so each fc backward is one packed launch with its weight
+    gradient and the fc3 aux blocks; "conv": the conv4 / conv3 data gradients on 13 with their
+    weight gradients on the one-wave tile — the pair the fc backward packs; a conv pair runs
+    back to back instead (engine_impl.h run_dual_inst)."""
     eng, flat, params, grads, x, y = setup
     base_cfg, base_s, base_w = eng.get_cfg(), eng.get_splits(), eng.get_workers()
     try:
         if packed:
             cfg, spl = list(base_cfg), list(base_s)
-            for op in (6, 8):  # fc2_dgrad, fc1_dgrad
+            # conv4 / conv3 or fc data gradients (conv2's weight gradient is reduced inside
+            # conv1's launch from its split-K partials, so it keeps its split form)
+            dg = (10, 12) if packed == "conv" else (6, 8)
+            for op in dg:
                 cfg[op], spl[op] = 13, waves
+                if packed == "conv":
+                    cfg[op + 1] = 3
             eng.set_cfg(cfg)
             eng.set_splits(spl)
         else:
