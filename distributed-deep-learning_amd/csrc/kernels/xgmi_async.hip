@@ -295,10 +295,9 @@ DDL_DEV void publish_claim(const ClaimState* C) {
   __hip_atomic_store(C->host + 0, C->ended, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void __launch_bounds__(64) async_claim_kernel(const AsyncTable* __restrict__ Tp,
-                                                         ClaimState* __restrict__ C) {
-  const AsyncTable& T = *Tp;
-  const int lane = threadIdx.x;
+// One wave (lanes 0-63 of the calling workgroup) claims the next arrival into C.
+DDL_DEV void claim_body(const AsyncTable& T, ClaimState* __restrict__ C) {
+  const int lane = threadIdx.x & 63;
   const int world = C->world, pairs = C->nh * C->world;
   const uint32_t* posted = T.flags[C->me];
   const long long deadline = wall_clock64() + C->idle_ticks;
@@ -401,10 +400,79 @@ __global__ void __launch_bounds__(64) async_claim_kernel(const AsyncTable* __res
   }
   C->cur_valid = valid;
   C->ended += 1;
+}
+
+__global__ void __launch_bounds__(64) async_claim_kernel(const AsyncTable* __restrict__ Tp,
+                                                         ClaimState* __restrict__ C) {
+  claim_body(*Tp, C);
   // the host-visible copies of these counters: stored by the apply kernel behind (default), or
   // here (DDL_ASYNC_PUBLISH=claim: holds this kernel's end, and so the apply's start, for a
   // PCIe round trip)
-  if (C->publish_in_claim) publish_claim(C);
+  if (threadIdx.x == 0 && C->publish_in_claim) publish_claim(C);
+}
+
+// Claim and apply in ONE launch (DDL_ASYNC_FUSED=1): wave 0 of block 0 claims; the claim goes
+// to every block through a record in this rank's uncached flags (payload words, a drain, then
+// the launch's sequence number), and the `grid` blocks apply the claimed shard's slices
+// j = block, block + grid, ...  No kernel boundary between the claim and the apply; the
+// waiting blocks sleep ~0.45 us per poll.  Bounded: block 0 always publishes a record (the
+// claim loop ends on idle / hold / error), and a block that never sees one gives up with
+// error 8 after the idle bound plus 1 s.
+__global__ void __launch_bounds__(256) async_fused_claim_apply_kernel(
+    const AsyncTable* __restrict__ Tp, ClaimState* __restrict__ C, uint32_t seq) {
+  const AsyncTable& T = *Tp;
+  uint32_t* rec = T.flags[C->me] + kAsyncClaimRec;
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    claim_body(T, C);
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(rec + 1, (uint32_t)C->cur_valid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(rec + 2, (uint32_t)C->cur_pl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(rec + 3, (uint32_t)C->cur_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(rec + 4, C->cur_e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(rec + 5, __float_as_uint(C->cur_lr_t), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      drain_vm();
+      __hip_atomic_store(rec, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  __shared__ uint32_t got[6];
+  if (threadIdx.x == 0) {
+    const long long deadline = wall_clock64() + C->idle_ticks + 100000000LL;
+    while (__hip_atomic_load(rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+      if (wall_clock64() > deadline) {
+        __hip_atomic_store(C->err, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        got[1] = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(16);
+    }
+    if (__hip_atomic_load(rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq)
+      for (int i = 1; i < 6; ++i)
+        got[i] = __hip_atomic_load(rec + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  if (got[1]) {
+    const int pl = (int)got[2];
+    ApplyArgs a;
+    a.me = C->me;
+    a.ps = C->ps[pl];
+    a.worker = (int)got[3];
+    a.epoch = got[4];
+    a.ps_params = C->params[pl];
+    a.m = C->m[pl];
+    a.v = C->v[pl];
+    a.opt = C->opt;
+    a.lr_t = __uint_as_float(got[5]);
+    a.c1 = C->c1;
+    a.c2 = C->c2;
+    a.eps = C->eps;
+    a.lr = C->lr;
+    a.mu = C->mu;
+    a.scale = C->scale;
+    const int ns = T.shard[a.ps].nslice;
+    for (int j = blockIdx.x; j < ns; j += gridDim.x) apply_body(T, a, j);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) publish_claim(C);
 }
 
 __global__ void __launch_bounds__(256) async_claimed_apply_kernel(const AsyncTable* __restrict__ Tp,
@@ -871,6 +939,8 @@ AsyncService::AsyncService(AsyncPeer* peer, int world, int device,
   if (const char* c = getenv("DDL_ASYNC_CLAIM")) claim_ = atoi(c) != 0;
   if (const char* d = getenv("DDL_ASYNC_CLAIM_DEPTH")) depth_ = std::max(1, atoi(d));
   if (const char* u = getenv("DDL_ASYNC_CLAIM_IDLE_US")) idle_us_ = std::max(10.0, atof(u));
+  if (const char* f = getenv("DDL_ASYNC_FUSED")) fused_ = atoi(f) != 0;
+  if (const char* g = getenv("DDL_ASYNC_FUSED_GRID")) fused_grid_ = std::max(1, atoi(g));
   if ((int)ps.size() > kAsyncMaxPs) throw std::invalid_argument("async service: too many PS");
 }
 
@@ -900,9 +970,14 @@ void AsyncService::start(int64_t expected) {
   // HIGH priority: HIP pools hardware queues per priority, so the applies (and the claim
   // kernels in front of them) never share a queue with the compute stream, where the worker's
   // GPU-side pull gate may be waiting for them (async_runner.hip)
+  // (DDL_ASYNC_PS_PRIORITY=low: the least priority instead — also a pool of its own, so the
+  // deadlock argument holds; the dispatcher then prefers the compute stream's waves over the
+  // overlapped applies)
   int lo = 0, hi = 0;
   X_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  if (!stream_) X_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
+  const char* pp = getenv("DDL_ASYNC_PS_PRIORITY");
+  const int prio = pp && std::string(pp) == "low" ? lo : hi;
+  if (!stream_) X_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, prio));
   expected_ = expected;
   const int nh = (int)ps_.size();
   if (claim_ && nh > 0 && expected % nh == 0) {
@@ -957,6 +1032,9 @@ void AsyncService::start(int64_t expected) {
     cs->idle_ticks = (long long)(idle_us_ * 100.0);  // wall_clock64: 100 MHz
     const char* pub = getenv("DDL_ASYNC_PUBLISH");
     cs->publish_in_claim = pub && std::string(pub) == "claim";
+    // (the fused kernel's claim record: a stale sequence number of an earlier service must
+    // not match this one's launches)
+    X_CHECK(hipMemset(peer_->flags_ + kAsyncClaimRec, 0, 64 * sizeof(uint32_t)));
     X_CHECK(hipMalloc(reinterpret_cast<void**>(&cs_dev_), sizeof(ClaimState)));
     X_CHECK(hipMemcpy(cs_dev_, cs.get(), sizeof(ClaimState), hipMemcpyHostToDevice));
     th_ = std::thread([this] { run_claim(); });
@@ -989,11 +1067,17 @@ void AsyncService::run_claim() {
       {
         std::lock_guard<std::mutex> hold(pause_mu_);  // pause(): nothing enqueued while paused
         while (enq - ended < depth_ && enq - ended < expected_ - claims) {
-          hipLaunchKernelGGL(async_claim_kernel, dim3(1), dim3(64), 0, stream_, T, cs_dev_);
-          DDL_CHECK_LAUNCH();
-          hipLaunchKernelGGL(async_claimed_apply_kernel, dim3(maxs), dim3(256), 0, stream_, T,
-                             cs_dev_);
-          DDL_CHECK_LAUNCH();
+          if (fused_) {
+            hipLaunchKernelGGL(async_fused_claim_apply_kernel, dim3(std::min(fused_grid_, maxs)),
+                               dim3(256), 0, stream_, T, cs_dev_, (uint32_t)(enq + 1));
+            DDL_CHECK_LAUNCH();
+          } else {
+            hipLaunchKernelGGL(async_claim_kernel, dim3(1), dim3(64), 0, stream_, T, cs_dev_);
+            DDL_CHECK_LAUNCH();
+            hipLaunchKernelGGL(async_claimed_apply_kernel, dim3(maxs), dim3(256), 0, stream_, T,
+                               cs_dev_);
+            DDL_CHECK_LAUNCH();
+          }
           ++enq;
         }
       }
