@@ -55,6 +55,13 @@ void launch_head_fused(const float* h2, const float* w, const float* bias, const
                        float inv_keep, float* dlog, float* loss, float* dpre2, hipStream_t st);
 void launch_head_wgrad(const float* h2, const float* dlog, int B, float* gw, float* gb,
                        hipStream_t st);
+// launch_head_fused that first finishes fc2's forward: h2 = dropout(sum of the S split-K
+// partials of fc2's one-wave 32x32 tiles + b2) per sample, stored for fc3's weight gradient
+void launch_head_fused_fc2(const float* slab, int S, int gx, int ntiles, const float* b2,
+                           float* h2, const float* w, const float* bias, const int64_t* labels,
+                           int B, const uint32_t* seed, uint32_t seed_v, uint32_t thr24,
+                           float inv_keep, float* dlog, float* loss, float* dpre2,
+                           hipStream_t st);
 void launch_head_bwd(const float* h2, const float* w, const float* dlog, int B,
                      const uint32_t* seed, uint32_t seed_v, uint32_t thr24, float inv_keep,
                      float* gw, float* gb, float* dpre2, hipStream_t st);
@@ -174,6 +181,15 @@ struct Engine {
   }();
   // fc3 weight gradient still to compute (fused head kernel ran): taken by the fc2 dual launch
   int head_wgrad_pending = 0;
+  // fc2 forward's split-K partials whose reduce + epilogue the head kernel runs (the step's
+  // forward with defer_fc2, one-wave 32x32 split-K in mode 2): one launch fewer per step.
+  // DDL_FC2_REDUCE_IN_HEAD=0 keeps the separate reduce launch.
+  bool fc2_in_head = [] {
+    const char* e = getenv("DDL_FC2_REDUCE_IN_HEAD");
+    return !e || e[0] != '0';
+  }();
+  const float* fc2_slab = nullptr;  // pending partials (null: h2 is final)
+  int fc2_S = 0, fc2_gx = 0, fc2_ntiles = 0;
 
   Engine();
   ~Engine();
@@ -184,8 +200,13 @@ struct Engine {
   size_t workspace_bytes() const;
   void bind_workspace(void* base);
 
-  // forward through fc2 (train: dropout on, configured split-K; eval: no dropout, no split)
-  void forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st);
+  // forward through fc2 (train: dropout on, configured split-K; eval: no dropout, no split).
+  // defer_fc2: the caller runs backward_segment(0) next, so fc2's wide reduce may be left to
+  // the head kernel (fc2_in_head); otherwise h2 is final when forward returns
+  void forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st,
+               bool defer_fc2 = false);
+  // launch fc2's pending reduce on its own (no-op when none is pending)
+  void flush_fc2(const uint32_t* seed, int B, hipStream_t st);
   // backward segment s (0: head+fc, 1: conv4, 2: conv3, 3: conv2+conv1); weight-gradient
   // GEMMs fork onto the side stream and join back at the end of the segment
   void backward_segment(int s, const float* x, const int64_t* labels, int B,
@@ -619,8 +640,9 @@ class SyncRunner {
   PeerExchange* peer() const { return peer_; }
   void set_peer(PeerExchange* p) {
     peer_ = p;
-    if (p) p->set_gate_error(ready_err_);
+    if (p) p->set_gate_error(ready_err_dev());  // (device memory: read by every bucket wave)
   }
+  int* ready_err_dev() const { return ready_ ? reinterpret_cast<int*>(ready_ + kSegments) : nullptr; }
   // one full exchange of every bucket with w := sum over ranks of g (no optimizer) at the
   // next epoch; the caller fills g, checks w
   void peer_selftest_step(hipStream_t st);

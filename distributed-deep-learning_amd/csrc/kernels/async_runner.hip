@@ -85,7 +85,7 @@ void AsyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t se
   eng_->seed_value = seed;
   {
     TraceRange r("ddl.fwd");
-    eng_->forward(x, B, nullptr, true, st);
+    eng_->forward(x, B, nullptr, true, st, /*defer_fc2=*/true);  // backward_segment(0) follows
   }
   // the gate may only sit on a stream that is not high priority (queried once per stream: a
   // runtime call at the end of the step would sit in the window where this process's service

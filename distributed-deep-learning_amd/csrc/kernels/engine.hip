@@ -241,8 +241,16 @@ void Engine::flush_head_wgrad(int B, hipStream_t st) {
   head_wgrad_pending = 0;
 }
 
-void Engine::forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st) {
-  for (int op = OP_CONV1_FWD; op <= OP_FC2_FWD; ++op) run_op(op, x, B, seed, train, st, 0);
+void Engine::forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st,
+                     bool defer_fc2) {
+  flush_fc2(seed, B, st);  // (a deferred reduce nobody took: its slab is about to be reused)
+  for (int op = OP_CONV1_FWD; op < OP_FC2_FWD; ++op) run_op(op, x, B, seed, train, st, 0);
+  if (!(train && defer_fc2 && fc2_in_head && !concurrent && run_fc2_deferred(*this, x, B, seed, st)))
+    run_op(OP_FC2_FWD, x, B, seed, train, st, 0);
+}
+
+void Engine::flush_fc2(const uint32_t* seed, int B, hipStream_t st) {
+  if (fc2_slab) run_fc2_reduce(*this, seed, B, st);
 }
 
 // The side stream waits for everything enqueued on `st` so far.
@@ -266,6 +274,7 @@ void Engine::backward_segment(int s, const float* x, const int64_t* labels, int 
                               const uint32_t* seed, hipStream_t st) {
   if (concurrent && side) {  // weight gradients on the side stream (fork/join per segment)
     flush_tail(st);
+    flush_fc2(seed, B, st);
     switch (s) {
       case 0:
         launch_head_fwd(h2, P[12], P[13], labels, B, dlog, loss, nullptr, st);
@@ -297,9 +306,17 @@ void Engine::backward_segment(int s, const float* x, const int64_t* labels, int 
   // single stream: each layer's dgrad + wgrad as one dual launch
   switch (s) {
     case 0:
-      // one head launch (per-sample fwd + dlogits + dh2); fc3's dW/db ride in the fc2 dual
-      launch_head_fused(h2, P[12], P[13], labels, B, seed, seed_value, thr24, inv_keep, dlog,
-                        loss, dpre2fc, st);
+      // one head launch (per-sample fwd + dlogits + dh2); fc3's dW/db ride in the fc2 dual.
+      // With fc2's reduce deferred the head also finishes fc2 (h2 = its reduce + epilogue).
+      if (fc2_slab) {
+        launch_head_fused_fc2(fc2_slab, fc2_S, fc2_gx, fc2_ntiles, P[11], h2, P[12], P[13],
+                              labels, B, seed, seed_value, thr24, inv_keep, dlog, loss,
+                              dpre2fc, st);
+        fc2_slab = nullptr;
+      } else {
+        launch_head_fused(h2, P[12], P[13], labels, B, seed, seed_value, thr24, inv_keep, dlog,
+                          loss, dpre2fc, st);
+      }
       head_wgrad_pending = 1;
       run_dual_inst<OP_FC2_DGRAD, OP_FC2_WGRAD>(*this, x, B, seed, st);
       flush_head_wgrad(B, st);
@@ -315,7 +332,7 @@ void Engine::backward_segment(int s, const float* x, const int64_t* labels, int 
 }
 
 void Engine::eval_count(const float* x, const int64_t* labels, int B, hipStream_t st) {
-  forward(x, B, nullptr, false, st);
+  forward(x, B, nullptr, false, st);  // (flushes a pending fc2 reduce of a training forward)
   launch_head_fwd(h2, P[12], P[13], labels, B, nullptr, nullptr, correct, st);
 }
 

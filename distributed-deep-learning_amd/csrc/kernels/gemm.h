@@ -2020,8 +2020,10 @@ inline bool launch_reduce_tail(const P& p, const SubGrid& g, const UpdTail& t,
 
 template <int BM, int BN, int BK, int WM, int WN, int V = 0, class P>
 inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch& sc,
-                        hipStream_t stream, int workers = 0, int order = 0) {
+                        hipStream_t stream, int workers = 0, int order = 0,
+                        SubGrid* defer = nullptr) {
   const SubGrid g = plan_gemm<BM, BN, BK>(p, splits, workers, wide_thr, sc, order);
+  if (defer) *defer = g;
   if (g.nblocks == 0) return;
   if (g.streamk) {
     DDL_LAUNCH((gemm_streamk_kernel<BM, BN, BK, WM, WN, P, V>), dim3(g.nblocks),
@@ -2038,6 +2040,7 @@ inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch
                      dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets,
                      g.order);
 #endif
+  if (defer && g.mode == 2) return;  // the caller runs (or fuses) the wide reduce
   launch_reduce<BM, BN, BK, WM, WN, P>(p, g, stream);
 }
 

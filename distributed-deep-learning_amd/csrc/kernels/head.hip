@@ -8,6 +8,8 @@
 //              dropout backward fused (mask regenerated from the seed, nothing stored).
 //   head_fused: head_fwd + the dh2 part of head_bwd per sample (one launch in training; the
 //              fc3 weight gradient then rides in the next dual launch, head.h HeadWgradAux).
+#include <stdexcept>
+
 #include "common.h"
 #include "api.h"
 #include "head.h"
@@ -160,6 +162,126 @@ head_fused_kernel(const float* __restrict__ h2, const float* __restrict__ w,
     if (thr24) g = ddl_keep(key, (uint32_t)idx, thr24) ? g * inv_keep : 0.f;
     dpre2[idx] = g;
   }
+}
+
+// One output element of a mode-2 split-K reduce, summed in exactly the order of gemm.h
+// wide_reduce_body with RL lanes (lane j: z = j, j + RL, ... from 0; then common.h group_sum's
+// DPP stages, which form the balanced pairwise tree over the RL lane sums in lane order).
+// S <= 32.  All loads are issued before the adds.
+template <int RL>
+DDL_DEV float wide_sum(const float* __restrict__ slab, size_t zstride, size_t off, int S) {
+  float l[RL];
+#pragma unroll
+  for (int j = 0; j < RL; ++j) l[j] = 0.f;
+  float v[32];
+#pragma unroll
+  for (int z = 0; z < 32; ++z) v[z] = z < S ? slab[(size_t)z * zstride + off] : 0.f;
+#pragma unroll
+  for (int z = 0; z < 32; ++z)
+    if (z < S) l[z % RL] += v[z];
+  if constexpr (RL == 16) {
+    float q[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = (l[4 * i] + l[4 * i + 1]) + (l[4 * i + 2] + l[4 * i + 3]);
+    return (q[0] + q[1]) + (q[2] + q[3]);
+  } else {
+    return (l[0] + l[1]) + (l[2] + l[3]);
+  }
+}
+
+// head_fused with fc2's forward finished here: thread (wave, lane) sums the S split-K partials
+// of its two h2 columns k = wave*128 + t*64 + lane (one-wave 32x32 tiles: partial image
+// [z][tile][g][lane] float4, element (row r, col c) of a tile at g = r / 8, lane = c + 32 *
+// ((r % 8) / 4), component r % 4; gemm.h store_partial) in z order, adds b2, applies fc2's
+// dropout (layer key 2, the dh2 mask key) and stores h2 for fc3's weight gradient — fc2's
+// wide-reduce launch (4.7 us) folded into the head's.
+__global__ void __launch_bounds__(256)
+head_fused_fc2_kernel(const float* __restrict__ slab, int S, int gx, int ntiles,
+                      const float* __restrict__ b2, float* __restrict__ h2,
+                      const float* __restrict__ w, const float* __restrict__ bias,
+                      const int64_t* __restrict__ labels, int B, float inv_batch,
+                      const uint32_t* __restrict__ seed, uint32_t seed_v, uint32_t thr24,
+                      float inv_keep, float* __restrict__ dlog, float* __restrict__ loss,
+                      float* __restrict__ dpre2) {
+  __shared__ float part[4][HC];
+  const int row = blockIdx.x;
+  if (row >= B) return;
+  const uint32_t key = thr24 ? ddl_mix32((seed ? *seed : seed_v) + 2u * 0x9E3779B9u) : 0u;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int bx = row >> 5, r = row & 31;
+  const int fg = r >> 3, comp = r & 3, half = (r & 7) >> 2;
+  const size_t zstride = (size_t)ntiles * 256 * 4;  // floats per split (PART4 = 256 float4)
+  float hv[2];
+  size_t off[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int k = wave * 128 + t * 64 + lane;
+    const int tile = (k >> 5) * gx + bx;
+    off[t] = ((size_t)tile * 256 + fg * 64 + (k & 31) + 32 * half) * 4 + comp;
+    hv[t] = 0.f;
+  }
+  // the wide reduce's exact summation order (gemm.h wide_reduce_body + common.h group_sum, RL
+  // lanes per element: lane j sums z = j, j + RL, ... from 0, then the DPP tree over the RL
+  // lanes is the balanced pairwise tree in lane order), so h2 is bit-identical to the
+  // separate reduce launch; every partial load is issued before the adds
+  // (S > 32 is not deferred: engine_ops_fc.hip)
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+    hv[t] = S > 4 ? wide_sum<16>(slab, zstride, off[t], S) : wide_sum<4>(slab, zstride, off[t], S);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int k = wave * 128 + t * 64 + lane;
+    const uint32_t idx = (uint32_t)(row * HK + k);
+    float val = hv[t] + b2[k];  // FcFwd<false>: no ReLU
+    if (thr24) val = ddl_keep(key, idx, thr24) ? val * inv_keep : 0.f;
+    h2[idx] = val;
+    hv[t] = val;
+  }
+  float acc[HC];
+  head_logits_hv(hv, w, bias, part, acc);
+  float mx = acc[0];
+#pragma unroll
+  for (int c = 1; c < HC; ++c) mx = acc[c] > mx ? acc[c] : mx;
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < HC; ++c) se += __expf(acc[c] - mx);
+  const int lab = (int)labels[row];
+  float dl[HC];
+#pragma unroll
+  for (int c = 0; c < HC; ++c) dl[c] = (__expf(acc[c] - mx) / se - (c == lab ? 1.f : 0.f)) * inv_batch;
+  if (threadIdx.x == 0) {
+    float ll = 0.f;
+#pragma unroll
+    for (int c = 0; c < HC; ++c)
+      if (c == lab) ll = acc[c];
+    loss[row] = (mx + __logf(se)) - ll;
+  }
+  if (threadIdx.x < HC) {
+    float v = 0.f;
+#pragma unroll
+    for (int c = 0; c < HC; ++c)
+      if (c == (int)threadIdx.x) v = dl[c];
+    dlog[(size_t)row * HC + threadIdx.x] = v;
+  }
+  for (int i = threadIdx.x; i < HK; i += 256) {
+    float g = 0.f;
+#pragma unroll
+    for (int c = 0; c < HC; ++c) g = fmaf(dl[c], w[i * HC + c], g);
+    const int idx = row * HK + i;
+    if (thr24) g = ddl_keep(key, (uint32_t)idx, thr24) ? g * inv_keep : 0.f;
+    dpre2[idx] = g;
+  }
+}
+
+void launch_head_fused_fc2(const float* slab, int S, int gx, int ntiles, const float* b2,
+                           float* h2, const float* w, const float* bias, const int64_t* labels,
+                           int B, const uint32_t* seed, uint32_t seed_v, uint32_t thr24,
+                           float inv_keep, float* dlog, float* loss, float* dpre2,
+                           hipStream_t st) {
+  if (gx * 32 < B || ntiles != gx * (HK / 32))
+    throw std::invalid_argument("head_fused_fc2: fc2 partial tiles do not cover [B, 512]");
+  DDL_LAUNCH(head_fused_fc2_kernel, dim3(B), dim3(256), 0, st, slab, S, gx, ntiles, b2, h2, w,
+             bias, labels, B, 1.f / (float)B, seed, seed_v, thr24, inv_keep, dlog, loss, dpre2);
 }
 
 void launch_head_fused(const float* h2, const float* w, const float* bias, const int64_t* labels,

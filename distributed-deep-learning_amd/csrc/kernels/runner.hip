@@ -40,8 +40,13 @@ static ncclComm_t as_comm(void* c) { return reinterpret_cast<ncclComm_t>(c); }
 // the producer's dirty L2 lines back, so the gradients are in memory for this GPU's exchange
 // kernels and for a peer's P2P reads alike.  The comm stream has high priority, so this wait
 // never shares a hardware queue with the kernel that releases it.  Bounded (error word).
+// On a timeout it also raises the device copy of the error (err_dev, uncached device memory),
+// which the gated xGMI bucket kernels behind it read — a host-memory word read by every wave of
+// a 512-block bucket kernel was ~2,000 PCIe reads per launch: the forced xGMI rehearsal ran
+// 0.49 instead of 0.30 ms/step, the GEMMs beside it ~7x slower.
 __global__ void __launch_bounds__(64) ready_gate_kernel(const uint32_t* flag, uint32_t epoch,
-                                                        int* err, long long timeout_ticks) {
+                                                        int* err, int* err_dev,
+                                                        long long timeout_ticks) {
   if (threadIdx.x != 0) return;
   const long long deadline = wall_clock64() + timeout_ticks;
   // a long sleep between polls (~0.5 us): the first segment's gate of the next step is issued
@@ -50,6 +55,7 @@ __global__ void __launch_bounds__(64) ready_gate_kernel(const uint32_t* flag, ui
        (int32_t)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0;
        ++it) {
     if ((it & 15) == 15 && wall_clock64() > deadline) {
+      __hip_atomic_store(err_dev, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
@@ -84,9 +90,10 @@ SyncRunner::SyncRunner(Engine* eng, float* params, float* grads, int world, int 
                                       hipEventDisableTiming | hipEventDisableSystemFence));
   }
   HIP_CHECK(hipEventCreateWithFlags(&done_ev_, hipEventDisableTiming));
-  HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&ready_), kSegments * sizeof(uint32_t),
-                                  hipDeviceMallocUncached));
-  HIP_CHECK(hipMemset(ready_, 0, kSegments * sizeof(uint32_t)));
+  // READY[s] words, then the device copy of the gate's error word
+  HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&ready_),
+                                  (kSegments + 1) * sizeof(uint32_t), hipDeviceMallocUncached));
+  HIP_CHECK(hipMemset(ready_, 0, (kSegments + 1) * sizeof(uint32_t)));
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ready_err_), 64, hipHostMallocDefault));
   memset(ready_err_, 0, 64);
   HIP_CHECK(hipDeviceSynchronize());
@@ -361,7 +368,7 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
   // the remaining backward segments.
   {
     TraceRange r("ddl.fwd");
-    eng_->forward(x, B, seed, true, st);
+    eng_->forward(x, B, seed, true, st, /*defer_fc2=*/true);  // backward_segment(0) follows
   }
   if (all_local_ && local_on_main_ && use_tail_ && tail_ok_ && opt_ == 0 && coef_ == 1.f) {
     // segment s-1's update rides in segment s's dual launch (flushed as a launch of its own
@@ -470,7 +477,8 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
           t.first = 1;
           eng_->tail = t;
           hipLaunchKernelGGL(ready_gate_kernel, dim3(1), dim3(64), 0, cs_, ready_ + s,
-                             ready_epoch_, ready_err_, (long long)(gate_timeout_s_ * 1e8));
+                             ready_epoch_, ready_err_, ready_err_dev(),
+                             (long long)(gate_timeout_s_ * 1e8));
           DDL_CHECK_LAUNCH();
         } else {
           if (marker) HIP_CHECK(hipEventRecord(ev, st));

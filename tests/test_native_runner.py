@@ -66,6 +66,19 @@ def test_native_matches_python_exchange(data, kw):
             assert torch.equal(s_py[p][2], s_nat[p][2])
 
 
+def test_fc2_reduce_in_head_is_bit_identical(data, monkeypatch):
+    """The native step leaves fc2's split-K reduce to the head kernel (engine.hip
+    Engine::forward defer_fc2, head.hip head_fused_fc2_kernel: same summation order as the
+    wide reduce launch).  Parameters and Adam state match the separate-launch step bitwise."""
+    monkeypatch.setenv("DDL_FC2_REDUCE_IN_HEAD", "0")
+    p_sep, s_sep = _run(data, True, shard="flat")
+    monkeypatch.setenv("DDL_FC2_REDUCE_IN_HEAD", "1")
+    p_head, s_head = _run(data, True, shard="flat")
+    assert torch.equal(p_sep, p_head)
+    for p in s_sep:
+        assert torch.equal(s_sep[p][1], s_head[p][1])
+
+
 def test_native_runner_trains(data):
     env = DistEnv(0, 1, 0, torch.device("cuda", 0))
     cfg = TrainConfig(mode="sync", shard="contiguous", steps=60, batch_size=100, eval_every=0,
