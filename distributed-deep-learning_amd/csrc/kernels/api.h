@@ -370,9 +370,7 @@ constexpr int kAsyncMaxSlices = 512;
 // a rank's uncached device flags: [0, kAsyncDense) its DONE words as a worker (dense over all
 // PS' slices), then POSTED[worker][dense slice] as a PS host (what its claim kernel polls)
 constexpr int kAsyncDense = kAsyncMaxPs * kAsyncMaxSlices;
-// then 64 words: the fused claim + apply kernel's claim record (xgmi_async.hip)
-constexpr size_t kAsyncClaimRec = (size_t)kAsyncDense * (1 + kXgmiMaxPeers);
-constexpr size_t kAsyncFlagWords = kAsyncClaimRec + 64;
+constexpr size_t kAsyncFlagWords = (size_t)kAsyncDense * (1 + kXgmiMaxPeers);
 struct AsyncShard {              // one PS's contiguous range of the flat buffer
   int64_t lo, n, slice, inbox_off;
   int host, nslice;
@@ -487,8 +485,6 @@ class AsyncService {
   void serve(AsyncPsState& st, int worker);
   void free_claim();
   bool claim_ = true;
-  bool fused_ = false;           // DDL_ASYNC_FUSED=1: one claim + apply launch per arrival
-  int fused_grid_ = 64;
   int depth_ = 3;                // claim pairs in flight on the PS stream
   double idle_us_ = 500.0;       // a claim kernel with no arrival for this long ends empty
   ClaimState* cs_dev_ = nullptr;

@@ -245,21 +245,27 @@ __global__ void __launch_bounds__(256) async_apply_kernel(const AsyncTable* __re
 
 // ---- the on-GPU ANY_SOURCE pop (the default service) ------------------------------------------
 // The service keeps `depth` (claim, apply) kernel pairs enqueued on its high-priority PS stream.
-// The claim kernel (one wave) polls this host's arrival words in its own uncached device flags,
-// round-robin over (hosted PS, worker) from where the last claim stopped, takes the first push
-// whose every slice is posted — the reference's MPI.ANY_SOURCE receive in arrival order
-// (mnist_async_sharding/parameter_server.py:94-111) — advances that PS's step counter, looks up
-// its TF1 Adam step size in a table the host filled with the host formula (bit-identical to the
-// host service), and leaves the claim for the apply kernel behind it (grid = the largest hosted
-// shard's slices; blocks beyond the claimed shard's return).  No host thread and no host launch
-// sits between a push's last slice and its apply: the thread only tops the queue up.
-// The claim kernel waits `idle_us` at most and then ends without a claim (the host re-enqueues):
+// The claim kernel (one wave) polls this host's arrival words in its own uncached device flags
+// and, once at least one push is complete, takes EVERY complete (hosted PS, worker) push in
+// round-robin order from where the last claim stopped — the reference's MPI.ANY_SOURCE receive
+// (mnist_async_sharding/parameter_server.py:94-111) as an on-GPU pop of a batch of arrivals.
+// Each claim advances its PS's step counter and takes its TF1 step size from a table the host
+// filled with the host formula (bit-identical to the host service).  The apply kernel behind it
+// runs one block per hosted slice: the block applies the batch's claims of its PS one after
+// another, in claim order, to its slice — w, m and v read and written once for the whole batch,
+// the parameters after each claim's update stored to that claim's worker — so K arrivals of one
+// PS cost one pass instead of K kernel pairs, with the same per-element arithmetic in the same
+// order as K separate applies.  No host thread and no host launch sits between a push's last
+// slice and its apply: the thread only tops the queue up.
+// A claim kernel waits `idle_us` at most and then ends without a claim (the host re-enqueues):
 // a pair queued for a push that this very process issues only after a device-wide synchronize
 // (torch.cuda.synchronize() before the bench's timed window, a checkpoint, an in-line eval)
 // must not hold that synchronize forever.  It also ends at once when pause() raises `hold`.
+constexpr int kClaimBatch = 16;
 struct ClaimState {
   int me, world, nh, per_ps, opt;
   int ps[kAsyncMaxPs];             // hosted PS ids
+  int blk0[kAsyncMaxPs + 1];       // hosted PS i's apply blocks: [blk0[i], blk0[i + 1])
   float* params[kAsyncMaxPs];      // their private parameter copies and optimizer state
   float* m[kAsyncMaxPs];
   float* v[kAsyncMaxPs];
@@ -268,10 +274,11 @@ struct ClaimState {
   uint32_t last[kXgmiMaxPeers * kAsyncMaxPs];  // last claimed round per (worker, hosted PS)
   int start;                       // round-robin position of the next scan
   int64_t claims, ended;
-  // the current claim: written by a claim kernel, read by the apply kernel behind it
-  int cur_valid, cur_pl, cur_w;
-  uint32_t cur_e;
-  float cur_lr_t;
+  // the current batch: written by a claim kernel, read by the apply kernel behind it
+  int nb;                          // 0: the claim kernel ended empty
+  int b_pl[kClaimBatch], b_w[kClaimBatch];
+  uint32_t b_e[kClaimBatch];
+  float b_lr[kClaimBatch];
   const float* lr_tab;             // [nh][per_ps]: lr_t of step t0 + 1 + i
   int32_t* prov;                   // [claims][4] (worker, ps, round, t) or null
   int64_t* host;                   // pinned host words (api.h AsyncService::host_words_)
@@ -283,84 +290,87 @@ struct ClaimState {
 
 namespace {
 
-// The service thread's view of the claim in front (pinned host words).  Stored by block 0 AFTER
-// its slice's DONE flags: a wave's drain before its flag store would otherwise wait out these
-// stores' PCIe round trip, and the worker's gate waits for that flag.
+// The service thread's view of the claims in front (pinned host words).  Stored by block 0 of the
+// apply kernel AFTER its slice's DONE flags: a wave's drain before its flag store would otherwise
+// wait out these stores' PCIe round trip, and the worker's gate waits for that flag.
 DDL_DEV void publish_claim(const ClaimState* C) {
-  if (C->cur_valid)
-    __hip_atomic_store(C->host + 8 + C->cur_pl, C->t[C->cur_pl], __ATOMIC_RELAXED,
+  for (int c = 0; c < C->nb; ++c)
+    __hip_atomic_store(C->host + 8 + C->b_pl[c], C->t[C->b_pl[c]], __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(C->host + 1, C->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   // (release: a host that sees this `ended` sees the `claims` stored before it)
   __hip_atomic_store(C->host + 0, C->ended, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// One wave (lanes 0-63 of the calling workgroup) claims the next arrival into C.
+// One sweep over every (hosted PS, worker) pair, in round-robin order from C->start: bit i of
+// the returned mask (i = position in that order) is set when the pair's next round is posted in
+// full.  Lane i first loads ONE probe word per pair — the pair's last slice — and only pairs
+// whose probe landed are checked in full (64 lanes x 8 slices per batch, resuming at seen[q],
+// the first slice not yet seen posted, in this wave's LDS).  Polling every slice of every pair
+// on every sweep (round 5's first version) put ~400 uncached loads per sweep on the memory
+// system for as long as a claim kernel waited, and slowed the GEMMs of a co-located rank 3x
+// (one-card W = 2 async: 1.03 vs 0.62 ms/step with the host-scan service).
+DDL_DEV uint64_t claim_sweep(const AsyncTable& T, const ClaimState* C, const uint32_t* posted,
+                             int* seen, int pairs) {
+  const int lane = threadIdx.x & 63, world = C->world;
+  bool probe = false;
+  if (lane < pairs) {
+    int q = C->start + lane;
+    if (q >= pairs) q -= pairs;
+    const int pl = q / world, w = q - pl * world;
+    const AsyncShard& S = T.shard[C->ps[pl]];
+    const uint32_t e = C->last[w * kAsyncMaxPs + pl] + 1;
+    const uint32_t f = __hip_atomic_load(posted + posted_dev_idx(S, w, S.nslice - 1),
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    probe = (int32_t)(f - e) >= 0;
+  }
+  uint64_t cand = __ballot(probe), done = 0;
+  while (cand) {
+    const int i = __builtin_ctzll(cand);
+    cand &= cand - 1;
+    int q = C->start + i;
+    if (q >= pairs) q -= pairs;
+    const int pl = q / world, w = q - pl * world;
+    const AsyncShard& S = T.shard[C->ps[pl]];
+    const uint32_t e = C->last[w * kAsyncMaxPs + pl] + 1;
+    int k0 = seen[q];
+    bool all = true;
+    while (all && k0 < S.nslice) {  // 512 slices per batch
+      uint32_t v[8];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const int j = k0 + b * 64 + lane;
+        v[b] = j < S.nslice ? __hip_atomic_load(posted + posted_dev_idx(S, w, j),
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                            : e;
+      }
+      bool ok = true;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) ok &= (int32_t)(v[b] - e) >= 0;
+      all = __all(ok);
+      if (all) k0 += 512;
+    }
+    if (all) done |= 1ull << i;
+    else if (lane == 0) seen[q] = k0;  // (a batch that failed is re-read from its start)
+    __builtin_amdgcn_wave_barrier();
+  }
+  return done;
+}
+
+// One wave (lanes 0-63 of the calling workgroup) claims the complete arrivals into C's batch.
+// (pairs beyond 64 in scan order wait for a later claim kernel)
 DDL_DEV void claim_body(const AsyncTable& T, ClaimState* __restrict__ C) {
   const int lane = threadIdx.x & 63;
   const int world = C->world, pairs = C->nh * C->world;
   const uint32_t* posted = T.flags[C->me];
   const long long deadline = wall_clock64() + C->idle_ticks;
-  // per pair, the first slice of its next round not yet seen posted (LDS, this wave only).  A
-  // sweep issues one load per lane for up to 8 pairs at once (64 slices each, one round of
-  // uncached-load latency for all of them) and only follows a pair further, 512 slices per
-  // batch, once its first 64 landed: the pair whose push just completed is found within about
-  // one load latency, whatever the number of pairs
   __shared__ int seen[kAsyncMaxPs * kXgmiMaxPeers];
   for (int q = lane; q < pairs; q += 64) seen[q] = 0;
   __builtin_amdgcn_wave_barrier();
-  int hit = -1;
-  uint32_t hit_e = 0;
-  for (int it = 0; hit < 0; ++it) {
-    for (int g = 0; g < pairs && hit < 0; g += 8) {
-      uint32_t f[8], e[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        f[u] = e[u] = 0;
-        if (g + u >= pairs) continue;
-        int q = C->start + g + u;
-        if (q >= pairs) q -= pairs;
-        const int pl = q / world, w = q - pl * world;
-        const AsyncShard& S = T.shard[C->ps[pl]];
-        e[u] = C->last[w * kAsyncMaxPs + pl] + 1;
-        const int j = seen[q] + lane;
-        f[u] = j < S.nslice ? __hip_atomic_load(posted + posted_dev_idx(S, w, j),
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                            : e[u];
-      }
-      for (int u = 0; u < 8 && g + u < pairs && hit < 0; ++u) {
-        if (!__all((int32_t)(f[u] - e[u]) >= 0)) continue;
-        int q = C->start + g + u;
-        if (q >= pairs) q -= pairs;
-        const int pl = q / world, w = q - pl * world;
-        const AsyncShard& S = T.shard[C->ps[pl]];
-        int k0 = seen[q] + 64;
-        bool all = true;
-        while (all && k0 < S.nslice) {  // the rest of this pair, 512 slices per batch
-          uint32_t v[8];
-#pragma unroll
-          for (int b = 0; b < 8; ++b) {
-            const int j = k0 + b * 64 + lane;
-            v[b] = j < S.nslice ? __hip_atomic_load(posted + posted_dev_idx(S, w, j),
-                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                                : e[u];
-          }
-          bool ok = true;
-#pragma unroll
-          for (int b = 0; b < 8; ++b) ok &= (int32_t)(v[b] - e[u]) >= 0;
-          all = __all(ok);
-          if (all) k0 += 512;
-        }
-        if (all) {
-          hit = q;
-          hit_e = e[u];
-        } else if (lane == 0) {
-          seen[q] = k0;  // (a batch that failed is re-read from its start next sweep)
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
-    if (hit >= 0) break;
+  uint64_t done = 0;
+  for (int it = 0;; ++it) {
+    done = claim_sweep(T, C, posted, seen, pairs);
+    if (done) break;
     if ((it & 15) == 15) {
       if (__hip_atomic_load(C->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
       if (__hip_atomic_load(C->host + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
@@ -371,34 +381,40 @@ DDL_DEV void claim_body(const AsyncTable& T, ClaimState* __restrict__ C) {
     __builtin_amdgcn_s_sleep(16);
   }
   if (lane != 0) return;
-  int valid = 0;
-  if (hit >= 0) {
-    const int pl = hit / world, w = hit - pl * world;
+  int nb = 0, next = C->start;
+  for (int i = 0; i < pairs && i < 64 && nb < kClaimBatch; ++i) {
+    if (!((done >> i) & 1)) continue;
+    int q = C->start + i;
+    if (q >= pairs) q -= pairs;
+    const int pl = q / world, w = q - pl * world;
     const int64_t t = C->t[pl] + 1;
     const int64_t idx = t - C->t0[pl] - 1;
     if (idx < 0 || idx >= C->per_ps) {
       // more arrivals than the service was started for: a protocol error, not an update
       __hip_atomic_store(C->err, 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    } else {
-      valid = 1;
-      C->t[pl] = t;
-      C->last[w * kAsyncMaxPs + pl] = hit_e;
-      C->start = hit + 1 < pairs ? hit + 1 : 0;
-      C->cur_pl = pl;
-      C->cur_w = w;
-      C->cur_e = hit_e;
-      C->cur_lr_t = C->lr_tab[(int64_t)pl * C->per_ps + idx];
-      if (C->prov) {
-        int32_t* r = C->prov + C->claims * 4;
-        r[0] = w;
-        r[1] = C->ps[pl];
-        r[2] = (int32_t)hit_e;
-        r[3] = (int32_t)t;
-      }
-      C->claims += 1;
+      break;
     }
+    const uint32_t e = C->last[w * kAsyncMaxPs + pl] + 1;
+    C->t[pl] = t;
+    C->last[w * kAsyncMaxPs + pl] = e;
+    C->b_pl[nb] = pl;
+    C->b_w[nb] = w;
+    C->b_e[nb] = e;
+    C->b_lr[nb] = C->lr_tab[(int64_t)pl * C->per_ps + idx];
+    if (C->prov) {
+      int32_t* r = C->prov + C->claims * 4;
+      r[0] = w;
+      r[1] = C->ps[pl];
+      r[2] = (int32_t)e;
+      r[3] = (int32_t)t;
+    }
+    C->claims += 1;
+    ++nb;
+    next = q + 1 < pairs ? q + 1 : 0;
   }
-  C->cur_valid = valid;
+  // (more than 64 pairs: an empty claim moves the 64-pair window on, so no pair waits forever)
+  C->start = nb > 0 ? next : (pairs > 64 ? (C->start + 64) % pairs : C->start);
+  C->nb = nb;
   C->ended += 1;
 }
 
@@ -411,96 +427,75 @@ __global__ void __launch_bounds__(64) async_claim_kernel(const AsyncTable* __res
   if (threadIdx.x == 0 && C->publish_in_claim) publish_claim(C);
 }
 
-// Claim and apply in ONE launch (DDL_ASYNC_FUSED=1): wave 0 of block 0 claims; the claim goes
-// to every block through a record in this rank's uncached flags (payload words, a drain, then
-// the launch's sequence number), and the `grid` blocks apply the claimed shard's slices
-// j = block, block + grid, ...  No kernel boundary between the claim and the apply; the
-// waiting blocks sleep ~0.45 us per poll.  Bounded: block 0 always publishes a record (the
-// claim loop ends on idle / hold / error), and a block that never sees one gives up with
-// error 8 after the idle bound plus 1 s.
-__global__ void __launch_bounds__(256) async_fused_claim_apply_kernel(
-    const AsyncTable* __restrict__ Tp, ClaimState* __restrict__ C, uint32_t seq) {
-  const AsyncTable& T = *Tp;
-  uint32_t* rec = T.flags[C->me] + kAsyncClaimRec;
-  if (blockIdx.x == 0 && threadIdx.x < 64) {
-    claim_body(T, C);
-    if (threadIdx.x == 0) {
-      __hip_atomic_store(rec + 1, (uint32_t)C->cur_valid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(rec + 2, (uint32_t)C->cur_pl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(rec + 3, (uint32_t)C->cur_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(rec + 4, C->cur_e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(rec + 5, __float_as_uint(C->cur_lr_t), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-      drain_vm();
-      __hip_atomic_store(rec, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-  __shared__ uint32_t got[6];
-  if (threadIdx.x == 0) {
-    const long long deadline = wall_clock64() + C->idle_ticks + 100000000LL;
-    while (__hip_atomic_load(rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
-      if (wall_clock64() > deadline) {
-        __hip_atomic_store(C->err, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        got[1] = 0;
-        break;
+// Slice j of hosted PS pl for every claim of the batch on that PS, in claim order.
+DDL_DEV void apply_batch_body(const AsyncTable& T, const ClaimState* C, int pl, int j,
+                              const int (&cl)[kClaimBatch], int nc) {
+  const int ps = C->ps[pl], me = C->me;
+  const AsyncShard& S = T.shard[ps];
+  const int tid = threadIdx.x;
+  const int64_t s0 = (int64_t)j * S.slice;
+  const int64_t s1 = s0 + S.slice < S.n ? s0 + S.slice : S.n;
+  const int n4 = s0 < s1 ? (int)((s1 - s0) >> 2) : 0;
+  float4* w4 = reinterpret_cast<float4*>(C->params[pl] + s0);
+  float4* m4 = reinterpret_cast<float4*>(C->m[pl] + s0);
+  float4* v4 = C->v[pl] ? reinterpret_cast<float4*>(C->v[pl] + s0) : nullptr;
+  const int opt = C->opt;
+  const float c1 = C->c1, c2 = C->c2, eps = C->eps, lr = C->lr, mu = C->mu, sc = C->scale;
+  for (int i = tid; i < n4; i += 256) {
+    float4 w = w4[i];
+    float4 M = opt != 2 ? m4[i] : f4zero();
+    float4 V = opt == 0 ? v4[i] : f4zero();
+    for (int k = 0; k < nc; ++k) {
+      const int c = cl[k], wk = C->b_w[c];
+      const float* src = T.elide && wk == me
+                             ? T.grads + S.lo + s0  // the host's own push: no inbox copy
+                             : T.inbox[me] + S.inbox_off + (int64_t)wk * S.n + s0;
+      const float4 g = bload4_sys(make_rsrc(src, (uint32_t)n4 * 16u), i * 16);
+      if (opt == 0) {
+        const float lt = C->b_lr[c];
+        adam1(w.x, g.x * sc, M.x, V.x, lt, c1, c2, eps);
+        adam1(w.y, g.y * sc, M.y, V.y, lt, c1, c2, eps);
+        adam1(w.z, g.z * sc, M.z, V.z, lt, c1, c2, eps);
+        adam1(w.w, g.w * sc, M.w, V.w, lt, c1, c2, eps);
+      } else if (opt == 1) {
+        momentum1(w.x, g.x, M.x, lr, mu, sc);
+        momentum1(w.y, g.y, M.y, lr, mu, sc);
+        momentum1(w.z, g.z, M.z, lr, mu, sc);
+        momentum1(w.w, g.w, M.w, lr, mu, sc);
+      } else {
+        w = g;
       }
-      __builtin_amdgcn_s_sleep(16);
+      // the worker gets the parameters right after ITS update (the reference's Send back)
+      bstore4_sys(make_rsrc(T.params[wk] + S.lo + s0, (uint32_t)n4 * 16u), i * 16, w);
     }
-    if (__hip_atomic_load(rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq)
-      for (int i = 1; i < 6; ++i)
-        got[i] = __hip_atomic_load(rec + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    w4[i] = w;
+    if (opt != 2) m4[i] = M;
+    if (opt == 0) v4[i] = V;
   }
+  drain_vm();
   __syncthreads();
-  if (got[1]) {
-    const int pl = (int)got[2];
-    ApplyArgs a;
-    a.me = C->me;
-    a.ps = C->ps[pl];
-    a.worker = (int)got[3];
-    a.epoch = got[4];
-    a.ps_params = C->params[pl];
-    a.m = C->m[pl];
-    a.v = C->v[pl];
-    a.opt = C->opt;
-    a.lr_t = __uint_as_float(got[5]);
-    a.c1 = C->c1;
-    a.c2 = C->c2;
-    a.eps = C->eps;
-    a.lr = C->lr;
-    a.mu = C->mu;
-    a.scale = C->scale;
-    const int ns = T.shard[a.ps].nslice;
-    for (int j = blockIdx.x; j < ns; j += gridDim.x) apply_body(T, a, j);
+  if (tid < nc) {
+    const int c = cl[tid];
+    flag_store(T.flags[C->b_w[c]] + done_dev_idx(S, j), C->b_e[c]);     // the worker's gate
+    flag_store(T.done + done_word(C->b_w[c], ps, j), C->b_e[c]);        // the worker's host
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) publish_claim(C);
 }
 
+// One block per hosted slice (grid = blk0[nh]); block 0 also publishes the host counters.
 __global__ void __launch_bounds__(256) async_claimed_apply_kernel(const AsyncTable* __restrict__ Tp,
                                                                   const ClaimState* __restrict__ C) {
-  if (!C->cur_valid) {  // the claim kernel in front ended empty
-    if (blockIdx.x == 0 && threadIdx.x == 0 && !C->publish_in_claim) publish_claim(C);
-    return;
+  const int b = blockIdx.x;
+  const int nb = C->nb;
+  if (nb > 0) {
+    int pl = 0;
+    while (pl + 1 < C->nh && b >= C->blk0[pl + 1]) ++pl;
+    int cl[kClaimBatch];
+    int nc = 0;
+    for (int c = 0; c < nb; ++c)
+      if (C->b_pl[c] == pl) cl[nc++] = c;
+    if (nc > 0) apply_batch_body(*Tp, C, pl, b - C->blk0[pl], cl, nc);
   }
-  const int pl = C->cur_pl;
-  ApplyArgs a;
-  a.me = C->me;
-  a.ps = C->ps[pl];
-  a.worker = C->cur_w;
-  a.epoch = C->cur_e;
-  a.ps_params = C->params[pl];
-  a.m = C->m[pl];
-  a.v = C->v[pl];
-  a.opt = C->opt;
-  a.lr_t = C->cur_lr_t;
-  a.c1 = C->c1;
-  a.c2 = C->c2;
-  a.eps = C->eps;
-  a.lr = C->lr;
-  a.mu = C->mu;
-  a.scale = C->scale;
-  if ((int)blockIdx.x >= Tp->shard[a.ps].nslice) return;
-  apply_body(*Tp, a, blockIdx.x);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && !C->publish_in_claim) publish_claim(C);
+  if (b == 0 && threadIdx.x == 0 && !C->publish_in_claim) publish_claim(C);
 }
 
 // The worker's pull as a GPU-side gate (async_runner.hip): one wave on the compute stream,
@@ -553,7 +548,11 @@ DDL_DEV void gate_body(const AsyncTable& T, int rank, int total, uint32_t epoch,
         return;
       }
     }
-    __builtin_amdgcn_s_sleep(2);
+    // a tight poll for the first ~64 sweeps (the W = 1 wait for the last apply is a few us),
+    // then ~0.45 us apart: a gate waiting for another rank's applies must not load the memory
+    // system under that rank's GEMMs (one-card W = 2)
+    if (it < 64) __builtin_amdgcn_s_sleep(2);
+    else __builtin_amdgcn_s_sleep(16);
   }
 }
 
@@ -939,8 +938,6 @@ AsyncService::AsyncService(AsyncPeer* peer, int world, int device,
   if (const char* c = getenv("DDL_ASYNC_CLAIM")) claim_ = atoi(c) != 0;
   if (const char* d = getenv("DDL_ASYNC_CLAIM_DEPTH")) depth_ = std::max(1, atoi(d));
   if (const char* u = getenv("DDL_ASYNC_CLAIM_IDLE_US")) idle_us_ = std::max(10.0, atof(u));
-  if (const char* f = getenv("DDL_ASYNC_FUSED")) fused_ = atoi(f) != 0;
-  if (const char* g = getenv("DDL_ASYNC_FUSED_GRID")) fused_grid_ = std::max(1, atoi(g));
   if ((int)ps.size() > kAsyncMaxPs) throw std::invalid_argument("async service: too many PS");
 }
 
@@ -1007,7 +1004,9 @@ void AsyncService::start(int64_t expected) {
     cs->nh = nh;
     cs->per_ps = (int)std::min<int64_t>(per_ps, 0x7fffffff);
     cs->opt = opt_;
+    cs->blk0[0] = 0;
     for (int i = 0; i < nh; ++i) {
+      cs->blk0[i + 1] = cs->blk0[i] + peer_->table_.shard[ps_[i].ps].nslice;
       cs->ps[i] = ps_[i].ps;
       cs->params[i] = ps_[i].params;
       cs->m[i] = ps_[i].m;
@@ -1032,9 +1031,6 @@ void AsyncService::start(int64_t expected) {
     cs->idle_ticks = (long long)(idle_us_ * 100.0);  // wall_clock64: 100 MHz
     const char* pub = getenv("DDL_ASYNC_PUBLISH");
     cs->publish_in_claim = pub && std::string(pub) == "claim";
-    // (the fused kernel's claim record: a stale sequence number of an earlier service must
-    // not match this one's launches)
-    X_CHECK(hipMemset(peer_->flags_ + kAsyncClaimRec, 0, 64 * sizeof(uint32_t)));
     X_CHECK(hipMalloc(reinterpret_cast<void**>(&cs_dev_), sizeof(ClaimState)));
     X_CHECK(hipMemcpy(cs_dev_, cs.get(), sizeof(ClaimState), hipMemcpyHostToDevice));
     th_ = std::thread([this] { run_claim(); });
@@ -1051,8 +1047,8 @@ void AsyncService::run_claim() {
   try {
     X_CHECK(hipSetDevice(device_));
     const AsyncTable* T = peer_->table_dev_;
-    int maxs = 1;
-    for (const auto& s : ps_) maxs = std::max(maxs, peer_->table_.shard[s.ps].nslice);
+    int nblk = 0;  // every hosted slice: the apply grid
+    for (const auto& s : ps_) nblk += peer_->table_.shard[s.ps].nslice;
     int64_t enq = 0, last_claims = 0;
     auto idle_since = std::chrono::steady_clock::now();
     TraceRange wait_range("ddl.async.ps.claim_service");
@@ -1067,17 +1063,11 @@ void AsyncService::run_claim() {
       {
         std::lock_guard<std::mutex> hold(pause_mu_);  // pause(): nothing enqueued while paused
         while (enq - ended < depth_ && enq - ended < expected_ - claims) {
-          if (fused_) {
-            hipLaunchKernelGGL(async_fused_claim_apply_kernel, dim3(std::min(fused_grid_, maxs)),
-                               dim3(256), 0, stream_, T, cs_dev_, (uint32_t)(enq + 1));
-            DDL_CHECK_LAUNCH();
-          } else {
-            hipLaunchKernelGGL(async_claim_kernel, dim3(1), dim3(64), 0, stream_, T, cs_dev_);
-            DDL_CHECK_LAUNCH();
-            hipLaunchKernelGGL(async_claimed_apply_kernel, dim3(maxs), dim3(256), 0, stream_, T,
-                               cs_dev_);
-            DDL_CHECK_LAUNCH();
-          }
+          hipLaunchKernelGGL(async_claim_kernel, dim3(1), dim3(64), 0, stream_, T, cs_dev_);
+          DDL_CHECK_LAUNCH();
+          hipLaunchKernelGGL(async_claimed_apply_kernel, dim3(nblk), dim3(256), 0, stream_, T,
+                             cs_dev_);
+          DDL_CHECK_LAUNCH();
           ++enq;
         }
       }

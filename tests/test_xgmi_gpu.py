@@ -247,10 +247,7 @@ def _async_rank(rank, world, port, outdir, kw):
     pytest.param(2, dict(shard="contiguous", _env=dict(DDL_ASYNC_CLAIM="0")), id="2-host-service"),
     pytest.param(4, dict(shard="greedy", num_ps=4, _env=dict(DDL_ASYNC_CLAIM="0")),
                  id="4-host-service"),
-    # claim and apply in one launch (DDL_ASYNC_FUSED=1)
-    pytest.param(1, dict(shard="flat", _ps=4, _env=dict(DDL_ASYNC_FUSED="1")), id="1-flat-fused"),
-    pytest.param(4, dict(shard="greedy", num_ps=4, _env=dict(DDL_ASYNC_FUSED="1")),
-                 id="4-fused"),
+
     pytest.param(8, dict(shard="contiguous", _env=dict(GPU_MAX_HW_QUEUES="1",
                                                        DDL_XGMI_TIMEOUT_S="60")), id="w8-contig"),
     pytest.param(8, dict(shard="greedy", _env=dict(GPU_MAX_HW_QUEUES="1",
