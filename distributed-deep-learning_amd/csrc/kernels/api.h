@@ -475,8 +475,8 @@ class AsyncService {
   int64_t served() const;
   // (worker, ps, worker round, PS step) per apply, in service order
   const std::vector<std::array<int64_t, 4>>& provenance() const { return prov_; }
-  // "device-claim": pre-enqueued claim + apply kernel pairs pop arrivals on the GPU (default);
-  // "host": the thread scans the board and launches each apply (DDL_ASYNC_CLAIM=0)
+  // "host": the thread scans the board and launches each apply (default); "device-claim":
+  // pre-enqueued claim + apply kernel pairs pop arrivals on the GPU (DDL_ASYNC_CLAIM=1)
   const char* mode() const { return claim_ ? "device-claim" : "host"; }
 
  private:
@@ -484,7 +484,7 @@ class AsyncService {
   void run_claim();
   void serve(AsyncPsState& st, int worker);
   void free_claim();
-  bool claim_ = true;
+  bool claim_ = false;
   int depth_ = 3;                // claim pairs in flight on the PS stream
   double idle_us_ = 500.0;       // a claim kernel with no arrival for this long ends empty
   ClaimState* cs_dev_ = nullptr;

@@ -31,6 +31,8 @@
 // per completed push (Adam on the PS's private copy, the new shard stored into the worker's
 // buffer, DONE words in the worker's device flags and in shared host memory).  Staleness stays
 // one round per worker.
+#include <stdlib.h>
+
 #include <stdexcept>
 #include <string>
 
@@ -46,6 +48,10 @@ AsyncRunner::AsyncRunner(Engine* eng, AsyncPeer* peer, int world, int rank, int 
       epoch0_(epoch0) {
   const int P = peer->num_ps();
   if ((int)seg_of_ps.size() != P) throw std::invalid_argument("async runner: one segment per PS");
+  // (A/B switches: DDL_ASYNC_GATE=0 waits for the round on the host, DDL_ASYNC_TAIL=0 pushes
+  // with kernels of their own instead of tail blocks)
+  if (const char* g = getenv("DDL_ASYNC_GATE")) gate_ = g[0] != '0';
+  if (const char* t = getenv("DDL_ASYNC_TAIL")) use_tail_ = t[0] != '0';
   for (int p = 0; p < P; ++p) {
     if (seg_of_ps[p] < 0 || seg_of_ps[p] >= kSegments)
       throw std::invalid_argument("async runner: PS segment out of range");

@@ -12,12 +12,15 @@
 //             gradient -> each PS host's inbox slot [ps][worker] (system write-through stores);
 //             per workgroup, once its payload is acknowledged, POSTED[ps][worker][slice] = e on
 //             the ARRIVAL BOARD in host memory and in the PS host's uncached device flags
-//   serve     (PS host) default: pre-enqueued claim kernels on the PS stream poll the device
-//             copy and pop the next (worker, ps) whose every slice is posted, in the order they
-//             observe them (the reference's MPI.ANY_SOURCE order), each followed by a generic
-//             apply kernel of that claim; the native service thread only keeps that queue
-//             topped up (AsyncService::run_claim).  DDL_ASYNC_CLAIM=0: the thread scans the
-//             host board and launches each apply itself (AsyncService::run)
+//   serve     (PS host) default: a native service thread scans the host board and launches
+//             one apply per (worker, ps) whose every slice is posted, in the order it observes
+//             them (the reference's MPI.ANY_SOURCE order; AsyncService::run).
+//             DDL_ASYNC_CLAIM=1: pre-enqueued claim kernels on the PS stream poll the device
+//             copy and pop every complete push on the GPU, each followed by a batched apply
+//             kernel; the thread only keeps that queue topped up (AsyncService::run_claim).
+//             Same results; the claim service measured equal at W = 1 and 1.3-1.7x slower with
+//             several ranks on one card, where a claim kernel waiting on a high-priority queue
+//             slowed every rank's GEMMs (docs/DESIGN.md round 5), so it is opt-in
 //   apply     (PS host, its PS stream) Adam on the PS's private parameter copy (one step of its
 //             counter t per arrival, atomic per shard: the reference's per-tag mixing race Q3
 //             cannot happen), store the new shard into the WORKER's parameter buffer, then
@@ -243,7 +246,7 @@ __global__ void __launch_bounds__(256) async_apply_kernel(const AsyncTable* __re
 
 }  // namespace
 
-// ---- the on-GPU ANY_SOURCE pop (the default service) ------------------------------------------
+// ---- the on-GPU ANY_SOURCE pop (DDL_ASYNC_CLAIM=1) --------------------------------------------
 // The service keeps `depth` (claim, apply) kernel pairs enqueued on its high-priority PS stream.
 // The claim kernel (one wave) polls this host's arrival words in its own uncached device flags
 // and, once at least one push is complete, takes EVERY complete (hosted PS, worker) push in

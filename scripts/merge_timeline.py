@@ -2,7 +2,7 @@
 """Merged kernel timeline of several processes sharing one GPU (one rocprofv3 database per
 rank, same GPU clock): every kernel of every rank in start order over one step window of rank 0.
 
-usage: python scripts/merge_timeline.py <rank0.db> <rank1.db> ... [--step N] [--anchor SUBSTR]
+usage: python scripts/merge_timeline.py <rank0.db> <rank1.db> ... [--step N] [--steps K] [--anchor SUBSTR]
 Prints start offset (us, from rank 0's anchor), duration, rank, queue id and the kernel name.
 """
 import re
@@ -16,8 +16,8 @@ def short(name):
         d = subprocess.run(["c++filt", name], capture_output=True, text=True).stdout.strip() or name
     except Exception:
         d = name
-    d = re.sub(r"\(.*\)$", "", d).replace("ddl::", "").replace("void ", "")
     d = d.replace("(anonymous namespace)::", "")
+    d = re.sub(r"\(.*\)$", "", d).replace("ddl::", "").replace("void ", "")
     return d[:72] if d else "?"
 
 
@@ -34,9 +34,10 @@ def main():
             rows.append((s, e, r, q, name))
     rows.sort()
     a0 = [x for x in rows if x[2] == 0 and anchor in x[4]]
-    t0, t1 = a0[step][0], a0[step + 2][0]
+    span = int(opts[opts.index("--steps") + 1]) if "--steps" in opts else 2
+    t0, t1 = a0[step][0], a0[min(step + span, len(a0) - 1)][0]
     for s, e, r, q, name in rows:
-        if s < t0 or s >= t1:
+        if e <= t0 or s >= t1:  # (kernels running into the window from before it included)
             continue
         print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f}  r{r} q{q:<3} {short(name)}")
 

@@ -218,8 +218,8 @@ def _async_rank(rank, world, port, outdir, kw):
         assert (tr.exchange.runner is not None) == want_native, "native async step not taken"
         s = tr.train()  # verify_provenance runs inside (check_provenance=True)
         torch.cuda.synchronize()
-        if tr.servers:  # the PS service this host ran: claim kernels unless DDL_ASYNC_CLAIM=0
-            want = "host" if extra_env.get("DDL_ASYNC_CLAIM") == "0" else "device-claim"
+        if tr.servers:  # the PS service this host ran: the host scan unless DDL_ASYNC_CLAIM=1
+            want = "device-claim" if extra_env.get("DDL_ASYNC_CLAIM") == "1" else "host"
             assert tr.exchange.service_mode == want, tr.exchange.service_mode
         torch.save({"params": tr.params.cpu(), "served": tr.exchange.served,
                     "ps": {p: (sv.t, sv.params.cpu()) for p, sv in tr.servers.items()},
@@ -243,10 +243,12 @@ def _async_rank(rank, world, port, outdir, kw):
     # segment-aligned flat plans (sharding.segment_aligned_num_ps): 4 PS on one host, 6 on two
     pytest.param(1, dict(shard="flat", _ps=4), id="1-flat"),
     pytest.param(2, dict(shard="flat", _ps=6), id="2-flat"),
-    # the host-scan PS service (the default pops arrivals with claim kernels on the GPU)
-    pytest.param(2, dict(shard="contiguous", _env=dict(DDL_ASYNC_CLAIM="0")), id="2-host-service"),
-    pytest.param(4, dict(shard="greedy", num_ps=4, _env=dict(DDL_ASYNC_CLAIM="0")),
-                 id="4-host-service"),
+    # the device-side claim service (DDL_ASYNC_CLAIM=1: arrivals popped on the GPU in batches)
+    pytest.param(1, dict(shard="flat", _ps=4, _env=dict(DDL_ASYNC_CLAIM="1")), id="1-flat-claim"),
+    pytest.param(2, dict(shard="contiguous", _env=dict(DDL_ASYNC_CLAIM="1")), id="2-claim"),
+    pytest.param(4, dict(shard="greedy", num_ps=4, _env=dict(DDL_ASYNC_CLAIM="1")),
+                 id="4-claim"),
+    pytest.param(2, dict(shard="flat", _ps=6, _env=dict(DDL_ASYNC_CLAIM="1")), id="2-flat-claim"),
 
     pytest.param(8, dict(shard="contiguous", _env=dict(GPU_MAX_HW_QUEUES="1",
                                                        DDL_XGMI_TIMEOUT_S="60")), id="w8-contig"),
