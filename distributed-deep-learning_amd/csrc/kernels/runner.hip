@@ -38,7 +38,7 @@ static ncclComm_t as_comm(void* c) { return reinterpret_cast<ncclComm_t>(c); }
 // stream has started segment s+1 (READY[s] >= epoch, stored by that launch's first tail block,
 // tail.h kind 2), i.e. once every launch of segment s has completed — a kernel boundary writes
 // the producer's dirty L2 lines back, so the gradients are in memory for this GPU's exchange
-// kernels and for a peer's P2P reads alike.  The comm stream has high priority, so this wait
+// kernels and for a peer's P2P reads alike.  The comm stream has a priority of its own, so this wait
 // never shares a hardware queue with the kernel that releases it.  Bounded (error word).
 // On a timeout it also raises the device copy of the error (err_dev, uncached device memory),
 // which the gated xGMI bucket kernels behind it read — a host-memory word read by every wave of
@@ -68,7 +68,11 @@ SyncRunner::SyncRunner(Engine* eng, float* params, float* grads, int world, int 
   int lo = 0, hi = 0;
   HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   // collectives + optimizer on a high-priority stream so they are not starved by the GEMMs
-  HIP_CHECK(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, hi));
+  // (DDL_COMM_PRIORITY=low: the least priority instead — also a pool of its own, so the READY
+  // gate's argument holds; A/B for ranks sharing a card)
+  const char* cp = getenv("DDL_COMM_PRIORITY");
+  HIP_CHECK(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking,
+                                        cp && cp[0] == 'l' ? lo : hi));
   // The segment events hand gradients written by this device's GEMMs to RCCL kernels on this
   // device.  On the 1-rank rehearsal (W = 1, every collective a local copy) a device-scope
   // release suffices and removed a ~7 us gap per backward segment (forced 1-rank timeline).
@@ -510,14 +514,15 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
 }
 
 // The READY gate waits on the comm stream for a kernel of `st`: only safe when `st` cannot share
-// a hardware queue with the comm stream, i.e. when it is not itself a high-priority stream (HIP
-// pools hardware queues per priority).  Otherwise the segment falls back to the event hand-off.
+// a hardware queue with the comm stream, i.e. when its priority differs from the comm stream's
+// (HIP pools hardware queues per priority; the comm stream is the greatest priority, or the
+// least with DDL_COMM_PRIORITY=low).  Otherwise the segment falls back to the event hand-off.
 bool SyncRunner::gate_safe(hipStream_t st) {
   if (gate_checked_ && st == gate_checked_stream_) return gate_checked_ok_;
-  int lo = 0, hi = 0, p = 0;  // (the null stream is a normal-priority stream)
+  int lo = 0, hi = 0, p = 0, cp = 0;  // (the null stream is a normal-priority stream)
   gate_checked_ok_ = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
-                     (st == nullptr || hipStreamGetPriority(st, &p) == hipSuccess) && hi != lo &&
-                     p != hi;
+                     (st == nullptr || hipStreamGetPriority(st, &p) == hipSuccess) &&
+                     hipStreamGetPriority(cs_, &cp) == hipSuccess && hi != lo && p != cp;
   gate_checked_stream_ = st;
   gate_checked_ = true;
   return gate_checked_ok_;

@@ -74,6 +74,9 @@ DDL_DEV uint32_t flag_load(const uint32_t* f) {
 #ifndef DDL_XGMI_RELEASE
 #define DDL_XGMI_RELEASE 0
 #endif
+#ifndef DDL_XGMI_POLL_TIGHT
+#define DDL_XGMI_POLL_TIGHT 0
+#endif
 DDL_DEV void flag_store(uint32_t* f, uint32_t v) {
   if (DDL_XGMI_RELEASE) asm volatile("buffer_wbl2 sc0 sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -101,7 +104,15 @@ DDL_DEV bool wait_ge(const uint32_t* f, uint32_t target, long long deadline, int
         return false;
       }
     }
+    // tight for the first ~64 polls (a peer's flag normally lands within a few us), then
+    // ~0.45 us apart: waiting waves that poll hard slow the GEMMs running beside them
+    // (docs/DESIGN.md round 5, one-card async).  DDL_XGMI_POLL_TIGHT=1 (compile-time): always tight
+#if DDL_XGMI_POLL_TIGHT
     __builtin_amdgcn_s_sleep(2);
+#else
+    if (it < 64) __builtin_amdgcn_s_sleep(2);
+    else __builtin_amdgcn_s_sleep(16);
+#endif
   }
   return true;
 }

@@ -77,6 +77,10 @@ def share_gpu_queue_cap(local_world: int) -> Optional[str]:
     if ndev == 0 or local_world <= ndev:
         return None  # one process per GPU: HIP's default queues
     os.environ["GPU_MAX_HW_QUEUES"] = want
+    # and the sync runner's comm stream at the LEAST priority (a pool of its own, like the
+    # greatest): bucket kernels waiting on a high-priority queue slowed the other ranks' GEMMs on
+    # the shared card — one-card W = 2 sync 0.89 -> 0.77-0.81 ms/step (profiles/r5_one_card_poll_prio.txt)
+    os.environ.setdefault("DDL_COMM_PRIORITY", "low")
     return want
 
 

@@ -15,6 +15,21 @@ def pytest_configure(config):
 
 
 def free_port() -> int:
+    """A free TCP port for a rendezvous, drawn OUTSIDE the kernel's ephemeral range (32768+):
+    an ephemeral port found free here can be taken by any outgoing connection on the box before
+    the store binds it (EADDRINUSE flake seen on a shared GPU box)."""
+    import random
+    rng = random.Random()
+    for _ in range(200):
+        p = rng.randrange(15000, 30000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     p = s.getsockname()[1]

@@ -174,12 +174,14 @@ def test_reference_pickle_refuses_other_globals(tmp_path):
 def test_shared_gpu_ranks_get_one_hw_queue(monkeypatch):
     from ddl_amd.parallel import comm
     monkeypatch.delenv("DDL_SHARED_GPU_HW_QUEUES", raising=False)
+    monkeypatch.delenv("DDL_COMM_PRIORITY", raising=False)
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")          # what the GPU boxes export
     monkeypatch.setattr(comm.torch.cuda, "device_count", lambda: 1)
     assert comm.share_gpu_queue_cap(1) is None           # one process: HIP's default
     assert os.environ["GPU_MAX_HW_QUEUES"] == "4"
     assert comm.share_gpu_queue_cap(4) == "1"             # four ranks on one card
     assert os.environ["GPU_MAX_HW_QUEUES"] == "1"
+    assert os.environ["DDL_COMM_PRIORITY"] == "low"        # and the comm stream at low priority
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
     monkeypatch.setenv("DDL_SHARED_GPU_HW_QUEUES", "keep")
     assert comm.share_gpu_queue_cap(4) is None and os.environ["GPU_MAX_HW_QUEUES"] == "4"
