@@ -121,6 +121,8 @@ class PyEngine {
     return std::vector<int64_t>(e_.wide, e_.wide + ddl::OP_COUNT);
   }
   // per-op split-K block order (gemm.h split_coords; 0..3)
+  void set_dual_bfirst(int64_t m) { e_.dual_bfirst = (int)m; }
+  int64_t get_dual_bfirst() const { return e_.dual_bfirst; }
   void set_order(std::vector<int64_t> o) {
     TORCH_CHECK((int)o.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " orders");
     for (int i = 0; i < ddl::OP_COUNT; ++i) {
@@ -762,6 +764,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("conv1_wgrad_direct", [](PyEngine& e) { return e.raw()->conv1_wgrad_direct; })
       .def("set_wide_thr", &PyEngine::set_wide_thr)
       .def("set_wide", &PyEngine::set_wide)
+      .def("set_dual_bfirst", &PyEngine::set_dual_bfirst)
+      .def("get_dual_bfirst", &PyEngine::get_dual_bfirst)
       .def("set_order", &PyEngine::set_order)
       .def("get_order", &PyEngine::get_order)
       .def("get_wide", &PyEngine::get_wide)

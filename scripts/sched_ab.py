@@ -25,6 +25,9 @@ def main():
                          "to label it)")
     ap.add_argument("--order-variants", default="",
                     help="';'-separated block-order overrides (gemm.h split_coords), 'op=o,op=o'")
+    ap.add_argument("--bfirst-variants", default="",
+                    help="';'-separated dual_bfirst masks (bit op: that dual dispatches its "
+                         "second problem first; default 1<<14)")
     a = ap.parse_args()
     import torch
     from ddl_amd.config import TrainConfig
@@ -68,6 +71,8 @@ def main():
             op, val = kv.split("=")
             od[int(op)] = int(val)
         scheds["order[" + v + "]"] = dict(scheds["default"], order=od)
+    for v in filter(None, a.bfirst_variants.split(";")):
+        scheds["bfirst[" + v + "]"] = dict(scheds["default"], bfirst=int(v))
     res = {k: [] for k in scheds}
     step = 0
     for _ in range(a.rounds):
@@ -77,6 +82,7 @@ def main():
             e.set_workers(s["workers"])
             e.set_wide(s["wide"])
             e.set_order(s.get("order", scheds["default"]["order"]))
+            e.set_dual_bfirst(s.get("bfirst", 1 << 14))
             for _ in range(20):
                 tr.train_step(step)
                 step += 1
