@@ -243,7 +243,7 @@ void Engine::flush_head_wgrad(int B, hipStream_t st) {
 
 void Engine::forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st,
                      bool defer_fc2) {
-  flush_fc2(seed, B, st);  // (a deferred reduce nobody took: its slab is about to be reused)
+  fc2_slab = nullptr;  // (a deferred fc2 reduce nobody took: this forward rewrites h2 anyway)
   for (int op = OP_CONV1_FWD; op < OP_FC2_FWD; ++op) run_op(op, x, B, seed, train, st, 0);
   if (!(train && defer_fc2 && fc2_in_head && !concurrent && run_fc2_deferred(*this, x, B, seed, st)))
     run_op(OP_FC2_FWD, x, B, seed, train, st, 0);
