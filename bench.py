@@ -204,11 +204,15 @@ def main(argv=None):
             if ok:
                 try:
                     p0 = t.params.clone()
-                    for i in range(5):
+                    # untimed steps first: the first candidate would otherwise run on a cold GPU
+                    # (clocks ramp over ~100 steps); the same count for every candidate, so their
+                    # replicas stay comparable (same init, data and step count)
+                    nw = 5 + min(200, n_pre)
+                    for i in range(nw):
                         t.train_step(i)
                     sync()
                     t0 = time.perf_counter()
-                    for i in range(5, 5 + a.ab_steps):
+                    for i in range(nw, nw + a.ab_steps):
                         t.train_step(i)
                     sync()
                     ms = 1e3 * (time.perf_counter() - t0) / a.ab_steps
