@@ -314,6 +314,10 @@ def main(argv=None):
     # the record's facts about the benchmarked trainer, taken before any release below
     engine_name = getattr(tr.engine, "name", a.engine)
     num_ps, policy, exchange_name = tr.num_ps, tr.plan.policy, backend_of(tr)
+    # the replicated last bucket exchanged inside conv1's weight-gradient launch (xGMI runner)
+    runner = getattr(getattr(tr, "exchange", None), "runner", None)
+    last_fused = bool(runner is not None and hasattr(runner, "fused_last_taken")
+                      and runner.fused_last_taken())
     # W > 1 (sync, and async after its exchange joined): close and drop every trainer built so
     # far (collectively, between barriers, nothing in flight) before each time-to-accuracy run —
     # close() releases each runner's comm stream, events, flags and peer mappings, the side-
@@ -401,6 +405,7 @@ def main(argv=None):
                 "handoff": (handoff["handoff"] if handoff
                             else "n/a (W = 1, local updates)" if world == 1
                             else "n/a (no native runner)"),
+                "last_bucket_in_conv1_launch": last_fused,
             },
             "test_acc_after_run": round(acc, 4),
             "prewarm": {"steps": n_pre, "note": "untimed steps before the warmup steps: the "

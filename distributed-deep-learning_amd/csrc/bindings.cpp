@@ -656,6 +656,8 @@ class PyRunner {
   void set_ready_flags(int64_t mode) { r_->set_ready_flags((int)mode); }
   void set_use_tail(bool on) { r_->set_use_tail(on); }
   void set_final_in_reduce(bool on) { r_->set_final_in_reduce(on); }
+  void set_fused_last(bool on) { r_->set_fused_last(on); }
+  bool fused_last_taken() const { return r_->fused_last_taken(); }
   void set_tail_cfg(int64_t first, int64_t f4) { r_->set_tail_cfg((int)first, (int)f4); }
   void step(at::Tensor x, at::Tensor labels, int64_t seed, std::vector<double> lr_t) {
     eng_.check_batch(x);
@@ -796,6 +798,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_use_tail", &PyRunner::set_use_tail)
       .def("set_ready_flags", &PyRunner::set_ready_flags)
       .def("set_final_in_reduce", &PyRunner::set_final_in_reduce)
+      .def("set_fused_last", &PyRunner::set_fused_last)
+      .def("fused_last_taken", &PyRunner::fused_last_taken)
       .def("set_tail_cfg", &PyRunner::set_tail_cfg)
       .def("step", &PyRunner::step)
       .def("selftest", &PyRunner::selftest)

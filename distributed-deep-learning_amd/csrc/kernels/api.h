@@ -114,6 +114,8 @@ constexpr int CFG_RING2 = 20;
 inline bool ring_cfg(int c) { return c == CFG_RING3 || c == CFG_RING2; }
 inline bool dma_cfg(int c) { return dma_g_cfg(c) || ring_cfg(c); }
 
+struct XgmiLast;  // (xGMI section below)
+
 struct Engine {
   const float* P[14] = {};   // parameter tensors v0..v13 (any flat layout)
   float* G[14] = {};         // gradient tensors v0..v13
@@ -161,6 +163,13 @@ struct Engine {
   // reduce epilogue, the rest as tail blocks of that launch (engine_impl.h dual_then_b).
   // Cleared when taken; the runner launches it as before when it is still pending.
   UpdTail final_upd;
+  // W > 1 over xGMI: the replicated last bucket's exchange (push to every peer, rank-order sum,
+  // the replicated update) fused into that same launch (conv1.h conv1_wgrad_xgmi_kernel), with
+  // final_upd naming the bucket's spans.  Set by the runner for one step; final_xchg_taken tells
+  // it that xgmi_repl_kernel must not run.
+  const XgmiLast* final_xchg = nullptr;      // host copy (the launch's layout checks)
+  const XgmiLast* final_xchg_dev = nullptr;  // device copy (read by the kernel)
+  bool final_xchg_taken = false;
   // eval forward: conv2 on the tap-skipping K map (DDL_EVAL_KMAP2=0: the image-major GEMM)
   bool eval_kmap2 = [] {
     const char* e = getenv("DDL_EVAL_KMAP2");
@@ -284,6 +293,16 @@ struct XgmiLaunch {              // one bucket's kernel arguments
   int64_t run_lo[kXgmiMaxRuns], run_n[kXgmiMaxRuns], run_soff[kXgmiMaxRuns];
   int64_t run_voff[kXgmiMaxRuns], run_slice[kXgmiMaxRuns];
   int run_sl0[kXgmiMaxRuns + 1];
+  int64_t rslot;                 // the replicated bucket's inbox slot stride (floats)
+};
+// Floats per (parity, source) slot of the replicated bucket's inbox: the bucket itself, or what
+// the fused last launch exchanges if that is more — conv2's weight-gradient reduce in its tile
+// order (M = 801 rows, N = 64 columns; tiles up to 256 x 128: 1024 x 128) and conv1's 26 x 32
+// (conv1.h conv1_wgrad_xgmi_kernel checks the launch's layout against it).
+constexpr int64_t kXgmiReplFusedSlot = 1024 * 128 + 26 * 32;
+struct XgmiLast {                // the last bucket's exchange inside conv1's weight-gradient launch
+  XgmiTable T;
+  XgmiLaunch a;
 };
 // One bucket of a PeerExchange.  owner < 0: a single plan-buffer range split into W equal chunks,
 // chunk r owned by rank r (the flat plan: reduce-scatter form).  owner >= 0: one PS's exchange
@@ -323,6 +342,8 @@ class PeerExchange {
   // word before publishing anything)
   void launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool final_wait, hipStream_t st,
               bool gated = false);
+  // the replicated bucket's kernel arguments without launching (the fused last launch)
+  void fill_last(uint32_t epoch, const XgmiUpdate& u, bool final_wait, XgmiLast& out) const;
   int error() const;             // nonzero once a wait timed out (1 arrive, 2 done)
   // the runner's READY-gate error word, checked by every bucket kernel before it publishes
   void set_gate_error(const int* w) { gate_err_ = w; }
@@ -335,16 +356,20 @@ class PeerExchange {
   int owner(int b) const { return bk_[b].owner; }
   int world() const { return world_; }
   int repl_bucket() const { return repl_; }
+  bool check_mode() const { return check_; }
 
  private:
   struct Bucket {
     int64_t lo, c, inbox_off, slice;
+    int64_t slot = 0;  // the replicated bucket: floats per (parity, source) inbox slot
     int nslice;
     int owner = -1;
     std::vector<int64_t> run_lo, run_n, run_soff, run_voff, run_slice;
     std::vector<int> run_sl0;
   };
   void init(const std::vector<XgmiBucketSpec>& buckets, int max_slices);
+  void fill(int bucket, uint32_t epoch, const XgmiUpdate& u, bool final_wait, bool gated,
+            XgmiLaunch& a) const;
   int repl_ = -1;
   bool check_ = false;
   float* params_;
@@ -637,6 +662,7 @@ class SyncRunner {
   void set_peer(PeerExchange* p) {
     peer_ = p;
     if (p) p->set_gate_error(ready_err_dev());  // (device memory: read by every bucket wave)
+    if (p) alloc_last();
   }
   int* ready_err_dev() const { return ready_ ? reinterpret_cast<int*>(ready_ + kSegments) : nullptr; }
   // one full exchange of every bucket with w := sum over ranks of g (no optimizer) at the
@@ -723,6 +749,14 @@ class SyncRunner {
   // the GEMM conv1 path as tail blocks of the wide reduce (measured neutral).
   // DDL_FINAL_IN_REDUCE=0: the stand-alone Adam launch
   void set_final_in_reduce(bool on) { final_in_reduce_ = on; }
+  // W > 1 over xGMI: the replicated last bucket exchanged and updated inside conv1's weight-
+  // gradient launch (conv1.h conv1_wgrad_xgmi_kernel) instead of by xgmi_repl_kernel after it.
+  // Opt-in (DDL_XGMI_FUSED_LAST=1): bit-identical, but NOT faster on the forced 1-rank
+  // rehearsal (0.3037-0.3042 vs 0.3026 ms/step: the fused launch takes 23.2 us against 13.0 +
+  // 8.8), and the one-card W = 2 / 3 rehearsals (several ranks on one GPU) timed out
+  // intermittently with it — not root-caused (docs/DESIGN.md round 5)
+  void set_fused_last(bool on) { fused_last_ = on; }
+  bool fused_last_taken() const { return fused_last_taken_; }  // by the previous step
   // tail placement (1: before the GEMM blocks) and float4 per tail block (tuning)
   void set_tail_cfg(int first, int f4_per_block) {
     tail_first_ = first;
@@ -734,6 +768,21 @@ class SyncRunner {
   // block: 373 us/step vs 381 without the tail; before the GEMM blocks 375-378
   int tail_first_ = 0;
   int tail_f4_ = 4 * kTailF4PerBlock;
+  bool fused_last_ = [] {
+    const char* e = getenv("DDL_XGMI_FUSED_LAST");
+    return e && e[0] == '1';
+  }();
+  bool fused_last_taken_ = false;
+  XgmiLast xlast_{};             // the fused launch's exchange arguments (this step's)
+  XgmiLast xlast_up_{};          // what the device copy holds (epoch aside)
+  XgmiLast* xlast_dev_ = nullptr;  // device copy (hipMalloc; rewritten when it changes)
+  XgmiLast* xlast_host_ = nullptr; // its pinned staging copy (hipMemcpyAsync source)
+  bool xlast_up_valid_ = false;
+  void alloc_last();               // the two buffers above (set_peer: never inside a step)
+  // the last segment's XGMI_REPL unit when the fused launch may take it, else null
+  const RunnerUnit* fused_last_unit(bool on_main, hipStream_t st);
+  hipStream_t fused_prio_stream_ = nullptr;
+  bool fused_prio_checked_ = false, fused_prio_ok_ = false;
 };
 
 }  // namespace ddl

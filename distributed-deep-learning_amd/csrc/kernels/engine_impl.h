@@ -381,8 +381,8 @@ inline bool final_split_conv12(const Engine& e, const UpdTail& in, const PB& pb,
   const int64_t n2w = (int64_t)PB::KW * pb.N, n2b = pb.N, n1w = 800, n1b = 32;
   // every element of the pieces is one of the four tensors or the alignment padding that
   // follows a tensor in the plan buffer (< kPad elements: zero gradient and state, so skipping
-  // its update changes nothing)
-  constexpr int64_t kPad = 64;
+  // its update changes nothing; flat plans at W > 1 end the bucket on a 256-float boundary)
+  constexpr int64_t kPad = 256;
   const float* sw[4] = {e.P[0], e.P[1], e.P[2], e.P[3]};
   const int64_t sn[4] = {n1w, n1b, n2w, n2b};
   for (int i = 0; i < in.npieces; ++i) {
@@ -444,7 +444,33 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
     // conv1's weight gradient on the direct kernel (conv1.h), sharing its launch with OB's
     // pending reduce; scratch[0] is free here (OA's split-K finished inside the dual launch
     // or in its own reduce before this point)
-    if (e.conv1_wgrad_direct && conv1_wgrad_direct_ok(B, e.slab_floats, e.scratch[0].max_tiles)) {
+    const bool direct =
+        e.conv1_wgrad_direct && conv1_wgrad_direct_ok(B, e.slab_floats, e.scratch[0].max_tiles);
+    if (e.final_xchg) {
+      // W > 1 over xGMI: the replicated last bucket's exchange and update in this launch
+      // (conv1.h conv1_wgrad_xgmi_kernel); anything else leaves both to the runner's
+      // xgmi_repl_kernel — never to the local-update paths below
+      const XgmiLast& xl = *e.final_xchg;
+      const UpdTail fu = e.final_upd;
+      e.final_xchg = nullptr;  // (xl stays valid: the runner owns it)
+      e.final_upd = UpdTail();
+      if (direct) {
+        float* part = static_cast<float*>(e.scratch[0].slab);
+        WgradAdam<PB> pa;
+        C1Adam ad;
+        if (fu.npieces > 0 && final_split_conv12(e, fu, pb, pa, ad) &&
+            launch_conv1_wgrad_xgmi<CB, PB>(pa, gb, x, e.d1, B, e.G[0], e.G[1], part,
+                                            e.scratch[0].tickets, e.scratch[0].max_tiles, st, ad,
+                                            xl, e.final_xchg_dev)) {
+          e.final_xchg_taken = true;
+          return;
+        }
+        launch_conv1_wgrad<CB, PB>(pb, gb, x, e.d1, B, e.G[0], e.G[1], part,
+                                   e.scratch[0].tickets, st);
+        return;
+      }
+    }
+    if (direct) {
       float* part = static_cast<float*>(e.scratch[0].slab);
       // the last segment's update (W = 1 tail path) inside this launch: conv2's in its weight-
       // gradient reduce epilogue, conv1's in the final reduce level; no Adam launch follows

@@ -1791,6 +1791,25 @@ gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut, int bfirst) {
     run_sub<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB, CB::V, CB::V == 0>(pb, gb, ib, lds, flag);
 }
 
+// Output rows m0 .. m0 + 3 and column n of float4 element e of a mode-2 partial slab (the tile /
+// wave / fragment / lane order the GEMM tiles store their partials in).
+template <int BM, int BN, int WM, int WN>
+DDL_DEV void wide_elem_coords(int e, int gx, int& m0, int& n) {
+  using G = TileGeo<BM, BN, WM, WN>;
+  const int tile = e / G::PART4;
+  int r = e % G::PART4;
+  constexpr int WPART = G::FRAGS * 4 * 64;
+  const int wave = r / WPART;
+  r %= WPART;
+  const int fg = r / 64, lane = r % 64;
+  const int frag = fg / 4, g = fg % 4;
+  const int i = frag / G::TN, j = frag % G::TN;
+  const int wm = wave / WN, wn = wave % WN;
+  const int bx = tile % gx, by = tile / gx;
+  m0 = bx * BM + wm * G::WTM + i * 32 + 8 * g + 4 * (lane >> 5);
+  n = by * BN + wn * G::WTN + j * 32 + (lane & 31);
+}
+
 // Wide split-K reduce (mode 2): RL lanes cooperate on one float4 output element; `gid` is the
 // global thread index (any block size that is a multiple of RL).
 template <int BM, int BN, int WM, int WN, int RL, class P>
@@ -1813,18 +1832,8 @@ DDL_DEV void wide_reduce_body(const P& p, const float4* __restrict__ slab, int S
   s.z = group_sum<RL>(s.z);
   s.w = group_sum<RL>(s.w);
   if (!valid || sub != 0) return;
-  const int tile = e / G::PART4;
-  int r = e % G::PART4;
-  constexpr int WPART = G::FRAGS * 4 * 64;
-  const int wave = r / WPART;
-  r %= WPART;
-  const int fg = r / 64, lane = r % 64;
-  const int frag = fg / 4, g = fg % 4;
-  const int i = frag / G::TN, j = frag % G::TN;
-  const int wm = wave / WN, wn = wave % WN;
-  const int bx = tile % gx, by = tile / gx;
-  const int m0 = bx * BM + wm * G::WTM + i * 32 + 8 * g + 4 * (lane >> 5);
-  const int n = by * BN + wn * G::WTN + j * 32 + (lane & 31);
+  int m0, n;
+  wide_elem_coords<BM, BN, WM, WN>(e, gx, m0, n);
   if (n < p.N && m0 < p.M) p.epi(m0, n, f32x4{s.x, s.y, s.z, s.w});
 }
 

@@ -707,16 +707,26 @@ struct WgradAdam : P {
   float *w_w, *w_m, *w_v;  // weight span
   float *b_w, *b_m, *b_v;  // bias span
   float lr_t, c1, c2, eps, scale;
-  DDL_DEV void epi(int m0, int n, f32x4 v) const {
+  DDL_DEV void epi(int m0, int n, f32x4 v) const { apply<true>(m0, n, v); }
+  // STORE = false: the update alone (the fused xGMI last bucket: the gradient stored is this
+  // rank's, the update takes the sum over ranks; conv1.h conv1_wgrad_xgmi_kernel)
+  template <bool STORE>
+  DDL_DEV void apply(int m0, int n, f32x4 v) const {
     constexpr int KW = P::KW;  // gw is [KW, N] (N = COUT)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = m0 + r;
       float *pw, *pm, *pv;
       size_t i;
-      if (m < KW) { i = (size_t)m * this->N + n; pw = w_w; pm = w_m; pv = w_v; this->gw[i] = v[r]; }
-      else if (m == KW) { i = (size_t)n; pw = b_w; pm = b_m; pv = b_v; this->gb[i] = v[r]; }
-      else continue;
+      if (m < KW) {
+        i = (size_t)m * this->N + n; pw = w_w; pm = w_m; pv = w_v;
+        if (STORE) this->gw[i] = v[r];
+      } else if (m == KW) {
+        i = (size_t)n; pw = b_w; pm = b_m; pv = b_v;
+        if (STORE) this->gb[i] = v[r];
+      } else {
+        continue;
+      }
       float W = pw[i], M = pm[i], V = pv[i];
       adam1(W, v[r] * scale, M, V, lr_t, c1, c2, eps);
       pw[i] = W; pm[i] = M; pv[i] = V;

@@ -40,6 +40,7 @@
 
 #include "api.h"
 #include "common.h"
+#include "xgmi_dev.h"
 
 namespace ddl {
 
@@ -58,63 +59,12 @@ DDL_DEV float4 ld4_sys(brsrc_t r, int byte_off) {
 }
 DDL_DEV void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-DDL_DEV uint32_t flag_load(const uint32_t* f) {
-  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-// The flag that publishes a workgroup's payload.  Every payload store is a system-scope
-// (sc0|sc1) write-through store, and every storing wave drains vmcnt(0) before the workgroup
-// barrier that precedes the flag store: a write-through store is counted complete only once the
-// memory side (local HBM, or the peer over xGMI, or host memory) has acknowledged it, so the
-// payload is globally visible before the flag is issued — no L2 write-back is needed (the CDNA
-// guide's G16 write-through hand-off, at system scope).  DDL_XGMI_RELEASE=1 adds the full
-// system release anyway (L2 write-back + wait, as one asm statement: hipcc drops the wait of its
-// own release when the scoreboard is already drained, and schedules a separate asm wait above
-// the write-back); it writes back every dirty line of the XCD's L2 at each flag — the GEMMs'
-// output included — and measured 3.2 -> 5.4 ms/step on the two-ranks-on-one-GPU rehearsal.
-#ifndef DDL_XGMI_RELEASE
-#define DDL_XGMI_RELEASE 0
-#endif
-#ifndef DDL_XGMI_POLL_TIGHT
-#define DDL_XGMI_POLL_TIGHT 0
-#endif
-DDL_DEV void flag_store(uint32_t* f, uint32_t v) {
-  if (DDL_XGMI_RELEASE) asm volatile("buffer_wbl2 sc0 sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
-  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-DDL_DEV int arrive_idx(int b, int src, int j) { return (b * kXgmiMaxPeers + src) * kXgmiMaxSlices + j; }
-// one completion word per (bucket, owner, slice), written only by that owner's workgroup: every
-// flag has a single writer and is only ever stored (no read-modify-write: atomics through an
-// IPC mapping are performed in whichever XCD L2 the writer's mapping caches them in, so counters
-// bumped by several writers can lose updates); the final wait polls them all in parallel
-DDL_DEV int done_idx(int b, int src, int j) {
-  return kXgmiMaxBuckets * kXgmiMaxPeers * kXgmiMaxSlices + arrive_idx(b, src, j);
-}
-
-// Bounded wait until *f >= target (wrap-safe).  false on timeout or when another workgroup
-// already reported an error (then the caller just runs to the end).
+// the flag protocol's device side lives in xgmi_dev.h (shared with conv1.h's fused last bucket)
+DDL_DEV void flag_store(uint32_t* f, uint32_t v) { xg_flag_store(f, v); }
+DDL_DEV int arrive_idx(int b, int src, int j) { return xg_arrive_idx(b, src, j); }
+DDL_DEV int done_idx(int b, int src, int j) { return xg_done_idx(b, src, j); }
 DDL_DEV bool wait_ge(const uint32_t* f, uint32_t target, long long deadline, int* err, int code) {
-  // the error word lives in host memory (a PCIe round trip per load): look at it, and at the
-  // clock, only every 32nd poll, so a flag that lands is seen within one poll of local memory
-  for (int it = 0; (int32_t)(flag_load(f) - target) < 0; ++it) {
-    if ((it & 31) == 31) {
-      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return false;
-      if (wall_clock64() > deadline) {
-        __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return false;
-      }
-    }
-    // tight for the first ~64 polls (a peer's flag normally lands within a few us), then
-    // ~0.45 us apart: waiting waves that poll hard slow the GEMMs running beside them
-    // (docs/DESIGN.md round 5, one-card async).  DDL_XGMI_POLL_TIGHT=1 (compile-time): always tight
-#if DDL_XGMI_POLL_TIGHT
-    __builtin_amdgcn_s_sleep(2);
-#else
-    if (it < 64) __builtin_amdgcn_s_sleep(2);
-    else __builtin_amdgcn_s_sleep(16);
-#endif
-  }
-  return true;
+  return xg_wait_ge(f, target, deadline, err, code);
 }
 
 // The READY gate ahead of this kernel timed out (its gradients may be incomplete): publish
@@ -174,27 +124,10 @@ DDL_DEV bool check_piece(brsrc_t in, int off, int n4, const uint32_t* ck, int* e
   return false;
 }
 
-// The final wait of a step: every (bucket, owner, slice) DONE word of the step, except the
-// replicated bucket's (it has none), spread over all threads of the launch and polled at once.
-// An owner bucket's DONE words come from its one owner, an equal-chunk bucket's from every rank.
+// The final wait of a step (xgmi_dev.h xg_final_wait) over every thread of the launch.
 DDL_DEV void final_wait(const XgmiLaunch& a, const uint32_t* myflags, int W, long long deadline) {
-  auto words = [&](int bb) {
-    return bb == a.repl_bucket ? 0 : (a.owners[bb] >= 0 ? 1 : W) * a.nslices[bb];
-  };
-  int total = 0;
-  for (int bb = 0; bb < a.nbuckets; ++bb) total += words(bb);
-  for (int k = blockIdx.x * 256 + threadIdx.x; k < total; k += gridDim.x * 256) {
-    int bb = 0, x = k;
-    for (;;) {
-      const int nb = words(bb);
-      if (x < nb) break;
-      x -= nb;
-      ++bb;
-    }
-    const int q = x / a.nslices[bb], jj = x - q * a.nslices[bb];
-    wait_ge(myflags + done_idx(bb, a.owners[bb] >= 0 ? a.owners[bb] : q, jj), a.epoch, deadline,
-            a.err, 2);
-  }
+  xg_final_wait(a, a.epoch, myflags, W, deadline, blockIdx.x * 256 + threadIdx.x,
+                gridDim.x * 256);
 }
 
 // The owner-side optimizer update of one float4 (TF1 Adam, momentum, or the self-test's
@@ -367,7 +300,7 @@ __global__ void __launch_bounds__(256) xgmi_repl_kernel(XgmiTable T, XgmiLaunch 
   const float4* own = reinterpret_cast<const float4*>(a.grads + a.lo + s0);
   // slot (par, src) of rank r's replicated inbox, this slice
   auto slot = [&](int r, int src) {
-    return make_rsrc(T.inbox[r] + a.inbox_off + ((int64_t)par * W + src) * n + s0,
+    return make_rsrc(T.inbox[r] + a.inbox_off + ((int64_t)par * W + src) * a.rslot + s0,
                      (uint32_t)n4 * 16u);
   };
 
@@ -632,9 +565,11 @@ void PeerExchange::init(const std::vector<XgmiBucketSpec>& buckets, int max_slic
     if (ns < 1) ns = 1;
     B.slice = ((B.c + ns - 1) / ns + 3) & ~(int64_t)3;
     B.nslice = (int)((B.c + B.slice - 1) / B.slice);
-    if (B.c * 4 * world * (repl ? 2 : 1) > 0x7fffffffLL)
+    // the replicated bucket's slot also holds the fused last launch's exchange (api.h)
+    B.slot = repl ? (B.c > kXgmiReplFusedSlot ? B.c : kXgmiReplFusedSlot) : B.c;
+    if (B.slot * 4 * world * (repl ? 2 : 1) > 0x7fffffffLL)
       throw std::invalid_argument("xgmi: bucket too large");
-    inbox += B.c * world * (repl ? 2 : 1);  // replicated: two parity slots per source
+    inbox += B.slot * world * (repl ? 2 : 1);  // replicated: two parity slots per source
     bk_.push_back(B);
   }
   inbox_elems_ = inbox;
@@ -716,15 +651,14 @@ void PeerExchange::open(const std::vector<std::string>& handles) {
   opened_ok_ = true;
 }
 
-void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool final_wait,
-                          hipStream_t st, bool gated) {
+void PeerExchange::fill(int bucket, uint32_t epoch, const XgmiUpdate& u, bool final_wait,
+                        bool gated, XgmiLaunch& a) const {
   if (!opened_ok_) throw std::runtime_error("xgmi: open() the peer handles first");
   if (bucket < 0 || bucket >= (int)bk_.size()) throw std::invalid_argument("xgmi: bucket index");
   const Bucket& B = bk_[bucket];
   const bool owns = B.owner < 0 || B.owner == rank_;  // runs the update of (part of) the bucket
   if (owns && u.opt != 2 && !u.m) throw std::invalid_argument("xgmi: optimizer state missing");
   if (owns && u.opt == 0 && !u.v) throw std::invalid_argument("xgmi: Adam needs v");
-  XgmiLaunch a;
   memset(&a, 0, sizeof(a));
   a.world = world_;
   a.rank = rank_;
@@ -736,6 +670,7 @@ void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool 
   a.c = B.c;
   a.inbox_off = B.inbox_off;
   a.slice = B.slice;
+  a.rslot = B.slot;
   for (size_t i = 0; i < bk_.size(); ++i) a.nslices[i] = bk_[i].nslice;
   a.grads = grads_;
   a.m = u.m;
@@ -768,6 +703,22 @@ void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool 
       a.run_sl0[r] = B.run_sl0[r];
     }
     a.run_sl0[a.nruns] = B.run_sl0[a.nruns];
+  }
+}
+
+void PeerExchange::fill_last(uint32_t epoch, const XgmiUpdate& u, bool final_wait,
+                             XgmiLast& out) const {
+  if (repl_ < 0) throw std::runtime_error("xgmi: no replicated bucket");
+  fill(repl_, epoch, u, final_wait, false, out.a);
+  out.T = table_;
+}
+
+void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool final_wait,
+                          hipStream_t st, bool gated) {
+  XgmiLaunch a;
+  fill(bucket, epoch, u, final_wait, gated, a);
+  const Bucket& B = bk_[bucket];
+  if (B.owner >= 0) {
     switch (world_) {
 #define X_CASE(N) \
   case N: DDL_LAUNCH(xgmi_owner_kernel<N>, dim3(B.nslice), dim3(256), 0, st, table_, a); break;

@@ -105,6 +105,9 @@ def _rank(rank, world, port, outdir, kw):
         torch.cuda.synchronize()
         ex.check()
         acc = tr.evaluate()
+        # the replicated last bucket stays xgmi_repl_kernel at W > 1 (the fused launch is
+        # opt-in: DDL_XGMI_FUSED_LAST=1, docs/DESIGN.md round 5)
+        assert not ex.runner.fused_last_taken(), "fused last bucket taken by default"
         torch.save({"params": _canon(tr.params, tr.plan.tensor_offsets).cpu(), "acc": acc,
                     "sums": sums,
                     "t": {p: s.t for p, s in tr.servers.items()}},
