@@ -751,10 +751,9 @@ class SyncRunner {
   void set_final_in_reduce(bool on) { final_in_reduce_ = on; }
   // W > 1 over xGMI: the replicated last bucket exchanged and updated inside conv1's weight-
   // gradient launch (conv1.h conv1_wgrad_xgmi_kernel) instead of by xgmi_repl_kernel after it.
-  // Opt-in (DDL_XGMI_FUSED_LAST=1): bit-identical, but NOT faster on the forced 1-rank
-  // rehearsal (0.3037-0.3042 vs 0.3026 ms/step: the fused launch takes 23.2 us against 13.0 +
-  // 8.8), and the one-card W = 2 / 3 rehearsals (several ranks on one GPU) timed out
-  // intermittently with it — not root-caused (docs/DESIGN.md round 5)
+  // Opt-in (DDL_XGMI_FUSED_LAST=1): bit-identical and faster on the forced 1-rank rehearsal
+  // (0.2978-0.2990 vs 0.3018-0.3025 ms/step), but with several ranks time-sharing one GPU it
+  // stalled intermittently (W = 4 in the last run) — not root-caused (docs/DESIGN.md round 5)
   void set_fused_last(bool on) { fused_last_ = on; }
   bool fused_last_taken() const { return fused_last_taken_; }  // by the previous step
   // tail placement (1: before the GEMM blocks) and float4 per tail block (tuning)

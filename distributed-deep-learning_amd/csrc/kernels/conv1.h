@@ -182,8 +182,7 @@ DDL_DEV bool xf_arrive_wait(XfRef x, int j, int* flag, int code) {
 
 // conv1's final reduce level with the exchange: the summed partials are this rank's gradient
 // (stored to gw / gb as without the exchange), pushed to every peer's slot [par][me]; after the
-// peers' arrive, the W contributions in rank order go through the update; this block (one per
-// launch) also carries the step's final wait.
+// peers' arrive, the W contributions in rank order go through the update.
 DDL_DEV void c1w_sum_xgmi(brsrc_t part, int src, int n, float* gw, float* gb, const C1Adam& ad,
                           XfRef xl, int off, int j, int* flag) {
   constexpr int EPT = kC1wEPT;
@@ -209,14 +208,20 @@ DDL_DEV void c1w_sum_xgmi(brsrc_t part, int src, int n, float* gw, float* gb, co
     for (int jj = 0; jj < EPT; ++jj) {
       const int e = tid + 256 * jj;
       if (e >= kC1wElems) continue;
-      float xq[kXgmiMaxPeers];
-#pragma unroll
-      for (int q = 0; q < kXgmiMaxPeers; ++q)
-        if (q < W && q != me) xq[q] = xf_load1(in, (int)(((int64_t)q * a.rslot + off + e) * 4));
+      // rank order, as xgmi_repl_kernel, the loads of 4 ranks in flight at a time
       float g = 0.f;
+      for (int q0 = 0; q0 < W; q0 += 4) {
+        float xq[4];
 #pragma unroll
-      for (int q = 0; q < kXgmiMaxPeers; ++q)  // rank order, as xgmi_repl_kernel
-        if (q < W) g += q == me ? v[jj] : xq[q];
+        for (int u = 0; u < 4; ++u) {
+          const int q = q0 + u;
+          xq[u] = q < W && q != me
+                      ? xf_load1(in, (int)(((int64_t)q * a.rslot + off + e) * 4)) : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (q0 + u < W) g += q0 + u == me ? v[jj] : xq[u];
+      }
       const bool wrow = e < 25 * 32;
       const int i = wrow ? e : e - 25 * 32;
       float* pw = wrow ? ad.w_w : ad.b_w;
@@ -227,8 +232,6 @@ DDL_DEV void c1w_sum_xgmi(brsrc_t part, int src, int n, float* gw, float* gb, co
       pw[i] = Wt; pm[i] = M; pv[i] = V;
     }
   }
-  if (a.final_wait)
-    xg_final_wait(a, xl.epoch, xl.p->T.flags[me], W, wall_clock64() + a.timeout_ticks, tid, 256);
 }
 
 // conv1 wgrad of (image b, band h) + the two-level reduce; `blk` = 2b + h.  xl: the fused
@@ -333,6 +336,10 @@ inline void launch_conv1_wgrad(const PR& pr, const SubGrid& gr, const float* x, 
 #undef DDL_C1W
 }
 
+template <int BM, int BN, int WM, int WN, int RL, class PB>
+DDL_DEV void xf_group_update(const WgradAdam<PB>& p, int gx, int nelem, int grp, int kxf,
+                             int gcount, XfRef xl);
+
 // conv2's weight-gradient wide reduce with the exchange: block rb sums its elements as
 // wide_reduce_body, stores this rank's gradient (PB's epilogue) and pushes the sums to every
 // rank's slot [par][me] (its own included: the group's last arriver reads them back); the last
@@ -369,21 +376,41 @@ DDL_DEV void xf_reduce_block(const WgradAdam<PB>& p, const float4* __restrict__ 
   }
   const int grp = rb / kxf;
   const int gcount = min(kxf, nrb - grp * kxf);
-  if (!c1w_arrive(&tk[grp], gcount, flag)) return;  // (drains every wave's pushes first)
-  if (!xf_arrive_wait(xl, grp, flag, 100 + grp)) return;  // (error 100 + g: group g's wait)
+  // (c1w_arrive drains every wave's pushes first)
+  if (c1w_arrive(&tk[grp], gcount, flag) && xf_arrive_wait(xl, grp, flag, 100 + grp))
+    xf_group_update<BM, BN, WM, WN, RL, PB>(p, gx, nelem, grp, kxf, gcount, xl);
+  // the step's final wait (every owner bucket's DONE words), one word per thread of the first
+  // reduce blocks, after their group's work: its uncached polls overlap the rest of the launch
+  // instead of trailing conv1's final block (256 threads polling 1152 words: ~5 us)
+  if (a.final_wait)
+    xg_final_wait(a, xl.epoch, xl.p->T.flags[me], W, wall_clock64() + a.timeout_ticks, gid,
+                  nrb * 256);
+}
+
+// The last arriver of reduce group g: every rank's pushes of the group are here; sum them in
+// rank order and apply the update (xf_reduce_block)
+template <int BM, int BN, int WM, int WN, int RL, class PB>
+DDL_DEV void xf_group_update(const WgradAdam<PB>& p, int gx, int nelem, int grp, int kxf,
+                             int gcount, XfRef xl) {
+  const XgmiLaunch& a = xl.p->a;
+  const int W = a.world, me = a.rank, tid = threadIdx.x;
   constexpr int EPB = 256 / RL;  // elements per block
   const int e0 = grp * kxf * EPB;
   const int e1 = min(nelem, (grp * kxf + gcount) * EPB);
   const brsrc_t in = xf_slot(xl, me, 0);
   for (int el = e0 + tid; el < e1; el += 256) {
-    float4 xq[kXgmiMaxPeers];
-#pragma unroll
-    for (int q = 0; q < kXgmiMaxPeers; ++q)
-      if (q < W) xq[q] = bload4_sys(in, (int)(((int64_t)q * a.rslot) * 4) + el * 16);
+    // rank order, as xgmi_repl_kernel, the loads of 4 ranks in flight at a time
     float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q0 = 0; q0 < W; q0 += 4) {
+      float4 xq[4];
 #pragma unroll
-    for (int q = 0; q < kXgmiMaxPeers; ++q)  // rank order, as xgmi_repl_kernel
-      if (q < W) { g.x += xq[q].x; g.y += xq[q].y; g.z += xq[q].z; g.w += xq[q].w; }
+      for (int u = 0; u < 4; ++u)
+        xq[u] = q0 + u < W ? bload4_sys(in, (int)(((int64_t)(q0 + u) * a.rslot) * 4) + el * 16)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (q0 + u < W) { g.x += xq[u].x; g.y += xq[u].y; g.z += xq[u].z; g.w += xq[u].w; }
+    }
     int m0, n;
     wide_elem_coords<BM, BN, WM, WN>(el, gx, m0, n);
     if (n < p.N && m0 < p.M) p.template apply<false>(m0, n, f32x4{g.x, g.y, g.z, g.w});
