@@ -172,6 +172,8 @@ def _simulate(world, kw):
     pytest.param(3, dict(grad_reduce="mean", _env=FUSED_ENV), id="3-fused-last",
                  marks=FUSED_MARK),
     pytest.param(4, dict(_env=FUSED_ENV), id="4-fused-last", marks=FUSED_MARK),
+    pytest.param(8, dict(_env=dict(FUSED_ENV, GPU_MAX_HW_QUEUES="1", DDL_XGMI_TIMEOUT_S="60")),
+                 id="w8-fused-last", marks=FUSED_MARK),
     # control for the row above: the same high-priority comm streams, the separate kernel
     pytest.param(4, dict(_env=dict(DDL_COMM_PRIORITY="high")), id="4-high-separate",
                  marks=FUSED_MARK),
