@@ -126,12 +126,12 @@ def main(argv=None):
     total_steps = n_pre + a.warmup + a.steps
     data = synthetic_mnist()
 
-    def make_trainer(backend, shard=None):
+    def make_trainer(backend, shard=None, native=None):
         cfg = TrainConfig(mode=a.mode, shard=shard or a.shard, steps=total_steps,
                           batch_size=a.batch_size,
                           eval_every=0, engine=a.engine, graph=a.graph and not a.no_graph,
                           overlap=not a.no_overlap, quiet=True, data_sharding="stride",
-                          native_exchange=not a.no_native_exchange,
+                          native_exchange=(not a.no_native_exchange) if native is None else native,
                           force_collectives=a.force_collectives, exchange_backend=backend)
         t = Trainer(cfg, env, dataset=data)
         if a.splits and hasattr(t.engine, "set_splits"):
@@ -158,7 +158,7 @@ def main(argv=None):
         if a.mode == "async":
             if getattr(ex, "backend", "") != "xgmi":
                 return type(ex).__name__
-            svc = getattr(ex, "service_mode", None)  # PS side: device-claim / host service
+            svc = getattr(ex, "service_mode", None)  # PS side: the native host service
             return ("native-" if getattr(ex, "runner", None) is not None else "python-") + \
                 "xgmi-async" + (f" ({svc} service)" if svc else "")
         if not getattr(ex, "native", False):
@@ -184,6 +184,15 @@ def main(argv=None):
         exact) and whether every value is finite."""
         bits = int(p.view(torch.int32).to(torch.int64).sum().item())
         return bits, bool(torch.isfinite(p).all().item())
+
+    def replicas_consistent(t) -> bool:
+        """Sync PS: every worker pulled the same parameters, so the replicas must be bitwise
+        equal on all ranks and finite (collective)."""
+        dg = [digest(t.params)]
+        if world > 1:
+            dg = [None] * world
+            dist.all_gather_object(dg, digest(t.params))
+        return all(d[1] for d in dg) and len({d[0] for d in dg}) == 1
 
     if len(candidates) > 1:
         # short A/B before the benchmark proper (a wait that times out in the xGMI path raises
@@ -228,9 +237,7 @@ def main(argv=None):
                 continue
             ms = max_over_ranks(ms)
             ab[c] = {"ms_per_step": round(ms, 4), "exchange": backend_of(t)}
-            dg = [None] * world
-            dist.all_gather_object(dg, digest(t.params))
-            good = all(d[1] for d in dg) and len({d[0] for d in dg}) == 1
+            good = replicas_consistent(t)
             rel = None
             if ref_params is None:
                 ref_params = (t.params.clone(), p0)
@@ -266,7 +273,21 @@ def main(argv=None):
     handoff = None
     if (a.mode == "sync" and hasattr(tr.exchange, "handoff_check")
             and (world > 1 or a.force_collectives)):
-        handoff = tr.exchange.handoff_check(tr)
+        from ddl_amd.parallel.native_exchange import NativeUnavailable
+        try:
+            handoff = tr.exchange.handoff_check(tr)
+        except NativeUnavailable as e:
+            # the replicas diverged under the reference (event) hand-off on this data plane: it
+            # is refused on every rank (handoff_vote raises everywhere) and the job continues on
+            # the Python exchange (torch.distributed collectives)
+            from ddl_amd.parallel.roles import close_trainers
+            close_trainers([tr], env)
+            keep.remove(tr)
+            handoff = {"handoff": f"data plane '{chosen}' refused: {str(e)[:160]}"}
+            tr = make_trainer(chosen, native=False)
+            keep.append(tr)
+            cfg = tr.cfg
+    replica_check = None
 
     def timed_run(t):
         """prewarm + warmup (untimed), then exactly a.steps steps between barrier+sync pairs;
@@ -278,6 +299,15 @@ def main(argv=None):
         for i in range(n_pre + a.warmup):
             t.train_step(i)
         sync()
+        if a.mode == "sync" and world > 1 and t is tr:
+            # the replicas of a synchronous PS step must be bitwise equal on every rank: checked
+            # for the benchmarked data plane whether it was chosen by the A/B or named explicitly
+            nonlocal replica_check
+            replica_check = replicas_consistent(t)
+            if not replica_check:
+                raise RuntimeError(f"sync replicas diverge across ranks on the "
+                                   f"'{backend_of(t)}' data plane: refusing to benchmark it")
+            sync()
         t0 = time.perf_counter()
         for i in range(n_pre + a.warmup, total_steps):
             t.train_step(i)
@@ -314,10 +344,6 @@ def main(argv=None):
     # the record's facts about the benchmarked trainer, taken before any release below
     engine_name = getattr(tr.engine, "name", a.engine)
     num_ps, policy, exchange_name = tr.num_ps, tr.plan.policy, backend_of(tr)
-    # the replicated last bucket exchanged inside conv1's weight-gradient launch (xGMI runner)
-    runner = getattr(getattr(tr, "exchange", None), "runner", None)
-    last_fused = bool(runner is not None and hasattr(runner, "fused_last_taken")
-                      and runner.fused_last_taken())
     # W > 1 (sync, and async after its exchange joined): close and drop every trainer built so
     # far (collectively, between barriers, nothing in flight) before each time-to-accuracy run —
     # close() releases each runner's comm stream, events, flags and peer mappings, the side-
@@ -333,11 +359,6 @@ def main(argv=None):
         keep.clear()
         gc.collect()
         sync()
-        if os.environ.get("DDL_BENCH_DEBUG"):
-            from ddl_amd.parallel.roles import Trainer as _T
-            alive = sum(isinstance(o, _T) for o in gc.get_objects())
-            print(f"[bench] rank {env.rank}: {alive} trainer(s) alive after release",
-                  file=sys.stderr, flush=True)
 
     if release:
         t = best = tr = None  # noqa: F841 - drop the last references before the collect
@@ -405,7 +426,6 @@ def main(argv=None):
                 "handoff": (handoff["handoff"] if handoff
                             else "n/a (W = 1, local updates)" if world == 1
                             else "n/a (no native runner)"),
-                "last_bucket_in_conv1_launch": last_fused,
             },
             "test_acc_after_run": round(acc, 4),
             "prewarm": {"steps": n_pre, "note": "untimed steps before the warmup steps: the "
@@ -415,6 +435,8 @@ def main(argv=None):
         }
         if handoff:
             rec["handoff_check"] = handoff
+        if replica_check is not None:
+            rec["replicas_bit_identical_before_timing"] = replica_check
         if ab:
             rec["exchange_ab"] = ab
         if plans:

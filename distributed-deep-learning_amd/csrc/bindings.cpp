@@ -72,7 +72,7 @@ class PyEngine {
     TORCH_CHECK((int)c.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " tile configs");
     for (int i = 0; i < ddl::OP_COUNT; ++i) {
       TORCH_CHECK((c[i] >= 0 && c[i] < ddl::NUM_TILE_CFGS) || c[i] == ddl::CFG_KWAVE ||
-                      c[i] == ddl::CFG_MF16 || ddl::dma_cfg((int)c[i]),
+                      c[i] == ddl::CFG_MF16,
                   "tile config out of range");
       e_.cfg[i] = (int)c[i];
     }
@@ -120,19 +120,9 @@ class PyEngine {
   std::vector<int64_t> get_wide() const {
     return std::vector<int64_t>(e_.wide, e_.wide + ddl::OP_COUNT);
   }
-  // per-op split-K block order (gemm.h split_coords; 0..3)
+  // bit op: the dual launch of op's layer dispatches its second problem first
   void set_dual_bfirst(int64_t m) { e_.dual_bfirst = (int)m; }
   int64_t get_dual_bfirst() const { return e_.dual_bfirst; }
-  void set_order(std::vector<int64_t> o) {
-    TORCH_CHECK((int)o.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " orders");
-    for (int i = 0; i < ddl::OP_COUNT; ++i) {
-      TORCH_CHECK(o[i] >= 0 && o[i] <= 3, "block order must be 0..3");
-      e_.order[i] = (int)o[i];
-    }
-  }
-  std::vector<int64_t> get_order() const {
-    return std::vector<int64_t>(e_.order, e_.order + ddl::OP_COUNT);
-  }
 
   void set_keep_prob(double keep) {
     const double rate = 1.0 - keep;
@@ -148,19 +138,6 @@ class PyEngine {
   std::vector<int64_t> get_splits() const {
     return std::vector<int64_t>(e_.splits, e_.splits + ddl::OP_COUNT);
   }
-  // stream-K worker counts per op (0 = split-K by `splits`)
-  void set_workers(std::vector<int64_t> w) {
-    TORCH_CHECK((int)w.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " worker counts");
-    for (int i = 0; i < ddl::OP_COUNT; ++i) {
-      TORCH_CHECK(w[i] >= 0 && w[i] <= (1 << 20), "worker count out of range");
-      e_.workers[i] = (int)w[i];
-    }
-    realloc();
-  }
-  std::vector<int64_t> get_workers() const {
-    return std::vector<int64_t>(e_.workers, e_.workers + ddl::OP_COUNT);
-  }
-
   void forward(at::Tensor x, at::Tensor seed, bool train) {
     check_x(x);
     e_.forward(x.data_ptr<float>(), (int)x.size(0), seed_ptr(seed), train, cur_stream());
@@ -656,8 +633,6 @@ class PyRunner {
   void set_ready_flags(int64_t mode) { r_->set_ready_flags((int)mode); }
   void set_use_tail(bool on) { r_->set_use_tail(on); }
   void set_final_in_reduce(bool on) { r_->set_final_in_reduce(on); }
-  void set_fused_last(bool on) { r_->set_fused_last(on); }
-  bool fused_last_taken() const { return r_->fused_last_taken(); }
   void set_tail_cfg(int64_t first, int64_t f4) { r_->set_tail_cfg((int)first, (int)f4); }
   void step(at::Tensor x, at::Tensor labels, int64_t seed, std::vector<double> lr_t) {
     eng_.check_batch(x);
@@ -743,6 +718,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     ddl::launch_gemm_nomem(out.data_ptr<float>(), (int)M, (int)N, (int)K, (int)splits,
                            slab.data_ptr(), nullptr, cur_stream());
   }, "diagnostic: engine GEMM structure with register-only operand loads");
+  m.def("xcd_sweep", [](at::Tensor a, c10::optional<at::Tensor> want, at::Tensor out) {
+    check_f32_cuda(a, "a");
+    TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kInt && out.numel() >= 2, "out: 2 int32");
+    if (want) {
+      check_f32_cuda(*want, "want");
+      TORCH_CHECK(want->numel() == a.numel(), "want: same size as a");
+    }
+    ddl::launch_xcd_sweep(a.data_ptr<float>(), want ? want->data_ptr<float>() : nullptr,
+                          a.numel(), out.data_ptr<int>(), cur_stream());
+  }, "xGMI self-test probe: every XCD reads (warms) every line of a, or counts mismatches "
+     "against want into out[0]", py::arg("a"), py::arg("want"), py::arg("out"));
   m.attr("OP_COUNT") = (int)ddl::OP_COUNT;
 
   py::class_<PyEngine>(m, "Engine")
@@ -752,8 +738,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_keep_prob", &PyEngine::set_keep_prob)
       .def("set_splits", &PyEngine::set_splits)
       .def("get_splits", &PyEngine::get_splits)
-      .def("set_workers", &PyEngine::set_workers)
-      .def("get_workers", &PyEngine::get_workers)
       .def("set_cfg", &PyEngine::set_cfg)
       .def("get_cfg", &PyEngine::get_cfg)
       .def("set_eval_cfg", &PyEngine::set_eval_cfg)
@@ -768,8 +752,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_wide", &PyEngine::set_wide)
       .def("set_dual_bfirst", &PyEngine::set_dual_bfirst)
       .def("get_dual_bfirst", &PyEngine::get_dual_bfirst)
-      .def("set_order", &PyEngine::set_order)
-      .def("get_order", &PyEngine::get_order)
       .def("get_wide", &PyEngine::get_wide)
       .def("forward", &PyEngine::forward, py::arg("x"), py::arg("seed"), py::arg("train"))
       .def("backward_segment", &PyEngine::backward_segment)
@@ -798,8 +780,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_use_tail", &PyRunner::set_use_tail)
       .def("set_ready_flags", &PyRunner::set_ready_flags)
       .def("set_final_in_reduce", &PyRunner::set_final_in_reduce)
-      .def("set_fused_last", &PyRunner::set_fused_last)
-      .def("fused_last_taken", &PyRunner::fused_last_taken)
       .def("set_tail_cfg", &PyRunner::set_tail_cfg)
       .def("step", &PyRunner::step)
       .def("selftest", &PyRunner::selftest)

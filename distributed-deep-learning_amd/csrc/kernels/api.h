@@ -100,21 +100,8 @@ constexpr int CFG_KWAVE = 13;
 // (gemm.h GemmTile::mainloop_dma16); conv2-4 forward / data gradient / weight gradient only
 // (other ops fall back to config 3)
 constexpr int CFG_MF16 = 14;
-// training: one-wave multi-fragment tiles on the generic LDS-DMA main loop (gemm.h
-// GemmTile::mainloop_dma_g: any operand contiguity, no staging registers); conv2-4 forward /
-// data gradient / weight gradient only (other ops fall back to config 3).  64x32, 32x64, 64x64.
-constexpr int CFG_DMA_64x32 = 16;
-constexpr int CFG_DMA_32x64 = 17;
-constexpr int CFG_DMA_64x64 = 18;
-inline bool dma_g_cfg(int c) { return c >= CFG_DMA_64x32 && c <= CFG_DMA_64x64; }
-// training: the one-wave 32x32 tile on a ring of 3 / 2 LDS-DMA images with the next tiles' DMAs
-// interleaved into the MFMA cluster (gemm.h GemmTile::mainloop_ring); conv2-4 GEMMs only
-constexpr int CFG_RING3 = 19;
-constexpr int CFG_RING2 = 20;
-inline bool ring_cfg(int c) { return c == CFG_RING3 || c == CFG_RING2; }
-inline bool dma_cfg(int c) { return dma_g_cfg(c) || ring_cfg(c); }
-
-struct XgmiLast;  // (xGMI section below)
+// (configs 16-20 — one-wave multi-fragment LDS-DMA tiles and the 32x32 ring tiles — were
+// measured in round 5, never won a launch and were removed: docs/DESIGN.md)
 
 struct Engine {
   const float* P[14] = {};   // parameter tensors v0..v13 (any flat layout)
@@ -124,9 +111,6 @@ struct Engine {
   int splits[OP_COUNT];
   int cfg[OP_COUNT];
   int eval_cfg[OP_COUNT];    // tile configs of the no-split eval forward (train = false)
-  int workers[OP_COUNT];     // > 0: stream-K with this many workers (overrides splits)
-  int order[OP_COUNT];       // split-K block order (gemm.h split_coords: 0 round-robin, 1-3
-                             // XCD-contiguous with K splits / M rows / N tiles grouped)
   int wide_thr = 1;          // default split count above which the separate wide reduce is used
   int wide[OP_COUNT];        // per op: z > wide[op] -> separate wide reduce (mode 2), else the
                              // in-launch last-arriver reduction (mode 1)
@@ -163,13 +147,6 @@ struct Engine {
   // reduce epilogue, the rest as tail blocks of that launch (engine_impl.h dual_then_b).
   // Cleared when taken; the runner launches it as before when it is still pending.
   UpdTail final_upd;
-  // W > 1 over xGMI: the replicated last bucket's exchange (push to every peer, rank-order sum,
-  // the replicated update) fused into that same launch (conv1.h conv1_wgrad_xgmi_kernel), with
-  // final_upd naming the bucket's spans.  Set by the runner for one step; final_xchg_taken tells
-  // it that xgmi_repl_kernel must not run.
-  const XgmiLast* final_xchg = nullptr;      // host copy (the launch's layout checks)
-  const XgmiLast* final_xchg_dev = nullptr;  // device copy (read by the kernel)
-  bool final_xchg_taken = false;
   // eval forward: conv2 on the tap-skipping K map (DDL_EVAL_KMAP2=0: the image-major GEMM)
   bool eval_kmap2 = [] {
     const char* e = getenv("DDL_EVAL_KMAP2");
@@ -295,15 +272,6 @@ struct XgmiLaunch {              // one bucket's kernel arguments
   int run_sl0[kXgmiMaxRuns + 1];
   int64_t rslot;                 // the replicated bucket's inbox slot stride (floats)
 };
-// Floats per (parity, source) slot of the replicated bucket's inbox: the bucket itself, or what
-// the fused last launch exchanges if that is more — conv2's weight-gradient reduce in its tile
-// order (M = 801 rows, N = 64 columns; tiles up to 256 x 128: 1024 x 128) and conv1's 26 x 32
-// (conv1.h conv1_wgrad_xgmi_kernel checks the launch's layout against it).
-constexpr int64_t kXgmiReplFusedSlot = 1024 * 128 + 26 * 32;
-struct XgmiLast {                // the last bucket's exchange inside conv1's weight-gradient launch
-  XgmiTable T;
-  XgmiLaunch a;
-};
 // One bucket of a PeerExchange.  owner < 0: a single plan-buffer range split into W equal chunks,
 // chunk r owned by rank r (the flat plan: reduce-scatter form).  owner >= 0: one PS's exchange
 // unit of a tensor-granular plan (reference none / contiguous / greedy, lpt; or a flat plan with
@@ -321,6 +289,10 @@ struct XgmiUpdate {              // owner-side update of one bucket chunk
   float lr_t = 0.f, c1 = 0.1f, c2 = 0.001f, eps = 1e-8f, lr = 0.f, mu = 0.9f;
   float scale = 1.f, coef = 1.f;
 };
+
+// The xGMI self-test's stale-L2 probe (xgmi.hip): every XCD reads every line of `a` (want null:
+// warms the eight L2s) or counts into out[0] the elements that differ from `want`
+void launch_xcd_sweep(const float* a, const float* want, int64_t n, int* out, hipStream_t st);
 
 class PeerExchange {
  public:
@@ -342,8 +314,6 @@ class PeerExchange {
   // word before publishing anything)
   void launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool final_wait, hipStream_t st,
               bool gated = false);
-  // the replicated bucket's kernel arguments without launching (the fused last launch)
-  void fill_last(uint32_t epoch, const XgmiUpdate& u, bool final_wait, XgmiLast& out) const;
   int error() const;             // nonzero once a wait timed out (1 arrive, 2 done)
   // the runner's READY-gate error word, checked by every bucket kernel before it publishes
   void set_gate_error(const int* w) { gate_err_ = w; }
@@ -392,10 +362,9 @@ class PeerExchange {
 // ---- asynchronous PS over xGMI peer memory (xgmi_async.hip) ----------------------------------
 constexpr int kAsyncMaxPs = 64;
 constexpr int kAsyncMaxSlices = 512;
-// a rank's uncached device flags: [0, kAsyncDense) its DONE words as a worker (dense over all
-// PS' slices), then POSTED[worker][dense slice] as a PS host (what its claim kernel polls)
+// a rank's uncached device flags: its DONE words as a worker (dense over all PS' slices)
 constexpr int kAsyncDense = kAsyncMaxPs * kAsyncMaxSlices;
-constexpr size_t kAsyncFlagWords = (size_t)kAsyncDense * (1 + kXgmiMaxPeers);
+constexpr size_t kAsyncFlagWords = (size_t)kAsyncDense;
 struct AsyncShard {              // one PS's contiguous range of the flat buffer
   int64_t lo, n, slice, inbox_off;
   int host, nslice;
@@ -453,7 +422,6 @@ class AsyncPeer {
   int num_ps() const { return nps_; }
 
  private:
-  friend class AsyncService;     // its claim kernels read the table, flags and error word
   void upload_table();           // table_ -> table_dev_ (set-up only: open, attach_done)
   float* params_;
   const float* grads_;
@@ -482,8 +450,6 @@ struct AsyncPsState {            // one hosted PS as the service thread sees it
   int64_t t;                     // its step counter (advanced once per arrival)
 };
 
-struct ClaimState;               // the device-side service's state (xgmi_async.hip)
-
 class AsyncService {
  public:
   AsyncService(AsyncPeer* peer, int world, int device, const std::vector<AsyncPsState>& ps,
@@ -500,23 +466,12 @@ class AsyncService {
   int64_t served() const;
   // (worker, ps, worker round, PS step) per apply, in service order
   const std::vector<std::array<int64_t, 4>>& provenance() const { return prov_; }
-  // "host": the thread scans the board and launches each apply (default); "device-claim":
-  // pre-enqueued claim + apply kernel pairs pop arrivals on the GPU (DDL_ASYNC_CLAIM=1)
-  const char* mode() const { return claim_ ? "device-claim" : "host"; }
+  // the thread scans the board and launches each apply
+  const char* mode() const { return "host"; }
 
  private:
   void run();
-  void run_claim();
   void serve(AsyncPsState& st, int worker);
-  void free_claim();
-  bool claim_ = false;
-  int depth_ = 3;                // claim pairs in flight on the PS stream
-  double idle_us_ = 500.0;       // a claim kernel with no arrival for this long ends empty
-  ClaimState* cs_dev_ = nullptr;
-  float* lr_tab_ = nullptr;
-  int32_t* prov_dev_ = nullptr;
-  int64_t* host_words_ = nullptr;  // pinned: [0] claim kernels ended, [1] claims, [2] hold,
-                                   // [8 + i] hosted PS i's step counter
   AsyncPeer* peer_;
   int world_, device_;
   std::vector<AsyncPsState> ps_;
@@ -662,7 +617,6 @@ class SyncRunner {
   void set_peer(PeerExchange* p) {
     peer_ = p;
     if (p) p->set_gate_error(ready_err_dev());  // (device memory: read by every bucket wave)
-    if (p) alloc_last();
   }
   int* ready_err_dev() const { return ready_ ? reinterpret_cast<int*>(ready_ + kSegments) : nullptr; }
   // one full exchange of every bucket with w := sum over ranks of g (no optimizer) at the
@@ -749,13 +703,6 @@ class SyncRunner {
   // the GEMM conv1 path as tail blocks of the wide reduce (measured neutral).
   // DDL_FINAL_IN_REDUCE=0: the stand-alone Adam launch
   void set_final_in_reduce(bool on) { final_in_reduce_ = on; }
-  // W > 1 over xGMI: the replicated last bucket exchanged and updated inside conv1's weight-
-  // gradient launch (conv1.h conv1_wgrad_xgmi_kernel) instead of by xgmi_repl_kernel after it.
-  // Opt-in (DDL_XGMI_FUSED_LAST=1): bit-identical and faster on the forced 1-rank rehearsal
-  // (0.2978-0.2990 vs 0.3018-0.3025 ms/step), but with several ranks time-sharing one GPU it
-  // stalled intermittently (W = 4 in the last run) — not root-caused (docs/DESIGN.md round 5)
-  void set_fused_last(bool on) { fused_last_ = on; }
-  bool fused_last_taken() const { return fused_last_taken_; }  // by the previous step
   // tail placement (1: before the GEMM blocks) and float4 per tail block (tuning)
   void set_tail_cfg(int first, int f4_per_block) {
     tail_first_ = first;
@@ -767,21 +714,6 @@ class SyncRunner {
   // block: 373 us/step vs 381 without the tail; before the GEMM blocks 375-378
   int tail_first_ = 0;
   int tail_f4_ = 4 * kTailF4PerBlock;
-  bool fused_last_ = [] {
-    const char* e = getenv("DDL_XGMI_FUSED_LAST");
-    return e && e[0] == '1';
-  }();
-  bool fused_last_taken_ = false;
-  XgmiLast xlast_{};             // the fused launch's exchange arguments (this step's)
-  XgmiLast xlast_up_{};          // what the device copy holds (epoch aside)
-  XgmiLast* xlast_dev_ = nullptr;  // device copy (hipMalloc; rewritten when it changes)
-  XgmiLast* xlast_host_ = nullptr; // its pinned staging copy (hipMemcpyAsync source)
-  bool xlast_up_valid_ = false;
-  void alloc_last();               // the two buffers above (set_peer: never inside a step)
-  // the last segment's XGMI_REPL unit when the fused launch may take it, else null
-  const RunnerUnit* fused_last_unit(bool on_main, hipStream_t st);
-  hipStream_t fused_prio_stream_ = nullptr;
-  bool fused_prio_checked_ = false, fused_prio_ok_ = false;
 };
 
 }  // namespace ddl

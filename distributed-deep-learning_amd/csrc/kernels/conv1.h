@@ -17,7 +17,6 @@
 #pragma once
 #include "gemm.h"
 #include "layers.h"
-#include "xgmi_dev.h"
 
 namespace ddl {
 
@@ -25,10 +24,7 @@ constexpr int kC1wGroup = 8;       // block partials per first-level group
 // staged image row pitch: a half-wave's ds_read_b32 reads one pixel at the 25 tap offsets
 // ky * pitch + kx; pitch 37 (5 mod 32) puts the five tap rows in disjoint bank ranges
 // (pitch 32: 5-way conflicts)
-#ifndef DDL_C1W_PITCH
-#define DDL_C1W_PITCH 37
-#endif
-constexpr int kC1wPitch = DDL_C1W_PITCH;
+constexpr int kC1wPitch = 37;
 constexpr int kC1wLdsBand = 18 * kC1wPitch + 2;  // (+2: keeps the partials 16-B aligned)
 
 // optional optimizer on conv1's weight / bias as the final reduce writes them (the W = 1 tail
@@ -126,121 +122,11 @@ DDL_DEV void c1w_sum(brsrc_t part, int src, int n, brsrc_t out, int dst, float* 
   }
 }
 
-// ---- the replicated last bucket inside this launch (W > 1 over xGMI) ------
-// xgmi.hip xgmi_repl_kernel's exchange without a launch of its own: every rank pushes its
-// gradient of the bucket (conv1 + conv2) to every peer, sums the W contributions in rank order
-// and runs the update on its replicated optimizer state.  Here the pushes leave from the reduce
-// epilogues that produce the gradient, in the reduce's own element order (float4 runs, not the
-// parameter layout's scattered rows), so no partial gradient is re-read and no launch boundary
-// sits between the last reduce and the update.  Inbox slot (parity, source), a.rslot floats:
-//   [0, 4 nelem)                  conv2's weight-gradient reduce elements (wide_reduce order)
-//   [4 nelem, 4 nelem + 832)      conv1's dW_aug [26][32]
-// Same parity / reuse argument and flag words (ARRIVE[bucket][source][j]) as xgmi_repl_kernel;
-// j = reduce group g (kXf blocks) or, for conv1, ngroups.  Only a group's LAST ARRIVER waits,
-// i.e. after every block of its group on this GPU has pushed: no block waits for work of its own
-// launch that may not be resident yet.  Sums and update are bit-identical to xgmi_repl_kernel.
-// The exchange's arguments live in device memory (written by the runner when they change),
-// the step's epoch travels by value: a kernel-argument XgmiLast (~1.2 KB of peer tables indexed
-// per lane) was copied to scratch by every thread.
-struct XfRef {
-  const XgmiLast* p = nullptr;  // device copy; null: no exchange in this launch
-  uint32_t epoch = 0;
-};
-DDL_DEV brsrc_t xf_slot(XfRef x, int r, int src) {
-  const XgmiLaunch& a = x.p->a;
-  const int par = (int)(x.epoch & 1u);
-  // (the descriptor spans slots src .. W-1 of this parity: the sums index slot q from slot 0)
-  return make_rsrc(x.p->T.inbox[r] + a.inbox_off + ((int64_t)par * a.world + src) * a.rslot,
-                   (uint32_t)((a.world - src) * a.rslot * 4));
-}
-DDL_DEV void xf_store1(brsrc_t r, int byte_off, float v) {  // system write-through, 4 B
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, byte_off, 0, 1 | 16);
-}
-DDL_DEV float xf_load1(brsrc_t r, int byte_off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 1 | 16));
-}
-
-// Called by all 256 threads after every push of slice j has drained (a barrier in between):
-// ARRIVE[me][j] at every peer, then wait for every peer's ARRIVE[q][j] here.  false: a wait failed
-// (error word set; the caller then updates nothing, as xgmi_repl_kernel).
-DDL_DEV bool xf_arrive_wait(XfRef x, int j, int* flag, int code) {
-  const XgmiLaunch& a = x.p->a;
-  const int tid = threadIdx.x, W = a.world, me = a.rank;
-  if (tid < W && tid != me) xg_flag_store(x.p->T.flags[tid] + xg_arrive_idx(a.bucket, me, j), x.epoch);
-  if (tid == 0) *flag = 1;
-  __syncthreads();
-  const long long deadline = wall_clock64() + a.timeout_ticks;
-  if (tid < W && tid != me &&
-      !xg_wait_ge(x.p->T.flags[me] + xg_arrive_idx(a.bucket, tid, j), x.epoch, deadline, a.err,
-                  code))
-    *flag = 0;  // (benign race: every writer stores 0)
-  __syncthreads();
-  const bool ok = *flag != 0;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // keep the loads below the poll
-  return ok;
-}
-
-// conv1's final reduce level with the exchange: the summed partials are this rank's gradient
-// (stored to gw / gb as without the exchange), pushed to every peer's slot [par][me]; after the
-// peers' arrive, the W contributions in rank order go through the update.
-DDL_DEV void c1w_sum_xgmi(brsrc_t part, int src, int n, float* gw, float* gb, const C1Adam& ad,
-                          XfRef xl, int off, int j, int* flag) {
-  constexpr int EPT = kC1wEPT;
-  const XgmiLaunch& a = xl.p->a;
-  const int W = a.world, me = a.rank, tid = threadIdx.x;
-  float s[EPT], v[EPT];
-  c1w_accum<32>(part, src, n, s);  // B <= 128: one chunk
-#pragma unroll
-  for (int jj = 0; jj < EPT; ++jj) {
-    const int e = tid + 256 * jj;
-    v[jj] = a.coef != 1.f ? s[jj] * a.coef : s[jj];
-    if (e >= kC1wElems) continue;
-    const bool wrow = e < 25 * 32;
-    (wrow ? gw : gb)[wrow ? e : e - 25 * 32] = s[jj];
-    for (int k = 1; k < W; ++k) xf_store1(xf_slot(xl, (me + k) % W, me), (off + e) * 4, v[jj]);
-  }
-  drain_vmem();
-  __syncthreads();
-  const bool ok = xf_arrive_wait(xl, j, flag, 8);  // (error 8: conv1's ARRIVE wait)
-  if (ok) {
-    const brsrc_t in = xf_slot(xl, me, 0);  // slot (par, q) = this base + q * rslot floats
-#pragma unroll
-    for (int jj = 0; jj < EPT; ++jj) {
-      const int e = tid + 256 * jj;
-      if (e >= kC1wElems) continue;
-      // rank order, as xgmi_repl_kernel, the loads of 4 ranks in flight at a time
-      float g = 0.f;
-      for (int q0 = 0; q0 < W; q0 += 4) {
-        float xq[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int q = q0 + u;
-          xq[u] = q < W && q != me
-                      ? xf_load1(in, (int)(((int64_t)q * a.rslot + off + e) * 4)) : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (q0 + u < W) g += q0 + u == me ? v[jj] : xq[u];
-      }
-      const bool wrow = e < 25 * 32;
-      const int i = wrow ? e : e - 25 * 32;
-      float* pw = wrow ? ad.w_w : ad.b_w;
-      float* pm = wrow ? ad.w_m : ad.b_m;
-      float* pv = wrow ? ad.w_v : ad.b_v;
-      float Wt = pw[i], M = pm[i], V = pv[i];
-      adam1(Wt, g * ad.scale, M, V, ad.lr_t, ad.c1, ad.c2, ad.eps);
-      pw[i] = Wt; pm[i] = M; pv[i] = V;
-    }
-  }
-}
-
-// conv1 wgrad of (image b, band h) + the two-level reduce; `blk` = 2b + h.  xl: the fused
-// exchange (conv1's elements at slot offset xoff, slice index xj), else null
+// conv1 wgrad of (image b, band h) + the two-level reduce; `blk` = 2b + h
 DDL_DEV void conv1_wgrad_block(const float* __restrict__ x, const float* __restrict__ d1, int B,
                                int blk, float* __restrict__ gw, float* __restrict__ gb,
                                float* __restrict__ part, int* __restrict__ tickets, float* lds,
-                               int* flag, const C1Adam& ad, XfRef xl = XfRef(), int xoff = 0,
-                               int xj = 0) {
+                               int* flag, const C1Adam& ad) {
   const int b = blk >> 1, h = blk & 1;
   float* T = lds;                   // [18][kC1wPitch] image band
   float* R = lds + kC1wLdsBand;     // [4 waves][1024] wave partials
@@ -290,8 +176,7 @@ DDL_DEV void conv1_wgrad_block(const float* __restrict__ x, const float* __restr
   if (!c1w_arrive(&tickets[grp], gcount, flag)) return;
   c1w_sum<kC1wGroup>(pr, grp * kC1wGroup, gcount, pr, nblk + grp, nullptr, nullptr);
   if (!c1w_arrive(&tickets[ng], ng, flag)) return;
-  if (xl.p) c1w_sum_xgmi(pr, nblk, ng, gw, gb, ad, xl, xoff, xj, flag);
-  else c1w_sum<32>(pr, nblk, ng, pr, 0, gw, gb, &ad);  // B <= 128: one chunk
+  c1w_sum<32>(pr, nblk, ng, pr, 0, gw, gb, &ad);  // B <= 128: one chunk
 }
 
 // [2B conv1 wgrad blocks] then [conv2 wgrad wide reduce blocks (nrb, 256 threads, RL lanes per
@@ -321,7 +206,7 @@ template <class CR, class PR>
 inline void launch_conv1_wgrad(const PR& pr, const SubGrid& gr, const float* x, const float* d1,
                                int B, float* gw, float* gb, float* part, int* tickets,
                                hipStream_t st, const C1Adam& ad = C1Adam()) {
-  const bool red = !gr.streamk && gr.mode == 2 && gr.nblocks > 0;
+  const bool red = gr.mode == 2 && gr.nblocks > 0;
   using G = TileGeo<CR::BM, CR::BN, CR::WM, CR::WN>;
   const int ntiles = gr.gx * gr.gy, z = gr.gz;
   const size_t nelem = red ? (size_t)ntiles * G::PART4 : 0;
@@ -336,138 +221,9 @@ inline void launch_conv1_wgrad(const PR& pr, const SubGrid& gr, const float* x, 
 #undef DDL_C1W
 }
 
-template <int BM, int BN, int WM, int WN, int RL, class PB>
-DDL_DEV void xf_group_update(const WgradAdam<PB>& p, int gx, int nelem, int grp, int kxf,
-                             int gcount, XfRef xl);
-
-// conv2's weight-gradient wide reduce with the exchange: block rb sums its elements as
-// wide_reduce_body, stores this rank's gradient (PB's epilogue) and pushes the sums to every
-// rank's slot [par][me] (its own included: the group's last arriver reads them back); the last
-// arriver of group g (blocks [g kXf, g kXf + kXf)) then runs the group's exchange and update.
-template <int BM, int BN, int WM, int WN, int RL, class PB>
-DDL_DEV void xf_reduce_block(const WgradAdam<PB>& p, const float4* __restrict__ slab, int S,
-                             int gx, int ntiles, int rb, int nrb, int kxf, int* tk, int* flag,
-                             XfRef xl) {
-  using G = TileGeo<BM, BN, WM, WN>;
-  const XgmiLaunch& a = xl.p->a;
-  const int W = a.world, me = a.rank, tid = threadIdx.x;
-  const int nelem = ntiles * G::PART4;
-  const int gid = rb * 256 + tid;
-  const int elem = gid / RL, sub = gid % RL;
-  const bool valid = elem < nelem;
-  const int e = valid ? elem : 0;
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  const size_t zstride = (size_t)ntiles * G::PART4;
-  for (int z = sub; z < S; z += RL) {
-    const float4 t = slab[z * zstride + e];
-    s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
-  }
-  s.x = group_sum<RL>(s.x);  // (every lane of the wave is active: as wide_reduce_body)
-  s.y = group_sum<RL>(s.y);
-  s.z = group_sum<RL>(s.z);
-  s.w = group_sum<RL>(s.w);
-  if (valid && sub == 0) {
-    int m0, n;
-    wide_elem_coords<BM, BN, WM, WN>(e, gx, m0, n);
-    if (n < p.N && m0 < p.M) static_cast<const PB&>(p).epi(m0, n, f32x4{s.x, s.y, s.z, s.w});
-    float4 v = s;
-    if (a.coef != 1.f) { v.x *= a.coef; v.y *= a.coef; v.z *= a.coef; v.w *= a.coef; }
-    for (int k = 0; k < W; ++k) bstore4_sys(xf_slot(xl, (me + k) % W, me), e * 16, v);
-  }
-  const int grp = rb / kxf;
-  const int gcount = min(kxf, nrb - grp * kxf);
-  // (c1w_arrive drains every wave's pushes first)
-  if (c1w_arrive(&tk[grp], gcount, flag) && xf_arrive_wait(xl, grp, flag, 100 + grp))
-    xf_group_update<BM, BN, WM, WN, RL, PB>(p, gx, nelem, grp, kxf, gcount, xl);
-  // the step's final wait (every owner bucket's DONE words), one word per thread of the first
-  // reduce blocks, after their group's work: its uncached polls overlap the rest of the launch
-  // instead of trailing conv1's final block (256 threads polling 1152 words: ~5 us)
-  if (a.final_wait)
-    xg_final_wait(a, xl.epoch, xl.p->T.flags[me], W, wall_clock64() + a.timeout_ticks, gid,
-                  nrb * 256);
-}
-
-// The last arriver of reduce group g: every rank's pushes of the group are here; sum them in
-// rank order and apply the update (xf_reduce_block)
-template <int BM, int BN, int WM, int WN, int RL, class PB>
-DDL_DEV void xf_group_update(const WgradAdam<PB>& p, int gx, int nelem, int grp, int kxf,
-                             int gcount, XfRef xl) {
-  const XgmiLaunch& a = xl.p->a;
-  const int W = a.world, me = a.rank, tid = threadIdx.x;
-  constexpr int EPB = 256 / RL;  // elements per block
-  const int e0 = grp * kxf * EPB;
-  const int e1 = min(nelem, (grp * kxf + gcount) * EPB);
-  const brsrc_t in = xf_slot(xl, me, 0);
-  for (int el = e0 + tid; el < e1; el += 256) {
-    // rank order, as xgmi_repl_kernel, the loads of 4 ranks in flight at a time
-    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int q0 = 0; q0 < W; q0 += 4) {
-      float4 xq[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        xq[u] = q0 + u < W ? bload4_sys(in, (int)(((int64_t)(q0 + u) * a.rslot) * 4) + el * 16)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (q0 + u < W) { g.x += xq[u].x; g.y += xq[u].y; g.z += xq[u].z; g.w += xq[u].w; }
-    }
-    int m0, n;
-    wide_elem_coords<BM, BN, WM, WN>(el, gx, m0, n);
-    if (n < p.N && m0 < p.M) p.template apply<false>(m0, n, f32x4{g.x, g.y, g.z, g.w});
-  }
-}
-
-// [2B conv1 wgrad blocks, exchange fused] then [conv2 wgrad wide-reduce blocks, exchange fused]
-template <int BM, int BN, int WM, int WN, int RL, class PB>
-__global__ void __launch_bounds__(256)
-conv1_wgrad_xgmi_kernel(WgradAdam<PB> pr, const float4* __restrict__ rslab, int S, int rgx,
-                        int rntiles, int nrb, int kxf, const float* __restrict__ x,
-                        const float* __restrict__ d1, int B, float* __restrict__ gw,
-                        float* __restrict__ gb, float* __restrict__ part,
-                        int* __restrict__ tickets, C1Adam ad, XfRef xl) {
-  __shared__ float lds[kC1wLdsBand + 4 * 1024];
-  __shared__ int flag;
-  using G = TileGeo<BM, BN, WM, WN>;
-  const int nc = 2 * B;
-  const int nrg = (nrb + kxf - 1) / kxf;
-  if ((int)blockIdx.x < nc) {
-    conv1_wgrad_block(x, d1, B, (int)blockIdx.x, gw, gb, part, tickets, lds, &flag, ad, xl,
-                      4 * rntiles * G::PART4, nrg);
-    return;
-  }
-  xf_reduce_block<BM, BN, WM, WN, RL, PB>(pr, rslab, S, rgx, rntiles, (int)blockIdx.x - nc, nrb,
-                                          kxf, tickets + c1w_groups(B) + 1, &flag, xl);
-}
-
-// The fused launch (conv1 wgrad + conv2's pending mode-2 reduce + the last bucket's exchange and
-// replicated update); false (nothing launched) when its layout does not fit the exchange's
-// slot, flag or ticket space — the caller then takes the unfused path.
-template <class CR, class PB>
-inline bool launch_conv1_wgrad_xgmi(const WgradAdam<PB>& pr, const SubGrid& gr, const float* x,
-                                    const float* d1, int B, float* gw, float* gb, float* part,
-                                    int* tickets, int max_tickets, hipStream_t st,
-                                    const C1Adam& ad, const XgmiLast& xl,
-                                    const XgmiLast* xl_dev) {
-  if (gr.streamk || gr.mode != 2 || gr.nblocks <= 0 || !ad.on) return false;
-  using G = TileGeo<CR::BM, CR::BN, CR::WM, CR::WN>;
-  const int ntiles = gr.gx * gr.gy, z = gr.gz;
-  const int64_t nelem = (int64_t)ntiles * G::PART4;
-  const int RL = z > 32 ? 64 : (z > 4 ? 16 : 4);
-  const int nrb = (int)((nelem * RL + 255) / 256);
-  const int kxf = (nrb + 63) / 64 > 8 ? (nrb + 63) / 64 : 8;  // <= 64 groups: <= 64 waiting blocks per rank
-  const int nrg = (nrb + kxf - 1) / kxf;
-  if (!xl_dev || 4 * nelem + kC1wElems > xl.a.rslot || nrg + 1 > kXgmiMaxSlices ||
-      c1w_groups(B) + 1 + nrg > max_tickets || xl.a.world < 1 || xl.a.world > kXgmiMaxPeers)
-    return false;
-#define DDL_C1WX(RLV)                                                                         \
-  DDL_LAUNCH((conv1_wgrad_xgmi_kernel<CR::BM, CR::BN, CR::WM, CR::WN, RLV, PB>),             \
-             dim3(nrb + 2 * B), dim3(256), 0, st, pr, gr.slab, z, gr.gx, ntiles, nrb, kxf, x,   \
-             d1, B, gw, gb, part, tickets, ad, XfRef{xl_dev, xl.a.epoch})
-  if (RL == 64) DDL_C1WX(64);
-  else if (RL == 16) DDL_C1WX(16);
-  else DDL_C1WX(4);
-#undef DDL_C1WX
-  return true;
-}
+// (Round 5's opt-in fused last bucket — the W > 1 xGMI exchange of conv1 + conv2 inside this
+// launch — stalled intermittently with several ranks on one card, cause not established, and
+// was removed in round 6: docs/DESIGN.md.  The replicated bucket runs xgmi.hip's
+// xgmi_repl_kernel.)
 
 }  // namespace ddl

@@ -23,10 +23,7 @@ constexpr int kC1Rows = 18;                      // staged input rows per band
 // staged row pitch: 28 + 2 + 2 columns used; 48 = 16 mod 32, so the two image rows a half-wave's
 // ds_read_b32 touches (a 2x2 pool window spans rows y, y + 1) fall in disjoint bank halves
 // (ds_read_b32 serves 32 lanes at a time, bank = dword mod 32; pitch 32 put them 2-way)
-#ifndef DDL_C1_PITCH
-#define DDL_C1_PITCH 48
-#endif
-constexpr int kC1Pitch = DDL_C1_PITCH;
+constexpr int kC1Pitch = 48;
 constexpr int kC1Windows = 7 * 14;               // pool windows per band
 constexpr int kC1Tiles = (kC1Windows + 7) / 8;   // 32-row MFMA tiles per band (13)
 

@@ -19,7 +19,7 @@
 namespace ddl {
 
 Engine::Engine() {
-  // {tile config, split-K, stream-K workers} per op: whole-step coordinate-descent tune
+  // {tile config, split-K} per op: whole-step coordinate-descent tune
   // (scripts/step_tune.py over the scripts/op_bench.py per-op sweep) on one MI355X, batch 100,
   // single-stream backward with dual dgrad+wgrad launches: fwd+bwd 367 us (was 449 us)
   // (round 2, after the halo layout and the batch-minor weight-gradient enumeration: conv2
@@ -50,7 +50,6 @@ Engine::Engine() {
   // 3 / 3 / 6 instead of 2 / 4 / 8, 302.5 -> 299.0 us fwd+bwd, scripts/sched_ab.py
   // --splits-variants, profiles/r3_sched_ab_ldsdma.log)
   static const int defs[OP_COUNT] = {1, 3, 3, 6, 8, 16, 4, 1, 4, 1, 4, 8, 8, 12, 4, 32, 1024};
-  static const int defw[OP_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
   static const bool inl[OP_COUNT] = {0, 1, 1, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0};
   memcpy(cfg, defc, sizeof(defc));
@@ -67,8 +66,6 @@ Engine::Engine() {
   eval_cfg[OP_CONV3_FWD] = 0;
   eval_cfg[OP_CONV4_FWD] = 0;
   memcpy(splits, defs, sizeof(defs));
-  memcpy(workers, defw, sizeof(defw));
-  memset(order, 0, sizeof(order));
   for (int op = 0; op < OP_COUNT; ++op) wide[op] = inl[op] ? (1 << 20) : 1;
 }
 
@@ -120,26 +117,21 @@ void Engine::op_shape(int op, int B, int* M, int* N, int* K) {
 #define TILE_7 64, 32, 32, 2, 1   // 2 waves of 32x32 along M
 #define TILE_8 32, 64, 32, 1, 2   // 2 waves of 32x32 along N
 
-static size_t slab_need(int c, int M, int N, int K, int s, int w) {
+static size_t slab_need(int c, int M, int N, int K, int s) {
   switch (c) {
     // reduces in LDS; an op without a K-wave instantiation falls back to the 32x32 split-K
     // launch with the same split factor (engine_impl.h launch_cfg), so size for that
-    case CFG_KWAVE: return gemm_slab_f4<TILE_3>(M, N, K, s, w);
-    case CFG_MF16: return gemm_slab_f4<TILE_3>(M, N, K, s, w);  // same 32x32 partial layout
-    // the generic LDS-DMA tiles: the partial layouts of the one-wave tiles of their size
-    case CFG_DMA_64x32: return gemm_slab_f4<TILE_2>(M, N, K, s, w);
-    case CFG_DMA_32x64: return gemm_slab_f4<TILE_4>(M, N, K, s, w);
-    case CFG_DMA_64x64: return gemm_slab_f4<TILE_0>(M, N, K, s, w);
-    case CFG_RING3: case CFG_RING2: return gemm_slab_f4<TILE_3>(M, N, K, s, w);
-    case 0: return gemm_slab_f4<TILE_0>(M, N, K, s, w);
-    case 1: return gemm_slab_f4<TILE_1>(M, N, K, s, w);
-    case 2: return gemm_slab_f4<TILE_2>(M, N, K, s, w);
-    case 3: return gemm_slab_f4<TILE_3>(M, N, K, s, w);
-    case 4: return gemm_slab_f4<TILE_4>(M, N, K, s, w);
-    case 5: return gemm_slab_f4<TILE_5>(M, N, K, s, w);
-    case 6: return gemm_slab_f4<TILE_6>(M, N, K, s, w);
-    case 7: return gemm_slab_f4<TILE_7>(M, N, K, s, w);
-    default: return gemm_slab_f4<TILE_8>(M, N, K, s, w);
+    case CFG_KWAVE: return gemm_slab_f4<TILE_3>(M, N, K, s);
+    case CFG_MF16: return gemm_slab_f4<TILE_3>(M, N, K, s);  // same 32x32 partial layout
+    case 0: return gemm_slab_f4<TILE_0>(M, N, K, s);
+    case 1: return gemm_slab_f4<TILE_1>(M, N, K, s);
+    case 2: return gemm_slab_f4<TILE_2>(M, N, K, s);
+    case 3: return gemm_slab_f4<TILE_3>(M, N, K, s);
+    case 4: return gemm_slab_f4<TILE_4>(M, N, K, s);
+    case 5: return gemm_slab_f4<TILE_5>(M, N, K, s);
+    case 6: return gemm_slab_f4<TILE_6>(M, N, K, s);
+    case 7: return gemm_slab_f4<TILE_7>(M, N, K, s);
+    default: return gemm_slab_f4<TILE_8>(M, N, K, s);
   }
 }
 
@@ -148,7 +140,7 @@ size_t Engine::slab_floats_needed(int B) const {
   for (int op = 0; op < OP_COUNT; ++op) {
     int M, N, K;
     op_shape(op, B, &M, &N, &K);
-    const size_t f = 4 * slab_need(cfg[op], M, N, K, splits[op], workers[op]);
+    const size_t f = 4 * slab_need(cfg[op], M, N, K, splits[op]);
     if (f > mx) mx = f;
   }
   return mx;

@@ -31,17 +31,10 @@ namespace ddl {
 #define TILE_12 128, 128, 32, 4, 1
 // training: one-wave 32x32x32 on 16x16x4 MFMAs with LDS-DMA staging (CFG_MF16)
 #define TILE_14 32, 32, 32, 1, 1, 1
-// training: one-wave multi-fragment tiles on the generic LDS-DMA loop (CFG_DMA_*)
-#define TILE_16 64, 32, 32, 1, 1, 2
-#define TILE_17 32, 64, 32, 1, 1, 2
-#define TILE_18 64, 64, 32, 1, 1, 2
-// training: one-wave 32x32 on a ring of 3 / 2 LDS-DMA images (CFG_RING3 / CFG_RING2)
-#define TILE_19 32, 32, 32, 1, 1, 3
-#define TILE_20 32, 32, 32, 1, 1, 4
 
 template <class P>
-inline void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const SplitScratch& sc,
-                       hipStream_t st, int o = 0) {
+inline void launch_cfg(int c, const P& p, int s, int wide_thr, const SplitScratch& sc,
+                       hipStream_t st) {
   if (c == CFG_KWAVE) {
     if constexpr (KWaveOK<P>::value) {
       launch_gemm_kwave<32>(p, s < 0 ? -s : s, st);
@@ -51,38 +44,21 @@ inline void launch_cfg(int c, const P& p, int s, int w, int wide_thr, const Spli
   }
   if (c == CFG_MF16) {
     if constexpr (Mf16OK<P>::value) {
-      launch_gemm<TILE_14>(p, s, wide_thr, sc, st, w, o);
-      return;
-    }
-    c = 3;
-  }
-  if (ring_cfg(c)) {
-    if constexpr (DmaOK<P>::value) {
-      if (c == CFG_RING3) launch_gemm<TILE_19>(p, s, wide_thr, sc, st, w, o);
-      else launch_gemm<TILE_20>(p, s, wide_thr, sc, st, w, o);
-      return;
-    }
-    c = 3;
-  }
-  if (dma_g_cfg(c)) {
-    if constexpr (DmaOK<P>::value) {
-      if (c == CFG_DMA_64x32) launch_gemm<TILE_16>(p, s, wide_thr, sc, st, w, o);
-      else if (c == CFG_DMA_32x64) launch_gemm<TILE_17>(p, s, wide_thr, sc, st, w, o);
-      else launch_gemm<TILE_18>(p, s, wide_thr, sc, st, w, o);
+      launch_gemm<TILE_14>(p, s, wide_thr, sc, st);
       return;
     }
     c = 3;
   }
   switch (c) {
-    case 0: launch_gemm<TILE_0>(p, s, wide_thr, sc, st, w, o); break;
-    case 1: launch_gemm<TILE_1>(p, s, wide_thr, sc, st, w, o); break;
-    case 2: launch_gemm<TILE_2>(p, s, wide_thr, sc, st, w, o); break;
-    case 3: launch_gemm<TILE_3>(p, s, wide_thr, sc, st, w, o); break;
-    case 4: launch_gemm<TILE_4>(p, s, wide_thr, sc, st, w, o); break;
-    case 5: launch_gemm<TILE_5>(p, s, wide_thr, sc, st, w, o); break;
-    case 6: launch_gemm<TILE_6>(p, s, wide_thr, sc, st, w, o); break;
-    case 7: launch_gemm<TILE_7>(p, s, wide_thr, sc, st, w, o); break;
-    default: launch_gemm<TILE_8>(p, s, wide_thr, sc, st, w, o); break;
+    case 0: launch_gemm<TILE_0>(p, s, wide_thr, sc, st); break;
+    case 1: launch_gemm<TILE_1>(p, s, wide_thr, sc, st); break;
+    case 2: launch_gemm<TILE_2>(p, s, wide_thr, sc, st); break;
+    case 3: launch_gemm<TILE_3>(p, s, wide_thr, sc, st); break;
+    case 4: launch_gemm<TILE_4>(p, s, wide_thr, sc, st); break;
+    case 5: launch_gemm<TILE_5>(p, s, wide_thr, sc, st); break;
+    case 6: launch_gemm<TILE_6>(p, s, wide_thr, sc, st); break;
+    case 7: launch_gemm<TILE_7>(p, s, wide_thr, sc, st); break;
+    default: launch_gemm<TILE_8>(p, s, wide_thr, sc, st); break;
   }
 }
 
@@ -149,73 +125,49 @@ void run_op_inst(Engine& e, const float* x, int B, const uint32_t* seed, bool tr
     // eval: conv2 on the tap-skipping K map (group-major rows), one-wave 64x64 tiles
     if (!train && e.eval_kmap2 && e.eval_cfg[OP] == 0) {
       const ConvFwd<14, 32, 64, true> pk{p.M, p.N, p.K, p.x, p.w, p.bias, p.out, p.code};
-      launch_gemm<TILE_0>(pk, 1, 1, e.scratch[si], st, 0);
+      launch_gemm<TILE_0>(pk, 1, 1, e.scratch[si], st);
       return;
     }
   }
   if constexpr (OP == OP_CONV2_FWD || OP == OP_CONV3_FWD || OP == OP_CONV4_FWD) {
     if (!train && e.eval_cfg[OP] >= NUM_TILE_CFGS) {  // eval-only large tiles, no split
       switch (e.eval_cfg[OP]) {
-        case 9: launch_gemm<TILE_9>(p, 1, 1, e.scratch[si], st, 0); break;
-        case 10: launch_gemm<TILE_10>(p, 1, 1, e.scratch[si], st, 0); break;
-        case 11: launch_gemm<TILE_11>(p, 1, 1, e.scratch[si], st, 0); break;
-        default: launch_gemm<TILE_12>(p, 1, 1, e.scratch[si], st, 0); break;
+        case 9: launch_gemm<TILE_9>(p, 1, 1, e.scratch[si], st); break;
+        case 10: launch_gemm<TILE_10>(p, 1, 1, e.scratch[si], st); break;
+        case 11: launch_gemm<TILE_11>(p, 1, 1, e.scratch[si], st); break;
+        default: launch_gemm<TILE_12>(p, 1, 1, e.scratch[si], st); break;
       }
       return;
     }
   }
-  launch_cfg(train ? e.cfg[OP] : e.eval_cfg[OP], p, train ? e.splits[OP] : 1,
-             train ? e.workers[OP] : 0, e.wide[OP],
-             e.scratch[si], st, train ? e.order[OP] : 0);
+  launch_cfg(train ? e.cfg[OP] : e.eval_cfg[OP], p, train ? e.splits[OP] : 1, e.wide[OP],
+             e.scratch[si], st);
 }
 
 // ---- dual launches: data- and weight-gradient GEMM of one layer in one kernel -----------------
-// dual launches are instantiated for the one-wave configs: 32x32 (3), 32x32 BK 16 pipelined (5),
-// the 16x16x4 tile (CFG_MF16) and the generic LDS-DMA tiles (CFG_DMA_*; the register-staged
-// one-wave 64x64 / 32x64 tiles, 180-230 VGPRs, never won a dual launch in the real-step tuner)
-inline bool one_wave_cfg(int c) { return c == 3 || c == 5 || c == CFG_MF16 || dma_cfg(c); }
+// dual launches are instantiated for the one-wave configs: 32x32 (3), 32x32 BK 16 pipelined (5)
+// and the 16x16x4 tile (CFG_MF16) (the register-staged one-wave 64x64 / 32x64 tiles, 180-230
+// VGPRs, never won a dual launch in the real-step tuner)
+inline bool one_wave_cfg(int c) { return c == 3 || c == 5 || c == CFG_MF16; }
 
 template <int C> struct CfgOf;
 template <> struct CfgOf<3> { using T = TileCfg<TILE_3>; };
 template <> struct CfgOf<5> { using T = TileCfg<TILE_5>; };
 template <> struct CfgOf<CFG_MF16> { using T = TileCfg<TILE_14>; };
-template <> struct CfgOf<CFG_DMA_64x32> { using T = TileCfg<TILE_16>; };
-template <> struct CfgOf<CFG_DMA_32x64> { using T = TileCfg<TILE_17>; };
-template <> struct CfgOf<CFG_DMA_64x64> { using T = TileCfg<TILE_18>; };
-template <> struct CfgOf<CFG_RING3> { using T = TileCfg<TILE_19>; };
-template <> struct CfgOf<CFG_RING2> { using T = TileCfg<TILE_20>; };
 template <int C> using IC = std::integral_constant<int, C>;
 
 // f(IC<c'>) for the one-wave config c' that op policy P runs for run-time config c (configs P
-// has no instantiation for fall back to 3; anything but 5 / MF16 / DMA likewise)
+// has no instantiation for fall back to 3; anything but 5 / MF16 likewise)
 template <class P, class F>
 inline void with_one_wave_cfg(int c, F&& f) {
   if constexpr (Mf16OK<P>::value) {
     if (c == CFG_MF16) return f(IC<CFG_MF16>{});
   }
-  if constexpr (DmaOK<P>::value) {
-    if (c == CFG_DMA_64x32) return f(IC<CFG_DMA_64x32>{});
-    if (c == CFG_DMA_32x64) return f(IC<CFG_DMA_32x64>{});
-    if (c == CFG_DMA_64x64) return f(IC<CFG_DMA_64x64>{});
-    if (c == CFG_RING3) return f(IC<CFG_RING3>{});
-    if (c == CFG_RING2) return f(IC<CFG_RING2>{});
-  }
   if (c == 5) return f(IC<5>{});
   f(IC<3>{});
 }
-// the dual pairings that are instantiated: every pairing of the register-staged / 16x16x4
-// configs, every pairing of the DMA tiles with each other and with 3 / 5 (not DMA x MF16)
-constexpr bool dual_pair_ok(int a, int b) {
-  // the ring tiles pair with each other and with 3 / 5; the multi-fragment DMA tiles likewise;
-  // the two families do not mix
-  const bool ra = a == CFG_RING3 || a == CFG_RING2, rb = b == CFG_RING3 || b == CFG_RING2;
-  const bool ga = a >= CFG_DMA_64x32 && a <= CFG_DMA_64x64;
-  const bool gb = b >= CFG_DMA_64x32 && b <= CFG_DMA_64x64;
-  if ((ra && gb) || (ga && rb)) return false;
-  if ((ra || ga) && b == CFG_MF16) return false;
-  if ((rb || gb) && (a == CFG_MF16 || a == 5)) return false;
-  return true;
-}
+// every pairing of the one-wave configs is instantiated
+constexpr bool dual_pair_ok(int, int) { return true; }
 
 // fc3's weight gradient as aux blocks (head.h), pending after the fused head kernel
 inline HeadWgradAux head_aux(Engine& e, int B) {
@@ -244,10 +196,9 @@ inline void run_back_to_back(Engine& e, const float* x, int B, const uint32_t* s
 template <class CA, class CB, int OA, int OB, class PA, class PB>
 inline void dual_b(Engine& e, const PA& pa, const PB& pb, int B, hipStream_t st) {
   auto go = [&](const auto& aux) {
-    launch_gemm_dual<CA, PA, CB, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA],
-                                     pb, e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB],
-                                     st, aux, nullptr, e.dual_order(OA), e.order[OA],
-                                     e.order[OB]);
+    launch_gemm_dual<CA, PA, CB, PB>(pa, e.splits[OA], e.scratch[0], e.wide[OA], pb,
+                                     e.splits[OB], e.scratch[1], e.wide[OB], st, aux, nullptr,
+                                     e.dual_order(OA));
   };
   // the fc2 dual carries fc3's weight gradient; the others a pending optimizer tail
   if constexpr (OA == OP_FC2_DGRAD) {
@@ -434,10 +385,9 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
   using PN = std::decay_t<decltype(pn)>;
   using CN = TileCfg<TILE_3>;
   SubGrid gb;
-  launch_gemm_dual<CA, PA, CB, PB>(pa, e.splits[OA], e.workers[OA], e.scratch[0], e.wide[OA], pb,
-                                   e.splits[OB], e.workers[OB], e.scratch[1], e.wide[OB], st,
-                                   TailAux(e.tail), &gb, e.dual_order(OA), e.order[OA],
-                                   e.order[OB]);
+  launch_gemm_dual<CA, PA, CB, PB>(pa, e.splits[OA], e.scratch[0], e.wide[OA], pb,
+                                   e.splits[OB], e.scratch[1], e.wide[OB], st, TailAux(e.tail),
+                                   &gb, e.dual_order(OA));
   e.tail = UpdTail();
   constexpr bool kFinal = ON == OP_CONV1_WGRAD;
   if constexpr (kFinal) {
@@ -446,35 +396,11 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
     // or in its own reduce before this point)
     const bool direct =
         e.conv1_wgrad_direct && conv1_wgrad_direct_ok(B, e.slab_floats, e.scratch[0].max_tiles);
-    if (e.final_xchg) {
-      // W > 1 over xGMI: the replicated last bucket's exchange and update in this launch
-      // (conv1.h conv1_wgrad_xgmi_kernel); anything else leaves both to the runner's
-      // xgmi_repl_kernel — never to the local-update paths below
-      const XgmiLast& xl = *e.final_xchg;
-      const UpdTail fu = e.final_upd;
-      e.final_xchg = nullptr;  // (xl stays valid: the runner owns it)
-      e.final_upd = UpdTail();
-      if (direct) {
-        float* part = static_cast<float*>(e.scratch[0].slab);
-        WgradAdam<PB> pa;
-        C1Adam ad;
-        if (fu.npieces > 0 && final_split_conv12(e, fu, pb, pa, ad) &&
-            launch_conv1_wgrad_xgmi<CB, PB>(pa, gb, x, e.d1, B, e.G[0], e.G[1], part,
-                                            e.scratch[0].tickets, e.scratch[0].max_tiles, st, ad,
-                                            xl, e.final_xchg_dev)) {
-          e.final_xchg_taken = true;
-          return;
-        }
-        launch_conv1_wgrad<CB, PB>(pb, gb, x, e.d1, B, e.G[0], e.G[1], part,
-                                   e.scratch[0].tickets, st);
-        return;
-      }
-    }
     if (direct) {
       float* part = static_cast<float*>(e.scratch[0].slab);
       // the last segment's update (W = 1 tail path) inside this launch: conv2's in its weight-
       // gradient reduce epilogue, conv1's in the final reduce level; no Adam launch follows
-      if (e.final_upd.npieces > 0 && !gb.streamk && gb.mode == 2) {
+      if (e.final_upd.npieces > 0 && gb.mode == 2) {
         WgradAdam<PB> pa;
         C1Adam ad;
         if (final_split_conv12(e, e.final_upd, pb, pa, ad)) {
@@ -491,8 +417,8 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
   }
   const bool fin = kFinal && e.final_upd.npieces > 0;
   SubGrid gn;
-  if (!launch_reduce_with_gemm<CB, PB, CN, PN>(pb, gb, pn, e.splits[ON], e.workers[ON],
-                                               e.wide[ON], e.scratch[0], st,
+  if (!launch_reduce_with_gemm<CB, PB, CN, PN>(pb, gb, pn, e.splits[ON], e.wide[ON],
+                                               e.scratch[0], st,
                                                fin ? &gn : nullptr)) {
     launch_reduce<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB>(pb, gb, st);
     e.run_op(ON, x, B, seed, true, st, 0);
@@ -518,9 +444,8 @@ void dual_then_b(Engine& e, const float* x, int B, const uint32_t* seed, hipStre
 template <int OA, int OB, int ON>
 void run_dual_then_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
   const int ca = e.cfg[OA], cb = e.cfg[OB];
-  if (!e.dual || (ca != 3 && ca != CFG_MF16 && !dma_cfg(ca)) ||
-      (cb != 3 && cb != 5 && cb != CFG_MF16 && !dma_cfg(cb)) || e.cfg[ON] != 3 ||
-      e.workers[ON] > 0) {
+  if (!e.dual || (ca != 3 && ca != CFG_MF16) || (cb != 3 && cb != 5 && cb != CFG_MF16) ||
+      e.cfg[ON] != 3) {
     run_dual_inst<OA, OB>(e, x, B, seed, st);
     e.run_op(ON, x, B, seed, true, st, 0);
     return;

@@ -18,12 +18,11 @@ template void run_dual_inst<OP_FC1_DGRAD, OP_FC1_WGRAD>(Engine&, const float*, i
 
 bool run_fc2_deferred(Engine& e, const float* x, int B, const uint32_t* seed, hipStream_t st) {
   e.fc2_slab = nullptr;
-  if (e.cfg[OP_FC2_FWD] != 3 || e.workers[OP_FC2_FWD] != 0) return false;
+  if (e.cfg[OP_FC2_FWD] != 3) return false;
   const auto p = make_policy<OP_FC2_FWD>(e, B, x, seed, true);
   SubGrid g;
-  launch_gemm<TILE_3>(p, e.splits[OP_FC2_FWD], e.wide[OP_FC2_FWD], e.scratch[0], st, 0,
-                      e.order[OP_FC2_FWD], &g);
-  if (g.nblocks > 0 && !g.streamk && g.mode == 2) {
+  launch_gemm<TILE_3>(p, e.splits[OP_FC2_FWD], e.wide[OP_FC2_FWD], e.scratch[0], st, &g);
+  if (g.nblocks > 0 && g.mode == 2) {
     if (g.gz > 32) {  // (the head replicates the 4- and 16-lane reduce orders only)
       launch_reduce<TILE_3>(p, g, st);
       return true;

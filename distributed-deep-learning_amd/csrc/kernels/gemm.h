@@ -27,9 +27,7 @@
 //   MN-contiguous operand -> [BK][mn+4]  ds_read_b32; the two 32-lane halves read rows
 //                                        4 apart (separate conflict groups)
 //
-// Two drivers share the per-tile main loop / epilogue (GemmTile):
-// Stream-K (gemm_streamk_kernel): W one-block workers split the (tile, K-tile) iteration
-//   space evenly; partial boundary tiles are reduced in-launch by their last contributor.
+// The split-K driver runs the per-tile main loop / epilogue (GemmTile):
 // Split-K (gridDim.z = S > 1), deterministic, no float atomics:
 //   mode 1: every split stores its fp32 partial fragments (float4 per lane, coalesced,
 //     write-through sc1) and takes an arrival ticket; the last arriver of a tile sums the S
@@ -69,11 +67,8 @@ DDL_DEV void push_tail_body(const UpdTail& t, const UpdPiece& P, int b) {
     for (int i = lane; i < cnt; i += 64) bstore4_sys(dst, i * 16, src[i]);
     drain_vmem();
   }
-  if (lane == 0) {
+  if (lane == 0)
     __hip_atomic_store(P.posted + j, t.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    // the PS host's device copy of the word: what its claim kernel polls (xgmi_async.hip)
-    __hip_atomic_store(P.arrive + j, t.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
 }
 
 // One optimizer-tail block (tail.h): kTailF4PerLane float4 of one piece per lane, all loads
@@ -142,8 +137,8 @@ struct TileGeo {
 // its K range: `KWin kwin(m_lo, m_hi)` describes the rows' useful K sub-space (for a SAME
 // conv: the 5x5 taps that land inside the image for some row of the tile), `kvlen(win)` is its
 // length and the loaders take a *virtual* k (0 .. kvlen) plus the window: loadA(info, kv, win).
-// Split-K divides each tile's virtual length (balanced per tile); stream-K (uniform K per
-// tile) uses `kfull()`, the identity window.  Anything a window keeps beyond the useful set
+// Split-K divides each tile's virtual length (balanced per tile).  Anything a window keeps
+// beyond the useful set
 // reads zeros (halo layout), so a window only has to be a superset.
 template <class P, class = void>
 struct KMapOf {
@@ -202,25 +197,17 @@ struct GemmTile {
   // 16x16x4 MFMA + LDS-DMA one-wave tile (variant 1; instantiated only for policies with the
   // 16-byte gathers srcA / srcB: layers.h Mf16OK)
   static constexpr bool DMA16 = V == 1 && SOLO && BM == 32 && BN == 32 && BK == 32;
-  // generic one-wave LDS-DMA tile (variant 2, mainloop_dma_g): TM x TN <= 2 x 2 fragments, any
-  // operand contiguity (the conv data / weight gradients: K- / MN-contiguous pairs)
-  static constexpr bool DMA_G = V == 2 && SOLO && BK == 32 && TM <= 2 && TN <= 2;
-  // one-wave 32x32 tile on a RING of LDS-DMA images (variants 3 / 4: 3 / 2 stages), the next
-  // tiles' DMAs interleaved into the current tile's MFMA cluster (mainloop_ring)
-  static constexpr int RING = (V == 3) ? 3 : (V == 4 ? 2 : 0);
-  static constexpr bool DMA_R = RING > 0 && SOLO && BM == 32 && BN == 32 && BK == 32;
-  static_assert(V == 0 || DMA16 || DMA_G || DMA_R,
-                "variant 1 is the one-wave 32x32x32 tile, variant 2 a one-wave <= 64x64 tile, "
-                "variants 3 / 4 the one-wave 32x32 ring tiles");
+  // (variants 2-4 — generic multi-fragment LDS-DMA tiles and 32x32 rings of 2 / 3 LDS-DMA
+  // images — lost to these loops in every launch and were removed: docs/DESIGN.md round 5)
+  static_assert(V == 0 || DMA16, "variant 1 is the one-wave 32x32x32 16x16x4 tile");
   // LDS-DMA staging (mainloop_dma): unpadded 32x32 images, swizzled through the gather
   // addresses (the DMA writes lane-linearly), one image of A + B per block
   static constexpr bool DMA = V == 0 && HasDma<P>::value && SOLO && TM * TN == 1 && BM == 32 &&
                               BN == 32 && BK == 32;
   static constexpr bool DMA_MF = V == 0 && HasDma<P>::value && SOLO && TM * TN > 1 && BN == 64 &&
                                  BK == 32 && AK && !BKC && !HasOnesA<P>::value;
-  static constexpr int LDS_F4 = DMA_R ? 512 * RING
-                                : (DMA16 || DMA) ? 512
-                                : (DMA_MF || DMA_G) ? (BM * BK + BK * BN) / 4
+  static constexpr int LDS_F4 = (DMA16 || DMA) ? 512
+                                : DMA_MF ? (BM * BK + BK * BN) / 4
                                 : (NBUF * (A_ELEMS + B_ELEMS)) / 4;
   // A wave with a single 32x32 fragment alternates two accumulator chains (summed at the
   // end) so consecutive MFMAs are independent (one chain: measured 0.3050 -> 0.3070 ms/step)
@@ -245,9 +232,7 @@ struct GemmTile {
   // [kb, ke) is virtual (window w) for K-map policies
   static DDL_DEV void mainloop(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
                                f32x16 (&acc)[TM][TN], const Win& w = Win()) {
-    if constexpr (DMA_R) mainloop_ring(p, m_blk, n_blk, kb, ke, lds, acc, w);
-    else if constexpr (DMA_G) mainloop_dma_g(p, m_blk, n_blk, kb, ke, lds, acc, w);
-    else if constexpr (DMA16) mainloop_dma16(p, m_blk, n_blk, kb, ke, lds, acc, w);
+    if constexpr (DMA16) mainloop_dma16(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else if constexpr (DMA) mainloop_dma(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else if constexpr (DMA_MF) mainloop_dma_mf(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else if constexpr (PIPE) mainloop_pipe(p, m_blk, n_blk, kb, ke, lds, acc, w);
@@ -739,256 +724,6 @@ struct GemmTile {
     }
   }
 
-  // One-wave 32x32 tile on a ring of RING LDS-DMA images (variants 3 / 4).  Per-block
-  // timestamps of the real step (scripts/stamp_report.py) put a one-wave K tile at 1.2-1.9 us
-  // against 0.44 us of MFMA work, with only 1.3-2.5 waves resident per SIMD (the launches at
-  // batch 100 are too small to fill more): the loop is latency-bound per wave, and more waves
-  // cannot be had.  So one wave hides its own latency:
-  //  * tile kt + RING - 1 is DMA'd into the image that tile kt - 1 used (its fragments are in
-  //    registers since the previous iteration), issued INSIDE tile kt's MFMA cluster — one
-  //    1-KB DMA after every second MFMA, in the issue gaps of the 64-cycle 32x32x2 MFMAs
-  //    (sched_barrier pins the interleave; issued before the cluster they cost ~60-185 cycles
-  //    each of the wave's time, guide "LDS-DMA piece issue cost");
-  //  * a tile has RING - 1 MFMA clusters of cover before it is read (3 stages: 2 tiles,
-  //    ~2 us at the measured per-tile rates, 24 KB of LDS; 2 stages: 1 tile, 16 KB).
-  // Images, swizzles, the ones-row patch and the MFMA order are mainloop_dma's: same bits.
-  static DDL_DEV void mainloop_ring(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
-                                    f32x16 (&acc)[TM][TN], const Win& w) {
-    static_assert(FA == 4 && FB == 4 && R == 4, "32x32x32 one-wave tile");
-    static_assert(!(HasOnesA<P>::value && AK), "ones-row patch: MN-contiguous A");
-    constexpr int NS = RING;
-    const int lane = threadIdx.x & 63;
-    const int lr = lane & 31, lh = lane >> 5;
-    const int nk = (ke - kb + BK - 1) / BK;
-    typename P::AInfo ai[4];
-    typename P::BInfo bi[4];
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int sl = it * 64 + lane, row = sl >> 3, q = sl & 7;
-      if constexpr (AK) ai[it] = p.prepA(m_blk + row, (q ^ ((row >> 1) & 7)) * 4);
-      else ai[it] = p.prepA(m_blk + q * 4, row ^ ((row >> 2) & 1));
-      if constexpr (BKC) bi[it] = p.prepB(n_blk + row, (q ^ ((row >> 1) & 7)) * 4);
-      else bi[it] = p.prepB(n_blk + q * 4, row ^ ((row >> 2) & 1));
-    }
-    const uint32_t base = lds_addr(lds);
-    // DMA instruction `it` (0-3: A, 4-7: B) of the tile at k0 into stage st
-    auto dma_one = [&](int k0, int st, int it) {
-      const uint32_t img = base + st * 8192;
-      if (it < 4) dma16(srcA(p, ai[it], k0, w), img + it * 1024);
-      else dma16(srcB(p, bi[it - 4], k0, w), img + 4096 + (it - 4) * 1024);
-    };
-    auto patch = [&](int st, int k0) {
-      if constexpr (HasOnesA<P>::value) {
-#pragma unroll
-        for (int it = 0; it < 4; ++it)
-          if (p.ones_group(ai[it])) lds[st * 2048 + (it * 64 + lane) * 4] = p.ones_value(ai[it], k0, w);
-      }
-    };
-    auto rd = [&](int st, float (&av)[R][4], float (&bv)[R][4]) {
-      const float* As = lds + st * 2048;
-      const float* Bs = As + 1024;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int q = (2 * r + lh) ^ ((lr >> 1) & 7);
-        if constexpr (AK) {
-          const float4 t = *reinterpret_cast<const float4*>(As + lr * 32 + q * 4);
-          av[r][0] = t.x; av[r][1] = t.y; av[r][2] = t.z; av[r][3] = t.w;
-        } else {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) av[r][s] = As[((8 * r + 4 * lh + s) ^ lh) * 32 + lr];
-        }
-        if constexpr (BKC) {
-          const float4 u = *reinterpret_cast<const float4*>(Bs + lr * 32 + q * 4);
-          bv[r][0] = u.x; bv[r][1] = u.y; bv[r][2] = u.z; bv[r][3] = u.w;
-        } else {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) bv[r][s] = Bs[((8 * r + 4 * lh + s) ^ lh) * 32 + lr];
-        }
-      }
-    };
-    f32x16 acc2;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      acc2[q] = 0.f;
-      acc[0][0][q] = 0.f;
-    }
-    if (nk > 0) {
-#pragma unroll
-      for (int s = 0; s < NS - 1; ++s)
-        if (s < nk)
-#pragma unroll
-          for (int it = 0; it < 8; ++it) dma_one(kb + s * BK, s, it);
-      int st = 0;                // stage of tile kt
-      int pst = NS - 1;          // stage of tile kt + NS - 1
-      for (int kt = 0; kt < nk; ++kt) {
-        // tile kt has landed (3 stages: tile kt + 1's 8 DMAs may still be in flight)
-        if (NS == 3 && kt + 1 < nk) vm_wait<8>();
-        else vm_wait<0>();
-        patch(st, kb + kt * BK);
-        float a0[R][4], b0[R][4];
-        rd(st, a0, b0);
-        lgkm_wait0();
-        const bool pf = kt + NS - 1 < nk;
-        const int k1 = kb + (kt + NS - 1) * BK;
-        __builtin_amdgcn_sched_barrier(0);
-#if DDL_MFMA_PRIO
-        __builtin_amdgcn_s_setprio(1);
-#endif
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            if (s & 1) acc2 = mfma32x32x2(a0[r][s], b0[r][s], acc2);
-            else acc[0][0] = mfma32x32x2(a0[r][s], b0[r][s], acc[0][0]);
-            if (s & 1) {
-              __builtin_amdgcn_sched_barrier(0);
-              if (pf) dma_one(k1, pst, 2 * r + (s >> 1));
-              __builtin_amdgcn_sched_barrier(0);
-            }
-          }
-#if DDL_MFMA_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
-        st = st + 1 == NS ? 0 : st + 1;
-        pst = pst + 1 == NS ? 0 : pst + 1;
-      }
-    }
-    acc[0][0] += acc2;
-  }
-
-  // Generic one-wave LDS-DMA loop (variant 2; VERDICT r4 item 1: more MFMA work per staged byte
-  // for the conv backward).  A TM x TN-fragment tile (BM, BN = 32 or 64) stages each 32-deep K
-  // tile straight into one unpadded image per operand, BM/8 + BN/8 one-KB DMA instructions and no
-  // staging registers, for 16 TM TN MFMAs: a 64x32 tile moves 0.75x, a 64x64 tile 0.5x the bytes
-  // per MFMA of the 32x32 one, and its longer MFMA cluster (32 / 64 MFMAs) covers the next tile's
-  // DMA latency at fewer waves per SIMD.
-  //  * K-contiguous operand: image [rows][32 k], quad q of row r at quad q ^ ((r >> 1) & 7) (the
-  //    16 lanes of a ds_read_b128 group then hit 16 distinct bank groups), as mainloop_dma;
-  //  * MN-contiguous operand: image [32 k][BM or BN], read with ds_read_b32 (each 32-lane half of
-  //    a read covers 32 consecutive floats of one k-row: conflict-free without a swizzle).
-  // A's rows that are not in memory (HasOnesA: the weight gradients' ones row) arrive as zeros
-  // and are patched in the image once the tile has landed.  MFMA order as mainloop_basic (two
-  // accumulator chains for a single fragment).
-  static DDL_DEV void mainloop_dma_g(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
-                                     f32x16 (&acc)[TM][TN], const Win& w) {
-    static_assert(!(HasOnesA<P>::value && AK), "ones-row patch: MN-contiguous A");
-    constexpr int NDA = BM / 8, NDB = BN / 8;  // 1 KB DMAs per K tile
-    constexpr int QA = BM / 4, QB = BN / 4;    // quads per k-row of an MN-contiguous image
-    const int lane = threadIdx.x & 63;
-    const int lr = lane & 31, lh = lane >> 5;
-    const int nk = (ke - kb + BK - 1) / BK;
-    typename P::AInfo ai[NDA];
-    typename P::BInfo bi[NDB];
-#pragma unroll
-    for (int it = 0; it < NDA; ++it) {
-      const int sl = it * 64 + lane;
-      if constexpr (AK) {
-        const int row = sl >> 3;
-        ai[it] = p.prepA(m_blk + row, ((sl & 7) ^ ((row >> 1) & 7)) * 4);
-      } else {
-        ai[it] = p.prepA(m_blk + (sl % QA) * 4, sl / QA);
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < NDB; ++it) {
-      const int sl = it * 64 + lane;
-      if constexpr (BKC) {
-        const int row = sl >> 3;
-        bi[it] = p.prepB(n_blk + row, ((sl & 7) ^ ((row >> 1) & 7)) * 4);
-      } else {
-        bi[it] = p.prepB(n_blk + (sl % QB) * 4, sl / QB);
-      }
-    }
-    auto patch = [&](int k0) {
-      if constexpr (HasOnesA<P>::value) {
-#pragma unroll
-        for (int it = 0; it < NDA; ++it)
-          if (p.ones_group(ai[it])) lds[(it * 64 + lane) * 4] = p.ones_value(ai[it], k0, w);
-      }
-    };
-    const uint32_t base = lds_addr(lds);
-    auto dma = [&](int k0) {
-#pragma unroll
-      for (int it = 0; it < NDA; ++it) dma16(srcA(p, ai[it], k0, w), base + it * 1024);
-#pragma unroll
-      for (int it = 0; it < NDB; ++it)
-        dma16(srcB(p, bi[it], k0, w), base + BM * BK * 4 + it * 1024);
-    };
-    const float* As = lds;
-    const float* Bs = lds + BM * BK;
-    float av[R][TM][4], bv[R][TN][4];
-    auto rd = [&]() {
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int row = i * 32 + lr;
-          if constexpr (AK) {
-            const int q = (2 * r + lh) ^ ((row >> 1) & 7);
-            const float4 t = *reinterpret_cast<const float4*>(As + row * BK + q * 4);
-            av[r][i][0] = t.x; av[r][i][1] = t.y; av[r][i][2] = t.z; av[r][i][3] = t.w;
-          } else {
-#pragma unroll
-            for (int s = 0; s < 4; ++s) av[r][i][s] = As[(8 * r + 4 * lh + s) * BM + row];
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = j * 32 + lr;
-          if constexpr (BKC) {
-            const int q = (2 * r + lh) ^ ((col >> 1) & 7);
-            const float4 t = *reinterpret_cast<const float4*>(Bs + col * BK + q * 4);
-            bv[r][j][0] = t.x; bv[r][j][1] = t.y; bv[r][j][2] = t.z; bv[r][j][3] = t.w;
-          } else {
-#pragma unroll
-            for (int s = 0; s < 4; ++s) bv[r][j][s] = Bs[(8 * r + 4 * lh + s) * BN + col];
-          }
-        }
-      }
-    };
-    f32x16 acc2;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc2[q] = 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
-    if (nk > 0) {
-      dma(kb);
-      for (int kt = 0; kt < nk; ++kt) {
-        vm_wait<0>();   // tile kt is in the image
-        patch(kb + kt * BK);
-        rd();
-        lgkm_wait0();   // its fragments are in registers: the image may be restaged
-        if (kt + 1 < nk) dma(kb + (kt + 1) * BK);
-#if DDL_MFMA_PRIO
-        __builtin_amdgcn_s_setprio(1);
-#endif
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            if constexpr (NCH == 2) {
-              if (s & 1) acc2 = mfma32x32x2(av[r][0][s], bv[r][0][s], acc2);
-              else acc[0][0] = mfma32x32x2(av[r][0][s], bv[r][0][s], acc[0][0]);
-            } else {
-#pragma unroll
-              for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                  acc[i][j] = mfma32x32x2(av[r][i][s], bv[r][j][s], acc[i][j]);
-            }
-          }
-#if DDL_MFMA_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
-      }
-    }
-    if constexpr (NCH == 2) acc[0][0] += acc2;
-  }
-
   static DDL_DEV void mainloop_basic(const P& p, int m_blk, int n_blk, int kb, int ke,
                                      float* lds, f32x16 (&acc)[TM][TN], const Win& w) {
     float* const As0 = lds;
@@ -1201,10 +936,8 @@ struct GemmTile {
   // to zero() + one add_partial per z) with the loads of ZB partials in flight per round: one
   // add_partial per z waits a full sc1-load latency per partial, so a 12-way split's last
   // arriver spent ~12 load round trips in its epilogue — the longest block of the launch.
-#ifndef DDL_SPLITK_ZB
-#define DDL_SPLITK_ZB 4  // partials in flight per round for a one-fragment tile (1: the old chain)
-#endif
-  static constexpr int ZB = TM * TN >= DDL_SPLITK_ZB ? 1 : DDL_SPLITK_ZB / (TM * TN);
+  static constexpr int kZB = 4;  // partials in flight per round for a one-fragment tile
+  static constexpr int ZB = TM * TN >= kZB ? 1 : kZB / (TM * TN);
   static DDL_DEV void sum_partials(brsrc_t slab, size_t base0, size_t zstride, int gz,
                                    f32x16 (&acc)[TM][TN]) {
     zero(acc);
@@ -1275,7 +1008,7 @@ struct GemmTile {
 
 // ---- drivers ------------------------------------------------------------------------------
 // Each driver is a device-function body over a *virtual* block id, so a kernel can host one
-// problem (gemm_f32_kernel / gemm_streamk_kernel) or two independent problems side by side
+// problem (gemm_f32_kernel) or two independent problems side by side
 // (gemm_dual_kernel: the data- and weight-gradient GEMMs of one layer in ONE launch — their
 // concurrency without a second stream, whose cross-queue event waits cost tens of us).
 // `lds` is the block's staging array (>= GemmTile::LDS_F4 float4), `flag` one int of LDS.
@@ -1322,239 +1055,49 @@ DDL_DEV int splitk_body(const P& p, int kchunk, int mode, float4* __restrict__ s
   return nkt;
 }
 
-// Stream-K (balanced persistent schedule).  The iteration space is I = tiles * KI
-// (KI = K tiles of BK per output tile), tiles ordered m-fastest.  Worker w of the W
-// one-block workers owns iterations [w*I/W, (w+1)*I/W): every SIMD gets the same MFMA work
-// (+-1 K tile) whatever the tile count, instead of whole tiles/splits quantised over the
-// 1024 SIMDs.  A worker finishes whole tiles with the fused epilogue directly; its first and
-// last tile may be partial: those partials go to slab slot (w, 0|1) and the last of the
-// tile's contributors sums them in worker order (deterministic) and runs the epilogue — the
-// split-K reduction happens inside the same launch, with no separate reduce kernel.
-// Workers are numbered XCD-major (hardware dispatches block b to XCD b % 8), so the
-// neighbours that share a boundary tile, and adjacent tiles' operands, stay in one L2.
-template <int BM, int BN, int BK, int WM, int WN, class P, int V = 0>
-DDL_DEV void streamk_body(const P& p, int KI, int gx, long long I, float4* __restrict__ slab,
-                          int* __restrict__ tickets, int bid, int W, float* lds, int* flag) {
-  using T = GemmTile<BM, BN, BK, WM, WN, P, V>;
-  using G = typename T::G;
-  const int w = (bid & 7) * (W >> 3) + (bid >> 3);  // W % 8 == 0 (host)
-  const brsrc_t sr = make_rsrc(slab, (uint32_t)W * 2u * G::PART4 * 16u);
-  auto first_iter = [&](int ww) -> long long { return (long long)ww * I / W; };
-  // worker owning iteration x: the largest ww with first_iter(ww) <= x
-  auto owner = [&](long long x) -> int { return (int)(((x + 1) * W + I - 1) / I) - 1; };
-  long long it = first_iter(w);
-  const long long end = first_iter(w + 1);
-  const int start_tile = (int)(it / KI);
-  f32x16 acc[T::TM][T::TN];
-  typename T::Win win{};
-  if constexpr (T::KM) win = p.kfull();  // stream-K needs the same K per tile
-  while (it < end) {
-    const int tile = (int)(it / KI);
-    const int klo = (int)(it - (long long)tile * KI);
-    const int khi = (int)min((long long)KI, (long long)klo + (end - it));
-    const int m_blk = (tile % gx) * BM, n_blk = (tile / gx) * BN;
-    T::mainloop(p, m_blk, n_blk, klo * BK, min(p.K, khi * BK), lds, acc, win);
-    it += khi - klo;
-    if (klo == 0 && khi == KI) {
-      T::epilogue(p, m_blk, n_blk, acc);
-      continue;
-    }
-    const int slot = (tile == start_tile) ? 0 : 1;
-    T::store_partial(sr, ((size_t)w * 2 + slot) * G::PART4, acc);
-    const long long t0 = (long long)tile * KI;
-    const int wf = owner(t0), wl = owner(t0 + KI - 1);
-    if (!T::arrive(&tickets[tile], wl - wf + 1, flag)) continue;
-    T::zero(acc);
-    for (int ww = wf; ww <= wl; ++ww) {
-      const int s = (first_iter(ww) / KI == tile) ? 0 : 1;
-      T::add_partial(sr, ((size_t)ww * 2 + s) * G::PART4, acc);
-    }
-    T::epilogue(p, m_blk, n_blk, acc);
-  }
-}
-
-// K-mapped stream-K: prefix sums of the per-row-tile K-tile counts ride in the SubGrid (kernel
-// arguments), for up to this many row tiles (the tap-skipping conv GEMMs have <= 163)
-constexpr int kKmapTiles = 176;
-
 // Launch geometry of one GEMM problem under its schedule (host-computed, passed by value).
+// (Stream-K schedules — uniform and over the tap-window K maps — won conv launches in rounds
+// 1-2 and lost every one to split-K after the tap windows and dual launches; the stream-K body
+// also raised the dual kernels' register count, 120 -> 132 = 4 -> 3 waves per SIMD, and was
+// removed in round 6: docs/DESIGN.md.)
 struct SubGrid {
   int nblocks = 0;   // blocks (virtual ids 0..nblocks-1)
-  int streamk = 0;   // 1: stream-K with W = nblocks workers
   int gx = 1, gy = 1, gz = 1;
   int kchunk = 0, mode = 0;  // split-K
-  int KI = 0;                // stream-K
-  long long I = 0;
   float4* slab = nullptr;
   int* tickets = nullptr;
-  int order = 0;             // split-K block order (split_coords)
-  // stream-K over the K MAP (policies with tap windows): row tile bx owns iterations
-  // [kpre[bx], kpre[bx + 1]) of each column of tiles, kpre[gx] per column
-  int kmap = 0;
-  unsigned short kpre[kKmapTiles + 1];
 #if DDL_STAMPS
   unsigned long long* stamps = nullptr;  // diagnostic build: per-block timestamps (stamps.h)
 #endif
 };
 
-// Split-K block orders.  The hardware deals a launch's blocks round-robin over the 8 XCDs
-// (block b on XCD b % 8), each with its own 4 MB L2; in order 0 every XCD therefore sees the
-// whole operand footprint of a launch (the conv backward duals: 60-69 % L2 hits on 20 MB of
-// maps, profiles/r4_pmc_l2_hits.txt).  Orders 1-3 first renumber the sub-grid's blocks so the
-// blocks of one XCD get a contiguous range of logical ids (xcd_local), then decompose that id
-// with the locality axis slowest:
-//   0: bx fastest, then by, then bz, no renumbering (round-robin: the XCDs interleave tiles)
-//   1: (bx, by) fastest, bz slowest, XCD-contiguous: one XCD runs a contiguous range of K
-//      splits — the weight gradients (K = positions x images: a split is a band of the maps)
-//   2: bz fastest, then by, bx slowest, XCD-contiguous: one XCD runs a contiguous band of M
-//      rows with all its splits and N tiles — the data gradients (rows = pixels of the maps)
-//   3: by fastest, then bx, bz slowest, XCD-contiguous: the N tiles that read one A row band
-//      run back to back on one XCD (A from that L2 after the first)
-// The partial slab and tickets are indexed by (tile, z), so every order gives the same bits.
-DDL_DEV int xcd_local(int vb, int n, int off) {
-  const int c = (vb + off) & 7;          // this block's XCD class
-  const int q = n >> 3, r = n & 7;       // residues < r of vb have q + 1 members, the rest q
-  int before = 0;                        // blocks of the classes c' < c
-#pragma unroll
-  for (int c2 = 0; c2 < 8; ++c2)
-    if (c2 < c) before += q + (((c2 - off) & 7) < r ? 1 : 0);
-  return before + (vb >> 3);
+// virtual block vb -> (bx, by, bz): bx fastest, then by, then bz.  The hardware deals a launch's
+// blocks round-robin over the 8 XCDs; XCD-contiguous renumberings (each XCD's L2 holding a band
+// of the maps) measured +0.2 to +13 us/step and were removed (docs/DESIGN.md rounds 2 and 5)
+DDL_DEV void split_coords(const SubGrid& g, int vb, int& bx, int& by, int& bz) {
+  bx = vb % g.gx;
+  const int t = vb / g.gx;
+  by = t % g.gy;
+  bz = t / g.gy;
 }
 
-DDL_DEV void split_coords(const SubGrid& g, int vb, int off, int& bx, int& by, int& bz) {
-  if (g.order == 0) {
-    bx = vb % g.gx;
-    const int t = vb / g.gx;
-    by = t % g.gy;
-    bz = t / g.gy;
-    return;
-  }
-  const int L = xcd_local(vb, g.nblocks, off);
-  if (g.order == 1) {
-    bx = L % g.gx;
-    const int t = L / g.gx;
-    by = t % g.gy;
-    bz = t / g.gy;
-  } else if (g.order == 2) {
-    bz = L % g.gz;
-    const int t = L / g.gz;
-    by = t % g.gy;
-    bx = t / g.gy;
-  } else {
-    by = L % g.gy;
-    const int t = L / g.gy;
-    bx = t % g.gx;
-    bz = t / g.gx;
-  }
-}
-
-// Stream-K over the K map (per-block timestamps of the split-K launches,
-// scripts/stamp_report.py, show every block resident from the launch's first microsecond and the
-// launch lasting as long as its LONGEST block — 1.5-2x the median: tap windows give the split-K
-// blocks of centre tiles up to 1.7x the K tiles of corner ones).  The iteration space is each
-// tile's own virtual K range (its tap window, the policy's K map), concatenated: row tile bx of
-// tile column by owns iterations by * T + [kpre[bx], kpre[bx + 1]), T = kpre[gx].  W one-block
-// workers split it evenly, so every SIMD gets the same MFMA work (+-1 K tile) AND no worker
-// multiplies the zeros of a halo tap — the uniform stream-K (streamk_body) runs every tile over
-// the full K, the split-K schedule only the window but unbalanced.  Partial boundary tiles are
-// reduced in-launch by their last contributor, in worker order (deterministic), as streamk_body.
+// Split-K blocks keep the hardware's round-robin XCD placement (block b on XCD b % 8): with
+// tap windows the per-tile cost depends on the position, and contiguous ranges would hand one
+// XCD all the heavy centre tiles (docs/DESIGN.md).
 template <int BM, int BN, int BK, int WM, int WN, class P, int V = 0>
-DDL_DEV void streamk_kmap_body(const P& p, const SubGrid& g, int bid, float* lds, int* flag) {
-  using T = GemmTile<BM, BN, BK, WM, WN, P, V>;
-  using G = typename T::G;
-  static_assert(T::KM, "K-mapped stream-K needs a policy with a K map");
-  const int W = g.nblocks;
-  const int w = (bid & 7) * (W >> 3) + (bid >> 3);  // XCD-major, W % 8 == 0 (host)
-  const int TK = g.kpre[g.gx];                      // iterations per tile column
-  const long long I = (long long)TK * g.gy;
-  const brsrc_t sr = make_rsrc(g.slab, (uint32_t)W * 2u * G::PART4 * 16u);
-  auto first_iter = [&](int ww) -> long long { return (long long)ww * I / W; };
-  auto owner = [&](long long x) -> int { return (int)(((x + 1) * W + I - 1) / I) - 1; };
-  // row tile of iteration r of a column: the largest bx with kpre[bx] <= r (binary search over
-  // the scalar kernel-argument table)
-  auto row_of = [&](int r) -> int {
-    int lo = 0, hi = g.gx - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if ((int)g.kpre[mid] <= r) lo = mid;
-      else hi = mid - 1;
-    }
-    return lo;
-  };
-  auto tile_of = [&](long long x) -> int {
-    const int by = (int)(x / TK);
-    return by * g.gx + row_of((int)(x - (long long)by * TK));
-  };
-  long long it = first_iter(w);
-  const long long end = first_iter(w + 1);
-  const int start_tile = it < end ? tile_of(it) : -1;
-  f32x16 acc[T::TM][T::TN];
-  while (it < end) {
-    const int by = (int)(it / TK);
-    const int r = (int)(it - (long long)by * TK);
-    const int bx = row_of(r);
-    const int k0 = g.kpre[bx], KI = (int)g.kpre[bx + 1] - k0;
-    const int klo = r - k0;
-    const int khi = (int)min((long long)KI, (long long)klo + (end - it));
-    const int m_blk = bx * BM, n_blk = by * BN;
-    const typename T::Win win = p.kwin(m_blk, min(p.M, m_blk + BM));
-    T::mainloop(p, m_blk, n_blk, klo * BK, min(p.kvlen(win), khi * BK), lds, acc, win);
-    it += khi - klo;
-    if (klo == 0 && khi == KI) {
-      T::epilogue(p, m_blk, n_blk, acc);
-      continue;
-    }
-    const int tile = by * g.gx + bx;
-    const int slot = (tile == start_tile) ? 0 : 1;
-    T::store_partial(sr, ((size_t)w * 2 + slot) * G::PART4, acc);
-    const long long t0 = (long long)by * TK + k0;
-    const int wf = owner(t0), wl = owner(t0 + KI - 1);
-    if (!T::arrive(&g.tickets[tile], wl - wf + 1, flag)) continue;
-    T::zero(acc);
-    for (int ww = wf; ww <= wl; ++ww) {
-      const int s = (tile_of(first_iter(ww)) == tile) ? 0 : 1;
-      T::add_partial(sr, ((size_t)ww * 2 + s) * G::PART4, acc);
-    }
-    T::epilogue(p, m_blk, n_blk, acc);
-  }
-}
-
-// Split-K blocks keep the hardware's round-robin XCD placement (block b on XCD b % 8): an
-// XCD-contiguous numbering (each XCD's L2 holding its eighth of the maps) measured 0.318 ->
-// 0.331 ms/step — with tap windows the per-tile cost depends on the position and contiguous
-// ranges hand one XCD all the heavy centre tiles (docs/DESIGN.md).
-// SK = false: no stream-K body in the kernel (its register count would set the launch's
-// occupancy even when the split-K body runs; the dual launch's 16x16x4 sub-problems)
-template <int BM, int BN, int BK, int WM, int WN, class P, int V = 0, bool SK = true>
 DDL_DEV void run_sub(const P& p, const SubGrid& g, int vb, float* lds, int* flag) {
-  if (SK && g.streamk) {
+  int bx, by, bz;
+  split_coords(g, vb, bx, by, bz);
 #if DDL_STAMPS
-    const Stamp st0 = stamp_now();
-    const int nkt = (int)((long long)(vb + 1) * g.I / g.nblocks - (long long)vb * g.I / g.nblocks);
+  const Stamp st0 = stamp_now();
 #endif
-    if constexpr (KMapOf<P>::value) {
-      if (g.kmap) streamk_kmap_body<BM, BN, BK, WM, WN, P, V>(p, g, vb, lds, flag);
-    }
-    if (!g.kmap)
-      streamk_body<BM, BN, BK, WM, WN, P, V>(p, g.KI, g.gx, g.I, g.slab, g.tickets, vb,
-                                             g.nblocks, lds, flag);
+  const int nkt = splitk_body<BM, BN, BK, WM, WN, P, V>(p, g.kchunk, g.mode, g.slab, g.tickets,
+                                                        bx, by, bz, g.gx, g.gy, g.gz, lds, flag);
 #if DDL_STAMPS
-    stamp_block(g.stamps, vb, st0, nkt, 0, 0, 0);
-#endif
-  } else {
-    int bx, by, bz;
-    split_coords(g, vb, (int)blockIdx.x - vb, bx, by, bz);
-#if DDL_STAMPS
-    const Stamp st0 = stamp_now();
-#endif
-    const int nkt = splitk_body<BM, BN, BK, WM, WN, P, V>(p, g.kchunk, g.mode, g.slab, g.tickets,
-                                                          bx, by, bz, g.gx, g.gy, g.gz, lds, flag);
-#if DDL_STAMPS
-    stamp_block(g.stamps, vb, st0, nkt, bx, by, bz);
+  stamp_block(g.stamps, vb, st0, nkt, bx, by, bz);
 #else
-    (void)nkt;
+  (void)nkt;
 #endif
-  }
 }
 
 // (No amdgpu_waves_per_eu occupancy hints: forcing 4 waves per SIMD on the 32x32x2 tiles
@@ -1562,8 +1105,7 @@ DDL_DEV void run_sub(const P& p, const SubGrid& g, int vb, float* lds, int* flag
 // extra wave hides; the 16x16x4 tile reaches 5 waves by its register budget instead.)
 template <int BM, int BN, int BK, int WM, int WN, class P, int V = 0>
 __global__ void __launch_bounds__(WM * WN * 64)
-gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets,
-                int order
+gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets
 #if DDL_STAMPS
                 , unsigned long long* stamps
 #endif
@@ -1573,14 +1115,7 @@ gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __res
   // loop, whose last LDS reads have retired) — one array (guide §5 trap 4a), and no extra 16 B
   // that would push an 8 / 16 KB LDS-DMA block past an occupancy step
   __shared__ float4 lds4[T::LDS_F4 > 0 ? T::LDS_F4 : 1];
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (order != 0) {  // the hardware's linear block id, renumbered (split_coords)
-    SubGrid g;
-    g.gx = gridDim.x; g.gy = gridDim.y; g.gz = gridDim.z;
-    g.nblocks = g.gx * g.gy * g.gz;
-    g.order = order;
-    split_coords(g, bx + g.gx * (by + g.gy * bz), 0, bx, by, bz);
-  }
+  const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
 #if DDL_STAMPS
   const Stamp st0 = stamp_now();
 #endif
@@ -1593,23 +1128,6 @@ gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __res
 #else
   (void)nkt;
 #endif
-}
-
-template <int BM, int BN, int BK, int WM, int WN, class P, int V = 0>
-__global__ void __launch_bounds__(WM * WN * 64)
-gemm_streamk_kernel(P p, SubGrid g) {
-  using T = GemmTile<BM, BN, BK, WM, WN, P, V>;
-  __shared__ float4 lds4[T::LDS_F4 > 0 ? T::LDS_F4 : 1];  // (flag in the first word: see above)
-  if constexpr (KMapOf<P>::value) {
-    if (g.kmap) {
-      streamk_kmap_body<BM, BN, BK, WM, WN, P, V>(p, g, blockIdx.x, reinterpret_cast<float*>(lds4),
-                                                  reinterpret_cast<int*>(lds4));
-      return;
-    }
-  }
-  streamk_body<BM, BN, BK, WM, WN, P, V>(p, g.KI, g.gx, g.I, g.slab, g.tickets, blockIdx.x,
-                                         gridDim.x, reinterpret_cast<float*>(lds4),
-                                         reinterpret_cast<int*>(lds4));
 }
 
 // K split inside ONE workgroup, for the skinny GEMMs (the fc layers at M = batch): KW waves each
@@ -1786,9 +1304,9 @@ gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut, int bfirst) {
   const int ia = bfirst ? b - gb.nblocks : b;
   const int ib = bfirst ? b : b - ga.nblocks;
   if (is_a)
-    run_sub<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA, CA::V, CA::V == 0>(pa, ga, ia, lds, flag);
+    run_sub<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA, CA::V>(pa, ga, ia, lds, flag);
   else
-    run_sub<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB, CB::V, CB::V == 0>(pb, gb, ib, lds, flag);
+    run_sub<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB, CB::V>(pb, gb, ib, lds, flag);
 }
 
 // Output rows m0 .. m0 + 3 and column n of float4 element e of a mode-2 partial slab (the tile /
@@ -1908,73 +1426,22 @@ inline size_t splitk_slab_f4(int M, int N, int K, int splits) {
   return (size_t)z * tiles * TileGeo<BM, BN, WM, WN>::PART4;
 }
 
-// Stream-K worker count actually launched for a requested `workers` (0 = stream-K off):
-// a multiple of 8 (XCD-major numbering), at most one worker per K iteration.
-template <int BM, int BN, int BK>
-inline int streamk_workers(int M, int N, int K, int workers) {
-  if (workers <= 0) return 0;
-  const long long I = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN) * ((K + BK - 1) / BK);
-  long long w = workers < I ? workers : I;
-  w &= ~7LL;
-  return w < 8 ? 0 : (int)w;
-}
-
-// float4 partial-slab elements a launch needs (stream-K when workers > 0, else split-K)
+// float4 partial-slab elements a launch needs
 template <int BM, int BN, int BK, int WM, int WN>
-inline size_t gemm_slab_f4(int M, int N, int K, int splits, int workers) {
-  // (max of both: a stream-K launch with more tiles than tickets falls back to split-K)
-  const int w = streamk_workers<BM, BN, BK>(M, N, K, workers);
-  const size_t sk = (size_t)w * 2 * TileGeo<BM, BN, WM, WN>::PART4;
-  const size_t sp = splitk_slab_f4<BM, BN, BK, WM, WN>(M, N, K, splits);
-  return sk > sp ? sk : sp;
+inline size_t gemm_slab_f4(int M, int N, int K, int splits) {
+  return splitk_slab_f4<BM, BN, BK, WM, WN>(M, N, K, splits);
 }
 
-// Schedule of one launch: stream-K when workers > 0 (and the tile count fits the tickets),
-// else split-K with `splits`: z > wide_thr uses mode 2 (separate wide reduce), else mode 1
-// (last arriver).
+// Schedule of one launch: split-K with `splits`: z > wide_thr uses mode 2 (separate wide reduce),
+// else mode 1 (last arriver).
 template <int BM, int BN, int BK, class P>
-inline SubGrid plan_gemm(const P& p, int splits, int workers, int wide_thr,
-                         const SplitScratch& sc, int order = 0) {
+inline SubGrid plan_gemm(const P& p, int splits, int wide_thr, const SplitScratch& sc) {
   SubGrid g;
-  g.order = order;
   g.slab = reinterpret_cast<float4*>(sc.slab);
   g.tickets = sc.tickets;
   if (p.M <= 0 || p.N <= 0) return g;
   g.gx = (p.M + BM - 1) / BM;
   g.gy = (p.N + BN - 1) / BN;
-  if constexpr (KMapOf<P>::value) {
-    // K-mapped stream-K (streamk_kmap_body): the per-row-tile K-tile counts of the tap windows
-    if (workers > 0 && g.gx <= kKmapTiles && (long long)g.gx * g.gy <= sc.max_tiles) {
-      int tot = 0;
-      bool ok = true;
-      g.kpre[0] = 0;
-      for (int bx = 0; bx < g.gx && ok; ++bx) {
-        const int lo = bx * BM, hi = lo + BM < p.M ? lo + BM : p.M;
-        const int ki = (p.kvlen(p.kwin(lo, hi)) + BK - 1) / BK;
-        tot += ki;
-        ok = ki > 0 && tot < 65536;
-        g.kpre[bx + 1] = (unsigned short)tot;
-      }
-      const long long I = (long long)tot * g.gy;
-      long long w = workers < I ? workers : I;
-      w &= ~7LL;
-      if (ok && w >= 8) {
-        g.streamk = 1;
-        g.kmap = 1;
-        g.nblocks = (int)w;
-        g.I = I;
-        return g;
-      }
-    }
-  }
-  const int W = streamk_workers<BM, BN, BK>(p.M, p.N, p.K, workers);
-  if (W > 0 && (long long)g.gx * g.gy <= sc.max_tiles) {
-    g.streamk = 1;
-    g.nblocks = W;
-    g.KI = (p.K + BK - 1) / BK;
-    g.I = (long long)g.gx * g.gy * g.KI;
-    return g;
-  }
   g.gz = splitk_z<BK>(p.K, splits);
   g.kchunk = g.gz > 1 ? splitk_kchunk<BK>(p.K, splits) : p.K;
   g.mode = g.gz == 1 ? 0 : (g.gz > wide_thr ? 2 : 1);
@@ -1986,7 +1453,7 @@ inline SubGrid plan_gemm(const P& p, int splits, int workers, int wide_thr,
 // The separate reduce of a mode-2 split-K launch (no-op otherwise).
 template <int BM, int BN, int BK, int WM, int WN, class P>
 inline void launch_reduce(const P& p, const SubGrid& g, hipStream_t stream) {
-  if (g.streamk || g.mode != 2 || g.nblocks == 0) return;
+  if (g.mode != 2 || g.nblocks == 0) return;
   using G = TileGeo<BM, BN, WM, WN>;
   const int ntiles = g.gx * g.gy, z = g.gz;
   const size_t nelem = (size_t)ntiles * G::PART4;
@@ -2011,7 +1478,7 @@ inline void launch_reduce(const P& p, const SubGrid& g, hipStream_t stream) {
 template <int BM, int BN, int BK, int WM, int WN, class P>
 inline bool launch_reduce_tail(const P& p, const SubGrid& g, const UpdTail& t,
                                hipStream_t stream) {
-  if (g.streamk || g.mode != 2 || g.nblocks == 0) return false;
+  if (g.mode != 2 || g.nblocks == 0) return false;
   using G = TileGeo<BM, BN, WM, WN>;
   const int ntiles = g.gx * g.gy, z = g.gz;
   const size_t nelem = (size_t)ntiles * G::PART4;
@@ -2029,25 +1496,18 @@ inline bool launch_reduce_tail(const P& p, const SubGrid& g, const UpdTail& t,
 
 template <int BM, int BN, int BK, int WM, int WN, int V = 0, class P>
 inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch& sc,
-                        hipStream_t stream, int workers = 0, int order = 0,
-                        SubGrid* defer = nullptr) {
-  const SubGrid g = plan_gemm<BM, BN, BK>(p, splits, workers, wide_thr, sc, order);
+                        hipStream_t stream, SubGrid* defer = nullptr) {
+  const SubGrid g = plan_gemm<BM, BN, BK>(p, splits, wide_thr, sc);
   if (defer) *defer = g;
   if (g.nblocks == 0) return;
-  if (g.streamk) {
-    DDL_LAUNCH((gemm_streamk_kernel<BM, BN, BK, WM, WN, P, V>), dim3(g.nblocks),
-                       dim3(WM * WN * 64), 0, stream, p, g);
-    return;
-  }
 #if DDL_STAMPS
   unsigned long long* const stamps = stamp_slot(g.nblocks, 2, g.gx, g.gy, g.gz);
   DDL_LAUNCH((gemm_f32_kernel<BM, BN, BK, WM, WN, P, V>), dim3(g.gx, g.gy, g.gz),
                      dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets,
-                     g.order, stamps);
+                     stamps);
 #else
   DDL_LAUNCH((gemm_f32_kernel<BM, BN, BK, WM, WN, P, V>), dim3(g.gx, g.gy, g.gz),
-                     dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets,
-                     g.order);
+                     dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets);
 #endif
   if (defer && g.mode == 2) return;  // the caller runs (or fuses) the wide reduce
   launch_reduce<BM, BN, BK, WM, WN, P>(p, g, stream);
@@ -2055,15 +1515,15 @@ inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch
 
 // Launch R's pending wide reduce (SubGrid gr of a mode-2 split-K launch, tile config CR) fused
 // with GEMM problem G (config CG, its own schedule/scratch); G's own mode-2 reduce follows.
-// Returns false (nothing launched) when R has no pending wide reduce or G is stream-K.
+// Returns false (nothing launched) when R has no pending wide reduce.
 // defer_g: G's own reduce is left to the caller (its SubGrid is returned there).
 template <class CR, class PR, class CG, class PG>
-inline bool launch_reduce_with_gemm(const PR& pr, const SubGrid& gr, const PG& pg, int sg, int wg,
+inline bool launch_reduce_with_gemm(const PR& pr, const SubGrid& gr, const PG& pg, int sg,
                                     int wide_g, const SplitScratch& scg, hipStream_t stream,
                                     SubGrid* defer_g = nullptr) {
-  if (gr.streamk || gr.mode != 2 || gr.nblocks == 0) return false;
-  const SubGrid gg = plan_gemm<CG::BM, CG::BN, CG::BK>(pg, sg, wg, wide_g, scg);
-  if (gg.streamk || gg.nblocks == 0) return false;
+  if (gr.mode != 2 || gr.nblocks == 0) return false;
+  const SubGrid gg = plan_gemm<CG::BM, CG::BN, CG::BK>(pg, sg, wide_g, scg);
+  if (gg.nblocks == 0) return false;
   using G = TileGeo<CR::BM, CR::BN, CR::WM, CR::WN>;
   const int ntiles = gr.gx * gr.gy, z = gr.gz;
   const size_t nelem = (size_t)ntiles * G::PART4;
@@ -2085,16 +1545,12 @@ inline bool launch_reduce_with_gemm(const PR& pr, const SubGrid& gr, const PG& p
 // Problems A and B (one-wave tile configs CA / CB) in one launch, each with its own schedule
 // and its own scratch (slab + tickets); mode-2 reduces follow on the same stream.
 template <class CA, class PA, class CB, class PB, class AUX = TailAux>
-inline void launch_gemm_dual(const PA& pa, int sa, int wa, const SplitScratch& sca, int wide_a,
-                             const PB& pb, int sb, int wb, const SplitScratch& scb, int wide_b,
+inline void launch_gemm_dual(const PA& pa, int sa, const SplitScratch& sca, int wide_a,
+                             const PB& pb, int sb, const SplitScratch& scb, int wide_b,
                              hipStream_t stream, const AUX& ut = AUX(),
-                             SubGrid* defer_b = nullptr, int bfirst = 0, int order_a = 0,
-                             int order_b = 0) {
-  // (a 16x16x4 sub-problem runs split-K only in a dual launch: see run_sub's SK)
-  SubGrid ga =
-      plan_gemm<CA::BM, CA::BN, CA::BK>(pa, sa, CA::V ? 0 : wa, wide_a, sca, order_a);
-  SubGrid gb =
-      plan_gemm<CB::BM, CB::BN, CB::BK>(pb, sb, CB::V ? 0 : wb, wide_b, scb, order_b);
+                             SubGrid* defer_b = nullptr, int bfirst = 0) {
+  SubGrid ga = plan_gemm<CA::BM, CA::BN, CA::BK>(pa, sa, wide_a, sca);
+  SubGrid gb = plan_gemm<CB::BM, CB::BN, CB::BK>(pb, sb, wide_b, scb);
 #if DDL_STAMPS
   ga.stamps = stamp_slot(ga.nblocks, 0, ga.gx, ga.gy, ga.gz);
   gb.stamps = stamp_slot(gb.nblocks, 1, gb.gx, gb.gy, gb.gz);

@@ -707,11 +707,7 @@ struct WgradAdam : P {
   float *w_w, *w_m, *w_v;  // weight span
   float *b_w, *b_m, *b_v;  // bias span
   float lr_t, c1, c2, eps, scale;
-  DDL_DEV void epi(int m0, int n, f32x4 v) const { apply<true>(m0, n, v); }
-  // STORE = false: the update alone (the fused xGMI last bucket: the gradient stored is this
-  // rank's, the update takes the sum over ranks; conv1.h conv1_wgrad_xgmi_kernel)
-  template <bool STORE>
-  DDL_DEV void apply(int m0, int n, f32x4 v) const {
+  DDL_DEV void epi(int m0, int n, f32x4 v) const {
     constexpr int KW = P::KW;  // gw is [KW, N] (N = COUT)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -720,10 +716,10 @@ struct WgradAdam : P {
       size_t i;
       if (m < KW) {
         i = (size_t)m * this->N + n; pw = w_w; pm = w_m; pv = w_v;
-        if (STORE) this->gw[i] = v[r];
+        this->gw[i] = v[r];
       } else if (m == KW) {
         i = (size_t)n; pw = b_w; pm = b_m; pv = b_v;
-        if (STORE) this->gb[i] = v[r];
+        this->gb[i] = v[r];
       } else {
         continue;
       }
@@ -901,11 +897,6 @@ struct Mf16OK<ConvDgrad<H, CIN, COUT, HPREV>> : std::true_type {};
 template <int H, int CIN, int COUT>
 struct Mf16OK<ConvWgradBM<H, CIN, COUT>> : std::true_type {};
 
-// ops the generic LDS-DMA tiles (CFG_DMA_*, gemm.h mainloop_dma_g) are instantiated for: the
-// same 16-byte-gather set
-template <class P>
-using DmaOK = Mf16OK<P>;
-
 // ops the K-wave launch (gemm.h gemm_kwave_kernel, CFG_KWAVE) is instantiated for
 template <class P>
 struct KWaveOK : std::false_type {};
@@ -915,11 +906,7 @@ template <>
 struct KWaveOK<FcDgradAct> : std::true_type {};
 template <int HP, int C>
 struct KWaveOK<FcDgradPool<HP, C>> : std::true_type {};
-// conv backward as K-wave tiles (round 5 experiment: the split-K partial slab, tickets and
-// last-arriver sums replaced by an LDS reduction inside the workgroup; not dual-launched)
-template <int H, int CIN, int COUT>
-struct KWaveOK<ConvWgradBM<H, CIN, COUT>> : std::true_type {};
-template <int H, int CIN, int COUT, int HPREV>
-struct KWaveOK<ConvDgrad<H, CIN, COUT, HPREV>> : std::true_type {};
+// (the conv backward as K-wave tiles lost to the dual launches in every variant, 312-402 vs
+// 289.5 us/step, and was removed: docs/DESIGN.md round 5)
 
 }  // namespace ddl

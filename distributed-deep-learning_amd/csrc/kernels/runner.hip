@@ -78,12 +78,11 @@ SyncRunner::SyncRunner(Engine* eng, float* params, float* grads, int world, int 
   // device.  On the 1-rank rehearsal (W = 1, every collective a local copy) a device-scope
   // release suffices and removed a ~7 us gap per backward segment (forced 1-rank timeline).
   // With W > 1, RCCL's P2P transports may read these buffers from a peer GPU, and the relaxed
-  // fence has not been validated there, so W > 1 keeps the system-scope fence unless
-  // DDL_EVENT_SYSFENCE=0 asks for the device scope explicitly (A/B).  The end-of-exchange
-  // event keeps the system scope: it orders the next forward after collectives that received
-  // peer data, and it is recorded on the comm stream, off the compute stream's critical path.
-  const char* sf = getenv("DDL_EVENT_SYSFENCE");
-  const bool sysfence = sf ? sf[0] == '1' : world_ > 1;
+  // fence has not been validated there, so W > 1 keeps the system-scope fence.  The
+  // end-of-exchange event keeps the system scope: it orders the next forward after collectives
+  // that received peer data, and it is recorded on the comm stream, off the compute stream's
+  // critical path.
+  const bool sysfence = world_ > 1;
   const unsigned ev_flags =
       hipEventDisableTiming | (sysfence ? 0u : (unsigned)hipEventDisableSystemFence);
   for (int s = 0; s < kSegments; ++s) {
@@ -131,11 +130,6 @@ void SyncRunner::release() {
   ready_ = nullptr;
   if (ready_err_) (void)hipHostFree(ready_err_);
   ready_err_ = nullptr;
-  if (xlast_dev_) (void)hipFree(xlast_dev_);
-  xlast_dev_ = nullptr;
-  if (xlast_host_) (void)hipHostFree(xlast_host_);
-  xlast_host_ = nullptr;
-  xlast_up_valid_ = false;
   if (cs_) (void)hipStreamDestroy(cs_);
   cs_ = nullptr;
   closed_ = true;
@@ -453,59 +447,6 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
     // bound to the segment's LAST launch (its count is learned from the previous step; a
     // wrong or unknown count falls back to a marker record below, which supersedes the binding)
     bool marker = !bind;
-    // the last bucket's exchange inside conv1's weight-gradient launch (api.h set_fused_last)
-    const RunnerUnit* fused =
-        xlast_dev_ ? fused_last_unit(on_main && s == kSegments - 1, st) : nullptr;
-    if (fused) {
-      const auto& r = fused->ranges[0];
-      UpdTail t;
-      t.c1 = 1.f - b1_;
-      t.c2 = 1.f - b2_;
-      t.eps = eps_;
-      t.scale = grad_scale_;
-      UpdPiece& q = t.p[t.npieces++];
-      q.w = w_ + r.lo;
-      q.g = g_ + r.lo;
-      q.m = fused->m + r.state_off;
-      q.v = fused->v + r.state_off;
-      q.n = r.hi - r.lo;
-      q.lr_t = lr_t[fused->ps];
-      eng_->final_upd = t;
-      XgmiUpdate up;
-      up.opt = opt_;
-      up.m = q.m;
-      up.v = q.v;
-      up.lr_t = q.lr_t;
-      up.c1 = t.c1;
-      up.c2 = t.c2;
-      up.eps = eps_;
-      up.scale = grad_scale_;
-      up.coef = coef_;
-      peer_->fill_last(epoch_, up, (int)(fused - units_.data()) == last_xgmi_, xlast_);
-      // the kernel reads the arguments from device memory (conv1.h XfRef): the epoch travels
-      // as a launch argument, the step size inside the launch's Adam spans (final_upd), the rest
-      // is uploaded when it changes (in practice once) — stream-ordered from a pinned staging
-      // copy.  Never a synchronous hipMemcpy here: it may wait for the comm stream, whose READY
-      // gate waits for a launch of this step that is not enqueued yet (a deadlock)
-      xlast_.a.epoch = 0;
-      xlast_.a.lr_t = 0.f;
-      // (both buffers come from set_peer: an allocation here may synchronise the device —
-      // the same deadlock; one-card W = 2 / 3 rehearsals timed out at the first step)
-      if (!xlast_up_valid_ || memcmp(&xlast_, &xlast_up_, sizeof(XgmiLast)) != 0) {
-        if (xlast_up_valid_) HIP_CHECK(hipStreamSynchronize(st));  // (staging copy reuse; the
-        // per-step fields are zeroed, so only a new peer table gets here)
-        memcpy(xlast_host_, &xlast_, sizeof(XgmiLast));
-        HIP_CHECK(hipMemcpyAsync(xlast_dev_, xlast_host_, sizeof(XgmiLast),
-                                 hipMemcpyHostToDevice, st));
-        xlast_up_ = xlast_;
-        xlast_up_valid_ = true;
-      }
-      xlast_.a.epoch = epoch_;
-      xlast_.a.lr_t = q.lr_t;
-      eng_->final_xchg = &xlast_;
-      eng_->final_xchg_dev = xlast_dev_;
-      eng_->final_xchg_taken = false;
-    }
     {
       TraceRange r(kBwdRange[s]);
       StopEventScope scope(bind ? ev : nullptr, seg_launches_[s] > 0 ? seg_launches_[s] - 1
@@ -516,14 +457,6 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
         if (scope.bound() != n - 1) marker = true;
         seg_launches_[s] = n;
       }
-    }
-    bool fused_taken = false;
-    if (fused) {
-      fused_taken = eng_->final_xchg_taken;
-      eng_->final_xchg = nullptr;
-      eng_->final_xchg_taken = false;
-      eng_->final_upd = UpdTail();
-      fused_last_taken_ = fused_taken;
     }
     TraceRange ex_range(kExRange[s]);
     hipStream_t xs = on_main ? st : cs_;
@@ -557,7 +490,6 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
         }
         waited = true;
       }
-      if (fused_taken && &u == fused) continue;  // exchanged and applied by the last launch
       if (u.kind == RunnerUnit::XGMI || u.kind == RunnerUnit::XGMI_REPL) {
         // the final wait orders the next forward after every owner's pushes; only if it runs
         // on the comm stream does the compute stream need the end-of-exchange event
@@ -579,41 +511,6 @@ void SyncRunner::step(const float* x, const int64_t* labels, int B, uint32_t see
     HIP_CHECK(hipEventRecord(done_ev_, cs_));
     HIP_CHECK(hipStreamWaitEvent(st, done_ev_, 0));
   }
-}
-
-// The fused launch's last arrivers wait for the peers' pushes of the SAME launch; the peers'
-// earlier bucket kernels must still get CUs meanwhile, so the comm stream has to outrank the
-// compute stream (one process per GPU: high-priority comm stream).  Ranks sharing a card run the
-// comm stream at the least priority (DDL_COMM_PRIORITY=low): there the waiting last arrivers of
-// several ranks plus their low-priority bucket kernels can fill the card and stall each other
-// (one-card W = 3 rehearsal: a 20 s timeout), so they keep xgmi_repl_kernel.
-void SyncRunner::alloc_last() {
-  if (xlast_dev_) return;
-  HIP_CHECK(hipMalloc(&xlast_dev_, sizeof(XgmiLast)));
-  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&xlast_host_), sizeof(XgmiLast),
-                          hipHostMallocDefault));
-  xlast_up_valid_ = false;
-}
-
-const RunnerUnit* SyncRunner::fused_last_unit(bool on_main, hipStream_t st) {
-  if (!on_main || !fused_last_ || !peer_ || opt_ != 0 || peer_->check_mode()) return nullptr;
-  if (!fused_prio_checked_ || st != fused_prio_stream_) {
-    int p = 0, cp = 0;  // (the null stream is a normal-priority stream)
-    fused_prio_ok_ = (st == nullptr || hipStreamGetPriority(st, &p) == hipSuccess) &&
-                     hipStreamGetPriority(cs_, &cp) == hipSuccess && cp < p;
-    fused_prio_stream_ = st;
-    fused_prio_checked_ = true;
-  }
-  if (!fused_prio_ok_) return nullptr;
-  const RunnerUnit* f = nullptr;
-  for (const auto& u : units_) {
-    if (u.seg != kSegments - 1) continue;
-    if (u.kind != RunnerUnit::XGMI_REPL || f) return nullptr;  // only the replicated bucket
-    f = &u;
-  }
-  if (!f || f->bucket != peer_->repl_bucket() || f->ranges.size() != 1 || !f->m || !f->v)
-    return nullptr;
-  return f;
 }
 
 // The READY gate waits on the comm stream for a kernel of `st`: only safe when `st` cannot share

@@ -37,7 +37,7 @@ struct UpdPiece {
   float lr_t = 0.f;        // TF1 Adam step size of the owning PS
   int blk0 = 0;            // first tail block of this piece
   // push (kind 1): slice j = block blk0 + j covers float4 [j * slice4, (j + 1) * slice4); its
-  // board word posted[j] (host memory) and arrive[j] (the PS host's device flags).  Ready flag
+  // board word posted[j] (host memory).  Ready flag
   // (kind 2): arrive[0]
   uint32_t* arrive = nullptr;
   uint32_t* posted = nullptr;

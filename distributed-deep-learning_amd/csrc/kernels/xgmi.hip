@@ -59,7 +59,7 @@ DDL_DEV float4 ld4_sys(brsrc_t r, int byte_off) {
 }
 DDL_DEV void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// the flag protocol's device side lives in xgmi_dev.h (shared with conv1.h's fused last bucket)
+// the flag protocol's device side lives in xgmi_dev.h
 DDL_DEV void flag_store(uint32_t* f, uint32_t v) { xg_flag_store(f, v); }
 DDL_DEV int arrive_idx(int b, int src, int j) { return xg_arrive_idx(b, src, j); }
 DDL_DEV int done_idx(int b, int src, int j) { return xg_done_idx(b, src, j); }
@@ -565,8 +565,7 @@ void PeerExchange::init(const std::vector<XgmiBucketSpec>& buckets, int max_slic
     if (ns < 1) ns = 1;
     B.slice = ((B.c + ns - 1) / ns + 3) & ~(int64_t)3;
     B.nslice = (int)((B.c + B.slice - 1) / B.slice);
-    // the replicated bucket's slot also holds the fused last launch's exchange (api.h)
-    B.slot = repl ? (B.c > kXgmiReplFusedSlot ? B.c : kXgmiReplFusedSlot) : B.c;
+    B.slot = B.c;
     if (B.slot * 4 * world * (repl ? 2 : 1) > 0x7fffffffLL)
       throw std::invalid_argument("xgmi: bucket too large");
     inbox += B.slot * world * (repl ? 2 : 1);  // replicated: two parity slots per source
@@ -706,13 +705,6 @@ void PeerExchange::fill(int bucket, uint32_t epoch, const XgmiUpdate& u, bool fi
   }
 }
 
-void PeerExchange::fill_last(uint32_t epoch, const XgmiUpdate& u, bool final_wait,
-                             XgmiLast& out) const {
-  if (repl_ < 0) throw std::runtime_error("xgmi: no replicated bucket");
-  fill(repl_, epoch, u, final_wait, false, out.a);
-  out.T = table_;
-}
-
 void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool final_wait,
                           hipStream_t st, bool gated) {
   XgmiLaunch a;
@@ -752,6 +744,43 @@ void PeerExchange::launch(int bucket, uint32_t epoch, const XgmiUpdate& u, bool 
 
 int PeerExchange::error() const {
   return err_ ? __atomic_load_n(err_, __ATOMIC_ACQUIRE) : 0;
+}
+
+// ---- the stale-L2 probe of the xGMI self-test (native_exchange.py) ----------------------------
+// A peer's parameter stores reach this GPU's HBM over xGMI without touching its eight per-XCD
+// L2s, so a line that some XCD cached BEFORE the exchange could be read back stale by the next
+// kernel unless that kernel's start acquire invalidates it (the protocol's assumption, header
+// comment above).  The probe makes the hazard reachable on purpose: the sweep is launched with 8
+// blocks per 16 KB chunk, block b on XCD b % 8 (the hardware's round-robin dispatch), so before
+// the exchange every XCD reads — and caches, with ordinary loads — every line of the buffer, and
+// after it every XCD compares every line with the expected values.  want == null: warm only.
+__global__ void __launch_bounds__(256) xcd_sweep_kernel(const float4* __restrict__ a,
+                                                        const float4* __restrict__ want,
+                                                        int64_t n4, int* __restrict__ out) {
+  const int64_t chunk = blockIdx.x >> 3;
+  const int64_t lo = chunk * 1024, hi = lo + 1024 < n4 ? lo + 1024 : n4;
+  int bad = 0;
+  float acc = 0.f;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+    const float4 v = a[i];
+    if (want) {
+      const float4 w = want[i];
+      bad += (v.x != w.x) + (v.y != w.y) + (v.z != w.z) + (v.w != w.w);
+    } else {
+      acc += v.x + v.y + v.z + v.w;
+    }
+  }
+  if (bad) atomicAdd(out, bad);
+  if (!want && acc == 1.2345e-30f) atomicAdd(out + 1, 1);  // keeps the warm loads alive
+}
+
+void launch_xcd_sweep(const float* a, const float* want, int64_t n, int* out, hipStream_t st) {
+  if (n % 4 || reinterpret_cast<uintptr_t>(a) % 16 || (want && reinterpret_cast<uintptr_t>(want) % 16))
+    throw std::invalid_argument("xcd sweep: 16-B aligned float4 buffers");
+  const int64_t n4 = n / 4, chunks = (n4 + 1023) / 1024;
+  if (chunks <= 0) return;
+  DDL_LAUNCH(xcd_sweep_kernel, dim3((unsigned)(chunks * 8)), dim3(256), 0, st,
+             reinterpret_cast<const float4*>(a), reinterpret_cast<const float4*>(want), n4, out);
 }
 
 }  // namespace ddl

@@ -11,16 +11,13 @@
 //             tail blocks of the next segment's launch, async_runner.hip) those PS shards of the
 //             gradient -> each PS host's inbox slot [ps][worker] (system write-through stores);
 //             per workgroup, once its payload is acknowledged, POSTED[ps][worker][slice] = e on
-//             the ARRIVAL BOARD in host memory and in the PS host's uncached device flags
-//   serve     (PS host) default: a native service thread scans the host board and launches
-//             one apply per (worker, ps) whose every slice is posted, in the order it observes
-//             them (the reference's MPI.ANY_SOURCE order; AsyncService::run).
-//             DDL_ASYNC_CLAIM=1: pre-enqueued claim kernels on the PS stream poll the device
-//             copy and pop every complete push on the GPU, each followed by a batched apply
-//             kernel; the thread only keeps that queue topped up (AsyncService::run_claim).
-//             Same results; the claim service measured equal at W = 1 and 1.3-1.7x slower with
-//             several ranks on one card, where a claim kernel waiting on a high-priority queue
-//             slowed every rank's GEMMs (docs/DESIGN.md round 5), so it is opt-in
+//             the ARRIVAL BOARD in host memory
+//   serve     (PS host) a native service thread scans the host board and launches one apply
+//             per (worker, ps) whose every slice is posted, in the order it observes them (the
+//             reference's MPI.ANY_SOURCE order; AsyncService::run).  (Round 5's on-GPU pop —
+//             claim kernels polling a device copy of the board — measured equal at W = 1 and
+//             1.3-1.7x slower with several ranks on one card, and was removed in round 6:
+//             docs/DESIGN.md.)
 //   apply     (PS host, its PS stream) Adam on the PS's private parameter copy (one step of its
 //             counter t per arrival, atomic per shard: the reference's per-tag mixing race Q3
 //             cannot happen), store the new shard into the WORKER's parameter buffer, then
@@ -35,22 +32,16 @@
 // release (an L2 write-back) and left a ~4.6 us hole on the compute stream after every push,
 // plus two host hand-offs (poster -> mailbox -> service) on the critical path of the last push
 // (docs/DESIGN.md, round 4 async timeline).
-// The hardware-queue argument (why no wait here can deadlock).  Two kinds of kernel wait:
-//   * the worker's pull gate (compute stream) waits for applies;
-//   * a claim kernel (PS stream) waits for pushes.
-// HIP maps a process's streams onto hardware queues pooled PER PRIORITY; the PS stream is HIGH
-// priority and the compute stream is not (async_runner.hip checks it and falls back to a host
-// wait), so no apply or claim kernel is ever queued behind a gate, and no push behind a claim.
-// A gate waits for applies that sit on PS queues (this process's or a peer's); an apply waits for
-// nothing but the claim kernel in front of it; a claim kernel waits for pushes, which are GEMM
-// tail blocks or push kernels on compute queues that never wait except at the gate of the NEXT
-// round — issued after those pushes in the same queue.  Every chain ends at a kernel that waits
-// for nothing, so there is no cycle under any stream -> queue mapping that keeps the two
-// priorities apart.  The one remaining hazard is time slicing of oversubscribed hardware
-// queues (several ranks on one card): a waiter then spins until the queue holding what it waits
-// for is mapped in again (milliseconds), which parallel/comm.py share_gpu_queue_cap avoids with
-// one hardware queue per process.  Every wait is bounded: the gate records an error word
-// instead of hanging, and a claim kernel ends empty after `idle_us` (the host re-enqueues it).
+// The hardware-queue argument (why no wait here can deadlock).  The only kernel wait is the
+// worker's pull gate (compute stream), which waits for applies.  HIP maps a process's streams
+// onto hardware queues pooled PER PRIORITY; the PS stream is HIGH priority and the compute
+// stream is not (async_runner.hip checks it and falls back to a host wait), so no apply is ever
+// queued behind a gate.  An apply waits for nothing (the host launches it once the push is on
+// the board), so every chain ends at a kernel that waits for nothing.  The one remaining hazard
+// is time slicing of oversubscribed hardware queues (several ranks on one card): a waiter then
+// spins until the queue holding what it waits for is mapped in again (milliseconds), which
+// parallel/comm.py share_gpu_queue_cap avoids with one hardware queue per process.  Every wait
+// is bounded: the gate records an error word instead of hanging.
 #include <fcntl.h>
 #include <stdlib.h>
 #include <string.h>
@@ -96,16 +87,10 @@ DDL_DEV bool wait_ge(const uint32_t* f, uint32_t target, long long deadline, int
 // barrier that precedes the flag store: a write-through store is counted complete only once the
 // memory side (local HBM, or the peer over xGMI, or host memory) has acknowledged it, so the
 // payload is globally visible before the flag is issued — no L2 write-back is needed (the CDNA
-// guide's G16 write-through hand-off, at system scope).  DDL_XGMI_RELEASE=1 adds the full
-// system release anyway (L2 write-back + wait, as one asm statement: hipcc drops the wait of its
-// own release when the scoreboard is already drained, and schedules a separate asm wait above
-// the write-back); it writes back every dirty line of the XCD's L2 at each flag — the GEMMs'
-// output included — and measured 3.2 -> 5.4 ms/step on the two-ranks-on-one-GPU rehearsal.
-#ifndef DDL_XGMI_RELEASE
-#define DDL_XGMI_RELEASE 0
-#endif
+// guide's G16 write-through hand-off, at system scope).  A full system release at each flag (L2
+// write-back + wait) writes back every dirty line of the XCD's L2 — the GEMMs' output included —
+// and measured 3.2 -> 5.4 ms/step on the two-ranks-on-one-GPU rehearsal (round 2).
 DDL_DEV void flag_store(uint32_t* f, uint32_t v) {
-  if (DDL_XGMI_RELEASE) asm volatile("buffer_wbl2 sc0 sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -121,11 +106,6 @@ __host__ __device__ inline size_t posted_word(int p, int w, int j) {
 // copy measured ~25 us late: the registered host segment is not guaranteed to bypass the GPU's
 // L2 for a system-scope load)
 DDL_DEV int done_dev_idx(const AsyncShard& S, int j) { return S.slice0 + j; }
-// the arrival words in the PS HOST's uncached device flags (what its claim kernel polls; the
-// host board copy serves the host-scan service, DDL_ASYNC_CLAIM=0)
-__host__ __device__ inline size_t posted_dev_idx(const AsyncShard& S, int w, int j) {
-  return (size_t)kAsyncDense * (1 + w) + S.slice0 + j;
-}
 
 struct PushArgs {
   int world, rank, nps;
@@ -176,7 +156,6 @@ __global__ void __launch_bounds__(256) async_push_kernel(const AsyncTable* __res
   if (tid == 0) {
     __hip_atomic_store(T.posted + posted_word(p, a.rank, j), a.epoch, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
-    flag_store(T.flags[S.host] + posted_dev_idx(S, a.rank, j), a.epoch);
   }
 }
 
@@ -191,7 +170,7 @@ struct ApplyArgs {
 };
 
 // Slice j of one apply.  No arrival poll: the apply runs only after every slice of the push was
-// seen posted (by the claim kernel in front of it, or by the host service), and a push block
+// seen posted by the host service, and a push block
 // posts only after its payload stores were acknowledged (the inbox loads below are
 // system-coherent, so they see that payload).
 DDL_DEV void apply_body(const AsyncTable& T, const ApplyArgs& a, int j) {
@@ -242,263 +221,6 @@ DDL_DEV void apply_body(const AsyncTable& T, const ApplyArgs& a, int j) {
 __global__ void __launch_bounds__(256) async_apply_kernel(const AsyncTable* __restrict__ Tp,
                                                           ApplyArgs a) {
   apply_body(*Tp, a, blockIdx.x);
-}
-
-}  // namespace
-
-// ---- the on-GPU ANY_SOURCE pop (DDL_ASYNC_CLAIM=1) --------------------------------------------
-// The service keeps `depth` (claim, apply) kernel pairs enqueued on its high-priority PS stream.
-// The claim kernel (one wave) polls this host's arrival words in its own uncached device flags
-// and, once at least one push is complete, takes EVERY complete (hosted PS, worker) push in
-// round-robin order from where the last claim stopped — the reference's MPI.ANY_SOURCE receive
-// (mnist_async_sharding/parameter_server.py:94-111) as an on-GPU pop of a batch of arrivals.
-// Each claim advances its PS's step counter and takes its TF1 step size from a table the host
-// filled with the host formula (bit-identical to the host service).  The apply kernel behind it
-// runs one block per hosted slice: the block applies the batch's claims of its PS one after
-// another, in claim order, to its slice — w, m and v read and written once for the whole batch,
-// the parameters after each claim's update stored to that claim's worker — so K arrivals of one
-// PS cost one pass instead of K kernel pairs, with the same per-element arithmetic in the same
-// order as K separate applies.  No host thread and no host launch sits between a push's last
-// slice and its apply: the thread only tops the queue up.
-// A claim kernel waits `idle_us` at most and then ends without a claim (the host re-enqueues):
-// a pair queued for a push that this very process issues only after a device-wide synchronize
-// (torch.cuda.synchronize() before the bench's timed window, a checkpoint, an in-line eval)
-// must not hold that synchronize forever.  It also ends at once when pause() raises `hold`.
-constexpr int kClaimBatch = 16;
-struct ClaimState {
-  int me, world, nh, per_ps, opt;
-  int ps[kAsyncMaxPs];             // hosted PS ids
-  int blk0[kAsyncMaxPs + 1];       // hosted PS i's apply blocks: [blk0[i], blk0[i + 1])
-  float* params[kAsyncMaxPs];      // their private parameter copies and optimizer state
-  float* m[kAsyncMaxPs];
-  float* v[kAsyncMaxPs];
-  int64_t t0[kAsyncMaxPs];         // step counters at start (the lr table's origin)
-  int64_t t[kAsyncMaxPs];          // step counters (claim kernels only)
-  uint32_t last[kXgmiMaxPeers * kAsyncMaxPs];  // last claimed round per (worker, hosted PS)
-  int start;                       // round-robin position of the next scan
-  int64_t claims, ended;
-  // the current batch: written by a claim kernel, read by the apply kernel behind it
-  int nb;                          // 0: the claim kernel ended empty
-  int b_pl[kClaimBatch], b_w[kClaimBatch];
-  uint32_t b_e[kClaimBatch];
-  float b_lr[kClaimBatch];
-  const float* lr_tab;             // [nh][per_ps]: lr_t of step t0 + 1 + i
-  int32_t* prov;                   // [claims][4] (worker, ps, round, t) or null
-  int64_t* host;                   // pinned host words (api.h AsyncService::host_words_)
-  int* err;
-  float c1, c2, eps, lr, mu, scale;
-  long long idle_ticks;
-  int publish_in_claim;            // DDL_ASYNC_PUBLISH=claim (A/B)
-};
-
-namespace {
-
-// The service thread's view of the claims in front (pinned host words).  Stored by block 0 of the
-// apply kernel AFTER its slice's DONE flags: a wave's drain before its flag store would otherwise
-// wait out these stores' PCIe round trip, and the worker's gate waits for that flag.
-DDL_DEV void publish_claim(const ClaimState* C) {
-  for (int c = 0; c < C->nb; ++c)
-    __hip_atomic_store(C->host + 8 + C->b_pl[c], C->t[C->b_pl[c]], __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(C->host + 1, C->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  // (release: a host that sees this `ended` sees the `claims` stored before it)
-  __hip_atomic_store(C->host + 0, C->ended, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// One sweep over every (hosted PS, worker) pair, in round-robin order from C->start: bit i of
-// the returned mask (i = position in that order) is set when the pair's next round is posted in
-// full.  Lane i first loads ONE probe word per pair — the pair's last slice — and only pairs
-// whose probe landed are checked in full (64 lanes x 8 slices per batch, resuming at seen[q],
-// the first slice not yet seen posted, in this wave's LDS).  Polling every slice of every pair
-// on every sweep (round 5's first version) put ~400 uncached loads per sweep on the memory
-// system for as long as a claim kernel waited, and slowed the GEMMs of a co-located rank 3x
-// (one-card W = 2 async: 1.03 vs 0.62 ms/step with the host-scan service).
-DDL_DEV uint64_t claim_sweep(const AsyncTable& T, const ClaimState* C, const uint32_t* posted,
-                             int* seen, int pairs) {
-  const int lane = threadIdx.x & 63, world = C->world;
-  bool probe = false;
-  if (lane < pairs) {
-    int q = C->start + lane;
-    if (q >= pairs) q -= pairs;
-    const int pl = q / world, w = q - pl * world;
-    const AsyncShard& S = T.shard[C->ps[pl]];
-    const uint32_t e = C->last[w * kAsyncMaxPs + pl] + 1;
-    const uint32_t f = __hip_atomic_load(posted + posted_dev_idx(S, w, S.nslice - 1),
-                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    probe = (int32_t)(f - e) >= 0;
-  }
-  uint64_t cand = __ballot(probe), done = 0;
-  while (cand) {
-    const int i = __builtin_ctzll(cand);
-    cand &= cand - 1;
-    int q = C->start + i;
-    if (q >= pairs) q -= pairs;
-    const int pl = q / world, w = q - pl * world;
-    const AsyncShard& S = T.shard[C->ps[pl]];
-    const uint32_t e = C->last[w * kAsyncMaxPs + pl] + 1;
-    int k0 = seen[q];
-    bool all = true;
-    while (all && k0 < S.nslice) {  // 512 slices per batch
-      uint32_t v[8];
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const int j = k0 + b * 64 + lane;
-        v[b] = j < S.nslice ? __hip_atomic_load(posted + posted_dev_idx(S, w, j),
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                            : e;
-      }
-      bool ok = true;
-#pragma unroll
-      for (int b = 0; b < 8; ++b) ok &= (int32_t)(v[b] - e) >= 0;
-      all = __all(ok);
-      if (all) k0 += 512;
-    }
-    if (all) done |= 1ull << i;
-    else if (lane == 0) seen[q] = k0;  // (a batch that failed is re-read from its start)
-    __builtin_amdgcn_wave_barrier();
-  }
-  return done;
-}
-
-// One wave (lanes 0-63 of the calling workgroup) claims the complete arrivals into C's batch.
-// (pairs beyond 64 in scan order wait for a later claim kernel)
-DDL_DEV void claim_body(const AsyncTable& T, ClaimState* __restrict__ C) {
-  const int lane = threadIdx.x & 63;
-  const int world = C->world, pairs = C->nh * C->world;
-  const uint32_t* posted = T.flags[C->me];
-  const long long deadline = wall_clock64() + C->idle_ticks;
-  __shared__ int seen[kAsyncMaxPs * kXgmiMaxPeers];
-  for (int q = lane; q < pairs; q += 64) seen[q] = 0;
-  __builtin_amdgcn_wave_barrier();
-  uint64_t done = 0;
-  for (int it = 0;; ++it) {
-    done = claim_sweep(T, C, posted, seen, pairs);
-    if (done) break;
-    if ((it & 15) == 15) {
-      if (__hip_atomic_load(C->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
-      if (__hip_atomic_load(C->host + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
-      if (wall_clock64() > deadline) break;
-    }
-    // ~0.45 us between sweeps: the claim wave polls while the backward's GEMMs run, and a
-    // tighter poll loop measurably slows them (the READY gate's lesson, runner.hip)
-    __builtin_amdgcn_s_sleep(16);
-  }
-  if (lane != 0) return;
-  int nb = 0, next = C->start;
-  for (int i = 0; i < pairs && i < 64 && nb < kClaimBatch; ++i) {
-    if (!((done >> i) & 1)) continue;
-    int q = C->start + i;
-    if (q >= pairs) q -= pairs;
-    const int pl = q / world, w = q - pl * world;
-    const int64_t t = C->t[pl] + 1;
-    const int64_t idx = t - C->t0[pl] - 1;
-    if (idx < 0 || idx >= C->per_ps) {
-      // more arrivals than the service was started for: a protocol error, not an update
-      __hip_atomic_store(C->err, 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      break;
-    }
-    const uint32_t e = C->last[w * kAsyncMaxPs + pl] + 1;
-    C->t[pl] = t;
-    C->last[w * kAsyncMaxPs + pl] = e;
-    C->b_pl[nb] = pl;
-    C->b_w[nb] = w;
-    C->b_e[nb] = e;
-    C->b_lr[nb] = C->lr_tab[(int64_t)pl * C->per_ps + idx];
-    if (C->prov) {
-      int32_t* r = C->prov + C->claims * 4;
-      r[0] = w;
-      r[1] = C->ps[pl];
-      r[2] = (int32_t)e;
-      r[3] = (int32_t)t;
-    }
-    C->claims += 1;
-    ++nb;
-    next = q + 1 < pairs ? q + 1 : 0;
-  }
-  // (more than 64 pairs: an empty claim moves the 64-pair window on, so no pair waits forever)
-  C->start = nb > 0 ? next : (pairs > 64 ? (C->start + 64) % pairs : C->start);
-  C->nb = nb;
-  C->ended += 1;
-}
-
-__global__ void __launch_bounds__(64) async_claim_kernel(const AsyncTable* __restrict__ Tp,
-                                                         ClaimState* __restrict__ C) {
-  claim_body(*Tp, C);
-  // the host-visible copies of these counters: stored by the apply kernel behind (default), or
-  // here (DDL_ASYNC_PUBLISH=claim: holds this kernel's end, and so the apply's start, for a
-  // PCIe round trip)
-  if (threadIdx.x == 0 && C->publish_in_claim) publish_claim(C);
-}
-
-// Slice j of hosted PS pl for every claim of the batch on that PS, in claim order.
-DDL_DEV void apply_batch_body(const AsyncTable& T, const ClaimState* C, int pl, int j,
-                              const int (&cl)[kClaimBatch], int nc) {
-  const int ps = C->ps[pl], me = C->me;
-  const AsyncShard& S = T.shard[ps];
-  const int tid = threadIdx.x;
-  const int64_t s0 = (int64_t)j * S.slice;
-  const int64_t s1 = s0 + S.slice < S.n ? s0 + S.slice : S.n;
-  const int n4 = s0 < s1 ? (int)((s1 - s0) >> 2) : 0;
-  float4* w4 = reinterpret_cast<float4*>(C->params[pl] + s0);
-  float4* m4 = reinterpret_cast<float4*>(C->m[pl] + s0);
-  float4* v4 = C->v[pl] ? reinterpret_cast<float4*>(C->v[pl] + s0) : nullptr;
-  const int opt = C->opt;
-  const float c1 = C->c1, c2 = C->c2, eps = C->eps, lr = C->lr, mu = C->mu, sc = C->scale;
-  for (int i = tid; i < n4; i += 256) {
-    float4 w = w4[i];
-    float4 M = opt != 2 ? m4[i] : f4zero();
-    float4 V = opt == 0 ? v4[i] : f4zero();
-    for (int k = 0; k < nc; ++k) {
-      const int c = cl[k], wk = C->b_w[c];
-      const float* src = T.elide && wk == me
-                             ? T.grads + S.lo + s0  // the host's own push: no inbox copy
-                             : T.inbox[me] + S.inbox_off + (int64_t)wk * S.n + s0;
-      const float4 g = bload4_sys(make_rsrc(src, (uint32_t)n4 * 16u), i * 16);
-      if (opt == 0) {
-        const float lt = C->b_lr[c];
-        adam1(w.x, g.x * sc, M.x, V.x, lt, c1, c2, eps);
-        adam1(w.y, g.y * sc, M.y, V.y, lt, c1, c2, eps);
-        adam1(w.z, g.z * sc, M.z, V.z, lt, c1, c2, eps);
-        adam1(w.w, g.w * sc, M.w, V.w, lt, c1, c2, eps);
-      } else if (opt == 1) {
-        momentum1(w.x, g.x, M.x, lr, mu, sc);
-        momentum1(w.y, g.y, M.y, lr, mu, sc);
-        momentum1(w.z, g.z, M.z, lr, mu, sc);
-        momentum1(w.w, g.w, M.w, lr, mu, sc);
-      } else {
-        w = g;
-      }
-      // the worker gets the parameters right after ITS update (the reference's Send back)
-      bstore4_sys(make_rsrc(T.params[wk] + S.lo + s0, (uint32_t)n4 * 16u), i * 16, w);
-    }
-    w4[i] = w;
-    if (opt != 2) m4[i] = M;
-    if (opt == 0) v4[i] = V;
-  }
-  drain_vm();
-  __syncthreads();
-  if (tid < nc) {
-    const int c = cl[tid];
-    flag_store(T.flags[C->b_w[c]] + done_dev_idx(S, j), C->b_e[c]);     // the worker's gate
-    flag_store(T.done + done_word(C->b_w[c], ps, j), C->b_e[c]);        // the worker's host
-  }
-}
-
-// One block per hosted slice (grid = blk0[nh]); block 0 also publishes the host counters.
-__global__ void __launch_bounds__(256) async_claimed_apply_kernel(const AsyncTable* __restrict__ Tp,
-                                                                  const ClaimState* __restrict__ C) {
-  const int b = blockIdx.x;
-  const int nb = C->nb;
-  if (nb > 0) {
-    int pl = 0;
-    while (pl + 1 < C->nh && b >= C->blk0[pl + 1]) ++pl;
-    int cl[kClaimBatch];
-    int nc = 0;
-    for (int c = 0; c < nb; ++c)
-      if (C->b_pl[c] == pl) cl[nc++] = c;
-    if (nc > 0) apply_batch_body(*Tp, C, pl, b - C->blk0[pl], cl, nc);
-  }
-  if (b == 0 && threadIdx.x == 0 && !C->publish_in_claim) publish_claim(C);
 }
 
 // The worker's pull as a GPU-side gate (async_runner.hip): one wave on the compute stream,
@@ -794,7 +516,6 @@ bool AsyncPeer::push_tail(const std::vector<int>& ps, uint32_t epoch, UpdTail& o
                                           : table_.inbox[S.host] + S.inbox_off + (int64_t)rank_ * S.n;
     q.n = S.n;
     q.posted = table_.posted + posted_word(p, rank_, 0);
-    q.arrive = table_.flags[S.host] + posted_dev_idx(S, rank_, 0);  // the host's device copy
     q.slice4 = (int)(S.slice / 4);
     q.nslice = S.nslice;
     q.blk0 = blk;
@@ -938,9 +659,6 @@ AsyncService::AsyncService(AsyncPeer* peer, int world, int device,
     if (s.ps < 0 || s.ps >= peer->num_ps() || !s.params || !s.m || (opt == 0 && !s.v))
       throw std::invalid_argument("async service: PS state");
   epoch_.assign((size_t)world * kAsyncMaxPs, epoch0);
-  if (const char* c = getenv("DDL_ASYNC_CLAIM")) claim_ = atoi(c) != 0;
-  if (const char* d = getenv("DDL_ASYNC_CLAIM_DEPTH")) depth_ = std::max(1, atoi(d));
-  if (const char* u = getenv("DDL_ASYNC_CLAIM_IDLE_US")) idle_us_ = std::max(10.0, atof(u));
   if ((int)ps.size() > kAsyncMaxPs) throw std::invalid_argument("async service: too many PS");
 }
 
@@ -950,26 +668,14 @@ AsyncService::~AsyncService() {
     (void)hipStreamSynchronize(stream_);
     (void)hipStreamDestroy(stream_);
   }
-  free_claim();
-}
-
-void AsyncService::free_claim() {
-  if (cs_dev_) (void)hipFree(cs_dev_);
-  if (lr_tab_) (void)hipFree(lr_tab_);
-  if (prov_dev_) (void)hipFree(prov_dev_);
-  if (host_words_) (void)hipHostFree(host_words_);
-  cs_dev_ = nullptr;
-  lr_tab_ = nullptr;
-  prov_dev_ = nullptr;
-  host_words_ = nullptr;
 }
 
 void AsyncService::start(int64_t expected) {
   if (th_.joinable()) throw std::runtime_error("async service already running");
   X_CHECK(hipSetDevice(device_));
-  // HIGH priority: HIP pools hardware queues per priority, so the applies (and the claim
-  // kernels in front of them) never share a queue with the compute stream, where the worker's
-  // GPU-side pull gate may be waiting for them (async_runner.hip)
+  // HIGH priority: HIP pools hardware queues per priority, so the applies never share a queue
+  // with the compute stream, where the worker's GPU-side pull gate may be waiting for them
+  // (async_runner.hip)
   // (DDL_ASYNC_PS_PRIORITY=low: the least priority instead — also a pool of its own, so the
   // deadlock argument holds; the dispatcher then prefers the compute stream's waves over the
   // overlapped applies)
@@ -979,123 +685,7 @@ void AsyncService::start(int64_t expected) {
   const int prio = pp && std::string(pp) == "low" ? lo : hi;
   if (!stream_) X_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, prio));
   expected_ = expected;
-  const int nh = (int)ps_.size();
-  if (claim_ && nh > 0 && expected % nh == 0) {
-    // every hosted PS serves the same number of arrivals (W x steps): one step-size table row
-    // each, filled with the host service's formula (double precision, rounded once)
-    free_claim();
-    const int64_t per_ps = expected / nh;
-    std::vector<float> tab((size_t)nh * per_ps);
-    for (int i = 0; i < nh; ++i)
-      for (int64_t k = 0; k < per_ps; ++k) {
-        const double t = (double)(ps_[i].t + 1 + k);
-        tab[(size_t)i * per_ps + k] =
-            (float)((double)lr_ * std::sqrt(1.0 - std::pow((double)b2_, t)) /
-                    (1.0 - std::pow((double)b1_, t)));
-      }
-    X_CHECK(hipMalloc(reinterpret_cast<void**>(&lr_tab_), tab.size() * sizeof(float)));
-    X_CHECK(hipMemcpy(lr_tab_, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice));
-    if (keep_prov_)
-      X_CHECK(hipMalloc(reinterpret_cast<void**>(&prov_dev_), (size_t)expected * 16));
-    X_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_words_), (8 + kAsyncMaxPs) * 8,
-                          hipHostMallocDefault));
-    memset(host_words_, 0, (8 + kAsyncMaxPs) * 8);
-    auto cs = std::make_unique<ClaimState>();
-    memset(cs.get(), 0, sizeof(ClaimState));
-    cs->me = peer_->rank_;
-    cs->world = world_;
-    cs->nh = nh;
-    cs->per_ps = (int)std::min<int64_t>(per_ps, 0x7fffffff);
-    cs->opt = opt_;
-    cs->blk0[0] = 0;
-    for (int i = 0; i < nh; ++i) {
-      cs->blk0[i + 1] = cs->blk0[i] + peer_->table_.shard[ps_[i].ps].nslice;
-      cs->ps[i] = ps_[i].ps;
-      cs->params[i] = ps_[i].params;
-      cs->m[i] = ps_[i].m;
-      cs->v[i] = ps_[i].v;
-      cs->t0[i] = cs->t[i] = ps_[i].t;
-      host_words_[8 + i] = ps_[i].t;
-      for (int w = 0; w < world_; ++w) cs->last[w * kAsyncMaxPs + i] = epoch_[(size_t)w * kAsyncMaxPs + ps_[i].ps];
-    }
-    cs->lr_tab = lr_tab_;
-    cs->prov = prov_dev_;
-    void* hd = nullptr;
-    X_CHECK(hipHostGetDevicePointer(&hd, host_words_, 0));
-    cs->host = reinterpret_cast<int64_t*>(hd);
-    X_CHECK(hipHostGetDevicePointer(&hd, peer_->err_, 0));
-    cs->err = reinterpret_cast<int*>(hd);
-    cs->c1 = 1.f - b1_;
-    cs->c2 = 1.f - b2_;
-    cs->eps = eps_;
-    cs->lr = lr_;
-    cs->mu = mu_;
-    cs->scale = scale_;
-    cs->idle_ticks = (long long)(idle_us_ * 100.0);  // wall_clock64: 100 MHz
-    const char* pub = getenv("DDL_ASYNC_PUBLISH");
-    cs->publish_in_claim = pub && std::string(pub) == "claim";
-    X_CHECK(hipMalloc(reinterpret_cast<void**>(&cs_dev_), sizeof(ClaimState)));
-    X_CHECK(hipMemcpy(cs_dev_, cs.get(), sizeof(ClaimState), hipMemcpyHostToDevice));
-    th_ = std::thread([this] { run_claim(); });
-    return;
-  }
-  claim_ = false;
   th_ = std::thread([this] { run(); });
-}
-
-// The thread of the device-side service: keep `depth_` claim + apply pairs in flight, never more
-// than the arrivals still to come (each pair claims at most one), and report errors.  It polls
-// two pinned words every ~20 us: nothing it does is on a worker's critical path any more.
-void AsyncService::run_claim() {
-  try {
-    X_CHECK(hipSetDevice(device_));
-    const AsyncTable* T = peer_->table_dev_;
-    int nblk = 0;  // every hosted slice: the apply grid
-    for (const auto& s : ps_) nblk += peer_->table_.shard[s.ps].nslice;
-    int64_t enq = 0, last_claims = 0;
-    auto idle_since = std::chrono::steady_clock::now();
-    TraceRange wait_range("ddl.async.ps.claim_service");
-    for (;;) {
-      // ended first, then claims: a pair that ends between the two reads is counted as
-      // outstanding AND its claim as done (conservative: never one pair too many)
-      const int64_t ended = __atomic_load_n(host_words_ + 0, __ATOMIC_ACQUIRE);
-      const int64_t claims = __atomic_load_n(host_words_ + 1, __ATOMIC_ACQUIRE);
-      if (claims >= expected_) break;
-      if (const int err = peer_->error())
-        throw std::runtime_error("async PS: kernel error (code " + std::to_string(err) + ")");
-      {
-        std::lock_guard<std::mutex> hold(pause_mu_);  // pause(): nothing enqueued while paused
-        while (enq - ended < depth_ && enq - ended < expected_ - claims) {
-          hipLaunchKernelGGL(async_claim_kernel, dim3(1), dim3(64), 0, stream_, T, cs_dev_);
-          DDL_CHECK_LAUNCH();
-          hipLaunchKernelGGL(async_claimed_apply_kernel, dim3(nblk), dim3(256), 0, stream_, T,
-                             cs_dev_);
-          DDL_CHECK_LAUNCH();
-          ++enq;
-        }
-      }
-      const auto now = std::chrono::steady_clock::now();
-      if (claims != last_claims) {
-        last_claims = claims;
-        idle_since = now;
-      } else if (std::chrono::duration<double>(now - idle_since).count() > 600.0) {
-        throw std::runtime_error("async PS: no arrival within 600 s");
-      }
-      std::this_thread::sleep_for(std::chrono::microseconds(20));
-    }
-    X_CHECK(hipStreamSynchronize(stream_));
-    if (prov_dev_ && keep_prov_) {
-      std::vector<int32_t> r((size_t)expected_ * 4);
-      X_CHECK(hipMemcpy(r.data(), prov_dev_, r.size() * 4, hipMemcpyDeviceToHost));
-      for (int64_t k = 0; k < expected_; ++k)
-        prov_.push_back({r[k * 4], r[k * 4 + 1], r[k * 4 + 2], r[k * 4 + 3]});
-    }
-    if (const int err = peer_->error())
-      throw std::runtime_error("async PS: kernel error (code " + std::to_string(err) + ")");
-  } catch (const std::exception& ex) {
-    error_ = ex.what();
-    if (stream_) (void)hipStreamSynchronize(stream_);  // no pair left running on an error path
-  }
 }
 
 void AsyncService::serve(AsyncPsState& st, int w) {
@@ -1182,9 +772,6 @@ void AsyncService::join() {
 
 void AsyncService::pause() {
   pause_mu_.lock();
-  // device-side service: `hold` ends every queued claim kernel without a claim (a claim already
-  // taken still applies before the stream drains), and the thread enqueues nothing until resume
-  if (host_words_) __atomic_store_n(host_words_ + 2, (int64_t)1, __ATOMIC_RELEASE);
   if (stream_) {
     const hipError_t e = hipStreamSynchronize(stream_);
     if (e != hipSuccess) {
@@ -1195,21 +782,18 @@ void AsyncService::pause() {
 }
 
 void AsyncService::resume() {
-  if (host_words_) __atomic_store_n(host_words_ + 2, (int64_t)0, __ATOMIC_RELEASE);
   pause_mu_.unlock();
 }
 
 int64_t AsyncService::t(int ps) const {
   for (size_t i = 0; i < ps_.size(); ++i)  // lock-free: also read while paused
     if (ps_[i].ps == ps)
-      return claim_ && host_words_ ? __atomic_load_n(host_words_ + 8 + i, __ATOMIC_ACQUIRE)
-                                   : __atomic_load_n(&ps_[i].t, __ATOMIC_ACQUIRE);
+      return __atomic_load_n(&ps_[i].t, __ATOMIC_ACQUIRE);
   throw std::invalid_argument("async service: PS not hosted here");
 }
 
 int64_t AsyncService::served() const {
-  return claim_ && host_words_ ? __atomic_load_n(host_words_ + 1, __ATOMIC_ACQUIRE)
-                               : served_.load();
+  return served_.load();
 }
 
 }  // namespace ddl

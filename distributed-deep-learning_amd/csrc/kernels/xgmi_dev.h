@@ -1,6 +1,5 @@
-// Device side of the xGMI peer-memory flag protocol (xgmi.hip header comment), shared by the
-// bucket kernels of xgmi.hip and the replicated last bucket fused into conv1's weight-gradient
-// launch (conv1.h conv1_wgrad_xgmi_kernel).
+// Device side of the xGMI peer-memory flag protocol (xgmi.hip header comment): flag stores,
+// bounded waits and the final DONE wait of the bucket kernels.
 #pragma once
 #include "api.h"
 #include "common.h"
@@ -12,23 +11,14 @@ namespace ddl {
 // barrier that precedes the flag store: a write-through store is counted complete only once the
 // memory side (local HBM, or the peer over xGMI, or host memory) has acknowledged it, so the
 // payload is globally visible before the flag is issued — no L2 write-back is needed (the CDNA
-// guide's G16 write-through hand-off, at system scope).  DDL_XGMI_RELEASE=1 adds the full
-// system release anyway (L2 write-back + wait, as one asm statement: hipcc drops the wait of its
-// own release when the scoreboard is already drained, and schedules a separate asm wait above
-// the write-back); it writes back every dirty line of the XCD's L2 at each flag — the GEMMs'
-// output included — and measured 3.2 -> 5.4 ms/step on the two-ranks-on-one-GPU rehearsal.
-#ifndef DDL_XGMI_RELEASE
-#define DDL_XGMI_RELEASE 0
-#endif
-#ifndef DDL_XGMI_POLL_TIGHT
-#define DDL_XGMI_POLL_TIGHT 0
-#endif
+// guide's G16 write-through hand-off, at system scope).  A full system release at each flag (L2
+// write-back + wait) writes back every dirty line of the XCD's L2 — the GEMMs' output included —
+// and measured 3.2 -> 5.4 ms/step on the two-ranks-on-one-GPU rehearsal (round 2).
 
 DDL_DEV uint32_t xg_flag_load(const uint32_t* f) {
   return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 DDL_DEV void xg_flag_store(uint32_t* f, uint32_t v) {
-  if (DDL_XGMI_RELEASE) asm volatile("buffer_wbl2 sc0 sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -58,13 +48,9 @@ DDL_DEV bool xg_wait_ge(const uint32_t* f, uint32_t target, long long deadline, 
     }
     // tight for the first ~64 polls (a peer's flag normally lands within a few us), then
     // ~0.45 us apart: waiting waves that poll hard slow the GEMMs running beside them
-    // (docs/DESIGN.md round 5, one-card async).  DDL_XGMI_POLL_TIGHT=1 (compile-time): always tight
-#if DDL_XGMI_POLL_TIGHT
-    __builtin_amdgcn_s_sleep(2);
-#else
+    // (docs/DESIGN.md round 5, one-card async)
     if (it < 64) __builtin_amdgcn_s_sleep(2);
     else __builtin_amdgcn_s_sleep(16);
-#endif
   }
   return true;
 }

@@ -74,14 +74,6 @@ class HipEngine:
     def get_cfg(self) -> List[int]:
         return list(self.eng.get_cfg())
 
-    def set_workers(self, workers: List[int]) -> None:
-        """Per-op stream-K worker counts (0 = split-K by `splits`; csrc/kernels/gemm.h)."""
-        self.eng.set_workers(list(workers))
-        self.graphs = None
-
-    def get_workers(self) -> List[int]:
-        return list(self.eng.get_workers())
-
     def set_wide(self, wide: List[int]) -> None:
         """Per-op split-K reduce threshold: splits > wide[op] use the separate wide-reduce
         kernel, otherwise the in-launch last-arriver reduction (csrc/kernels/gemm.h)."""
@@ -89,15 +81,6 @@ class HipEngine:
 
     def get_wide(self) -> List[int]:
         return list(self.eng.get_wide())
-
-    def set_order(self, order: List[int]) -> None:
-        """Per-op split-K block order: 0 round-robin over the XCDs, 1-3 XCD-contiguous with the
-        K splits / M rows / N tiles grouped on one XCD (csrc/kernels/gemm.h split_coords)."""
-        self.eng.set_order(list(order))
-        self.graphs = None
-
-    def get_order(self) -> List[int]:
-        return list(self.eng.get_order())
 
     def set_concurrent(self, on: bool) -> None:
         """Weight-gradient GEMMs on a second stream (fork/join per backward segment)."""

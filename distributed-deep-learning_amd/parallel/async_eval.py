@@ -40,12 +40,10 @@ class AsyncEvaluator:
         self.on_result = on_result
         dev = tr.params.device
         # Stream priorities.  torch's HIP stream pool offers priorities <= 0 only (a positive
-        # request maps to 0), so "low" does not exist here: by default (DDL_EVAL_PRIORITY=train)
-        # the eval stream and the training stream are both NORMAL priority (0) and share the
-        # normal hardware-queue pool; with =eval the eval stream is HIGH priority (-1), so when a
-        # CU frees up the dispatcher prefers the eval's GEMMs (the evals are the time-to-accuracy
-        # critical path).  Measured the same time to 95 % either way (0.1404-0.1417 vs
-        # 0.1415-0.1422 s, profiles/r3_ab_evalprio.log).
+        # request maps to 0), so "low" does not exist here: the eval stream and the training
+        # stream are both NORMAL priority (0) and share the normal hardware-queue pool (a HIGH
+        # priority eval stream measured the same time to 95 %: 0.1404-0.1417 vs 0.1415-0.1422 s,
+        # profiles/r3_ab_evalprio.log).
         # The training stream is NORMAL priority in both modes: the native runners' GPU-side
         # gates rely on the training (compute) stream never sharing a hardware queue with their
         # high-priority comm / PS-service streams, and HIP pools hardware queues per priority
@@ -54,8 +52,7 @@ class AsyncEvaluator:
         # (torch's pooled streams: the pool is fixed per device and priority, so evaluators
         # built one after another reuse the same streams and hardware queues; destroying an
         # external stream instead left the caching allocator's blocks tied to a dead stream)
-        eval_first = os.environ.get("DDL_EVAL_PRIORITY", "train") == "eval"
-        self.stream = torch.cuda.Stream(device=dev, priority=-1 if eval_first else 0)
+        self.stream = torch.cuda.Stream(device=dev, priority=0)
         self.train_stream = torch.cuda.Stream(device=dev, priority=0)
         self.snap = torch.empty_like(tr.params)
         chunk = int(os.environ.get("DDL_EVAL_CHUNK", "10000"))

@@ -213,7 +213,7 @@ class AsyncPeerExchange:
             self.peer, self.env.world, ps_list, self.opt, h.lr, h.beta1, h.beta2, h.eps, mom,
             self.grad_scale, 1, self.check_provenance)
         self._svc.start(n)
-        self.service_mode = self._svc.mode()  # "device-claim" (default) or "host"
+        self.service_mode = self._svc.mode()  # "host": the native board-scan service
 
     def _sync_counters(self, svc) -> None:
         """The native service advances each hosted PS's step counter; mirror it into the

@@ -132,8 +132,8 @@ class NativeSyncExchange(SyncExchange):
             if not ok:
                 raise RuntimeError(f"RCCL 1-rank self-test failed: {why}")
         seg_sets = [set(s) for s in segments]
-        # DDL_SEG_ISSUE="a,b,c,d": the backward segment after which each segment's units are
-        # issued.  Every issue point costs an event record on the compute stream (~4.5 us gap,
+        # issue_after[s]: the backward segment after which segment s's units are issued.
+        # Every issue point costs an event record on the compute stream (~4.5 us gap,
         # forced-rehearsal timeline), so the RCCL path issues the fc bucket together with conv4's
         # after segment 1 (still overlapped by the conv3 + conv2 backward): forced 1-rank
         # rehearsal 0.405 -> 0.3965 ms/step.  The xGMI kernels are one launch per bucket with no
@@ -142,11 +142,6 @@ class NativeSyncExchange(SyncExchange):
         issue_after = list(range(len(seg_sets)))
         if self.backend == "rccl" and len(seg_sets) == 4:
             issue_after = [1, 1, 2, 3]
-        env_map = os.environ.get("DDL_SEG_ISSUE")
-        if env_map:
-            m = [int(v) for v in env_map.split(",")]
-            if len(m) == len(seg_sets) and all(i <= j < len(seg_sets) for i, j in enumerate(m)):
-                issue_after = m
 
         def seg_of(tensors):
             if not overlap:
@@ -257,7 +252,7 @@ class NativeSyncExchange(SyncExchange):
             peer = ops.PeerExchange(params, grads, env.world, env.rank, buckets, slices,
                                     self.repl[0] if self.repl is not None else -1)
             mine = peer.handle()
-        except RuntimeError as e:
+        except (RuntimeError, ValueError) as e:  # (pybind11: invalid_argument -> ValueError)
             mine, why = None, str(e)
         agree(mine is not None, why, "xGMI buffer export")
         handles = [mine]
@@ -267,7 +262,7 @@ class NativeSyncExchange(SyncExchange):
         try:
             peer.open(handles)
             why = ""
-        except RuntimeError as e:
+        except (RuntimeError, ValueError) as e:
             why = str(e)
         agree(not why, why, "xGMI peer mapping")
         self.runner.set_peer(peer)
@@ -277,12 +272,27 @@ class NativeSyncExchange(SyncExchange):
         i = torch.arange(n, device=params.device)
         pat = (i % 13 + 1).to(torch.float32)
         grads.copy_(pat * float(env.rank + 1))
+        want = pat * float(env.world * (env.world + 1) // 2)
+        # The stale-L2 probe (must stay: it is the one check between a real node and silent
+        # replica drift).  Peers store the new parameters into this GPU's HBM over xGMI; none of
+        # those stores passes through this GPU's per-XCD L2s, and the protocol relies on the next
+        # kernel's start-of-kernel acquire to drop any line cached before the exchange
+        # (xgmi.hip header).  So before the exchange EVERY XCD reads (caches) EVERY parameter
+        # line, and after it every XCD compares every line with the expected sums: a line served
+        # stale from some XCD's L2 counts as a mismatch (ops.xcd_sweep, xgmi.hip).
+        probe = torch.zeros(2, dtype=torch.int32, device=params.device)
+        ops.xcd_sweep(params, None, probe)
         torch.cuda.synchronize(params.device)
         self.runner.peer_selftest_step()
-        want = pat * float(env.world * (env.world + 1) // 2)
         ok, why = True, ""
+        if not peer.error():
+            ops.xcd_sweep(params, want, probe)
+            torch.cuda.synchronize(params.device)
         if peer.error():
             ok, why = False, f"timed out (code {peer.error()})"
+        elif int(probe[0].item()) != 0:
+            ok, why = False, (f"{int(probe[0].item())} stale parameter reads across the XCDs "
+                              f"after the exchange (L2 not invalidated)")
         else:
             spans = ([r for runs, _, _ in specs for r in runs] if specs is not None
                      else plan.bucket_ranges)
@@ -334,7 +344,7 @@ class NativeSyncExchange(SyncExchange):
                     dst.copy_(src)
         torch.cuda.synchronize(self.params.device)
 
-    def handoff_check(self, trainer, steps: int = 6) -> dict:
+    def handoff_check(self, trainer, steps: int = 6, _perturb_rank=None) -> dict:
         """Prove the READY-flag hand-off on THIS job before trusting it.
 
         The comm stream's exchange of segment s starts behind a READY flag that the next
@@ -344,7 +354,10 @@ class NativeSyncExchange(SyncExchange):
         state, ``steps`` steps with the event hand-off (system fence) and ``steps`` steps with
         the READY flags, a SHA-256 of the resulting parameters on every rank; the flags are kept
         only if both modes give the same bits and every rank agrees, otherwise every rank falls
-        back to the events.  The state (parameters, PS m / v / t, replicated state) is restored
+        back to the events.  If the ranks' digests disagree under the EVENT hand-off too, the
+        replicas have diverged — not a hand-off-ordering problem, so events cannot repair it:
+        every rank raises NativeUnavailable and the job refuses this data plane
+        (``handoff_vote``).  The state (parameters, PS m / v / t, replicated state) is restored
         afterwards — with the trainer's global step (its dropout seeds) — so the caller's run
         starts where it would have."""
         import hashlib
@@ -367,20 +380,15 @@ class NativeSyncExchange(SyncExchange):
         finally:
             self._restore(snap)
             trainer.global_step = g0
-        same = digests["events"] == digests["ready_flags"]
-        votes = [(same, digests["ready_flags"])]
-        if self.env.world > 1:
-            votes = [None] * self.env.world
-            dist.all_gather_object(votes, (same, digests["ready_flags"]))
-        modes_agree = all(v[0] for v in votes)
-        ranks_agree = len({v[1] for v in votes}) == 1
-        ok = modes_agree and ranks_agree
+        if _perturb_rank is not None and self.env.rank == _perturb_rank:  # (test hook)
+            digests = {k: "0" * 64 for k in digests}
+        v = handoff_vote(self.env, digests["events"], digests["ready_flags"])
         forced = os.environ.get("DDL_READY_FLAGS")  # an explicit choice stays in force
-        self.runner.set_ready_flags(int(forced) if forced is not None else (2 if ok else 0))
-        return {"handoff": ("ready_flags" if ok else "events (READY flags failed the check)")
+        self.runner.set_ready_flags(int(forced) if forced is not None else (2 if v["ok"] else 0))
+        return {"handoff": ("ready_flags" if v["ok"] else "events (READY flags failed the check)")
                 + (f" (DDL_READY_FLAGS={forced} in force)" if forced is not None else ""),
-                "check_steps": steps, "modes_bit_identical": modes_agree,
-                "ranks_bit_identical": ranks_agree,
+                "check_steps": steps, "modes_bit_identical": v["modes_agree"],
+                "ranks_bit_identical": v["ranks_agree"],
                 "params_sha256": digests["ready_flags"][:16]}
 
     # -- replicated last bucket <-> the PS objects (checkpoint / resume) ---------------------------
@@ -433,6 +441,33 @@ class NativeSyncExchange(SyncExchange):
         self.runner.close()
         if self.peer is not None:
             self.peer.close()
+
+
+def handoff_vote(env, digest_events: str, digest_flags: str) -> dict:
+    """The collective verdict of a hand-off check (every rank calls it with its own digests of
+    the same steps from the same state).
+
+    * every rank's event-hand-off digest equal, and each rank's two modes equal: the READY flags
+      are proven on this job (ok);
+    * event digests equal across ranks, but the READY-flag run differs somewhere: the flags are
+      what diverged, so every rank falls back to the events (not ok);
+    * event digests differ across ranks: the replicas of a synchronous PS step diverged under
+      the reference hand-off itself.  That is not an ordering problem — events cannot repair it
+      — so every rank raises NativeUnavailable (the caller drops this data plane)."""
+    votes = [(digest_events, digest_flags)]
+    if env.world > 1:
+        votes = [None] * env.world
+        dist.all_gather_object(votes, (digest_events, digest_flags))
+    events_agree = len({v[0] for v in votes}) == 1
+    modes_agree = all(v[0] == v[1] for v in votes)
+    ranks_agree = events_agree and len({v[1] for v in votes}) == 1
+    if not events_agree:
+        bad = sorted({r for r, v in enumerate(votes) if v[0] != votes[0][0]} | {0})
+        raise NativeUnavailable(
+            f"replicas diverge across ranks under the event hand-off (ranks {bad} disagree): "
+            f"refusing this data plane")
+    return {"ok": modes_agree and ranks_agree, "modes_agree": modes_agree,
+            "ranks_agree": ranks_agree}
 
 
 def make_sync_exchange(plan, env, params, grads, segments, servers, engine, cfg, hyper):

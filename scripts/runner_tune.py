@@ -17,7 +17,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from op_bench import OPS  # noqa: E402
 
-STREAMK_OK = {1, 2, 3, 10, 11, 12, 13, 14, 15}  # conv GEMMs (K-mapped stream-K on the tap windows)
 KWAVE_OK = {4, 5, 6, 8}  # fc forward / data-gradient GEMMs (csrc/kernels/layers.h KWaveOK)
 MF16_OK = {1, 2, 3, 10, 11, 12, 13, 14, 15}  # conv GEMMs with 16-byte gathers (layers.h Mf16OK)
 
@@ -34,8 +33,7 @@ def main():
                          "forward convolutions (not dual-launched, so any tile config runs)")
     ap.add_argument("--verbose", action="store_true", help="print every candidate's time")
     ap.add_argument("--dma", action="store_true",
-                    help="also try the generic LDS-DMA multi-fragment tiles (configs 16-18) on "
-                         "the conv GEMMs, at 0.5x / 1x / 2x / 4x the split")
+                    help="also try the 16x16x4 tile (config 14) at 0.5x and 4x the split")
     a = ap.parse_args()
     import torch
     from ddl_amd.config import TrainConfig
@@ -49,14 +47,12 @@ def main():
     tr = Trainer(cfg, env, dataset=synthetic_mnist())
     e = tr.engine.eng
     W = 1 << 20
-    cur = {"cfg": e.get_cfg(), "splits": e.get_splits(), "workers": e.get_workers(),
-           "wide": e.get_wide()}
+    cur = {"cfg": e.get_cfg(), "splits": e.get_splits(), "wide": e.get_wide()}
     step = [0]
 
     def apply(s):
         e.set_cfg(s["cfg"])
         e.set_splits(s["splits"])
-        e.set_workers(s["workers"])
         e.set_wide(s["wide"])
 
     def timed(s):
@@ -73,34 +69,27 @@ def main():
         return 1e6 * (time.perf_counter() - t0) / a.steps
 
     def cands(op):
-        c, s, w, wd = cur["cfg"][op], cur["splits"][op], cur["workers"][op], cur["wide"][op]
+        c, s, wd = cur["cfg"][op], cur["splits"][op], cur["wide"][op]
         out = []
 
-        def mk(c2, s2, w2, wd2):
+        def mk(c2, s2, _w, wd2):
             d = {k: list(v) for k, v in cur.items()}
-            d["cfg"][op], d["splits"][op], d["workers"][op], d["wide"][op] = c2, s2, w2, wd2
+            d["cfg"][op], d["splits"][op], d["wide"][op] = c2, s2, wd2
             return d
         for s2 in {max(1, s // 2), min(2048, s * 2)} - {s}:
             out.append(mk(c, s2, 0, wd))
-        out.append(mk(c, s, w, 1 if wd > 1 else W))            # toggle the reduce mode
-        if op in STREAMK_OK:
-            for w2 in (512, 1024, 1536, 2048, 3072):
-                if w2 != w:
-                    out.append(mk(c, 1, w2, wd))
-            if w:
-                out.append(mk(c, s if s > 1 else 4, 0, wd))
+        out.append(mk(c, s, 0, 1 if wd > 1 else W))            # toggle the reduce mode
         for c2 in (0, 3, 4, 5):  # the one-wave configs (dual launches instantiate these)
             if c2 != c:
-                out.append(mk(c2, s, w, wd))
+                out.append(mk(c2, s, 0, wd))
         if op in MF16_OK:  # CFG_MF16 (16x16x4 MFMA, LDS-DMA), at the split and twice it
             for s2 in sorted({s, min(2048, s * 2)}):
                 if (c, s) != (14, s2):
                     out.append(mk(14, s2, 0, wd))
-        if op in MF16_OK and a.dma:  # generic LDS-DMA tiles 64x32 / 32x64 / 64x64 (16 / 17 / 18)
-            for c2 in (16, 17, 18, 19, 20):
-                for s2 in sorted({s, min(2048, s * 2), min(2048, s * 4), max(1, s // 2)}):
-                    if (c, s) != (c2, s2):
-                        out.append(mk(c2, s2, 0, wd))
+        if op in MF16_OK and a.dma:  # (configs 16-20 were removed in round 6)
+            for s2 in sorted({min(2048, s * 4), max(1, s // 2)}):
+                if (c, s) != (14, s2):
+                    out.append(mk(14, s2, 0, wd))
         if a.multiwave and op in (0, 1, 2, 3):
             for c2 in (1, 2, 6, 7, 8):
                 for s2 in sorted({s, min(2048, s * 2), max(1, s // 2)}):
@@ -122,7 +111,7 @@ def main():
                 t = timed(cand)
                 if a.verbose:
                     print(f"    {name:12s} c{cand['cfg'][op]} s{cand['splits'][op]} "
-                          f"w{cand['workers'][op]} {'inl' if cand['wide'][op] > 1 else 'wide'} "
+                          f"{'inl' if cand['wide'][op] > 1 else 'wide'} "
                           f"{t:.1f}", flush=True)
                 if best_t is None or t < best_t:
                     best, best_t = cand, t
@@ -132,7 +121,7 @@ def main():
             if t_new < t_inc * (1 - a.gain):
                 cur = best
                 print(f"pass {p} {name:12s} -> c{cur['cfg'][op]} s{cur['splits'][op]} "
-                      f"w{cur['workers'][op]} {'inl' if cur['wide'][op] > 1 else 'wide'}  "
+                      f"{'inl' if cur['wide'][op] > 1 else 'wide'}  "
                       f"{t_inc:.1f} -> {t_new:.1f} us", flush=True)
             else:
                 print(f"pass {p} {name:12s} keep ({t_inc:.1f} vs best cand {t_new:.1f})", flush=True)
@@ -140,7 +129,6 @@ def main():
     print(f"final {final:.1f} us/step (start {base:.1f})")
     print("DEFAULT_CFG", ",".join(map(str, cur["cfg"])))
     print("DEFAULT_SPLITS", ",".join(map(str, cur["splits"])))
-    print("DEFAULT_WORKERS", ",".join(map(str, cur["workers"])))
     print("DEFAULT_INL", ",".join("1" if w > 1 else "0" for w in cur["wide"]))
     if a.json:
         json.dump(dict(cur, step_us=final, start_us=base), open(a.json, "w"), indent=1)

@@ -23,8 +23,10 @@ def main():
     ap.add_argument("--cfg-variants", default="",
                     help="';'-separated tile-config overrides 'op=cfg[:split],...' (name=... first "
                          "to label it)")
-    ap.add_argument("--order-variants", default="",
-                    help="';'-separated block-order overrides (gemm.h split_coords), 'op=o,op=o'")
+    ap.add_argument("--wide-variants", default="",
+                    help="';'-separated split-K reduce overrides 'op=inl|wide,...' (inl: the "
+                         "in-launch last arriver; wide: the separate reduce kernel); a "
+                         "'name=...' first labels it, and 'op=cfg:split' items set the config")
     ap.add_argument("--bfirst-variants", default="",
                     help="';'-separated dual_bfirst masks (bit op: that dual dispatches its "
                          "second problem first; default 1<<14)")
@@ -40,9 +42,7 @@ def main():
                       engine="hip", quiet=True, data_sharding="stride")
     tr = Trainer(cfg, env, dataset=synthetic_mnist())
     e = tr.engine.eng
-    scheds = {"default": {"cfg": e.get_cfg(), "splits": e.get_splits(),
-                          "workers": e.get_workers(), "wide": e.get_wide(),
-                          "order": e.get_order()}}
+    scheds = {"default": {"cfg": e.get_cfg(), "splits": e.get_splits(), "wide": e.get_wide()}}
     for p in a.tuned:
         scheds[os.path.basename(p)] = json.load(open(p))
     for v in filter(None, a.splits_variants.split(";")):
@@ -65,12 +65,24 @@ def main():
             if spl:
                 sp[int(op)] = int(spl)
         scheds["cfg[" + label + "]"] = dict(scheds["default"], cfg=cf, splits=sp)
-    for v in filter(None, a.order_variants.split(";")):
-        od = list(scheds["default"]["order"])
+    for v in filter(None, a.wide_variants.split(";")):
+        wd = list(scheds["default"]["wide"])
+        cf = list(scheds["default"]["cfg"])
+        sp = list(scheds["default"]["splits"])
+        label = v
         for kv in v.split(","):
+            if kv.startswith("name="):
+                label = kv[5:]
+                continue
             op, val = kv.split("=")
-            od[int(op)] = int(val)
-        scheds["order[" + v + "]"] = dict(scheds["default"], order=od)
+            if val in ("inl", "wide"):
+                wd[int(op)] = (1 << 20) if val == "inl" else 1
+            else:
+                c, _, spl = val.partition(":")
+                cf[int(op)] = int(c)
+                if spl:
+                    sp[int(op)] = int(spl)
+        scheds["wide[" + label + "]"] = dict(scheds["default"], wide=wd, cfg=cf, splits=sp)
     for v in filter(None, a.bfirst_variants.split(";")):
         scheds["bfirst[" + v + "]"] = dict(scheds["default"], bfirst=int(v))
     res = {k: [] for k in scheds}
@@ -79,9 +91,7 @@ def main():
         for name, s in scheds.items():
             e.set_cfg(s["cfg"])
             e.set_splits(s["splits"])
-            e.set_workers(s["workers"])
             e.set_wide(s["wide"])
-            e.set_order(s.get("order", scheds["default"]["order"]))
             e.set_dual_bfirst(s.get("bfirst", 1 << 14))
             for _ in range(20):
                 tr.train_step(step)

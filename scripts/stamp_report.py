@@ -46,7 +46,7 @@ def main():
     e = tr.engine.eng
     if a.sched:
         sc = json.load(open(a.sched))
-        e.set_cfg(sc["cfg"]), e.set_splits(sc["splits"]), e.set_workers(sc["workers"])
+        e.set_cfg(sc["cfg"]), e.set_splits(sc["splits"])
         e.set_wide(sc["wide"])
     if a.nodual:
         e.set_dual(False)

@@ -138,3 +138,29 @@ def eval_rank(rank, world, port, outdir):
     except Exception:
         traceback.print_exc()
         raise
+
+
+def handoff_vote_rank(rank, world, port, outdir, case):
+    """One rank of the hand-off vote (native_exchange.handoff_vote) over gloo: `case` names the
+    digests this rank reports; the verdict (or the refusal) is saved per rank."""
+    _setup(rank, world, port)
+    try:
+        import torch.distributed as dist
+        from ddl_amd.parallel.comm import init_distributed
+        from ddl_amd.parallel.native_exchange import NativeUnavailable, handoff_vote
+        env = init_distributed(device="cpu")
+        ev, fl = "a" * 64, "a" * 64
+        if case == "replicas_diverge" and rank == world - 1:
+            ev = fl = "b" * 64      # this rank's replica differs under both hand-offs
+        elif case == "flags_diverge" and rank == world - 1:
+            fl = "c" * 64           # only the READY-flag run differs
+        try:
+            out = handoff_vote(env, ev, fl)
+        except NativeUnavailable as e:
+            out = {"refused": str(e)}
+        torch.save(out, os.path.join(outdir, f"rank{rank}.pt"))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        traceback.print_exc()
+        raise

@@ -178,3 +178,23 @@ def test_distributed_eval_equals_full_eval(tmp_path, world):
     res = [torch.load(tmp_path / f"eval{r}.pt") for r in range(world)]
     for r in res:
         assert r["dist"] == r["full"] == res[0]["full"]
+
+
+@pytest.mark.parametrize("case", ["agree", "flags_diverge", "replicas_diverge"])
+def test_handoff_vote_refuses_diverged_replicas(tmp_path, case):
+    """The READY-flag hand-off check's collective verdict (native_exchange.handoff_vote) over
+    gloo, W = 2: every rank agreeing keeps the flags; a rank whose READY-flag run alone differs
+    sends every rank back to the event hand-off; a rank whose replica differs under the event
+    hand-off too makes EVERY rank refuse the data plane (NativeUnavailable) instead of training
+    on diverged replicas."""
+    from dist_helpers import handoff_vote_rank
+    world = 2
+    spawn(handoff_vote_rank, world, free_port(), str(tmp_path), case)
+    outs = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=False)
+            for r in range(world)]
+    if case == "agree":
+        assert all(o["ok"] and o["ranks_agree"] and o["modes_agree"] for o in outs)
+    elif case == "flags_diverge":
+        assert all(not o["ok"] and "refused" not in o for o in outs)
+    else:
+        assert all("refused" in o and "diverge" in o["refused"] for o in outs)

@@ -253,56 +253,34 @@ def test_split_k_variants_agree(setup):
             assert err < tol, (t.name, name, err, e32)
 
 
-@pytest.mark.parametrize("order", [1, 2, 3])
-def test_block_orders_are_bit_identical(setup, order):
-    """Every split-K block order (gemm.h split_coords: XCD-contiguous renumbering with the K
-    splits, M rows or N tiles grouped) on every op — forward convs on the 3-D split-K grid,
-    the backward dual launches, in-launch and wide reduces — gives the default order's bits:
-    the partial slab and tickets are indexed by (tile, split), not by block id."""
-    eng, flat, params, grads, x, y = setup
-    base = eng.get_order()
-    grads.zero_()
-    eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 41)
-    torch.cuda.synchronize()
-    ref = grads.clone()
-    try:
-        eng.set_order([order] * len(base))
-        for _ in range(2):
-            grads.zero_()
-            eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 41)
-            torch.cuda.synchronize()
-            assert torch.equal(grads, ref), f"order {order}"
-    finally:
-        eng.set_order(base)
-
-
 @pytest.mark.parametrize("cfg", [None, 0, 1, 2, 4, 5, 6, 7, 8])
-def test_stream_k_matches_reference(setup, cfg):
-    """Stream-K schedules (several worker counts, every tile config) give the fp64-reference
-    gradients, and a given schedule is bit-deterministic across runs."""
+def test_split_factors_match_reference(setup, cfg):
+    """Split-K schedules (several split factors, every tile config) give the fp64-reference
+    gradients, and a given schedule is bit-deterministic across runs (the stream-K schedules
+    this test covered until round 5 were removed: docs/DESIGN.md round 6)."""
     eng, flat, params, grads, x, y = setup
-    base_cfg, base_w = eng.get_cfg(), eng.get_workers()
+    base_cfg, base_s = eng.get_cfg(), eng.get_splits()
     if cfg is not None:
         eng.set_cfg([cfg] * len(base_cfg))
     _, r64 = ref_grads(flat, x, y, 0.5, 31, torch.float64)
     try:
-        for workers in (8, 200, 1024, 4096):
-            eng.set_workers([workers] * len(base_w))
+        for f in (1, 3, 8):
+            eng.set_splits([max(1, s * f // 4) for s in base_s])
             outs = []
             for _ in range(2):
                 grads.zero_()
                 eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 31)
                 torch.cuda.synchronize()
                 outs.append(grads.clone())
-            assert torch.equal(outs[0], outs[1]), f"workers={workers} not deterministic"
+            assert torch.equal(outs[0], outs[1]), f"split x{f}/4 not deterministic"
             for t in TENSORS:
                 o = CANON_OFFSETS[t.index]
                 tol = 5e-5 if t.index > 7 else 5e-3
                 err = rel_err(outs[0][o:o + t.numel], r64[t.index].reshape(-1))
-                assert err < tol, (t.name, workers, err)
+                assert err < tol, (t.name, f, err)
     finally:
         eng.set_cfg(base_cfg)
-        eng.set_workers(base_w)
+        eng.set_splits(base_s)
 
 
 @pytest.mark.parametrize("cfg", [None, 6, 7, 8])
@@ -312,15 +290,14 @@ def test_inlaunch_splitk_reduce_matches_reference(setup, cfg, wide):
     wide-reduce kernel) for every op, default and multi-wave tile configs: fp64 reference
     gradients, bit-deterministic across runs."""
     eng, flat, params, grads, x, y = setup
-    base_w, base_s, base_wide = eng.get_workers(), eng.get_splits(), eng.get_wide()
+    base_s, base_wide = eng.get_splits(), eng.get_wide()
     base_cfg = eng.get_cfg()
     _, r64 = ref_grads(flat, x, y, 0.5, 77, torch.float64)
     try:
         if cfg is not None:
             eng.set_cfg([cfg] * len(base_cfg))
-        eng.set_workers([0] * len(base_w))
         eng.set_splits([max(2, min(s, 64)) for s in base_s])
-        eng.set_wide([wide] * len(base_w))
+        eng.set_wide([wide] * len(base_s))
         outs = []
         for _ in range(2):
             grads.zero_()
@@ -334,40 +311,31 @@ def test_inlaunch_splitk_reduce_matches_reference(setup, cfg, wide):
             assert rel_err(outs[0][o:o + t.numel], r64[t.index].reshape(-1)) < tol, t.name
     finally:
         eng.set_cfg(base_cfg)
-        eng.set_workers(base_w)
         eng.set_splits(base_s)
         eng.set_wide(base_wide)
 
 
 @pytest.mark.parametrize("waves", [4, 8, 16])
-@pytest.mark.parametrize("packed", [False, True, "conv"])  # "conv": back to back (no pack)
+@pytest.mark.parametrize("packed", [False, True])
 def test_kwave_config_matches_reference(setup, waves, packed):
     """The GEMMs on the K-wave launch (CFG_KWAVE = 13: K split over the waves of one
     workgroup, LDS reduction, fused epilogue): fp64-reference gradients, bit-deterministic
     across runs.  packed=False: every op set to 13 (the forward convs fall back to one-wave
-    32x32, the fc and conv backward pairs run back to back as K-wave launches); packed=True:
-    only the fc data gradients on 13, so each fc backward is one packed launch with its weight
-    gradient and the fc3 aux blocks; "conv": the conv4 / conv3 data gradients on 13 with their
-    weight gradients on the one-wave tile — the pair the fc backward packs; a conv pair runs
-    back to back instead (engine_impl.h run_dual_inst)."""
+    32x32 and so do the conv GEMMs, which have no K-wave instantiation; the fc backward pairs
+    run back to back as K-wave launches); packed=True: only the fc data gradients on 13, so
+    each fc backward is one packed launch with its weight gradient and the fc3 aux blocks."""
     eng, flat, params, grads, x, y = setup
-    base_cfg, base_s, base_w = eng.get_cfg(), eng.get_splits(), eng.get_workers()
+    base_cfg, base_s = eng.get_cfg(), eng.get_splits()
     try:
         if packed:
             cfg, spl = list(base_cfg), list(base_s)
-            # conv4 / conv3 or fc data gradients (conv2's weight gradient is reduced inside
-            # conv1's launch from its split-K partials, so it keeps its split form)
-            dg = (10, 12) if packed == "conv" else (6, 8)
-            for op in dg:
+            for op in (6, 8):  # the fc data gradients
                 cfg[op], spl[op] = 13, waves
-                if packed == "conv":
-                    cfg[op + 1] = 3
             eng.set_cfg(cfg)
             eng.set_splits(spl)
         else:
             eng.set_cfg([13] * len(base_cfg))
             eng.set_splits([waves] * len(base_s))
-        eng.set_workers([0] * len(base_w))
         outs = []
         for _ in range(2):
             grads.zero_()
@@ -381,25 +349,24 @@ def test_kwave_config_matches_reference(setup, waves, packed):
     finally:
         eng.set_cfg(base_cfg)
         eng.set_splits(base_s)
-        eng.set_workers(base_w)
 
 
 # conv2-4 forward, conv4..conv2 data / weight gradient (csrc/kernels/api.h op order)
 MF16_OPS = (1, 2, 3, 10, 11, 12, 13, 14, 15)
 
 
-@pytest.mark.parametrize("mode", ["default", "split1", "wide", "streamk", "nodual", "mixed"])
+@pytest.mark.parametrize("mode", ["default", "split1", "wide", "nodual", "mixed"])
 def test_mf16_config_matches_reference(setup, mode):
     """CFG_MF16 = 14 (gemm.h mainloop_dma16: one-wave 32x32x32 tile on v_mfma_f32_16x16x4_f32,
     LDS-DMA staging with the 16x16 image swizzles, accumulators re-laid out through LDS into the
     32x32 layout) on every conv GEMM: the fp32 / fp64 autograd gradients (check_grads) under
     every schedule that consumes its accumulators — fused epilogue (split 1), in-launch
-    last-arriver reduce, separate wide reduce, stream-K partial hand-off, dual and back-to-back
+    last-arriver reduce, separate wide reduce, dual and back-to-back
     launches, and mixed with the 32x32x2 tiles in one dual launch — bit-deterministic across
     reruns, and the forward activations within fp32 noise of the reference."""
     eng, flat, params, grads, x, y = setup
-    base = (eng.get_cfg(), eng.get_splits(), eng.get_workers(), eng.get_wide())
-    cfg, spl, wrk, wide = (list(v) for v in base)
+    base = (eng.get_cfg(), eng.get_splits(), eng.get_wide())
+    cfg, spl, wide = (list(v) for v in base)
     ops = MF16_OPS if mode != "mixed" else (1, 3, 10, 13, 14)  # the others stay on 32x32x2
     for op in ops:
         cfg[op] = 14
@@ -407,12 +374,9 @@ def test_mf16_config_matches_reference(setup, mode):
             spl[op] = 1
         elif mode == "wide":
             spl[op], wide[op] = max(2, spl[op]), 1
-        elif mode == "streamk":
-            wrk[op] = 1024
     try:
         eng.set_cfg(cfg)
         eng.set_splits(spl)
-        eng.set_workers(wrk)
         eng.set_wide(wide)
         eng.set_dual(mode != "nodual")
         outs = []
@@ -432,57 +396,7 @@ def test_mf16_config_matches_reference(setup, mode):
         eng.set_dual(True)
         eng.set_cfg(base[0])
         eng.set_splits(base[1])
-        eng.set_workers(base[2])
-        eng.set_wide(base[3])
-
-
-@pytest.mark.parametrize("tile", [16, 17, 18, 19, 20])
-@pytest.mark.parametrize("mode", ["default", "split1", "wide", "nodual"])
-def test_dma_g_configs_match_reference(setup, tile, mode):
-    """The LDS-DMA tiles — one-wave multi-fragment (CFG_DMA_64x32 / 32x64 / 64x64 = 16 / 17 / 18,
-    gemm.h mainloop_dma_g: K- and MN-contiguous images, the ones-row patch of the weight
-    gradients) and the 32x32 ring tiles (CFG_RING3 / CFG_RING2 = 19 / 20, mainloop_ring: 3 / 2
-    LDS images, next tiles' DMAs inside the MFMA cluster, split-K 1 = long K loops) — on
-    every conv GEMM, under every schedule that consumes their 2- and 4-fragment accumulators —
-    fused epilogue (split 1), in-launch reduce, wide reduce, dual and back-to-back launches (and
-    the conv2 dual fused with conv1's weight gradient): fp32 / fp64 autograd gradients,
-    bit-deterministic across reruns, forward activations within fp32 noise."""
-    eng, flat, params, grads, x, y = setup
-    base = (eng.get_cfg(), eng.get_splits(), eng.get_workers(), eng.get_wide())
-    cfg, spl, wrk, wide = (list(v) for v in base)
-    for op in MF16_OPS:
-        cfg[op], wrk[op] = tile, 0
-        if mode == "split1":
-            spl[op] = 1
-        elif mode == "wide":
-            spl[op], wide[op] = max(2, spl[op]), 1
-        else:
-            spl[op] = max(1, spl[op])
-    try:
-        eng.set_cfg(cfg)
-        eng.set_splits(spl)
-        eng.set_workers(wrk)
-        eng.set_wide(wide)
-        eng.set_dual(mode != "nodual")
-        outs = []
-        for _ in range(2):
-            grads.zero_()
-            eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 67)
-            torch.cuda.synchronize()
-            outs.append(grads.clone())
-        assert torch.equal(outs[0], outs[1])
-        check_grads(outs[0], flat, x, y, 0.5, 67)
-        pv = param_views(flat, CANON_OFFSETS)
-        pooled, _, _ = ref_intermediates(pv, x, 0.5, 67)
-        for name, ref in zip(["p1", "p2", "p3", "p4"], pooled):
-            got = eng.eng.buffer(name, x.shape[0])
-            assert rel_err(got.reshape(ref.shape), ref) < 2e-5, name
-    finally:
-        eng.set_dual(True)
-        eng.set_cfg(base[0])
-        eng.set_splits(base[1])
-        eng.set_workers(base[2])
-        eng.set_wide(base[3])
+        eng.set_wide(base[2])
 
 
 @pytest.mark.parametrize("conc,dual", [(False, True), (False, False), (True, False)])

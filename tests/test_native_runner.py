@@ -21,15 +21,13 @@ def data():
     return synthetic_mnist(n_train=2000, n_test=500, seed=5)
 
 
-def _run(data, native, steps=6, ready=None, fused_last=None, **kw):
+def _run(data, native, steps=6, ready=None, **kw):
     env = DistEnv(0, 1, 0, torch.device("cuda", 0))
     cfg = TrainConfig(mode="sync", steps=steps, batch_size=100, eval_every=0, engine="hip",
                       quiet=True, native_exchange=native, **kw)
     tr = Trainer(cfg, env, dataset=data)
     if ready is not None:
         tr.exchange.runner.set_ready_flags(ready)
-    if fused_last is not None:
-        tr.exchange.runner.set_fused_last(fused_last)
     assert getattr(tr.exchange, "native", False) == native
     if kw.get("force_collectives"):
         if kw.get("exchange_backend") == "xgmi":
@@ -40,8 +38,6 @@ def _run(data, native, steps=6, ready=None, fused_last=None, **kw):
     for i in range(steps):
         tr.train_step(i)
     torch.cuda.synchronize()
-    if fused_last is not None:
-        assert tr.exchange.runner.fused_last_taken() == fused_last, "fused last bucket"
     sync = getattr(tr.exchange, "sync_ps_state", None)  # replicated last-bucket state -> PS
     if sync is not None:
         sync()
@@ -123,23 +119,6 @@ def test_forced_collectives_on_one_rank_match_local(data, kw):
         assert torch.equal(s_loc[p][1], s_col[p][1])
         if s_loc[p][2] is not None:
             assert torch.equal(s_loc[p][2], s_col[p][2])
-
-
-def test_fused_last_bucket_matches_separate_kernel(data):
-    """The replicated last bucket exchanged inside conv1's weight-gradient launch (conv1.h
-    conv1_wgrad_xgmi_kernel: pushes from the reduce epilogues, the group's last arriver sums in
-    rank order and updates) vs xgmi_repl_kernel after the launch, on the forced 1-rank xGMI
-    rehearsal: bit-identical parameters and moments, and both equal the local step."""
-    kw = dict(shard="flat", exchange_backend="xgmi", force_collectives=True)
-    p_sep, s_sep = _run(data, True, fused_last=False, **kw)
-    p_fus, s_fus = _run(data, True, fused_last=True, **kw)
-    p_loc, _ = _run(data, True, shard="flat")
-    assert torch.equal(p_sep, p_fus)
-    assert torch.equal(p_loc, p_fus)
-    for p in s_sep:
-        assert s_sep[p][0] == s_fus[p][0]
-        assert torch.equal(s_sep[p][1], s_fus[p][1])
-        assert torch.equal(s_sep[p][2], s_fus[p][2])
 
 
 @pytest.mark.parametrize("shard", ["flat", "contiguous"])

@@ -34,9 +34,6 @@ def _canon(params, offsets):
 # W = 8 runs stalled in), and with the inbox checksums on (DDL_XGMI_CHECK=1: every owner
 # verifies every pushed slice against its pusher's checksum, error code 3 on a mismatch).
 W8_ENV = dict(GPU_MAX_HW_QUEUES="1", DDL_XGMI_CHECK="1", DDL_XGMI_TIMEOUT_S="60")
-FUSED_ENV = dict(DDL_XGMI_FUSED_LAST="1", DDL_COMM_PRIORITY="high")
-FUSED_MARK = pytest.mark.skipif(os.environ.get("DDL_TEST_FUSED_LAST") != "1",
-                                reason="opt-in fused last bucket stress rows (DDL_TEST_FUSED_LAST=1)")
 # W = 8 on one card runs with EXACTLY eight GPU processes: rank 0 is this pytest process
 # (which already holds a GPU context from the earlier tests) and ranks 1..7 are spawned.  The
 # round-3 abort (HSA_STATUS_ERROR_ILLEGAL_INSTRUCTION in a GEMM dual kernel,
@@ -108,11 +105,6 @@ def _rank(rank, world, port, outdir, kw):
         torch.cuda.synchronize()
         ex.check()
         acc = tr.evaluate()
-        # the replicated last bucket stays xgmi_repl_kernel at W > 1 unless the fused launch is
-        # asked for (DDL_XGMI_FUSED_LAST=1, docs/DESIGN.md round 5)
-        if shard == "flat" and not owner and extra_env.get("DDL_XGMI_CHECK") != "1":
-            want = extra_env.get("DDL_XGMI_FUSED_LAST") == "1"
-            assert ex.runner.fused_last_taken() == want, "fused last bucket"
         torch.save({"params": _canon(tr.params, tr.plan.tensor_offsets).cpu(), "acc": acc,
                     "sums": sums,
                     "t": {p: s.t for p, s in tr.servers.items()}},
@@ -165,20 +157,6 @@ def _simulate(world, kw):
     (2, dict(_env=dict(DDL_REPL_LAST="0"))),     # last bucket by its chunk owners
     (4, dict(_env=dict(DDL_XGMI_CHECK="1"))),
     pytest.param(8, dict(_env=W8_ENV), id="w8"),  # the 8-worker size of BASELINE configs 3-5
-    # the opt-in fused last bucket (conv1.h conv1_wgrad_xgmi_kernel) with ranks sharing this card
-    # (high-priority comm streams, which the fused launch requires): these timed out
-    # intermittently in round 5 (docs/DESIGN.md), so they run only with DDL_TEST_FUSED_LAST=1
-    pytest.param(2, dict(_env=FUSED_ENV), id="2-fused-last", marks=FUSED_MARK),
-    pytest.param(3, dict(grad_reduce="mean", _env=FUSED_ENV), id="3-fused-last",
-                 marks=FUSED_MARK),
-    pytest.param(4, dict(_env=FUSED_ENV), id="4-fused-last", marks=FUSED_MARK),
-    pytest.param(8, dict(_env=dict(FUSED_ENV, GPU_MAX_HW_QUEUES="1", DDL_XGMI_TIMEOUT_S="60")),
-                 id="w8-fused-last", marks=FUSED_MARK),
-    # control for the row above: the same high-priority comm streams, the separate kernel
-    pytest.param(4, dict(_env=dict(DDL_COMM_PRIORITY="high")), id="4-high-separate",
-                 marks=FUSED_MARK),
-    pytest.param(3, dict(grad_reduce="mean", _env=dict(DDL_COMM_PRIORITY="high")),
-                 id="3-high-separate", marks=FUSED_MARK),
     # tensor-granular plans on owner buckets (every rank pushes a unit to the rank hosting its
     # PS, which sums, updates and pushes the parameters back):
     pytest.param(2, dict(shard="none"), id="2-none"),              # BASELINE config 2: 1 PS + 2
@@ -207,6 +185,60 @@ def test_xgmi_exchange_matches_simulation(tmp_path, world, kw):
     # per-step parameter checksums localise a divergence (which step, which rank)
     steps = [[rec["sums"][i] for rec in recs] for i in range(STEPS)]
     assert torch.equal(got, ref), f"max |diff| {diff}; per-step sums {steps} vs {ref_sums}"
+
+
+def _handoff_rank(rank, world, port, outdir, perturb):
+    """One-card W = 2 xGMI sync trainer; its READY-flag hand-off check with (perturb) or without
+    an injected digest disagreement on the last rank."""
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DDL_DIST_BACKEND="gloo",
+                      DDL_XGMI_TIMEOUT_S="20")
+    try:
+        import torch.distributed as dist
+        from ddl_amd.config import TrainConfig
+        from ddl_amd.parallel.comm import init_distributed
+        from ddl_amd.parallel.native_exchange import NativeUnavailable
+        from ddl_amd.parallel.roles import Trainer
+        from ddl_amd.utils.data import synthetic_mnist
+        env = init_distributed()
+        cfg = TrainConfig(mode="sync", shard="flat", steps=STEPS, batch_size=100, eval_every=0,
+                          engine="hip", quiet=True, data_sharding="stride",
+                          exchange_backend="xgmi")
+        tr = Trainer(cfg, env, dataset=synthetic_mnist(2000, 500, seed=5))
+        assert tr.exchange.peer is not None, "xgmi path not taken"
+        try:
+            out = tr.exchange.handoff_check(tr, steps=2,
+                                            _perturb_rank=world - 1 if perturb else None)
+        except NativeUnavailable as e:
+            out = {"refused": str(e)}
+        torch.cuda.synchronize()
+        torch.save(out, os.path.join(outdir, f"rank{rank}.pt"))
+        dist.barrier()
+        tr.exchange.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        traceback.print_exc()
+        raise
+
+
+@pytest.mark.parametrize("perturb", [False, True])
+def test_handoff_check_refuses_diverged_replicas(tmp_path, perturb):
+    """One card, W = 2 over xGMI: the hand-off check proves the READY flags (both ranks, same
+    bits); with a digest disagreement injected on rank 1 both ranks refuse the data plane
+    (NativeUnavailable) instead of falling back to events."""
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_handoff_rank, args=(world, free_port(), str(tmp_path), perturb), nprocs=world,
+             join=True)
+    outs = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=False)
+            for r in range(world)]
+    if perturb:
+        assert all("refused" in o and "diverge" in o["refused"] for o in outs), outs
+    else:
+        assert all(o["handoff"] == "ready_flags" and o["ranks_bit_identical"] for o in outs), outs
 
 
 ASYNC_STEPS = 6
@@ -240,9 +272,8 @@ def _async_rank(rank, world, port, outdir, kw):
         assert (tr.exchange.runner is not None) == want_native, "native async step not taken"
         s = tr.train()  # verify_provenance runs inside (check_provenance=True)
         torch.cuda.synchronize()
-        if tr.servers:  # the PS service this host ran: the host scan unless DDL_ASYNC_CLAIM=1
-            want = "device-claim" if extra_env.get("DDL_ASYNC_CLAIM") == "1" else "host"
-            assert tr.exchange.service_mode == want, tr.exchange.service_mode
+        if tr.servers:  # the PS service this host ran: the native host scan
+            assert tr.exchange.service_mode == "host", tr.exchange.service_mode
         torch.save({"params": tr.params.cpu(), "served": tr.exchange.served,
                     "ps": {p: (sv.t, sv.params.cpu()) for p, sv in tr.servers.items()},
                     "ranges": {p: tr.plan.ps_segments(p)[0] for p in tr.servers},
@@ -265,12 +296,6 @@ def _async_rank(rank, world, port, outdir, kw):
     # segment-aligned flat plans (sharding.segment_aligned_num_ps): 4 PS on one host, 6 on two
     pytest.param(1, dict(shard="flat", _ps=4), id="1-flat"),
     pytest.param(2, dict(shard="flat", _ps=6), id="2-flat"),
-    # the device-side claim service (DDL_ASYNC_CLAIM=1: arrivals popped on the GPU in batches)
-    pytest.param(1, dict(shard="flat", _ps=4, _env=dict(DDL_ASYNC_CLAIM="1")), id="1-flat-claim"),
-    pytest.param(2, dict(shard="contiguous", _env=dict(DDL_ASYNC_CLAIM="1")), id="2-claim"),
-    pytest.param(4, dict(shard="greedy", num_ps=4, _env=dict(DDL_ASYNC_CLAIM="1")),
-                 id="4-claim"),
-    pytest.param(2, dict(shard="flat", _ps=6, _env=dict(DDL_ASYNC_CLAIM="1")), id="2-flat-claim"),
 
     pytest.param(8, dict(shard="contiguous", _env=dict(GPU_MAX_HW_QUEUES="1",
                                                        DDL_XGMI_TIMEOUT_S="60")), id="w8-contig"),
