@@ -394,15 +394,25 @@ __global__ void __launch_bounds__(256) xgmi_owner_kernel(XgmiTable T, XgmiLaunch
   const int64_t lo = a.run_lo[r] + s0;    // plan-buffer offset of the slice
   const int64_t vo = a.run_voff[r] + s0;  // its offset in the unit's inbox slot
   uint32_t* myflags = T.flags[me];
+  __shared__ uint32_t red[4];
   __shared__ int arrived;
   const float4* mine = reinterpret_cast<const float4*>(a.grads + lo);
 
   if (me != own) {
     const brsrc_t dst = make_rsrc(T.inbox[own] + a.inbox_off + (int64_t)me * a.c + vo,
                                   (uint32_t)n4 * 16u);
+    uint32_t cs = 0;
     for (int i = tid; i < n4; i += 256) {
       const float4 x = mine[i];
-      st4_sys(dst, i * 16, a.coef != 1.f ? scale4(x, a.coef) : x);
+      const float4 v = a.coef != 1.f ? scale4(x, a.coef) : x;
+      st4_sys(dst, i * 16, v);
+      if (a.check) cs += bits4(v);
+    }
+    if (a.check) {  // the slice's checksum at the owner, before the ARRIVE word (same drain)
+      const uint32_t t = block_sum(cs, red);
+      if (tid == 0)
+        __hip_atomic_store(T.flags[own] + ck_idx(b, me, j), t, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     }
     drain_vm();
     __syncthreads();
@@ -418,8 +428,17 @@ __global__ void __launch_bounds__(256) xgmi_owner_kernel(XgmiTable T, XgmiLaunch
     arrived = 0;  // (no update on a failed wait: see xgmi_ps_kernel)
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  const int n4u = arrived ? n4 : 0;
   const brsrc_t inbox = make_rsrc(T.inbox[me] + a.inbox_off, (uint32_t)(W * a.c * 4));
+  if (a.check && arrived) {  // every pusher's slice against its published checksum
+    bool ok = true;
+    for (int q = 0; q < W; ++q)
+      if (q != me)
+        ok &= check_piece(inbox, (int)(((int64_t)q * a.c + vo) * 4), n4,
+                          myflags + ck_idx(b, q, j), a.err, red);
+    if (!ok && tid == 0) arrived = 0;
+    __syncthreads();
+  }
+  const int n4u = arrived ? n4 : 0;
   float4* m4 = a.m ? reinterpret_cast<float4*>(a.m + a.run_soff[r] + s0) : nullptr;
   float4* v4 = a.v ? reinterpret_cast<float4*>(a.v + a.run_soff[r] + s0) : nullptr;
   float4* w4 = reinterpret_cast<float4*>(T.params[me] + lo);

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import json
 import os
+import sys
 from typing import Dict, List, Tuple
 
 import torch
@@ -174,9 +175,15 @@ def load(trainer, path: str) -> None:
                     ps.v[s0:s0 + (b - a)].copy_(full[i]["v"][a:b])
                 if ps.params is not None:
                     ps.params[s0:s0 + (b - a)].copy_(full[i]["w"][a:b])
-        same_plan = (man["policy"] == plan.policy and man["num_ps"] == plan.num_ps
-                     and man.get("ps_segments") == [[list(map(int, r)) for r in plan.ps_segments(q)]
-                                                    for q in range(plan.num_ps)])
+        same_plan = man["policy"] == plan.policy and man["num_ps"] == plan.num_ps
+        if "ps_segments" in man:
+            same_plan = same_plan and man["ps_segments"] == [
+                [list(map(int, r)) for r in plan.ps_segments(q)] for q in range(plan.num_ps)]
+        elif same_plan and p == next(iter(trainer.servers)):
+            # a manifest from before round 5 carries no PS ranges: policy + PS count is the best
+            # identity it offers, so the per-PS counters are kept on that basis (said once)
+            print("[ddl_amd] checkpoint manifest has no ps_segments: per-PS step counters "
+                  "restored by policy and PS count only", file=sys.stderr)
         ps.t = int(man["ps_t"].get(str(p)) or t_resume) if same_plan else t_resume
     trainer.global_step = int(man["global_step"])
     load_state = getattr(trainer.exchange, "load_ps_state", None)

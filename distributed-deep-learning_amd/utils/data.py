@@ -89,6 +89,57 @@ def synthetic_mnist(n_train: int = TRAIN_SIZE, n_test: int = TEST_SIZE,
     return Dataset(xtr, ytr, xte, yte, "synthetic")
 
 
+# The "hard" synthetic set: the default set is separable enough that the
+# reference recipe ends its epoch at ~0.998 and crosses 95 % after ~0.14 s, so it cannot show
+# what async staleness or the replicate protocol cost in convergence.  Here every class has
+# several writing STYLES (independent prototypes), samples blend two styles of their class with a
+# distractor of another class, translate by up to +-4 px, get a random contrast and heavier pixel
+# noise — intra-class variety and inter-class confusion instead of one template per class.
+# Calibrated on MI355X (scripts/tta_calibrate.py, profiles/r6_tta_calibration.txt) so the
+# reference recipe (one epoch: 500 steps of batch 100, Adam 1e-4, keep 0.5) ends near MNIST's
+# ~0.97-0.98.
+HARD = dict(styles=4, noise=0.55, mix=0.35, shift=4, contrast=0.35)
+
+
+def synthetic_mnist_hard(n_train: int = TRAIN_SIZE, n_test: int = TEST_SIZE, seed: int = 4321,
+                         styles: int = HARD["styles"], noise: float = HARD["noise"],
+                         mix: float = HARD["mix"], shift: int = HARD["shift"],
+                         contrast: float = HARD["contrast"]) -> Dataset:
+    """MNIST-shaped set on which the reference recipe converges like MNIST (see HARD)."""
+    g = torch.Generator().manual_seed(seed)
+    low = torch.rand(NUM_CLASSES * styles, 1, 7, 7, generator=g)
+    proto = F.interpolate(low, size=(IMAGE, IMAGE), mode="bicubic", align_corners=False)
+    proto = ((proto - proto.mean(dim=(2, 3), keepdim=True)) * 3.0).clamp(0.0, 1.0)
+    proto = proto.reshape(NUM_CLASSES, styles, IMAGE, IMAGE)
+
+    def make(n: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        y = torch.randint(0, NUM_CLASSES, (n,), generator=g)
+        s1 = torch.randint(0, styles, (n,), generator=g)
+        s2 = torch.randint(0, styles, (n,), generator=g)
+        a = torch.rand(n, 1, 1, generator=g)
+        own = proto[y, s1] * a + proto[y, s2] * (1.0 - a)  # a point between two styles
+        other = torch.randint(1, NUM_CLASSES, (n,), generator=g)
+        other = (y + other) % NUM_CLASSES                   # a different class
+        so = torch.randint(0, styles, (n,), generator=g)
+        img = own * (1.0 - mix) + proto[other, so] * mix
+        gain = 1.0 - contrast * torch.rand(n, 1, 1, generator=g)
+        img = img * gain
+        sx = torch.randint(-shift, shift + 1, (n,), generator=g)
+        sy = torch.randint(-shift, shift + 1, (n,), generator=g)
+        out = torch.empty(n, IMAGE, IMAGE)
+        for dx in range(-shift, shift + 1):
+            for dy in range(-shift, shift + 1):
+                sel = (sx == dx) & (sy == dy)
+                if sel.any():
+                    out[sel] = torch.roll(img[sel], shifts=(dy, dx), dims=(1, 2))
+        out = out + noise * torch.randn(n, IMAGE, IMAGE, generator=g)
+        return out.clamp(0.0, 1.0).reshape(n, INPUT_DIM).contiguous(), y
+
+    xtr, ytr = make(n_train)
+    xte, yte = make(n_test)
+    return Dataset(xtr, ytr, xte, yte, "synthetic-hard")
+
+
 # The only globals a pickle of numpy arrays needs (numpy 1.x and 2.x module paths): the array
 # reconstructor, the ndarray / dtype types and the buffer constructor of newer protocols, plus
 # _codecs.encode, which protocol-2 pickles written by python 3 use to rebuild a bytes object
@@ -145,6 +196,8 @@ def load_file(path: str) -> Dataset:
 def get_dataset(spec: str = "synthetic", seed: int = 1234) -> Dataset:
     if spec in ("synthetic", "", None):
         return synthetic_mnist(seed=seed)
+    if spec == "synthetic-hard":
+        return synthetic_mnist_hard()
     if spec.startswith("synthetic:"):
         n = int(spec.split(":", 1)[1])
         return synthetic_mnist(n_train=n, n_test=max(n // 5, 100), seed=seed)

@@ -106,3 +106,26 @@ def test_async_w2_resume_continues_ps_step_counters(tmp_path):
         assert rec["summary"]["steps"] == STEPS and rec["summary"]["images"] == (STEPS - CUT) * 20
         assert torch.isfinite(rec["params"]).all()
     assert ps_t == {0: 2 * STEPS, 1: 2 * STEPS}
+
+
+def test_resume_from_manifest_without_ps_segments_keeps_ps_counters(tmp_path, capsys):
+    """A manifest written before round 5 has no ``ps_segments``: resuming it with the same
+    policy and PS count restores every PS's own step counter (Adam's bias correction) instead of
+    resetting them all to the global step, and says so."""
+    import glob
+    import json
+    full = _train(_cfg(tmp_path / "full"))
+    _train(_cfg(tmp_path / "cut", max_steps=CUT))
+    mans = glob.glob(os.path.join(str(tmp_path / "cut"), "**", "manifest.json"), recursive=True)
+    assert mans
+    for mp in mans:
+        man = json.load(open(mp))
+        man.pop("ps_segments", None)
+        json.dump(man, open(mp, "w"))
+    capsys.readouterr()
+    res = _train(_cfg(tmp_path / "cut", resume=True))
+    err = capsys.readouterr().err
+    assert "no ps_segments" in err
+    assert torch.equal(res.params, full.params)
+    for p, ps in full.servers.items():
+        assert res.servers[p].t == ps.t == STEPS
