@@ -167,6 +167,10 @@ struct Engine {
   }();
   // fc3 weight gradient still to compute (fused head kernel ran): taken by the fc2 dual launch
   int head_wgrad_pending = 0;
+  // the fc backward's packed launches leave the fc weight gradients (bit 0: fc2, bit 1: fc1) to
+  // the conv4 dual launch (engine_impl.h FcWgradAux); false: they stay in the packs
+  bool fc_wgrad_defer = true;
+  int fc_wgrad_pending = 0;
   // fc2 forward's split-K partials whose reduce + epilogue the head kernel runs (the step's
   // forward with defer_fc2, one-wave 32x32 split-K in mode 2): one launch fewer per step.
   // DDL_FC2_REDUCE_IN_HEAD=0 keeps the separate reduce launch.
@@ -205,6 +209,8 @@ struct Engine {
   // launch a pending optimizer tail on its own (no-op when none is pending)
   void flush_tail(hipStream_t st);
   void flush_head_wgrad(int B, hipStream_t st);
+  // launch pending fc weight gradients on their own (no-op when none are pending)
+  void flush_fc_wgrad(const float* x, int B, const uint32_t* seed, hipStream_t st);
 
  private:
   void fork(hipStream_t st);

@@ -227,6 +227,13 @@ void Engine::flush_tail(hipStream_t st) {
   tail = UpdTail();
 }
 
+void Engine::flush_fc_wgrad(const float* x, int B, const uint32_t* seed, hipStream_t st) {
+  const int pend = fc_wgrad_pending;
+  fc_wgrad_pending = 0;
+  if (pend & 1) run_op(OP_FC2_WGRAD, x, B, seed, true, st, 0);
+  if (pend & 2) run_op(OP_FC1_WGRAD, x, B, seed, true, st, 0);
+}
+
 void Engine::flush_head_wgrad(int B, hipStream_t st) {
   if (!head_wgrad_pending) return;
   launch_head_wgrad(h2, dlog, B, G[12], G[13], st);
@@ -236,6 +243,7 @@ void Engine::flush_head_wgrad(int B, hipStream_t st) {
 void Engine::forward(const float* x, int B, const uint32_t* seed, bool train, hipStream_t st,
                      bool defer_fc2) {
   fc2_slab = nullptr;  // (a deferred fc2 reduce nobody took: this forward rewrites h2 anyway)
+  fc_wgrad_pending = 0;  // (likewise: their inputs are about to be rewritten)
   for (int op = OP_CONV1_FWD; op < OP_FC2_FWD; ++op) run_op(op, x, B, seed, train, st, 0);
   if (!(train && defer_fc2 && fc2_in_head && !concurrent && run_fc2_deferred(*this, x, B, seed, st)))
     run_op(OP_FC2_FWD, x, B, seed, train, st, 0);
@@ -314,7 +322,10 @@ void Engine::backward_segment(int s, const float* x, const int64_t* labels, int 
       flush_head_wgrad(B, st);
       run_dual_inst<OP_FC1_DGRAD, OP_FC1_WGRAD>(*this, x, B, seed, st);
       break;
-    case 1: run_dual_inst<OP_CONV4_DGRAD, OP_CONV4_WGRAD>(*this, x, B, seed, st); break;
+    case 1:
+      run_dual_inst<OP_CONV4_DGRAD, OP_CONV4_WGRAD>(*this, x, B, seed, st);
+      flush_fc_wgrad(x, B, seed, st);  // (a conv4 pair that ran back to back took none of them)
+      break;
     case 2: run_dual_inst<OP_CONV3_DGRAD, OP_CONV3_WGRAD>(*this, x, B, seed, st); break;
     case 3:
       run_dual_then_inst<OP_CONV2_DGRAD, OP_CONV2_WGRAD, OP_CONV1_WGRAD>(*this, x, B, seed, st);

@@ -169,6 +169,53 @@ inline void with_one_wave_cfg(int c, F&& f) {
 // every pairing of the one-wave configs is instantiated
 constexpr bool dual_pair_ok(int, int) { return true; }
 
+// The fc1 / fc2 weight gradients as extra blocks of the conv4 dual launch:
+// dW1 / dW2 feed only the optimizer, so they leave the fc backward's packed launches (which then
+// carry only the data-gradient chain to conv4) and fill the conv4 dual's idle SIMD slots.  The
+// tiles are the packs' (one-wave 32x32, BK 32, unsplit over K = batch): the same bits.  The
+// segment's optimizer tail (tail.h) follows them.  models/__init__.py HIP_SEGMENTS lists fc1 / fc2
+// in segment 1 accordingly.
+struct FcWgradAux {
+  using T = GemmTile<32, 32, 32, 1, 1, FcWgrad>;
+  static constexpr int LDS_F4 = T::LDS_F4;
+  FcWgrad p2{}, p1{};           // fc2, fc1
+  int n2 = 0, n1 = 0, gx2 = 1, gx1 = 1;
+  UpdTail t;
+  int nblk = 0;
+  int first_ = 0;
+  static DDL_DEV void tile(const FcWgrad& p, int i, int gx, float* lds) {
+    const int m_blk = (i % gx) * 32, n_blk = (i / gx) * 32;
+    f32x16 acc[1][1];
+    T::mainloop(p, m_blk, n_blk, 0, p.K, lds, acc);
+    T::epilogue(p, m_blk, n_blk, acc);
+  }
+  DDL_DEV void run(int b, float* lds) const {
+    if (b < n2) tile(p2, b, gx2, lds);
+    else if (b < n2 + n1) tile(p1, b - n2, gx1, lds);
+    else tail_body(t, b - n2 - n1);
+  }
+};
+
+inline FcWgradAux fc_wgrad_aux(Engine& e, int B, const float* x, const uint32_t* seed) {
+  FcWgradAux a;
+  if (e.fc_wgrad_pending & 1) {
+    a.p2 = make_policy<OP_FC2_WGRAD>(e, B, x, seed, true);
+    a.gx2 = (a.p2.M + 31) / 32;
+    a.n2 = a.gx2 * ((a.p2.N + 31) / 32);
+  }
+  if (e.fc_wgrad_pending & 2) {
+    a.p1 = make_policy<OP_FC1_WGRAD>(e, B, x, seed, true);
+    a.gx1 = (a.p1.M + 31) / 32;
+    a.n1 = a.gx1 * ((a.p1.N + 31) / 32);
+  }
+  e.fc_wgrad_pending = 0;
+  a.t = e.tail;
+  e.tail = UpdTail();
+  a.first_ = 0;  // (tiles, then the tail, after the GEMM blocks)
+  a.nblk = a.n2 + a.n1 + a.t.nblocks;
+  return a;
+}
+
 // fc3's weight gradient as aux blocks (head.h), pending after the fused head kernel
 inline HeadWgradAux head_aux(Engine& e, int B) {
   HeadWgradAux a;
@@ -200,10 +247,18 @@ inline void dual_b(Engine& e, const PA& pa, const PB& pb, int B, hipStream_t st)
                                      e.splits[OB], e.scratch[1], e.wide[OB], st, aux, nullptr,
                                      e.dual_order(OA));
   };
-  // the fc2 dual carries fc3's weight gradient; the others a pending optimizer tail
+  // the fc2 dual carries fc3's weight gradient; the conv4 dual the deferred fc weight
+  // gradients (if any) and the pending optimizer tail; the others the tail
   if constexpr (OA == OP_FC2_DGRAD) {
     e.flush_tail(st);
     go(head_aux(e, B));
+  } else if constexpr (OA == OP_CONV4_DGRAD) {
+    if (e.fc_wgrad_pending) {
+      go(fc_wgrad_aux(e, B, nullptr, nullptr));
+    } else {
+      go(TailAux(e.tail));
+      e.tail = UpdTail();
+    }
   } else {
     go(TailAux(e.tail));
     e.tail = UpdTail();
@@ -220,8 +275,14 @@ void run_dual_inst(Engine& e, const float* x, int B, const uint32_t* seed, hipSt
   constexpr bool fc_pair = OA == OP_FC2_DGRAD || OA == OP_FC1_DGRAD;
   if (fc_pair && e.dual && e.cfg[OA] == CFG_KWAVE && (e.cfg[OB] == 3 || e.cfg[OB] == 5)) {
     const auto pa = make_policy<OA>(e, B, x, seed, true);
-    const auto pb = make_policy<OB>(e, B, x, seed, true);
+    auto pb = make_policy<OB>(e, B, x, seed, true);
     if constexpr (fc_pair && KWaveOK<std::decay_t<decltype(pa)>>::value) {
+      // the weight gradient left to the conv4 dual launch (FcWgradAux): the pack carries the
+      // data gradient (and its aux work) only
+      if (e.fc_wgrad_defer) {
+        e.fc_wgrad_pending |= OA == OP_FC2_DGRAD ? 1 : 2;
+        pb.M = 0;
+      }
       if constexpr (OA == OP_FC2_DGRAD) {
         e.flush_tail(st);
         launch_gemm_pack(pa, e.splits[OA], pb, head_aux(e, B), st);

@@ -44,6 +44,9 @@
 
 // s_setprio 1 around each K tile's MFMA cluster (guide T5; measured 0.3753 -> 0.3747 ms/step)
 #define DDL_MFMA_PRIO 1
+#ifndef DDL_EPI_PRIO
+#define DDL_EPI_PRIO 0
+#endif
 #include "scratch.h"
 #include "stamps.h"
 #include "tail.h"
@@ -1049,10 +1052,14 @@ DDL_DEV int splitk_body(const P& p, int kchunk, int mode, float4* __restrict__ s
     T::store_partial(sr, ((size_t)bz * ntiles + tile) * G::PART4, acc);
     if (mode == 2) return nkt;
     if (!T::arrive(&tickets[tile], gz, flag)) return nkt;
+#if DDL_EPI_PRIO
+    // the last arriver's sum + fused epilogue end the tile: ahead of the MFMA loops
+    __builtin_amdgcn_s_setprio(DDL_EPI_PRIO);
+#endif
     T::sum_partials(sr, (size_t)tile * G::PART4, (size_t)ntiles * G::PART4, gz, acc);
   }
   T::epilogue(p, m_blk, n_blk, acc);
-  return nkt;
+  return nkt | (1 << 20);  // (bit 20: this block ran the epilogue — diagnostics, stamps.h)
 }
 
 // Launch geometry of one GEMM problem under its schedule (host-computed, passed by value).
@@ -1141,7 +1148,9 @@ template <int BK, int KW, class P>
 DDL_DEV void kwave_body(const P& p, int bx, int by, float4* lds4, int L) {
   using T = GemmTile<32, 32, BK, 1, 1, P>;
   static_assert(KW == 4 || KW == 8 || KW == 16, "4, 8 or 16 waves");
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // (wave-uniform by construction; readfirstlane tells the compiler, so the LDS-DMA main loop
+  // gets its image address in an SGPR)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int m_blk = bx * 32, n_blk = by * 32;
   float* mine = reinterpret_cast<float*>(lds4 + wave * L);
   f32x16 acc[1][1];
@@ -1267,6 +1276,18 @@ struct TailAux {
   DDL_DEV void run(int b) const { tail_body(t, b); }
 };
 
+// An aux type that needs the block's LDS staging array (AUX::LDS_F4 > 0: its GEMM tiles) is
+// called as run(b, lds); the dual launch sizes its LDS for it.
+template <class A, class = void>
+struct AuxLds : std::integral_constant<int, 0> {};
+template <class A>
+struct AuxLds<A, std::void_t<decltype(A::LDS_F4)>> : std::integral_constant<int, A::LDS_F4> {};
+template <class A>
+DDL_DEV void run_aux(const A& ut, int b, float* lds) {
+  if constexpr (AuxLds<A>::value > 0) ut.run(b, lds);
+  else ut.run(b);
+}
+
 // Two independent GEMM problems in one launch: blocks [0, ga.nblocks) run problem A, the
 // rest problem B.  Both must use one-wave blocks.  An optional optimizer tail (tail.h) takes
 // ut.nblocks more blocks, after the GEMM blocks (ut.first = 0, measured faster: the update
@@ -1280,7 +1301,8 @@ gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut, int bfirst) {
   using TA = GemmTile<CA::BM, CA::BN, CA::BK, CA::WM, CA::WN, PA, CA::V>;
   using TB = GemmTile<CB::BM, CB::BN, CB::BK, CB::WM, CB::WN, PB, CB::V>;
   constexpr int L0 = TA::LDS_F4 > TB::LDS_F4 ? TA::LDS_F4 : TB::LDS_F4;
-  constexpr int L = L0 > 0 ? L0 : 1;
+  constexpr int L1 = L0 > AuxLds<AUX>::value ? L0 : AuxLds<AUX>::value;
+  constexpr int L = L1 > 0 ? L1 : 1;
   __shared__ float4 lds4[L];  // (the last-arriver flag in the first word: gemm_f32_kernel)
   float* lds = reinterpret_cast<float*>(lds4);
   int* flag = reinterpret_cast<int*>(lds4);
@@ -1288,12 +1310,12 @@ gemm_dual_kernel(PA pa, SubGrid ga, PB pb, SubGrid gb, AUX ut, int bfirst) {
   int b = blockIdx.x;
   if (ut.first_) {
     if (b < ut.nblk) {
-      ut.run(b);
+      run_aux(ut, b, lds);
       return;
     }
     b -= ut.nblk;
   } else if (b >= gemm_blocks) {
-    ut.run(b - gemm_blocks);
+    run_aux(ut, b - gemm_blocks, lds);
     return;
   }
   // bfirst 1: problem B's blocks are dispatched first (longest-first ordering shortens the

@@ -906,6 +906,10 @@ template <>
 struct KWaveOK<FcDgradAct> : std::true_type {};
 template <int HP, int C>
 struct KWaveOK<FcDgradPool<HP, C>> : std::true_type {};
+// the conv2-4 forwards (no dual partner): the K split inside one workgroup replaces the split-K
+// partial slab, the arrival tickets and the last arriver's sum (round 6 A/B)
+template <int H, int CIN, int COUT, bool KM>
+struct KWaveOK<ConvFwd<H, CIN, COUT, KM>> : std::bool_constant<(CIN % kBK == 0)> {};
 // (the conv backward as K-wave tiles lost to the dual launches in every variant, 312-402 vs
 // 289.5 us/step, and was removed: docs/DESIGN.md round 5)
 

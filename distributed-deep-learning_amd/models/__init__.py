@@ -7,8 +7,9 @@ from .layout import TENSORS, NUM_TENSORS, TOTAL_NUMEL  # noqa: F401
 
 # Backward segments of the HIP engine in completion order (fc head first), each the set
 # of tensors whose gradients are final when the segment's kernels have run
-# (SURVEY.md §5.8 bucket plan, refined per conv layer).
-HIP_SEGMENTS = [list(range(8, 14)), [6, 7], [4, 5], [0, 1, 2, 3]]
+# (SURVEY.md §5.8 bucket plan, refined per conv layer).  fc1 / fc2's weight gradients run in
+# the conv4 dual launch (csrc/kernels/engine_impl.h FcWgradAux), so they complete with segment 1.
+HIP_SEGMENTS = [[12, 13], [6, 7, 8, 9, 10, 11], [4, 5], [0, 1, 2, 3]]
 TORCH_SEGMENTS = [list(range(14))]
 
 

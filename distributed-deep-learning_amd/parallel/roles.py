@@ -35,7 +35,7 @@ from ..utils.tracing import trace_range
 from .comm import DistEnv, SyncExchange, AsyncExchange, init_distributed
 from .native_exchange import make_sync_exchange
 from .ps import ParameterServer
-from .sharding import make_plan, segment_aligned_num_ps
+from .sharding import async_groups, make_plan, segment_aligned_num_ps
 
 
 def _job_id(env: DistEnv) -> str:
@@ -93,12 +93,13 @@ class Trainer:
         aligned = (asyncm and not self.async_as_sync and cfg.shard == "flat" and cfg.overlap
                    and len(segs) > 1)
         if aligned:
-            self.num_ps = cfg.num_ps or segment_aligned_num_ps(W, segs)
-            aligned = self.num_ps >= len(segs)
+            groups = async_groups(segs)
+            self.num_ps = cfg.num_ps or segment_aligned_num_ps(W, groups)
+            aligned = self.num_ps >= len(groups)
             if not cfg.num_ps and env.rank == 0 and not cfg.quiet:
                 print(f"[ddl_amd] async flat plan: {self.num_ps} segment-aligned PS "
                       f"(--num-ps not given)", file=sys.stderr)
-            buckets = segs if aligned else None
+            buckets = groups if aligned else None
         self.plan = make_plan(shard, self.num_ps, buckets=buckets, segment_aligned=aligned)
         dev = env.device
         self.params = torch.zeros(self.plan.total, dtype=torch.float32, device=dev)

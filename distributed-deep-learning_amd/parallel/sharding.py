@@ -224,6 +224,26 @@ def host_imbalance(plan: ShardPlan, world: int) -> float:
     return max(load) / (sum(load) / world)
 
 
+def async_groups(segments: Sequence[Sequence[int]], min_frac: float = 0.01) -> List[List[int]]:
+    """The backward segments (completion order) as the async plan's PS groups: a segment with
+    less than ``min_frac`` of the parameters joins the segment completed after it — it is
+    pushed one segment later (harmless: it is tiny) instead of taking a PS of its own, which
+    would cost every host a PS at W = 4-8 for a few KB (HIP engine: fc3's 5,130 parameters
+    complete alone in segment 0 since fc1 / fc2's weight gradients moved to segment 1)."""
+    numel = [t.numel for t in TENSORS]
+    total = sum(numel)
+    out: List[List[int]] = []
+    carry: List[int] = []
+    for seg in segments:
+        g = carry + list(seg)
+        if sum(numel[i] for i in g) < min_frac * total and seg is not segments[-1]:
+            carry = g
+            continue
+        out.append(sorted(g))
+        carry = []
+    return out
+
+
 def segment_aligned_num_ps(world: int, groups: Sequence[Sequence[int]],
                            max_imbalance: float = 1.25) -> int:
     """PS count of the async segment-aligned flat plan: the smallest multiple of ``world``

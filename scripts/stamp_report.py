@@ -101,7 +101,20 @@ def main():
         for (off, nb, sub, gx, gy, gz) in group:
             rs = rec[off:off + nb]
             d = [(r[1] - r[0]) / 100.0 for r in rs]
-            kt = [r[5] for r in rs]
+            kt = [r[5] & 0xfffff for r in rs]
+            last = [(r[5] >> 20) & 1 for r in rs]
+            # block time = fixed + per_kt * K tiles (least squares over the blocks that did not
+            # run the epilogue, i.e. stored a partial and left) and the epilogue blocks' extra
+            fit = None
+            xs = [k for k, l in zip(kt, last) if not l]
+            ys = [t for t, l in zip(d, last) if not l]
+            if len(set(xs)) > 1:
+                n = len(xs)
+                mx, my = sum(xs) / n, sum(ys) / n
+                sxx = sum((x - mx) ** 2 for x in xs)
+                b = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sxx
+                fit = (my - b * mx, b)
+            ep = [t for t, l in zip(d, last) if l]
             us_kt = [x / max(1, k) for x, k in zip(d, kt)]
             starts = [(r[0] - t0) / 100.0 for r in rs]
             ends = sorted((r[1] - t0) / 100.0 for r in rs)
@@ -110,12 +123,16 @@ def main():
                        span=span, blk_med=pct(d, .5), blk_p10=pct(d, .1), blk_max=max(d),
                        us_per_kt=pct(us_kt, .5), kt_med=pct(kt, .5), kt_max=max(kt),
                        start90=pct(starts, .9), tail10=span - pct(ends, .9), waves_per_simd=wps,
-                       max_resident=maxres, simds=nsimd, ghz=pct(ghz, .5))
+                       max_resident=maxres, simds=nsimd, ghz=pct(ghz, .5),
+                       fixed_us=fit[0] if fit else None, per_kt_us=fit[1] if fit else None,
+                       epi_blocks=len(ep), epi_med=pct(ep, .5) if ep else None)
             out.append(row)
             print(f"{row['launch']:9s} {sub:3d} {nb:6d} {span:6.1f} {row['blk_med']:7.1f} "
                   f"{row['blk_p10']:7.1f} {row['blk_max']:7.1f} {row['us_per_kt']:6.2f} "
                   f"{row['kt_med']:6d} {row['kt_max']:6d} {row['start90']:7.1f} "
-                  f"{row['tail10']:6.1f} {wps:6.2f} {maxres:6d} {row['ghz']:5.2f}")
+                  f"{row['tail10']:6.1f} {wps:6.2f} {maxres:6d} {row['ghz']:5.2f}"
+                  + (f"  fit {fit[0]:5.2f} + {fit[1]:5.2f}/kt" if fit else "  fit -")
+                  + (f"  epi {len(ep)} med {row['epi_med']:5.1f}" if ep else ""))
     if a.json:
         json.dump(out, open(a.json, "w"), indent=1)
         # the last step's raw records (one row per block: stamps.h layout) + sub-grid table

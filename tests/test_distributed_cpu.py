@@ -126,12 +126,12 @@ def test_async_serves_every_push(tmp_path, world, shard):
         assert torch.isfinite(rec["params"]).all()
 
 
-@pytest.mark.parametrize("world,num_ps", [(2, 6), (3, 9)])
+@pytest.mark.parametrize("world,num_ps", [(2, 4), (3, 9)])
 def test_async_segment_aligned_flat_plan(tmp_path, world, num_ps):
-    """The async flat plan with the HIP engine's four backward segments (segment-aligned: every
-    PS range inside one segment, P the smallest balanced multiple of W): W = 2 -> 6 PS, W = 3 ->
-    9, three per host, uneven ranges — every push served once in order with checksummed bytes,
-    each PS at W x steps."""
+    """The async flat plan with the HIP engine's backward segments (segment-aligned: every PS
+    range inside one group, the tiny fc3 segment folded into the next, sharding.async_groups;
+    P the smallest balanced multiple of W): W = 2 -> 4 PS, W = 3 -> 9, uneven ranges — every
+    push served once in order with checksummed bytes, each PS at W x steps."""
     from ddl_amd.models import HIP_SEGMENTS
     recs, cfg = _run(tmp_path, world, mode="async", shard="flat", check_provenance=True,
                      _segments=HIP_SEGMENTS)

@@ -96,7 +96,7 @@ def test_async_eval_reports_the_same_accuracies(data):
 
 
 def test_async_local_elision_matches_inbox_copy(data, monkeypatch):
-    """W = 1 async over xGMI (4 PS, one worker: the arrival order is fixed): the local push
+    """W = 1 async over xGMI (3 PS, one worker: the arrival order is fixed): the local push
     elision on and off (the apply reads the gradient in place / from the inbox) apply the same
     Adam steps in the same order, so 12-step runs are bit-identical."""
     runs = []
@@ -112,7 +112,7 @@ def test_async_local_elision_matches_inbox_copy(data, monkeypatch):
 
 
 def test_async_xgmi_push_tails_match_push_kernels(data):
-    """W = 1 async over the xGMI data plane (segment-aligned flat plan: 4 PS): the gradient
+    """W = 1 async over the xGMI data plane (segment-aligned flat plan: 3 PS): the gradient
     pushes riding as tail blocks of the next segment's launch (default) and the stand-alone
     push kernels deliver the same bytes, and the GPU-side pull gate (default) orders the next
     forward after the round exactly like the host wait, so 12-step runs are bit-identical.  One step of the
@@ -123,7 +123,7 @@ def test_async_xgmi_push_tails_match_push_kernels(data):
     runs = []
     for tail, gate in ((True, True), (False, True), (True, False)):
         tr = _trainer(data, mode="async", shard="flat", steps=12, exchange_backend="xgmi")
-        assert tr.num_ps == 4 and tr.exchange.runner is not None
+        assert tr.num_ps == 3 and tr.exchange.runner is not None
         tr.exchange.runner.set_use_tail(tail)
         tr.exchange.runner.set_gate(gate)
         s = tr.train()

@@ -123,7 +123,7 @@ def test_replicated_bucket_is_the_last_backward_segments():
     assert last_segment_bucket(plan, segs) == 0 and len(plan.bucket_ranges) == 1
 
 
-SEGS = [list(range(8, 14)), [6, 7], [4, 5], [0, 1, 2, 3]]  # models.HIP_SEGMENTS
+SEGS = [list(range(8, 14)), [6, 7], [4, 5], [0, 1, 2, 3]]  # models.HIP_SEGMENTS until round 5
 
 
 @pytest.mark.parametrize("P", [4, 5, 6, 8, 16])
@@ -161,3 +161,20 @@ def test_segment_aligned_ps_counts():
         make_plan("flat", 3, buckets=SEGS, segment_aligned=True)
     with pytest.raises(ValueError):
         make_plan("contiguous", 4, buckets=SEGS, segment_aligned=True)
+
+
+def test_async_groups_merge_the_tiny_head_segment():
+    """The HIP engine's segment 0 holds only fc3 (5,130 parameters: fc1 / fc2's weight
+    gradients run in the conv4 dual launch since round 6); the async plan folds it into the
+    segment completed after it instead of spending a PS per host on it."""
+    from ddl_amd.models import HIP_SEGMENTS
+    from ddl_amd.parallel.sharding import async_groups
+    g = async_groups(HIP_SEGMENTS)
+    assert g == [list(range(6, 14)), [4, 5], [0, 1, 2, 3]]
+    got = {W: segment_aligned_num_ps(W, g) for W in (1, 2, 4, 8)}
+    assert got == {1: 3, 2: 4, 4: 8, 8: 8}
+    for W, P in got.items():
+        plan = make_plan("flat", P, buckets=g, segment_aligned=True)
+        assert host_imbalance(plan, W) <= 1.25
+    # a plan whose groups are all large is left alone
+    assert async_groups(SEGS) == [sorted(x) for x in SEGS]

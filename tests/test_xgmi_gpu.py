@@ -293,9 +293,10 @@ def _async_rank(rank, world, port, outdir, kw):
     (4, dict(shard="greedy", num_ps=4)),         # mnist_async_sharding_greedy
     (3, dict(shard="contiguous", num_ps=5)),     # several PS per host
     (2, dict(shard="greedy", _env=dict(DDL_ASYNC_NATIVE="0"))),  # the Python push_pull path
-    # segment-aligned flat plans (sharding.segment_aligned_num_ps): 4 PS on one host, 6 on two
-    pytest.param(1, dict(shard="flat", _ps=4), id="1-flat"),
-    pytest.param(2, dict(shard="flat", _ps=6), id="2-flat"),
+    # segment-aligned flat plans (sharding.async_groups + segment_aligned_num_ps): 3 PS on one
+    # host, 4 on two
+    pytest.param(1, dict(shard="flat", _ps=3), id="1-flat"),
+    pytest.param(2, dict(shard="flat", _ps=4), id="2-flat"),
 
     pytest.param(8, dict(shard="contiguous", _env=dict(GPU_MAX_HW_QUEUES="1",
                                                        DDL_XGMI_TIMEOUT_S="60")), id="w8-contig"),
