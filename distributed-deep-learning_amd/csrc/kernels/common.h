@@ -132,6 +132,26 @@ DDL_DEV float group_sum(float v) {
 }
 DDL_DEV float wave_sum(float v) { return group_sum<64>(v); }
 
+// 4x4 transpose inside each lane quad: lane qi (= lane & 3) holds a0..a3 (rows 0..3 of column
+// qi) and gets row qi of columns 0..3.  Round k: every lane sends a[(qi + k) & 3]; DPP
+// quad_perm makes lane qi read lane (qi - k) & 3, whose value is its a[qi] = element (qi, that
+// column).  Every lane of the wave must be active.
+template <int CTRL>
+DDL_DEV float quad_rot(float v) { return dpp_f<CTRL>(v); }
+DDL_DEV float4 quad_transpose(float a0, float a1, float a2, float a3, int qi) {
+  auto pick = [&](int s) { return s == 0 ? a0 : s == 1 ? a1 : s == 2 ? a2 : a3; };
+  float b[4];
+  b[0] = b[1] = b[2] = b[3] = 0.f;
+  const float own = pick(qi);
+  const float r1 = quad_rot<0x93>(pick((qi + 1) & 3));  // quad_perm [3, 0, 1, 2]
+  const float r2 = quad_rot<0x4E>(pick((qi + 2) & 3));  // quad_perm [2, 3, 0, 1]
+  const float r3 = quad_rot<0x39>(pick((qi + 3) & 3));  // quad_perm [1, 2, 3, 0]
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    b[c] = c == qi ? own : c == ((qi + 3) & 3) ? r1 : c == ((qi + 2) & 3) ? r2 : r3;
+  return make_float4(b[0], b[1], b[2], b[3]);
+}
+
 DDL_DEV float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
 // ---------------------------------------------------------------------------------------------

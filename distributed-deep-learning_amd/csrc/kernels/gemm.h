@@ -44,9 +44,6 @@
 
 // s_setprio 1 around each K tile's MFMA cluster (guide T5; measured 0.3753 -> 0.3747 ms/step)
 #define DDL_MFMA_PRIO 1
-#ifndef DDL_EPI_PRIO
-#define DDL_EPI_PRIO 0
-#endif
 #include "scratch.h"
 #include "stamps.h"
 #include "tail.h"
@@ -166,6 +163,13 @@ struct HasOnesA : std::false_type {};
 template <class P>
 struct HasOnesA<P, std::void_t<decltype(std::declval<const P&>().ones_group(
                        std::declval<const typename P::AInfo&>()))>> : std::true_type {};
+// a policy with a row-wise epilogue epi_t(m, n0, float4 = row m, columns n0 .. n0 + 3): the tile
+// epilogue transposes each lane quad's 4 rows x 4 columns first (GemmTile::epilogue)
+template <class P, class = void>
+struct HasEpiT : std::false_type {};
+template <class P>
+struct HasEpiT<P, std::void_t<decltype(std::declval<const P&>().epi_t(0, 0, float4{}))>>
+    : std::true_type {};
 template <class P, class = void>
 struct HasDma : std::false_type {};
 template <class P>
@@ -889,6 +893,25 @@ struct GemmTile {
     const int lane = threadIdx.x & 63, wave = (threadIdx.x & (NT - 1)) >> 6;
     const int wm = wave / WN, wn = wave % WN;
     const int lr = lane & 31, lh = lane >> 5;
+    if constexpr (HasEpiT<P>::value) {
+      // row-wise: lane quad (columns 4k .. 4k+3, one row group) transposed so lane k of the
+      // quad holds row m0 + k, columns 4k' .. 4k'+3 — one 16-byte store where the column-wise
+      // epilogue issued four 4-byte ones (every lane active here: the guards follow the DPP)
+      const int qi = lane & 3;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x16& v = acc[i][j];
+            const float4 t = quad_transpose(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3], qi);
+            const int n0 = n_blk + wn * WTN + j * 32 + (lr & ~3);
+            const int m = m_blk + wm * WTM + i * 32 + 8 * g + 4 * lh + qi;
+            if (n0 < p.N && m < p.M) p.epi_t(m, n0, t);
+          }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -1022,7 +1045,7 @@ struct GemmTile {
 template <int BM, int BN, int BK, int WM, int WN, class P, int V = 0>
 DDL_DEV int splitk_body(const P& p, int kchunk, int mode, float4* __restrict__ slab,
                          int* __restrict__ tickets, int bx, int by, int bz, int gx, int gy,
-                         int gz, float* lds, int* flag) {
+                         int gz, float* lds, int* flag, unsigned long long* mid = nullptr) {
   using T = GemmTile<BM, BN, BK, WM, WN, P, V>;
   using G = typename T::G;
   const int m_blk = bx * BM;
@@ -1045,17 +1068,22 @@ DDL_DEV int splitk_body(const P& p, int kchunk, int mode, float4* __restrict__ s
     nkt = (max(0, ke - kb) + BK - 1) / BK;
     T::mainloop(p, m_blk, n_blk, kb, ke, lds, acc);
   }
+#if DDL_STAMPS
+  if (mid) mid[0] = __builtin_amdgcn_s_memrealtime();  // main loop done
+#else
+  (void)mid;
+#endif
   if (mode != 0) {
     const int tile = by * gx + bx;
     const int ntiles = gx * gy;
     const brsrc_t sr = make_rsrc(slab, (uint32_t)(gz * ntiles * G::PART4 * 16u));
     T::store_partial(sr, ((size_t)bz * ntiles + tile) * G::PART4, acc);
     if (mode == 2) return nkt;
-    if (!T::arrive(&tickets[tile], gz, flag)) return nkt;
-#if DDL_EPI_PRIO
-    // the last arriver's sum + fused epilogue end the tile: ahead of the MFMA loops
-    __builtin_amdgcn_s_setprio(DDL_EPI_PRIO);
+    const bool last = T::arrive(&tickets[tile], gz, flag);
+#if DDL_STAMPS
+    if (mid) mid[1] = __builtin_amdgcn_s_memrealtime();  // partial stored, ticket back
 #endif
+    if (!last) return nkt;
     T::sum_partials(sr, (size_t)tile * G::PART4, (size_t)ntiles * G::PART4, gz, acc);
   }
   T::epilogue(p, m_blk, n_blk, acc);
@@ -1097,12 +1125,14 @@ DDL_DEV void run_sub(const P& p, const SubGrid& g, int vb, float* lds, int* flag
   split_coords(g, vb, bx, by, bz);
 #if DDL_STAMPS
   const Stamp st0 = stamp_now();
-#endif
+  unsigned long long mid[2] = {0, 0};
+  const int nkt = splitk_body<BM, BN, BK, WM, WN, P, V>(p, g.kchunk, g.mode, g.slab, g.tickets,
+                                                        bx, by, bz, g.gx, g.gy, g.gz, lds, flag,
+                                                        mid);
+  stamp_block(g.stamps, vb, st0, nkt, bx, by, bz, mid);
+#else
   const int nkt = splitk_body<BM, BN, BK, WM, WN, P, V>(p, g.kchunk, g.mode, g.slab, g.tickets,
                                                         bx, by, bz, g.gx, g.gy, g.gz, lds, flag);
-#if DDL_STAMPS
-  stamp_block(g.stamps, vb, st0, nkt, bx, by, bz);
-#else
   (void)nkt;
 #endif
 }
@@ -1125,13 +1155,16 @@ gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __res
   const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
 #if DDL_STAMPS
   const Stamp st0 = stamp_now();
+  unsigned long long mid[2] = {0, 0};
+#else
+  unsigned long long* mid = nullptr;
 #endif
   const int nkt = splitk_body<BM, BN, BK, WM, WN, P, V>(
       p, kchunk, mode, slab, tickets, bx, by, bz, gridDim.x, gridDim.y, gridDim.z,
-      reinterpret_cast<float*>(lds4), reinterpret_cast<int*>(lds4));
+      reinterpret_cast<float*>(lds4), reinterpret_cast<int*>(lds4), mid);
 #if DDL_STAMPS
   stamp_block(stamps, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), st0, nkt,
-              bx, by, bz);
+              bx, by, bz, mid);
 #else
   (void)nkt;
 #endif
@@ -1178,7 +1211,13 @@ DDL_DEV void kwave_body(const P& p, int bx, int by, float4* lds4, int L) {
       for (int j = 0; j < 4; ++j) v[j] += red[(ww * 16 + 4 * g + j) * 64 + lane];
     const int n = n_blk + (lane & 31);
     const int m0 = m_blk + 8 * g + 4 * (lane >> 5);
-    if (n < p.N && m0 < p.M) p.epi(m0, n, f32x4{v[0], v[1], v[2], v[3]});
+    if constexpr (HasEpiT<P>::value) {  // row-wise (GemmTile::epilogue): whole wave active here
+      const int qi = lane & 3;
+      const float4 t = quad_transpose(v[0], v[1], v[2], v[3], qi);
+      if (n - qi < p.N && m0 + qi < p.M) p.epi_t(m0 + qi, n - qi, t);
+    } else {
+      if (n < p.N && m0 < p.M) p.epi(m0, n, f32x4{v[0], v[1], v[2], v[3]});
+    }
   }
 }
 

@@ -390,14 +390,60 @@ struct ConvDgrad {
     return loadB(b, kreal(win, kv));
   }
   DDL_DEV void epi(int m0, int n, f32x4 v) const {
+    // one row decode per group of 4 (its runtime division by the image count), then a carry:
+    // the pixel-major K-map order puts 4 images of one pixel in a group (wrapping at most once)
+    int b, y, xx;
+    row_pix(m0 < M ? m0 : 0, b, y, xx);
+    const int nimg = M / (H * H);
+    uint8_t cd[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {  // every code load issued before the first store
+      int br = b, yr = y, xr = xx;
+      step_row(br, yr, xr, r, nimg);
+      cd[r] = m0 + r < M ? code_prev[((size_t)(br * H + yr) * H + xr) * CIN + n] : 0;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int m = m0 + r;
-      if (m >= M) break;
-      int b, y, xx;
-      row_pix(m, b, y, xx);
-      const size_t px = (size_t)(b * H + y) * H + xx;
-      pool_bwd_scatter<HPREV, CIN>(dpre_prev, b, y, xx, n, code_prev[px * CIN + n], v[r]);
+      if (m0 + r >= M) break;
+      int br = b, yr = y, xr = xx;
+      step_row(br, yr, xr, r, nimg);
+      pool_bwd_scatter<HPREV, CIN>(dpre_prev, br, yr, xr, n, cd[r], v[r]);
+    }
+  }
+  // row m, columns n0 .. n0 + 3 (the tile epilogue's quad transpose, gemm.h HasEpiT): one
+  // 4-byte load of the four codes, then one 16-byte store per pool-window position
+  DDL_DEV void epi_t(int m, int n0, float4 v) const {
+    int b, y, xx;
+    row_pix(m, b, y, xx);
+    const size_t px = (size_t)(b * H + y) * H + xx;
+    const uint32_t cw = *reinterpret_cast<const uint32_t*>(code_prev + px * CIN + n0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int yy = 2 * y + (q >> 1), x2 = 2 * xx + (q & 1);
+      if (yy >= HPREV || x2 >= HPREV) continue;
+      const uint32_t qq = (uint32_t)q;
+      float4 o;
+      o.x = (cw & 0xFFu) == qq ? v.x : 0.f;
+      o.y = ((cw >> 8) & 0xFFu) == qq ? v.y : 0.f;
+      o.z = ((cw >> 16) & 0xFFu) == qq ? v.z : 0.f;
+      o.w = (cw >> 24) == qq ? v.w : 0.f;
+      *reinterpret_cast<float4*>(dpre_prev + map_off<HPREV, CIN, (HPREV < 28)>(b, yy, x2, n0)) = o;
+    }
+  }
+  // (b, y, x) of row m0 + r from that of m0 (r < 4)
+  DDL_DEV void step_row(int& b, int& y, int& x, int r, int nimg) const {
+    if constexpr (KMAP) {  // m = (y*H + x)*nimg + b: image fastest
+      b += r;
+      while (b >= nimg) {  // (once for batches >= 4)
+        b -= nimg;
+        if (++x == H) { x = 0; ++y; }
+      }
+    } else {  // m = (b*H + y)*H + x: pixel fastest
+      x += r;
+      if (x >= H) {
+        x -= H;
+        if (++y == H) { y = 0; ++b; }
+      }
     }
   }
 };
@@ -817,6 +863,17 @@ struct FcDgradAct : FcDgradBase {
       dx[o] = hpost[o] > 0.f ? v[r] * inv_keep : 0.f;
     }
   }
+  // row m, columns n0 .. n0 + 3 (gemm.h HasEpiT): 16-byte load and store
+  DDL_DEV void epi_t(int m, int n0, float4 v) const {
+    const size_t o = (size_t)m * this->N + n0;
+    const float4 h = *reinterpret_cast<const float4*>(hpost + o);
+    float4 d;
+    d.x = h.x > 0.f ? v.x * inv_keep : 0.f;
+    d.y = h.y > 0.f ? v.y * inv_keep : 0.f;
+    d.z = h.z > 0.f ? v.z * inv_keep : 0.f;
+    d.w = h.w > 0.f ? v.w * inv_keep : 0.f;
+    *reinterpret_cast<float4*>(dx + o) = d;
+  }
 };
 
 template <int HP, int C>
@@ -834,6 +891,23 @@ struct FcDgradPool : FcDgradBase {
       const int m = m0 + r;
       if (m >= M) break;
       pool_bwd_scatter<HPREV, C>(dpre_prev, m, py, px, c, code[(size_t)m * N + n], v[r]);
+    }
+  }
+  // row m, columns n0 .. n0 + 3 (gemm.h HasEpiT): one 4-byte code load, four 16-byte stores
+  DDL_DEV void epi_t(int m, int n0, float4 v) const {
+    const int c0 = n0 % C, t = n0 / C;
+    const int px = t % HP, py = t / HP;
+    const uint32_t cw = *reinterpret_cast<const uint32_t*>(code + (size_t)m * this->N + n0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t qq = (uint32_t)q;
+      float4 o;
+      o.x = (cw & 0xFFu) == qq ? v.x : 0.f;
+      o.y = ((cw >> 8) & 0xFFu) == qq ? v.y : 0.f;
+      o.z = ((cw >> 16) & 0xFFu) == qq ? v.z : 0.f;
+      o.w = (cw >> 24) == qq ? v.w : 0.f;
+      *reinterpret_cast<float4*>(
+          dpre_prev + map_off<HPREV, C, true>(m, 2 * py + (q >> 1), 2 * px + (q & 1), c0)) = o;
     }
   }
 };
@@ -906,10 +980,9 @@ template <>
 struct KWaveOK<FcDgradAct> : std::true_type {};
 template <int HP, int C>
 struct KWaveOK<FcDgradPool<HP, C>> : std::true_type {};
-// the conv2-4 forwards (no dual partner): the K split inside one workgroup replaces the split-K
-// partial slab, the arrival tickets and the last arriver's sum (round 6 A/B)
-template <int H, int CIN, int COUT, bool KM>
-struct KWaveOK<ConvFwd<H, CIN, COUT, KM>> : std::bool_constant<(CIN % kBK == 0)> {};
+// (the conv2-4 forwards as K-wave launches — the K split inside one workgroup instead of the
+// split-K partials, tickets and last arriver — measured 277.9-288.6 us/step against 278.3 for
+// 4 / 8 / 16 waves: no gain, not instantiated; profiles/r6_sched_ab_kwave_fwd.log)
 // (the conv backward as K-wave tiles lost to the dual launches in every variant, 312-402 vs
 // 289.5 us/step, and was removed: docs/DESIGN.md round 5)
 

@@ -48,8 +48,10 @@ struct Stamp {
 DDL_DEV Stamp stamp_now() {
   return {__builtin_amdgcn_s_memrealtime(), __builtin_amdgcn_s_memtime()};
 }
+// mid (optional): the 100 MHz times at which the main loop ended and the split-K partial was
+// stored with its ticket back (splitk_body); they replace the shader-clock pair in r[2], r[3]
 DDL_DEV void stamp_block(unsigned long long* buf, int vb, const Stamp& s0, int nkt, int bx, int by,
-                         int bz) {
+                         int bz, const unsigned long long* mid = nullptr) {
   if (!buf || threadIdx.x != 0) return;
   const Stamp s1 = stamp_now();
   const unsigned hw = __builtin_amdgcn_s_getreg(0xf804);   // HW_REG_HW_ID
@@ -57,8 +59,8 @@ DDL_DEV void stamp_block(unsigned long long* buf, int vb, const Stamp& s0, int n
   unsigned long long* r = buf + (size_t)vb * 8;
   r[0] = s0.real;
   r[1] = s1.real;
-  r[2] = s0.cyc;
-  r[3] = s1.cyc;
+  r[2] = mid ? mid[0] : s0.cyc;
+  r[3] = mid ? mid[1] : s1.cyc;
   r[4] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
   r[5] = (unsigned long long)nkt;
   r[6] = (unsigned long long)bx | ((unsigned long long)by << 32);

@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--wide-variants", default="",
                     help="';'-separated split-K reduce overrides 'op=inl|wide,...' (inl: the "
                          "in-launch last arriver; wide: the separate reduce kernel); a "
-                         "'name=...' first labels it, and 'op=cfg:split' items set the config")
+                         "'name=...' first labels it, 'op=cfg:split' items set the config and "
+                         "'bf=mask' the dual_bfirst mask")
     ap.add_argument("--bfirst-variants", default="",
                     help="';'-separated dual_bfirst masks (bit op: that dual dispatches its "
                          "second problem first; default 1<<14)")
@@ -70,11 +71,15 @@ def main():
         cf = list(scheds["default"]["cfg"])
         sp = list(scheds["default"]["splits"])
         label = v
+        bf = 1 << 14
         for kv in v.split(","):
             if kv.startswith("name="):
                 label = kv[5:]
                 continue
             op, val = kv.split("=")
+            if op == "bf":
+                bf = int(val)
+                continue
             if val in ("inl", "wide"):
                 wd[int(op)] = (1 << 20) if val == "inl" else 1
             else:
@@ -82,7 +87,7 @@ def main():
                 cf[int(op)] = int(c)
                 if spl:
                     sp[int(op)] = int(spl)
-        scheds["wide[" + label + "]"] = dict(scheds["default"], wide=wd, cfg=cf, splits=sp)
+        scheds["wide[" + label + "]"] = dict(scheds["default"], wide=wd, cfg=cf, splits=sp, bfirst=bf)
     for v in filter(None, a.bfirst_variants.split(";")):
         scheds["bfirst[" + v + "]"] = dict(scheds["default"], bfirst=int(v))
     res = {k: [] for k in scheds}

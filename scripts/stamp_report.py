@@ -115,24 +115,34 @@ def main():
                 b = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sxx
                 fit = (my - b * mx, b)
             ep = [t for t, l in zip(d, last) if l]
+            # phases (diagnostic build with mid stamps): main loop, partial + ticket, epilogue
+            loop = [(r[2] - r[0]) / 100.0 for r in rs if r[2] > r[0]]
+            tick = [(r[3] - r[2]) / 100.0 for r in rs if r[3] > r[2] > 0]
+            epil = [(r[1] - r[3]) / 100.0 for r, l in zip(rs, last) if l and r[3] > 0]
             us_kt = [x / max(1, k) for x, k in zip(d, kt)]
             starts = [(r[0] - t0) / 100.0 for r in rs]
             ends = sorted((r[1] - t0) / 100.0 for r in rs)
-            ghz = [(r[3] - r[2]) / max(1, r[1] - r[0]) / 10.0 for r in rs if r[1] > r[0]]
+            ghz = [0.0]  # (r[2], r[3] hold the phase stamps now, not the shader clock)
             row = dict(launch=names[li % per_step], step=li // per_step, sub=sub, blocks=nb,
                        span=span, blk_med=pct(d, .5), blk_p10=pct(d, .1), blk_max=max(d),
                        us_per_kt=pct(us_kt, .5), kt_med=pct(kt, .5), kt_max=max(kt),
                        start90=pct(starts, .9), tail10=span - pct(ends, .9), waves_per_simd=wps,
                        max_resident=maxres, simds=nsimd, ghz=pct(ghz, .5),
                        fixed_us=fit[0] if fit else None, per_kt_us=fit[1] if fit else None,
-                       epi_blocks=len(ep), epi_med=pct(ep, .5) if ep else None)
+                       epi_blocks=len(ep), epi_med=pct(ep, .5) if ep else None,
+                       loop_med=pct(loop, .5) if loop else None,
+                       ticket_med=pct(tick, .5) if tick else None,
+                       epilogue_med=pct(epil, .5) if epil else None)
             out.append(row)
             print(f"{row['launch']:9s} {sub:3d} {nb:6d} {span:6.1f} {row['blk_med']:7.1f} "
                   f"{row['blk_p10']:7.1f} {row['blk_max']:7.1f} {row['us_per_kt']:6.2f} "
                   f"{row['kt_med']:6d} {row['kt_max']:6d} {row['start90']:7.1f} "
                   f"{row['tail10']:6.1f} {wps:6.2f} {maxres:6d} {row['ghz']:5.2f}"
                   + (f"  fit {fit[0]:5.2f} + {fit[1]:5.2f}/kt" if fit else "  fit -")
-                  + (f"  epi {len(ep)} med {row['epi_med']:5.1f}" if ep else ""))
+                  + (f"  epi {len(ep)} med {row['epi_med']:5.1f}" if ep else "")
+                  + (f"  phases loop {row['loop_med']:5.1f}" if loop else "")
+                  + (f" ticket {row['ticket_med']:4.1f}" if tick else "")
+                  + (f" epi {row['epilogue_med']:4.1f}" if epil else ""))
     if a.json:
         json.dump(out, open(a.json, "w"), indent=1)
         # the last step's raw records (one row per block: stamps.h layout) + sub-grid table

@@ -73,6 +73,9 @@ def test_bench_torchrun_two_ranks_json(port):
     assert rec["time_to_acc"]["data_sharding"] == "stride"
     assert rec["time_to_acc_replicate"]["data_sharding"] == "replicate"
     assert rec["time_to_acc_replicate"]["steps_per_worker"] == 2
+    # and on the hard synthetic set, under both protocols
+    assert rec["time_to_acc_hard"]["data"].startswith("synthetic-hard")
+    assert rec["time_to_acc_hard_replicate"]["data_sharding"] == "replicate"
 
 
 @pytest.mark.slow
