@@ -163,7 +163,8 @@ def main(argv=None):
                 return type(ex).__name__
             svc = getattr(ex, "service_mode", None)  # PS side: the native host service
             return ("native-" if getattr(ex, "runner", None) is not None else "python-") + \
-                "xgmi-async" + (f" ({svc} service)" if svc else "")
+                "xgmi-async" + (" (in-line applies)" if svc == "inline" else
+                                f" ({svc} service)" if svc else "")
         if not getattr(ex, "native", False):
             return "python"
         return "native-" + getattr(ex, "backend", "rccl")

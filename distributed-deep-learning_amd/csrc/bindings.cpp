@@ -532,9 +532,39 @@ class PyAsyncRunner {
   int64_t epoch() const { return r_->epoch(); }
   void set_use_tail(bool on) { r_->set_use_tail(on); }
   void set_gate(bool on) { r_->set_gate(on); }
+  // ps: list of (ps id, private params, m, v, t), every PS (W = 1, Adam)
+  void set_inline(py::list ps, double lr, double b1, double b2, double eps, double scale,
+                  bool provenance) {
+    std::vector<ddl::AsyncPsState> st;
+    for (auto item : ps) {
+      auto t = item.cast<py::tuple>();
+      ddl::AsyncPsState s;
+      s.ps = t[0].cast<int>();
+      at::Tensor w = t[1].cast<at::Tensor>(), m = t[2].cast<at::Tensor>();
+      TORCH_CHECK(!t[3].is_none(), "in-line applies are Adam: v required");
+      at::Tensor v = t[3].cast<at::Tensor>();
+      check_f32_cuda(w, "ps params");
+      check_f32_cuda(m, "m");
+      check_f32_cuda(v, "v");
+      keep_.push_back(w);
+      keep_.push_back(m);
+      keep_.push_back(v);
+      s.params = w.data_ptr<float>();
+      s.m = m.data_ptr<float>();
+      s.v = v.data_ptr<float>();
+      s.t = t[4].cast<int64_t>();
+      st.push_back(s);
+    }
+    r_->set_inline(st, (float)lr, (float)b1, (float)b2, (float)eps, (float)scale, provenance);
+  }
+  bool inline_on() const { return r_->inline_on(); }
+  int64_t inline_t(int64_t ps) const { return r_->inline_t((int)ps); }
+  void inline_sync_ps() { r_->inline_sync_ps(cur_stream()); }
+  std::vector<std::array<int64_t, 4>> inline_provenance() const { return r_->inline_provenance(); }
 
  private:
   PyEngine& eng_;
+  std::vector<at::Tensor> keep_;
   std::unique_ptr<ddl::AsyncRunner> r_;
 };
 
@@ -841,7 +871,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("finish", &PyAsyncRunner::finish)
       .def("epoch", &PyAsyncRunner::epoch)
       .def("set_use_tail", &PyAsyncRunner::set_use_tail)
-      .def("set_gate", &PyAsyncRunner::set_gate);
+      .def("set_gate", &PyAsyncRunner::set_gate)
+      .def("set_inline", &PyAsyncRunner::set_inline)
+      .def("inline_on", &PyAsyncRunner::inline_on)
+      .def("inline_t", &PyAsyncRunner::inline_t)
+      .def("inline_sync_ps", &PyAsyncRunner::inline_sync_ps)
+      .def("inline_provenance", &PyAsyncRunner::inline_provenance);
 
   py::class_<PyPeer>(m, "PeerExchange")
       .def(py::init<at::Tensor, at::Tensor, int64_t, int64_t, py::list, int64_t, int64_t>(),

@@ -125,7 +125,7 @@ struct Engine {
   // bit op: that dual launch dispatches its second problem first.  conv2's (weight gradient
   // split 32 ways, the longer pole) measured 0.3663 -> 0.3650 ms/step; conv4's / conv3's worse
   // (their data gradients are the longer poles; conv4's stream-K loses its XCD-major numbering).
-  int dual_bfirst = 1 << OP_CONV2_DGRAD;
+  int dual_bfirst = (1 << OP_CONV2_DGRAD) | (1 << OP_CONV3_DGRAD);
   int dual_order(int op) const { return (dual_bfirst >> op) & 1; }
 
   // workspace carve-out
@@ -426,6 +426,10 @@ class AsyncPeer {
              hipStream_t st);
   int error() const;
   int num_ps() const { return nps_; }
+  // PS p's range of the parameter / gradient buffers and its host
+  void shard(int p, int64_t& lo, int64_t& n, int& host) const;
+  float* params() const { return params_; }
+  const float* grads() const { return grads_; }
 
  private:
   void upload_table();           // table_ -> table_dev_ (set-up only: open, attach_done)
@@ -513,10 +517,33 @@ class AsyncRunner {
   void set_use_tail(bool on) { use_tail_ = on; }
   // the pull as a GPU-side gate before the next forward (default) or a host wait
   void set_gate(bool on) { gate_ = on; }
+  // In-line applies (one worker, every PS hosted by it, Adam): each push is applied on the
+  // compute stream as Adam tail blocks of the next segment's launch — the last segment's inside
+  // conv1's weight-gradient launch — with the PS's m / v and its own step counter t, in push
+  // order.  A sole pusher's push order IS the arrival order, so no board claim, apply kernel,
+  // DONE word or gate is needed; the PS's private parameter copy is not touched per step (it
+  // equals the worker's buffer: inline_sync_ps() writes it back for checkpoints).  `ps` gives
+  // every PS's m, v and t (its params pointer: the private copy).
+  void set_inline(const std::vector<AsyncPsState>& ps, float lr, float b1, float b2, float eps,
+                  float scale, bool provenance);
+  bool inline_on() const { return inline_; }
+  int64_t inline_t(int ps) const;
+  void inline_sync_ps(hipStream_t st);  // worker buffer -> every PS's private copy
+  // (worker, ps, round, t) per in-line apply, when provenance was asked for
+  const std::vector<std::array<int64_t, 4>>& inline_provenance() const { return prov_; }
 
  private:
   void wait_round(double timeout_s);
   void check_round(uint32_t e, double timeout_s);
+  void step_inline(const float* x, const int64_t* labels, int B, hipStream_t st);
+  UpdTail inline_tail(int seg, int f4_per_block);
+  bool inline_ = false, keep_prov_ = false;
+  std::vector<AsyncPsState> ips_;  // by PS id
+  float lr_ = 0.f, b1_ = 0.f, b2_ = 0.f, eps_ = 0.f, scale_ = 1.f;
+  std::vector<float> lr_t_;        // this round's TF1 Adam step size per PS
+  std::vector<std::array<int64_t, 4>> prov_;
+  hipStream_t last_st_ = nullptr;
+  bool stepped_ = false;
   bool use_tail_ = true;
   bool gate_ = true;
   uint32_t gated_ = 0;  // the round the last step's gate waits for (0: none)

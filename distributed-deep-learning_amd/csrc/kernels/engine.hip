@@ -49,9 +49,14 @@ Engine::Engine() {
   // (round 3, conv forwards on the LDS-DMA main loop: conv2 / conv3 / conv4 forward split-K
   // 3 / 3 / 6 instead of 2 / 4 / 8, 302.5 -> 299.0 us fwd+bwd, scripts/sched_ab.py
   // --splits-variants, profiles/r3_sched_ab_ldsdma.log)
-  static const int defs[OP_COUNT] = {1, 3, 3, 6, 8, 16, 4, 1, 4, 1, 4, 8, 8, 12, 4, 32, 1024};
+  // (round 6, after the row-wise data-gradient epilogues made the last arriver cheap: conv4's
+  // data gradient split-K 5 with the in-launch reduce instead of 4 + the separate wide reduce,
+  // conv3's split-K 5 instead of 8, and the conv3 dual dispatching its weight-gradient blocks
+  // first (api.h dual_bfirst): 279.2 -> 267.7 us/step, scripts/sched_ab.py,
+  // profiles/r6_sched_ab_grid.log)
+  static const int defs[OP_COUNT] = {1, 3, 3, 6, 8, 16, 4, 1, 4, 1, 5, 8, 5, 12, 4, 32, 1024};
   // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
-  static const bool inl[OP_COUNT] = {0, 1, 1, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0};
+  static const bool inl[OP_COUNT] = {0, 1, 1, 1, 0, 0, 1, 0, 0, 0, 1, 1, 1, 1, 1, 0, 0};
   memcpy(cfg, defc, sizeof(defc));
   memcpy(eval_cfg, defc, sizeof(defc));
   // eval forward at 10k-row chunks (scripts/eval_sweep.py, after the compact conv3 rows):

@@ -44,6 +44,26 @@ DDL_DEV void head_logits_hv(const float (&hv)[2], const float* __restrict__ w,
   for (int c = 0; c < HC; ++c)
     acc[c] = ((part[0][c] + part[1][c]) + (part[2][c] + part[3][c])) + bias[c];
 }
+// the same with the thread's two W3 rows and fc3's bias already in registers (bitwise equal)
+DDL_DEV void head_logits_regs(const float (&hv)[2], const float (&wv)[2][HC], const float (&bb)[HC],
+                              float (&part)[4][HC], float (&acc)[HC]) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < HC; ++c) acc[c] = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int c = 0; c < HC; ++c) acc[c] = fmaf(hv[t], wv[t][c], acc[c]);
+#pragma unroll
+  for (int c = 0; c < HC; ++c) {
+    const float v = wave_sum(acc[c]);
+    if (lane == 0) part[wave][c] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < HC; ++c)
+    acc[c] = ((part[0][c] + part[1][c]) + (part[2][c] + part[3][c])) + bb[c];
+}
 // thread (wave, lane) holds h2 columns k = wave*128 + t*64 + lane, t = 0, 1
 DDL_DEV void head_logits(const float* __restrict__ hr, const float* __restrict__ w,
                          const float* __restrict__ bias, float (&part)[4][HC],
@@ -208,6 +228,20 @@ head_fused_fc2_kernel(const float* __restrict__ slab, int S, int gx, int ntiles,
   if (row >= B) return;
   const uint32_t key = thr24 ? ddl_mix32((seed ? *seed : seed_v) + 2u * 0x9E3779B9u) : 0u;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // every operand that does not depend on the partial sums is loaded up front, so the kernel's
+  // dependent chain is one round of partial loads instead of four load rounds: this thread's two
+  // W3 rows (the logits AND its two dh2 columns below), fc2's bias, fc3's bias, the label
+  float wv[2][HC], b2v[2], bb[HC];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int k = wave * 128 + t * 64 + lane;
+#pragma unroll
+    for (int c = 0; c < HC; ++c) wv[t][c] = w[k * HC + c];
+    b2v[t] = b2[k];
+  }
+#pragma unroll
+  for (int c = 0; c < HC; ++c) bb[c] = bias[c];
+  const int lab = (int)labels[row];
   const int bx = row >> 5, r = row & 31;
   const int fg = r >> 3, comp = r & 3, half = (r & 7) >> 2;
   const size_t zstride = (size_t)ntiles * 256 * 4;  // floats per split (PART4 = 256 float4)
@@ -232,20 +266,19 @@ head_fused_fc2_kernel(const float* __restrict__ slab, int S, int gx, int ntiles,
   for (int t = 0; t < 2; ++t) {
     const int k = wave * 128 + t * 64 + lane;
     const uint32_t idx = (uint32_t)(row * HK + k);
-    float val = hv[t] + b2[k];  // FcFwd<false>: no ReLU
+    float val = hv[t] + b2v[t];  // FcFwd<false>: no ReLU
     if (thr24) val = ddl_keep(key, idx, thr24) ? val * inv_keep : 0.f;
     h2[idx] = val;
     hv[t] = val;
   }
   float acc[HC];
-  head_logits_hv(hv, w, bias, part, acc);
+  head_logits_regs(hv, wv, bb, part, acc);
   float mx = acc[0];
 #pragma unroll
   for (int c = 1; c < HC; ++c) mx = acc[c] > mx ? acc[c] : mx;
   float se = 0.f;
 #pragma unroll
   for (int c = 0; c < HC; ++c) se += __expf(acc[c] - mx);
-  const int lab = (int)labels[row];
   float dl[HC];
 #pragma unroll
   for (int c = 0; c < HC; ++c) dl[c] = (__expf(acc[c] - mx) / se - (c == lab ? 1.f : 0.f)) * inv_batch;
@@ -263,11 +296,15 @@ head_fused_fc2_kernel(const float* __restrict__ slab, int S, int gx, int ntiles,
       if (c == (int)threadIdx.x) v = dl[c];
     dlog[(size_t)row * HC + threadIdx.x] = v;
   }
-  for (int i = threadIdx.x; i < HK; i += 256) {
+  // dh2 of this thread's two columns from the W3 rows already in registers (the same fmaf chain
+  // per element as head_fused_kernel's loop over i)
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int k = wave * 128 + t * 64 + lane;
     float g = 0.f;
 #pragma unroll
-    for (int c = 0; c < HC; ++c) g = fmaf(dl[c], w[i * HC + c], g);
-    const int idx = row * HK + i;
+    for (int c = 0; c < HC; ++c) g = fmaf(dl[c], wv[t][c], g);
+    const int idx = row * HK + k;
     if (thr24) g = ddl_keep(key, (uint32_t)idx, thr24) ? g * inv_keep : 0.f;
     dpre2[idx] = g;
   }

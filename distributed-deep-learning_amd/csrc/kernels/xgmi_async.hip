@@ -434,6 +434,13 @@ void AsyncPeer::open(const std::vector<std::string>& handles) {
   opened_ok_ = true;
 }
 
+void AsyncPeer::shard(int p, int64_t& lo, int64_t& n, int& host) const {
+  if (p < 0 || p >= nps_) throw std::invalid_argument("async xgmi: PS id");
+  lo = table_.shard[p].lo;
+  n = table_.shard[p].n;
+  host = table_.shard[p].host;
+}
+
 void AsyncPeer::upload_table() {
   X_CHECK(hipMemcpy(table_dev_, &table_, sizeof(AsyncTable), hipMemcpyHostToDevice));
 }

@@ -28,6 +28,7 @@ tested on a one-GPU box (``tests/test_xgmi_gpu.py``).
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -41,6 +42,13 @@ from .sharding import ShardPlan
 
 class AsyncPeerUnavailable(RuntimeError):
     pass
+
+
+class _RunnerCounters:
+    """The runner's in-line step counters behind the service's ``t(ps)``."""
+
+    def __init__(self, runner):
+        self.t = runner.inline_t
 
 
 class AsyncPeerExchange:
@@ -124,6 +132,8 @@ class AsyncPeerExchange:
         self.provenance: List[Tuple[int, int, int, int]] = []
         self.runner = None
         self.service_mode = None
+        self.inline = False
+        self.inline_ok = False
 
     # -- the native worker step ----------------------------------------------------------------------
     def attach_runner(self, engine, segments) -> None:
@@ -132,7 +142,6 @@ class AsyncPeerExchange:
         itself on the arrival board), the previous round's pull as a host wait at the start of
         the step — when the engine is the HIP one.  DDL_ASYNC_NATIVE=0 keeps the Python
         push_pull path."""
-        import os
         from ..models.layout import TENSORS
         if getattr(engine, "name", "") != "hip" or os.environ.get("DDL_ASYNC_NATIVE", "1") != "1":
             return
@@ -144,6 +153,12 @@ class AsyncPeerExchange:
             seg_of_ps.append(max(seg_of[t] for t in ts))
         self.runner = native.ops().AsyncRunner(engine.eng, self.peer, self.env.world,
                                                self.env.rank, seg_of_ps, self.epoch)
+        # one worker hosting every PS (W = 1) with Adam: the pushes are applied in-line, as
+        # tail blocks of the next backward launch (async_runner.hip set_inline); start() turns
+        # it on once the PS state is final (a resume loads it after this point).
+        # DDL_ASYNC_INLINE=0 keeps the push / board / apply / gate chain at W = 1.
+        self.inline_ok = (self.env.world == 1 and self.opt == 0
+                          and os.environ.get("DDL_ASYNC_INLINE", "1") == "1")
 
     def native_step(self, engine, x, y, keep_prob: float, seed: int) -> None:
         engine._set_keep(keep_prob)
@@ -156,6 +171,9 @@ class AsyncPeerExchange:
         until its next step (checkpoint hook)."""
         if self.runner is not None:
             self.runner.finish(self.timeout_s)
+            if self.inline:  # the PS private copies follow the worker buffer they equal
+                self.runner.inline_sync_ps()
+                torch.cuda.synchronize(self.params.device)
 
     # -- set-up check ------------------------------------------------------------------------------
     def _selftest(self, agree) -> None:
@@ -208,6 +226,17 @@ class AsyncPeerExchange:
             return
         ps_list = [(p, ps.params, ps.m, ps.v, ps.t) for p, ps in self.servers.items()]
         h = next(iter(self.servers.values())).h
+        if self.runner is not None and self.inline_ok and len(ps_list) == self.plan.num_ps and \
+                all(torch.equal(ps.params, self.params[lo:hi])
+                    for p, ps in self.servers.items() for lo, hi in [self.ranges[p]]):
+            # (a PS that does not start from the worker's parameters — --ref-quirks Q4 — keeps
+            # the service: its apply stores the PS copy into the worker buffer)
+            self.runner.set_inline(ps_list, h.lr, h.beta1, h.beta2, h.eps, self.grad_scale,
+                                   self.check_provenance)
+            self.inline = True
+            self._inline_t0 = {p: ps.t for p, ps in self.servers.items()}
+            self.service_mode = "inline"
+            return
         mom = next(iter(self.servers.values())).momentum if self.mu is None else self.mu
         self._svc = native.ops().AsyncService(
             self.peer, self.env.world, ps_list, self.opt, h.lr, h.beta1, h.beta2, h.eps, mom,
@@ -223,10 +252,20 @@ class AsyncPeerExchange:
             ps.t += n
             ps.updates += n
 
+    def _sync_inline(self) -> None:
+        """In-line applies: the runner holds the step counters and the worker buffer holds the
+        parameters (drain_round wrote them back into the PS objects' private copies)."""
+        self._sync_counters(_RunnerCounters(self.runner))
+
     @contextlib.contextmanager
     def paused(self):
         """Checkpoint hook: no PS update is issued inside the block and every issued one has
         completed, so each hosted PS's parameters, m, v and t are one consistent step."""
+        if self.inline:  # every apply is on this worker's stream: drained by drain_round
+            self.drain_round()
+            self._sync_inline()
+            yield
+            return
         svc = self._svc
         if svc is None:  # not started (or joined): no update in flight
             yield
@@ -240,6 +279,12 @@ class AsyncPeerExchange:
 
     def join(self) -> None:
         self.drain_round()  # this worker's last round (the reference's final pull)
+        if self.inline:
+            self._sync_inline()
+            self.served = sum(self.runner.inline_t(p) - t0 for p, t0 in self._inline_t0.items())
+            if self.check_provenance:
+                self.provenance = [(w, p, e - 2, t)
+                                   for (w, p, e, t) in self.runner.inline_provenance()]
         if self._svc is not None:
             svc, self._svc = self._svc, None
             try:

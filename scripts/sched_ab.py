@@ -30,7 +30,7 @@ def main():
                          "'bf=mask' the dual_bfirst mask")
     ap.add_argument("--bfirst-variants", default="",
                     help="';'-separated dual_bfirst masks (bit op: that dual dispatches its "
-                         "second problem first; default 1<<14)")
+                         "second problem first)")
     a = ap.parse_args()
     import torch
     from ddl_amd.config import TrainConfig
@@ -43,7 +43,8 @@ def main():
                       engine="hip", quiet=True, data_sharding="stride")
     tr = Trainer(cfg, env, dataset=synthetic_mnist())
     e = tr.engine.eng
-    scheds = {"default": {"cfg": e.get_cfg(), "splits": e.get_splits(), "wide": e.get_wide()}}
+    scheds = {"default": {"cfg": e.get_cfg(), "splits": e.get_splits(), "wide": e.get_wide(),
+                          "bfirst": e.get_dual_bfirst()}}
     for p in a.tuned:
         scheds[os.path.basename(p)] = json.load(open(p))
     for v in filter(None, a.splits_variants.split(";")):
@@ -71,7 +72,7 @@ def main():
         cf = list(scheds["default"]["cfg"])
         sp = list(scheds["default"]["splits"])
         label = v
-        bf = 1 << 14
+        bf = scheds["default"]["bfirst"]
         for kv in v.split(","):
             if kv.startswith("name="):
                 label = kv[5:]
@@ -97,7 +98,7 @@ def main():
             e.set_cfg(s["cfg"])
             e.set_splits(s["splits"])
             e.set_wide(s["wide"])
-            e.set_dual_bfirst(s.get("bfirst", 1 << 14))
+            e.set_dual_bfirst(s["bfirst"])
             for _ in range(20):
                 tr.train_step(step)
                 step += 1

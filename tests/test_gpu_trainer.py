@@ -98,7 +98,9 @@ def test_async_eval_reports_the_same_accuracies(data):
 def test_async_local_elision_matches_inbox_copy(data, monkeypatch):
     """W = 1 async over xGMI (3 PS, one worker: the arrival order is fixed): the local push
     elision on and off (the apply reads the gradient in place / from the inbox) apply the same
-    Adam steps in the same order, so 12-step runs are bit-identical."""
+    Adam steps in the same order, so 12-step runs are bit-identical.  (The service path: at W = 1
+    the default is the runner's in-line applies, tests/test_xgmi_gpu.py.)"""
+    monkeypatch.setenv("DDL_ASYNC_INLINE", "0")
     runs = []
     for elide in ("1", "0"):
         monkeypatch.setenv("DDL_ASYNC_ELIDE_LOCAL", elide)
@@ -111,7 +113,7 @@ def test_async_local_elision_matches_inbox_copy(data, monkeypatch):
     assert torch.equal(runs[0], runs[1])
 
 
-def test_async_xgmi_push_tails_match_push_kernels(data):
+def test_async_xgmi_push_tails_match_push_kernels(data, monkeypatch):
     """W = 1 async over the xGMI data plane (segment-aligned flat plan: 3 PS): the gradient
     pushes riding as tail blocks of the next segment's launch (default) and the stand-alone
     push kernels deliver the same bytes, and the GPU-side pull gate (default) orders the next
@@ -119,7 +121,9 @@ def test_async_xgmi_push_tails_match_push_kernels(data):
     async plane equals one local (sync-path) step to rounding: the update is the same Adam in a
     different kernel (FMA contraction may differ by an ulp; over later steps Adam's early
     sign-normalised updates and the ReLU / max-pool switches amplify that into ~1e-4 parameter
-    differences, scripts/async_parity_probe.py, so only the first step is compared)."""
+    differences, scripts/async_parity_probe.py, so only the first step is compared).  The push /
+    board / apply / gate chain: DDL_ASYNC_INLINE=0 (the W = 1 default applies in line)."""
+    monkeypatch.setenv("DDL_ASYNC_INLINE", "0")
     runs = []
     for tail, gate in ((True, True), (False, True), (True, False)):
         tr = _trainer(data, mode="async", shard="flat", steps=12, exchange_backend="xgmi")

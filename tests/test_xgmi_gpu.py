@@ -272,8 +272,12 @@ def _async_rank(rank, world, port, outdir, kw):
         assert (tr.exchange.runner is not None) == want_native, "native async step not taken"
         s = tr.train()  # verify_provenance runs inside (check_provenance=True)
         torch.cuda.synchronize()
-        if tr.servers:  # the PS service this host ran: the native host scan
-            assert tr.exchange.service_mode == "host", tr.exchange.service_mode
+        if tr.servers:  # the PS service this host ran: the native host scan, or at W = 1 the
+            # runner's in-line applies (async_runner.hip set_inline)
+            inline = (world == 1 and want_native
+                      and extra_env.get("DDL_ASYNC_INLINE", "1") == "1")
+            want = "inline" if inline else "host"
+            assert tr.exchange.service_mode == want, tr.exchange.service_mode
         torch.save({"params": tr.params.cpu(), "served": tr.exchange.served,
                     "ps": {p: (sv.t, sv.params.cpu()) for p, sv in tr.servers.items()},
                     "ranges": {p: tr.plan.ps_segments(p)[0] for p in tr.servers},
@@ -288,7 +292,8 @@ def _async_rank(rank, world, port, outdir, kw):
 
 
 @pytest.mark.parametrize("world,kw", [
-    (1, dict(shard="none")),                     # one worker, its own PS through the mailbox
+    (1, dict(shard="none")),                     # one worker, its own PS: in-line applies
+    pytest.param(1, dict(shard="none", _env=dict(DDL_ASYNC_INLINE="0")), id="1-service"),
     (2, dict(shard="contiguous")),               # mnist_async_sharding
     (4, dict(shard="greedy", num_ps=4)),         # mnist_async_sharding_greedy
     (3, dict(shard="contiguous", num_ps=5)),     # several PS per host
@@ -326,6 +331,31 @@ def test_async_xgmi_serves_every_push(tmp_path, world, kw):
             assert any(torch.equal(o["params"][lo:hi], ps_params) for o in recs), p
 
 
+@pytest.mark.parametrize("shard,ps", [("none", 1), ("flat", 3)])
+def test_async_inline_apply_equals_service_w1(tmp_path, shard, ps):
+    """at W = 1 the pushes to the self-hosted PS are applied in-line (tail
+    blocks of the next backward launch) instead of through the board, the service's apply kernel
+    and the gate.  Same Adam arithmetic, same per-PS step counters, same order: the worker's
+    parameters and every PS's state must be bit-identical to the service path's."""
+    import torch.multiprocessing as mp
+    recs = {}
+    for mode in ("1", "0"):
+        d = tmp_path / f"inline{mode}"
+        d.mkdir()
+        kw = dict(shard=shard, _ps=ps, _env=dict(DDL_ASYNC_INLINE=mode))
+        mp.spawn(_async_rank, args=(1, free_port(), str(d), kw), nprocs=1, join=True)
+        recs[mode] = torch.load(d / "rank0.pt")
+    a, b = recs["1"], recs["0"]
+    assert len(a["ps"]) == ps
+    assert a["served"] == b["served"] == ps * ASYNC_STEPS
+    assert torch.equal(a["params"], b["params"])
+    for p in a["ps"]:
+        assert a["ps"][p][0] == b["ps"][p][0] == ASYNC_STEPS
+        assert torch.equal(a["ps"][p][1], b["ps"][p][1]), p
+        lo, hi = a["ranges"][p]
+        assert torch.equal(a["ps"][p][1], a["params"][lo:hi]), p
+
+
 def _ckpt_rank(rank, world, port, outdir, kw):
     if ROOT not in sys.path:
         sys.path.insert(0, ROOT)
@@ -346,21 +376,22 @@ def _ckpt_rank(rank, world, port, outdir, kw):
         tr.train()  # checkpoint_every=3: a mid-run snapshot while the PS services run
         torch.save({"t": {p: s.t for p, s in tr.servers.items()}},
                    os.path.join(outdir, f"final{rank}.pt"))
-        dist.barrier()
-        dist.destroy_process_group()
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
     except Exception:
         traceback.print_exc()
         raise
 
 
-def test_async_xgmi_midrun_checkpoint_is_consistent(tmp_path):
+@pytest.mark.parametrize("world", [2, 1])  # W = 1: the in-line applies
+def test_async_xgmi_midrun_checkpoint_is_consistent(tmp_path, world):
     """a mid-run async checkpoint must carry the PS step counters the native service
     advanced (beta powers consistent with the manifest's t) and a snapshot taken with the
     service paused; the final one equals the services' end state."""
     import json
     import torch.multiprocessing as mp
     from safetensors.torch import load_file
-    world = 2
     # the step-3 save runs while the peer's pushes are being served (it must neither deadlock
     # against the peer nor tear the PS state); the end-of-run save overwrites it and is checked
     mp.spawn(_ckpt_rank, args=(world, free_port(), str(tmp_path), dict(checkpoint_every=3)),
