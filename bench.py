@@ -383,10 +383,14 @@ def main(argv=None):
         tr2 = Trainer(cfg2, env, dataset=hard_data[0] if hard else data)
         keep.append(tr2)
         s = tr2.train()
+        hit = next((h for h in tr2.history if h["acc"] >= a.tta), None)
         if release:
             tr2 = None  # noqa: F841 - the frame's own reference, before the collect
             release_all()
         return {"target_acc": a.tta, "time_to_target_s": s["time_to_target"],
+                # the global step of the first eval at the target: convergence without the clock
+                # (ranks sharing one card slow the clock, not the steps)
+                "steps_to_target": hit["step"] if hit else None,
                 "final_acc": round(s["final_acc"], 4), "epoch_wall_s": round(s["wall_time"], 4),
                 "steps_per_worker": s["steps"], "eval_every": 10, "data_sharding": sharding,
                 "data": "synthetic-hard (utils/data.py HARD)" if hard else "synthetic",

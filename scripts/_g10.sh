@@ -7,7 +7,7 @@ import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 def f(k):
     t = d.get(k)
-    return "-" if not t else f"t95={t['time_to_target_s']} final={t['final_acc']} steps={t['steps_per_worker']}"
+    return "-" if not t else f"t95={t['time_to_target_s']} at-step={t.get('steps_to_target')} final={t['final_acc']}"
 print(sys.argv[2], d["ms_per_step"], d["config"].get("exchange"), "| easy", f("time_to_acc"), "| easy-rep", f("time_to_acc_replicate"), "| hard", f("time_to_acc_hard"), "| hard-rep", f("time_to_acc_hard_replicate"))
 PY
 }

@@ -71,6 +71,7 @@ def test_bench_torchrun_two_ranks_json(port):
     # shards, and time to accuracy under both them and the reference's replicated batches
     assert rec["config"]["data_sharding"] == "stride"
     assert rec["time_to_acc"]["data_sharding"] == "stride"
+    assert "steps_to_target" in rec["time_to_acc"]
     assert rec["time_to_acc_replicate"]["data_sharding"] == "replicate"
     assert rec["time_to_acc_replicate"]["steps_per_worker"] == 2
     # and on the hard synthetic set, under both protocols
