@@ -54,8 +54,10 @@ Engine::Engine() {
   // conv3's split-K 5 instead of 8, and the conv3 dual dispatching its weight-gradient blocks
   // first (api.h dual_bfirst): 279.2 -> 267.7 us/step, scripts/sched_ab.py,
   // profiles/r6_sched_ab_grid.log; then conv2's weight gradient split-K 48 instead of 32 and
-  // conv4's 6 instead of 8: 267.2 -> 264.8, profiles/r6_sched_ab_wgrad.log)
-  static const int defs[OP_COUNT] = {1, 3, 3, 6, 8, 16, 4, 1, 4, 1, 5, 6, 5, 12, 4, 48, 1024};
+  // conv4's 6 instead of 8: 267.2 -> 264.8, profiles/r6_sched_ab_wgrad.log; conv4's forward
+  // split-K 5 instead of 6 once the last arriver sums its partials in one batched round per 4:
+  // 264.4 -> 262.9, profiles/r6_runner_tune.log, r6_sched_ab_zb.log)
+  static const int defs[OP_COUNT] = {1, 3, 3, 5, 8, 16, 4, 1, 4, 1, 5, 6, 5, 12, 4, 48, 1024};
   // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
   static const bool inl[OP_COUNT] = {0, 1, 1, 1, 0, 0, 1, 0, 0, 0, 1, 1, 1, 1, 1, 0, 0};
   memcpy(cfg, defc, sizeof(defc));

@@ -48,6 +48,11 @@
 #include "stamps.h"
 #include "tail.h"
 
+// partials in flight per round of a one-fragment tile's split-K sum (sum_partials)
+#ifndef DDL_SPLITK_ZB
+#define DDL_SPLITK_ZB 4
+#endif
+
 namespace ddl {
 
 // One push-tail block (tail.h kind 1): arrival slice j of piece P — the gradient slice into the
@@ -962,7 +967,7 @@ struct GemmTile {
   // to zero() + one add_partial per z) with the loads of ZB partials in flight per round: one
   // add_partial per z waits a full sc1-load latency per partial, so a 12-way split's last
   // arriver spent ~12 load round trips in its epilogue — the longest block of the launch.
-  static constexpr int kZB = 4;  // partials in flight per round for a one-fragment tile
+  static constexpr int kZB = DDL_SPLITK_ZB;  // partials in flight per round, one-fragment tile
   static constexpr int ZB = TM * TN >= kZB ? 1 : kZB / (TM * TN);
   static DDL_DEV void sum_partials(brsrc_t slab, size_t base0, size_t zstride, int gz,
                                    f32x16 (&acc)[TM][TN]) {
@@ -970,18 +975,22 @@ struct GemmTile {
     const int lane_off = ((threadIdx.x & (NT - 1)) >> 6) * WPART + (threadIdx.x & 63);
     int z = 0;
     if constexpr (ZB > 1) {
-      for (; z + ZB <= gz; z += ZB) {
+      // the last round is a partial batch too (its missing partials add 0), so a split of up
+      // to ZB partials is ONE load round trip and g partials take ceil(g / ZB)
+      for (; z < gz; z += ZB) {
         float4 t[ZB][TM][TN][4];
 #pragma unroll
         for (int b = 0; b < ZB; ++b) {
           const int src = (int)(base0 + (size_t)(z + b) * zstride) + lane_off;
+          const bool have = z + b < gz;  // wave-uniform
 #pragma unroll
           for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
               for (int g = 0; g < 4; ++g)
-                t[b][i][j][g] = bload4_sc1(slab, (src + ((i * TN + j) * 4 + g) * 64) * 16);
+                t[b][i][j][g] = have ? bload4_sc1(slab, (src + ((i * TN + j) * 4 + g) * 64) * 16)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
         for (int b = 0; b < ZB; ++b)
@@ -996,7 +1005,7 @@ struct GemmTile {
               }
       }
     }
-    for (; z < gz; ++z) add_partial(slab, base0 + (size_t)z * zstride, acc);
+    for (; z < gz; ++z) add_partial(slab, base0 + (size_t)z * zstride, acc);  // (ZB == 1)
   }
   static DDL_DEV void zero(f32x16 (&acc)[TM][TN]) {
 #pragma unroll

@@ -1,4 +1,4 @@
-# usage: bash scripts/_ab_so.sh "so1 so2 ..." ROUNDS [bench args]  (A/B of in-tree builds)
+# usage: bash scripts/ab_so.sh "so1 so2 ..." ROUNDS [bench args]  (A/B of in-tree builds)
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out

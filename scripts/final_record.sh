@@ -1,3 +1,7 @@
+# Final-record GPU run: the GPU suite, smoke(), the headline bench (300-step windows and the
+# driver command), the async / forced-collective / contiguous variants, kernel stats, the step
+# timeline and per-block stamps -> gpurun_out/final_record.log (+ logs).  usage (GPU box):
+#   bash scripts/final_record.sh
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out

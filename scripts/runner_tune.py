@@ -14,8 +14,11 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from op_bench import OPS  # noqa: E402
+
+# engine op order (csrc/kernels/api.h enum Op)
+OPS = ["conv1_fwd", "conv2_fwd", "conv3_fwd", "conv4_fwd", "fc1_fwd", "fc2_fwd",
+       "fc2_dgrad", "fc2_wgrad", "fc1_dgrad", "fc1_wgrad", "conv4_dgrad", "conv4_wgrad",
+       "conv3_dgrad", "conv3_wgrad", "conv2_dgrad", "conv2_wgrad", "conv1_wgrad"]
 
 KWAVE_OK = {4, 5, 6, 8}  # fc forward / data-gradient GEMMs (csrc/kernels/layers.h KWaveOK)
 MF16_OK = {1, 2, 3, 10, 11, 12, 13, 14, 15}  # conv GEMMs with 16-byte gathers (layers.h Mf16OK)
@@ -76,7 +79,9 @@ def main():
             d = {k: list(v) for k, v in cur.items()}
             d["cfg"][op], d["splits"][op], d["wide"][op] = c2, s2, wd2
             return d
-        for s2 in {max(1, s // 2), min(2048, s * 2)} - {s}:
+        # x0.5 / x2, and the neighbours (+-1, x0.75 / x1.5) for a fine pass
+        for s2 in sorted({max(1, s // 2), min(2048, s * 2), max(1, s - 1), s + 1,
+                          max(1, (3 * s) // 4), min(2048, (3 * s) // 2)} - {s}):
             out.append(mk(c, s2, 0, wd))
         out.append(mk(c, s, 0, 1 if wd > 1 else W))            # toggle the reduce mode
         for c2 in (0, 3, 4, 5):  # the one-wave configs (dual launches instantiate these)

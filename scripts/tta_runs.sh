@@ -1,3 +1,5 @@
+# Time to accuracy (easy + hard synthetic sets) for sync / async at W = 1, and W = 2 / 4 as
+# processes sharing one card (gloo rehearsal) -> gpurun_out/tta_w*.json.  usage: bash scripts/tta_runs.sh
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
