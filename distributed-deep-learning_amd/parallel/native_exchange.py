@@ -241,12 +241,15 @@ class NativeSyncExchange(SyncExchange):
         peer, why = None, ""
         try:
             # at most this many workgroups per bucket kernel (>= 1024 elements each;
-            # DDL_XGMI_SLICES): forced W = 1 rehearsal 128 -> 256 -> 384: 0.3288 -> 0.3243 ->
-            # 0.3230 ms/step (fewer: 64 0.331, 32 0.42 — the bucket kernels outlast the
-            # backward).  Ranks sharing one GPU (the one-box rehearsals) keep 128: their
-            # spinning bucket kernels must all find room on the one card.
+            # DDL_XGMI_SLICES): forced W = 1 rehearsal, round 4: 128 -> 256 -> 384: 0.3288 ->
+            # 0.3243 -> 0.3230 ms/step (fewer: 64 0.331, 32 0.42 — the bucket kernels outlast
+            # the backward); round 6, with the shorter duals: 160 / 192 / 224 / 256 / 384:
+            # 0.2747-0.2751 / 0.2745 / 0.2759-0.2760 / 0.2774-0.2778 / 0.2784-0.2798 (the
+            # high-priority bucket kernel takes fewer of the slots the duals free,
+            # profiles/r6_xgmi_slices.log).  Ranks sharing one GPU (the one-box rehearsals)
+            # keep 128: their spinning bucket kernels must all find room on the one card.
             shared_gpu = env.world > max(1, torch.cuda.device_count())
-            slices = int(os.environ.get("DDL_XGMI_SLICES", "128" if shared_gpu else "384"))
+            slices = int(os.environ.get("DDL_XGMI_SLICES", "128" if shared_gpu else "192"))
             buckets = (specs if specs is not None
                        else [tuple(map(int, b)) for b in plan.bucket_ranges])
             peer = ops.PeerExchange(params, grads, env.world, env.rank, buckets, slices,
