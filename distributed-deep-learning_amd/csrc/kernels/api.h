@@ -30,7 +30,7 @@ void launch_adam(float* w, const float* g, float* m, float* v, int64_t n, float 
                  float b2, float eps, float scale, hipStream_t st);
 // same with c1 = 1 - beta1, c2 = 1 - beta2 precomputed (bit-identical to launch_adam)
 void launch_adam_c(float* w, const float* g, float* m, float* v, int64_t n, float lr_t, float c1,
-                   float c2, float eps, float scale, hipStream_t st);
+                   float c2, float eps, float scale, hipStream_t st, int max_grid = 2048);
 void launch_momentum(float* w, const float* g, float* m, int64_t n, float lr, float mu,
                      float scale, hipStream_t st);
 void launch_scale(float* p, int64_t n, float a, hipStream_t st);

@@ -67,9 +67,9 @@ __global__ void __launch_bounds__(256) scale_kernel(float* __restrict__ p, int64
        i += (int64_t)gridDim.x * blockDim.x)
     p[i] *= a;
 }
-static int grid_for(int64_t n) {
+static int grid_for(int64_t n, int max_grid = 2048) {
   int64_t b = (n + 255) / 256;
-  if (b > 2048) b = 2048;  // 8 blocks per CU, grid-stride beyond
+  if (b > max_grid) b = max_grid;  // (2048: 8 blocks per CU) grid-stride beyond
   return b < 1 ? 1 : (int)b;
 }
 
@@ -79,14 +79,14 @@ void launch_adam(float* w, const float* g, float* m, float* v, int64_t n, float 
 }
 
 void launch_adam_c(float* w, const float* g, float* m, float* v, int64_t n, float lr_t, float c1,
-                   float c2, float eps, float scale, hipStream_t st) {
+                   float c2, float eps, float scale, hipStream_t st, int max_grid) {
   if (n <= 0) return;
   const uintptr_t al = (uintptr_t)w | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v;
   if ((al & 15) == 0) {
-    DDL_LAUNCH(adam_vec_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, (float4*)w,
-                       (const float4*)g, (float4*)m, (float4*)v, n, lr_t, c1, c2, eps, scale);
+    DDL_LAUNCH(adam_vec_kernel, dim3(grid_for((n + 3) / 4, max_grid)), dim3(256), 0, st,
+               (float4*)w, (const float4*)g, (float4*)m, (float4*)v, n, lr_t, c1, c2, eps, scale);
   } else {
-    DDL_LAUNCH(adam_scalar_kernel, dim3(grid_for(n)), dim3(256), 0, st, w, g, m, v, n,
+    DDL_LAUNCH(adam_scalar_kernel, dim3(grid_for(n, max_grid)), dim3(256), 0, st, w, g, m, v, n,
                        lr_t, c1, c2, eps, scale);
   }
 }

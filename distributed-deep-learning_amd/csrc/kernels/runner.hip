@@ -281,9 +281,19 @@ void SyncRunner::set_optimizer(int kind, float lr, float b1, float b2, float eps
   opt_ = kind; lr_ = lr; b1_ = b1; b2_ = b2; eps_ = eps; mu_ = mu;
 }
 
+// An update on the comm stream overlaps the backward's dual launches: fewer workgroups leave
+// the slots those free to the duals (as the xGMI bucket kernels' cap, native_exchange.py).
+// Forced RCCL rehearsal, 300-step bench: 2048 / 512 / 256 / 128 / 64 workgroups: 0.2762-0.2771 /
+// 0.2745-0.2755 / 0.2723-0.2741 / 0.2717-0.2718 / 0.2752-0.2756 ms/step
+// (profiles/r6_comm_adam_grid.log)
+#ifndef DDL_COMM_ADAM_GRID
+#define DDL_COMM_ADAM_GRID 128
+#endif
 void SyncRunner::update(float* w, const float* g, float* m, float* v, int64_t n, float lr_t,
                         hipStream_t st) {
-  if (opt_ == 0) launch_adam(w, g, m, v, n, lr_t, b1_, b2_, eps_, grad_scale_, st);
+  if (opt_ == 0)
+    launch_adam_c(w, g, m, v, n, lr_t, 1.f - b1_, 1.f - b2_, eps_, grad_scale_, st,
+                  st == cs_ ? DDL_COMM_ADAM_GRID : 2048);
   else launch_momentum(w, g, m, n, lr_, mu_, grad_scale_, st);
 }
 

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--bfirst-variants", default="",
                     help="';'-separated dual_bfirst masks (bit op: that dual dispatches its "
                          "second problem first)")
+    ap.add_argument("--tail-variants", default="",
+                    help="';'-separated optimizer-tail layouts 'first:f4' (first: tail blocks "
+                         "ahead of the GEMM blocks; f4: float4 per tail block, default 0:512)")
     a = ap.parse_args()
     import torch
     from ddl_amd.config import TrainConfig
@@ -89,6 +92,9 @@ def main():
                 if spl:
                     sp[int(op)] = int(spl)
         scheds["wide[" + label + "]"] = dict(scheds["default"], wide=wd, cfg=cf, splits=sp, bfirst=bf)
+    for v in filter(None, a.tail_variants.split(";")):
+        fi, f4 = v.split(":")
+        scheds["tail[" + v + "]"] = dict(scheds["default"], tail=(int(fi), int(f4)))
     for v in filter(None, a.bfirst_variants.split(";")):
         scheds["bfirst[" + v + "]"] = dict(scheds["default"], bfirst=int(v))
     res = {k: [] for k in scheds}
@@ -99,6 +105,7 @@ def main():
             e.set_splits(s["splits"])
             e.set_wide(s["wide"])
             e.set_dual_bfirst(s["bfirst"])
+            tr.exchange.runner.set_tail_cfg(*s.get("tail", (0, 512)))
             for _ in range(20):
                 tr.train_step(step)
                 step += 1
