@@ -746,7 +746,7 @@ class SyncRunner {
   // measured (scripts/tail_probe.py, one MI355X): after the GEMM blocks, 512 float4 per
   // block: 373 us/step vs 381 without the tail; before the GEMM blocks 375-378
   int tail_first_ = 0;
-  int tail_f4_ = 4 * kTailF4PerBlock;
+  int tail_f4_ = kTailF4Default;
 };
 
 }  // namespace ddl

@@ -190,7 +190,7 @@ void AsyncRunner::step_inline(const float* x, const int64_t* labels, int B, hipS
   for (int s = 0; s < kSegments; ++s) {
     TraceRange r("ddl.bwd");
     if (s > 0 && !seg_ps_[s - 1].empty()) {
-      UpdTail t = inline_tail(s - 1, 4 * kTailF4PerBlock);
+      UpdTail t = inline_tail(s - 1, kTailF4Default);
       if (t.npieces) eng_->tail = t;
       else apply_now(s - 1);
     }

@@ -27,6 +27,11 @@ namespace ddl {
 constexpr int kTailPieces = 4;
 constexpr int kTailF4PerLane = 2;  // float4 per lane per pass: keeps the tail path under the GEMM paths' VGPRs
 constexpr int kTailF4PerBlock = 64 * kTailF4PerLane;  // one-wave blocks
+// float4 per tail block of a segment's Adam riding beside a dual launch's GEMM blocks (8 passes
+// of one wave; round 6, scripts/sched_ab.py --tail-variants: 256 / 512 / 768 / 1024 / 1280 /
+// 1536 / 2048 float4: 263.6 / 262.3-262.9 / 261.5 / 260.8-261.5 / 261.5 / 264.1 / 271.4 us/step,
+// profiles/r6_sched_ab_tail.log)
+constexpr int kTailF4Default = 8 * kTailF4PerBlock;
 
 struct UpdPiece {
   float* w = nullptr;      // 16-B aligned, n % 4 == 0 (checked by the host); push: the inbox slot

@@ -33,7 +33,7 @@ def main():
                          "second problem first)")
     ap.add_argument("--tail-variants", default="",
                     help="';'-separated optimizer-tail layouts 'first:f4' (first: tail blocks "
-                         "ahead of the GEMM blocks; f4: float4 per tail block, default 0:512)")
+                         "ahead of the GEMM blocks; f4: float4 per tail block, default 0:1024)")
     a = ap.parse_args()
     import torch
     from ddl_amd.config import TrainConfig
@@ -105,7 +105,7 @@ def main():
             e.set_splits(s["splits"])
             e.set_wide(s["wide"])
             e.set_dual_bfirst(s["bfirst"])
-            tr.exchange.runner.set_tail_cfg(*s.get("tail", (0, 512)))
+            tr.exchange.runner.set_tail_cfg(*s.get("tail", (0, 1024)))
             for _ in range(20):
                 tr.train_step(step)
                 step += 1
