@@ -1179,28 +1179,8 @@ gemm_f32_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __res
 #endif
 }
 
-// (Experiment, DDL_FWD_ITEMS > 1: each block of the LDS-DMA forward launches runs ITEMS work
-// items in turn — virtual blocks b, b + grid, ... in the 3-D grid's order — to measure what the
-// per-block fixed cost is worth: docs/DESIGN.md round 6.)
-#ifndef DDL_FWD_ITEMS
-#define DDL_FWD_ITEMS 1
-#endif
-template <int BM, int BN, int BK, int WM, int WN, class P, int V, int ITEMS>
-__global__ void __launch_bounds__(WM * WN * 64)
-gemm_items_kernel(P p, int kchunk, int mode, float4* __restrict__ slab, int* __restrict__ tickets,
-                  int gx, int gy, int gz, int nblocks) {
-  using T = GemmTile<BM, BN, BK, WM, WN, P, V>;
-  __shared__ float4 lds4[T::LDS_F4 > 0 ? T::LDS_F4 : 1];
-#pragma unroll 1
-  for (int it = 0; it < ITEMS; ++it) {
-    const int vb = (int)blockIdx.x + it * (int)gridDim.x;
-    if (vb >= nblocks) break;
-    const int bx = vb % gx, t = vb / gx, by = t % gy, bz = t / gy;
-    (void)splitk_body<BM, BN, BK, WM, WN, P, V>(p, kchunk, mode, slab, tickets, bx, by, bz, gx,
-                                                gy, gz, reinterpret_cast<float*>(lds4),
-                                                reinterpret_cast<int*>(lds4));
-  }
-}
+// (Blocks running several work items in turn — DDL_FWD_ITEMS — measured 5.7-18 us/step slower on
+// the conv forwards and were removed in round 6: docs/DESIGN.md.)
 
 // K split inside ONE workgroup, for the skinny GEMMs (the fc layers at M = batch): KW waves each
 // run the one-wave 32x32 tile over 1/KW of the K range (own LDS staging image, no barriers),
@@ -1599,15 +1579,8 @@ inline void launch_gemm(const P& p, int splits, int wide_thr, const SplitScratch
                      dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets,
                      stamps);
 #else
-  if constexpr (DDL_FWD_ITEMS > 1 && GemmTile<BM, BN, BK, WM, WN, P, V>::DMA) {
-    const int nb = (g.nblocks + DDL_FWD_ITEMS - 1) / DDL_FWD_ITEMS;
-    DDL_LAUNCH((gemm_items_kernel<BM, BN, BK, WM, WN, P, V, DDL_FWD_ITEMS>), dim3(nb),
-               dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets, g.gx, g.gy,
-               g.gz, g.nblocks);
-  } else {
-    DDL_LAUNCH((gemm_f32_kernel<BM, BN, BK, WM, WN, P, V>), dim3(g.gx, g.gy, g.gz),
-               dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets);
-  }
+  DDL_LAUNCH((gemm_f32_kernel<BM, BN, BK, WM, WN, P, V>), dim3(g.gx, g.gy, g.gz),
+             dim3(WM * WN * 64), 0, stream, p, g.kchunk, g.mode, g.slab, g.tickets);
 #endif
   if (defer && g.mode == 2) return;  // the caller runs (or fuses) the wide reduce
   launch_reduce<BM, BN, BK, WM, WN, P>(p, g, stream);
