@@ -100,9 +100,6 @@ constexpr int CFG_KWAVE = 13;
 // (gemm.h GemmTile::mainloop_dma16); conv2-4 forward / data gradient / weight gradient only
 // (other ops fall back to config 3)
 constexpr int CFG_MF16 = 14;
-// training-only: the one-wave 32x32x32 LDS-DMA tile with two images in a ring (gemm.h
-// GemmTile::mainloop_dma<2>); conv2-4 forward only (other ops fall back to config 3)
-constexpr int CFG_DMA2 = 15;
 // (configs 16-20 — one-wave multi-fragment LDS-DMA tiles and the 32x32 ring tiles — were
 // measured in round 5, never won a launch and were removed: docs/DESIGN.md)
 

@@ -131,7 +131,6 @@ static size_t slab_need(int c, int M, int N, int K, int s) {
     // launch with the same split factor (engine_impl.h launch_cfg), so size for that
     case CFG_KWAVE: return gemm_slab_f4<TILE_3>(M, N, K, s);
     case CFG_MF16: return gemm_slab_f4<TILE_3>(M, N, K, s);  // same 32x32 partial layout
-    case CFG_DMA2: return gemm_slab_f4<TILE_3>(M, N, K, s);
     case 0: return gemm_slab_f4<TILE_0>(M, N, K, s);
     case 1: return gemm_slab_f4<TILE_1>(M, N, K, s);
     case 2: return gemm_slab_f4<TILE_2>(M, N, K, s);

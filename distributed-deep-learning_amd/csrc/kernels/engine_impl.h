@@ -31,8 +31,6 @@ namespace ddl {
 #define TILE_12 128, 128, 32, 4, 1
 // training: one-wave 32x32x32 on 16x16x4 MFMAs with LDS-DMA staging (CFG_MF16)
 #define TILE_14 32, 32, 32, 1, 1, 1
-// training: one-wave 32x32x32 LDS-DMA tile, two-image ring (CFG_DMA2; conv2-4 forward)
-#define TILE_15 32, 32, 32, 1, 1, 2
 
 template <class P>
 inline void launch_cfg(int c, const P& p, int s, int wide_thr, const SplitScratch& sc,
@@ -47,13 +45,6 @@ inline void launch_cfg(int c, const P& p, int s, int wide_thr, const SplitScratc
   if (c == CFG_MF16) {
     if constexpr (Mf16OK<P>::value) {
       launch_gemm<TILE_14>(p, s, wide_thr, sc, st);
-      return;
-    }
-    c = 3;
-  }
-  if (c == CFG_DMA2) {
-    if constexpr (Dma2OK<P>::value) {
-      launch_gemm<TILE_15>(p, s, wide_thr, sc, st);
       return;
     }
     c = 3;

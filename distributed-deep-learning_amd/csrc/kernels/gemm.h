@@ -211,20 +211,14 @@ struct GemmTile {
   static constexpr bool DMA16 = V == 1 && SOLO && BM == 32 && BN == 32 && BK == 32;
   // (variants 2-4 — generic multi-fragment LDS-DMA tiles and 32x32 rings of 2 / 3 LDS-DMA
   // images — lost to these loops in every launch and were removed: docs/DESIGN.md round 5)
-  // LDS-DMA two-image ring (variant 2; conv forwards only: layers.h Dma2OK): tiles t+1 and t+2
-  // in flight during tile t's MFMAs — twice the bytes in flight per wave, for the launches whose
-  // grids leave only 1.3-1.6 waves per SIMD (conv3 / conv4 forward), at 16 KB of LDS per block
-  static constexpr bool DMA2 = V == 2 && HasDma<P>::value && SOLO && TM * TN == 1 && BM == 32 &&
-                               BN == 32 && BK == 32 && !HasOnesA<P>::value;
-  static_assert(V == 0 || DMA16 || DMA2, "variant 1: the 16x16x4 tile, 2: the LDS-DMA ring");
+  static_assert(V == 0 || DMA16, "variant 1 is the one-wave 32x32x32 16x16x4 tile");
   // LDS-DMA staging (mainloop_dma): unpadded 32x32 images, swizzled through the gather
   // addresses (the DMA writes lane-linearly), one image of A + B per block
   static constexpr bool DMA = V == 0 && HasDma<P>::value && SOLO && TM * TN == 1 && BM == 32 &&
                               BN == 32 && BK == 32;
   static constexpr bool DMA_MF = V == 0 && HasDma<P>::value && SOLO && TM * TN > 1 && BN == 64 &&
                                  BK == 32 && AK && !BKC && !HasOnesA<P>::value;
-  static constexpr int LDS_F4 = DMA2 ? 1024
-                                : (DMA16 || DMA) ? 512
+  static constexpr int LDS_F4 = (DMA16 || DMA) ? 512
                                 : DMA_MF ? (BM * BK + BK * BN) / 4
                                 : (NBUF * (A_ELEMS + B_ELEMS)) / 4;
   // A wave with a single 32x32 fragment alternates two accumulator chains (summed at the
@@ -251,8 +245,7 @@ struct GemmTile {
   static DDL_DEV void mainloop(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
                                f32x16 (&acc)[TM][TN], const Win& w = Win()) {
     if constexpr (DMA16) mainloop_dma16(p, m_blk, n_blk, kb, ke, lds, acc, w);
-    else if constexpr (DMA) mainloop_dma<1>(p, m_blk, n_blk, kb, ke, lds, acc, w);
-    else if constexpr (DMA2) mainloop_dma<2>(p, m_blk, n_blk, kb, ke, lds, acc, w);
+    else if constexpr (DMA) mainloop_dma(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else if constexpr (DMA_MF) mainloop_dma_mf(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else if constexpr (PIPE) mainloop_pipe(p, m_blk, n_blk, kb, ke, lds, acc, w);
     else mainloop_basic(p, m_blk, n_blk, kb, ke, lds, acc, w);
@@ -432,14 +425,9 @@ struct GemmTile {
   // is DMA'd into the one image once tile t's fragments are in registers; completion is
   // counted by hand (vm_wait).  (A second image — tile t+2 in flight during tile t's MFMAs —
   // measured 8 % slower: 152 registers and 16 KB of LDS cap the block at 2.5 waves per SIMD.)
-  // NIMG = 2 (variant 2): two images in a ring; tile t+2 is DMA'd into tile t's image once t's
-  // fragments are in registers, so tiles t+1 and t+2 are in flight under t's MFMAs (vmcnt 8 =
-  // the newer tile's 8 DMAs still outstanding).  Same MFMA order, same bits.
-  template <int NIMG>
   static DDL_DEV void mainloop_dma(const P& p, int m_blk, int n_blk, int kb, int ke, float* lds,
                                    f32x16 (&acc)[TM][TN], const Win& w) {
     static_assert(FA == 4 && FB == 4 && R == 4, "32x32x32 one-wave tile");
-    static_assert(NIMG == 1 || (NIMG == 2 && !HasOnesA<P>::value), "ring: no ones-row patch");
     static_assert(!(HasOnesA<P>::value && AK), "ones-row patch: MN-contiguous A");
     const int lane = threadIdx.x & 63;
     const int lr = lane & 31, lh = lane >> 5;
@@ -463,16 +451,15 @@ struct GemmTile {
       }
     };
     const uint32_t base = lds_addr(lds);
-    auto dma = [&](int k0, int img = 0) {
-      const uint32_t b0 = base + img * 8192;
+    auto dma = [&](int k0) {
 #pragma unroll
-      for (int it = 0; it < 4; ++it) dma16(srcA(p, ai[it], k0, w), b0 + it * 1024);
+      for (int it = 0; it < 4; ++it) dma16(srcA(p, ai[it], k0, w), base + it * 1024);
 #pragma unroll
-      for (int it = 0; it < 4; ++it) dma16(srcB(p, bi[it], k0, w), b0 + 4096 + it * 1024);
+      for (int it = 0; it < 4; ++it) dma16(srcB(p, bi[it], k0, w), base + 4096 + it * 1024);
     };
     // fragments of K step (r, s): lane half h holds k = 8r + 4h + s (the basic loop's order)
-    auto rd = [&](float (&av)[R][4], float (&bv)[R][4], int img = 0) {
-      const float* As = lds + img * 2048;
+    auto rd = [&](float (&av)[R][4], float (&bv)[R][4]) {
+      const float* As = lds;
       const float* Bs = As + 1024;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -518,7 +505,7 @@ struct GemmTile {
       __builtin_amdgcn_s_setprio(0);
 #endif
     };
-    if (nk > 0 && NIMG == 1) {
+    if (nk > 0) {
       float a0[R][4], b0[R][4];
       dma(kb);
       for (int kt = 0; kt < nk; ++kt) {
@@ -527,18 +514,6 @@ struct GemmTile {
         rd(a0, b0);
         lgkm_wait0();   // its fragments are in registers: the image may be restaged
         if (kt + 1 < nk) dma(kb + (kt + 1) * BK);
-        mma(a0, b0);
-      }
-    } else if (nk > 0) {
-      float a0[R][4], b0[R][4];
-      dma(kb, 0);
-      if (nk > 1) dma(kb + BK, 1);
-      for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) vm_wait<8>();  // tile kt is in its image (kt + 1 may be in flight)
-        else vm_wait<0>();
-        rd(a0, b0, kt & 1);
-        lgkm_wait0();   // its fragments are in registers: the image may be restaged
-        if (kt + 2 < nk) dma(kb + (kt + 2) * BK, kt & 1);
         mma(a0, b0);
       }
     }

@@ -971,13 +971,6 @@ struct Mf16OK<ConvDgrad<H, CIN, COUT, HPREV>> : std::true_type {};
 template <int H, int CIN, int COUT>
 struct Mf16OK<ConvWgradBM<H, CIN, COUT>> : std::true_type {};
 
-// ops the two-image LDS-DMA ring (CFG_DMA2, gemm.h mainloop_dma<2>) is instantiated for: the
-// halo-input conv forwards (conv2-4)
-template <class P>
-struct Dma2OK : std::false_type {};
-template <int H, int CIN, int COUT, bool KM>
-struct Dma2OK<ConvFwd<H, CIN, COUT, KM>> : std::bool_constant<CIN % kBK == 0> {};
-
 // ops the K-wave launch (gemm.h gemm_kwave_kernel, CFG_KWAVE) is instantiated for
 template <class P>
 struct KWaveOK : std::false_type {};

@@ -399,49 +399,6 @@ def test_mf16_config_matches_reference(setup, mode):
         eng.set_wide(base[2])
 
 
-@pytest.mark.parametrize("mode", ["default", "split1", "wide"])
-def test_dma2_ring_is_bit_identical(setup, mode):
-    """CFG_DMA2 = 15 (gemm.h mainloop_dma<2>: the one-wave LDS-DMA tile with two images in a
-    ring, tiles t+1 and t+2 in flight) on the conv2-4 forwards: same MFMA order as the one-image
-    loop (config 3), so the same bits — pooled activations and all 14 gradients — under the fused
-    epilogue (split 1), the in-launch last-arriver reduce and the separate wide reduce; and the
-    gradients match the fp32 / fp64 autograd reference."""
-    eng, flat, params, grads, x, y = setup
-    base = (eng.get_cfg(), eng.get_splits(), eng.get_wide())
-    fwd = (1, 2, 3)  # conv2-4 forward (api.h op order)
-
-    def run(c):
-        cfg, spl, wide = (list(v) for v in base)
-        for op in fwd:
-            cfg[op] = c
-            if mode == "split1":
-                spl[op] = 1
-            elif mode == "wide":
-                spl[op], wide[op] = max(2, spl[op]), 1
-        eng.set_cfg(cfg)
-        eng.set_splits(spl)
-        eng.set_wide(wide)
-        grads.zero_()
-        eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 67)
-        torch.cuda.synchronize()
-        acts = [eng.eng.buffer(n, x.shape[0]).clone() for n in ("p2", "p3", "p4")]
-        return grads.clone(), acts
-
-    try:
-        g3, a3 = run(3)
-        g15, a15 = run(15)
-        g15b, _ = run(15)
-        assert torch.equal(g15, g15b)
-        for name, u, v in zip(("p2", "p3", "p4"), a3, a15):
-            assert torch.equal(u, v), name
-        assert torch.equal(g3, g15)
-        check_grads(g15, flat, x, y, 0.5, 67)
-    finally:
-        eng.set_cfg(base[0])
-        eng.set_splits(base[1])
-        eng.set_wide(base[2])
-
-
 @pytest.mark.parametrize("conc,dual", [(False, True), (False, False), (True, False)])
 def test_backward_modes_match(setup, conc, dual):
     """Single-stream dual launches, single-stream back-to-back and the two-stream backward
