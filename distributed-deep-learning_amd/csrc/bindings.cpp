@@ -72,7 +72,7 @@ class PyEngine {
     TORCH_CHECK((int)c.size() == ddl::OP_COUNT, "expected ", (int)ddl::OP_COUNT, " tile configs");
     for (int i = 0; i < ddl::OP_COUNT; ++i) {
       TORCH_CHECK((c[i] >= 0 && c[i] < ddl::NUM_TILE_CFGS) || c[i] == ddl::CFG_KWAVE ||
-                      c[i] == ddl::CFG_MF16,
+                      c[i] == ddl::CFG_MF16 || c[i] == ddl::CFG_KW16,
                   "tile config out of range");
       e_.cfg[i] = (int)c[i];
     }

@@ -36,7 +36,10 @@ Engine::Engine() {
   // gradient split 8: 295.3 -> 293.0 us, profiles/r5_sched_ab_mf16.log; then conv3 weight
   // gradient on config 14 too: 293.5 -> 292.7 us, profiles/r5_sched_ab_conv3w.log — conv2's
   // weight gradient on it loses 6 us)
-  static const int defc[OP_COUNT] = {3, 3, 3, 3, CFG_KWAVE, 3, CFG_KWAVE, 5, CFG_KWAVE, 5,
+  // (round 6: fc1's and fc2's forwards on the 16-row K-wave launch, 8 waves — fc2 then writes h2
+  // itself and the head reads it instead of fc2's split-K partials: 260.7-261.0 -> 259.1-259.4
+  // us/step, 4 interleaved rounds, profiles/r6_sched_ab_kw16.log)
+  static const int defc[OP_COUNT] = {3, 3, 3, 3, CFG_KW16, CFG_KW16, CFG_KWAVE, 5, CFG_KWAVE, 5,
                                      3, CFG_MF16, 3, CFG_MF16, CFG_MF16, 3, 3};
   // (re-tuned in the real step with scripts/sched_ab.py after the compact 52-row conv3
   // enumeration and the wgrad row decode: conv3 forward split 4 + in-launch reduce instead of
@@ -57,7 +60,7 @@ Engine::Engine() {
   // conv4's 6 instead of 8: 267.2 -> 264.8, profiles/r6_sched_ab_wgrad.log; conv4's forward
   // split-K 5 instead of 6 once the last arriver sums its partials in one batched round per 4:
   // 264.4 -> 262.9, profiles/r6_runner_tune.log, r6_sched_ab_zb.log)
-  static const int defs[OP_COUNT] = {1, 3, 3, 5, 8, 16, 4, 1, 4, 1, 5, 6, 5, 12, 4, 48, 1024};
+  static const int defs[OP_COUNT] = {1, 3, 3, 5, 8, 8, 4, 1, 4, 1, 5, 6, 5, 12, 4, 48, 1024};
   // split-K reduce in-launch (last arriver) for these ops, separate wide-reduce kernel otherwise
   static const bool inl[OP_COUNT] = {0, 1, 1, 1, 0, 0, 1, 0, 0, 0, 1, 1, 1, 1, 1, 0, 0};
   memcpy(cfg, defc, sizeof(defc));
@@ -131,6 +134,7 @@ static size_t slab_need(int c, int M, int N, int K, int s) {
     // launch with the same split factor (engine_impl.h launch_cfg), so size for that
     case CFG_KWAVE: return gemm_slab_f4<TILE_3>(M, N, K, s);
     case CFG_MF16: return gemm_slab_f4<TILE_3>(M, N, K, s);  // same 32x32 partial layout
+    case CFG_KW16: return gemm_slab_f4<TILE_3>(M, N, K, s);  // (fallback: 32x32 split-K)
     case 0: return gemm_slab_f4<TILE_0>(M, N, K, s);
     case 1: return gemm_slab_f4<TILE_1>(M, N, K, s);
     case 2: return gemm_slab_f4<TILE_2>(M, N, K, s);

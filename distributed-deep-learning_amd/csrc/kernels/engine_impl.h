@@ -42,6 +42,13 @@ inline void launch_cfg(int c, const P& p, int s, int wide_thr, const SplitScratc
     }
     c = 3;  // not instantiated for this op: the one-wave 32x32 tile
   }
+  if (c == CFG_KW16) {
+    if constexpr (KW16OK<P>::value) {
+      launch_gemm_kw16(p, s < 0 ? -s : s, st);
+      return;
+    }
+    c = 3;
+  }
   if (c == CFG_MF16) {
     if constexpr (Mf16OK<P>::value) {
       launch_gemm<TILE_14>(p, s, wide_thr, sc, st);

@@ -971,6 +971,15 @@ struct Mf16OK<ConvDgrad<H, CIN, COUT, HPREV>> : std::true_type {};
 template <int H, int CIN, int COUT>
 struct Mf16OK<ConvWgradBM<H, CIN, COUT>> : std::true_type {};
 
+// ops the 16-row K-wave launch (gemm.h gemm_kw16_kernel, CFG_KW16) is instantiated for: the fc
+// forwards (fc2 on it writes h2 itself and the head reads h2 instead of fc2's split-K partials).
+// (The fc data gradients on its body inside the packed launches measured equal or slower,
+// profiles/r6_sched_ab_kw16_dgrad.log, and were not kept.)
+template <class P>
+struct KW16OK : std::false_type {};
+template <bool R>
+struct KW16OK<FcFwd<R>> : std::true_type {};
+
 // ops the K-wave launch (gemm.h gemm_kwave_kernel, CFG_KWAVE) is instantiated for
 template <class P>
 struct KWaveOK : std::false_type {};

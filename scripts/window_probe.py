@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--prewarm", type=int, default=1000)
     ap.add_argument("--gc-off", action="store_true", help="gc.disable() around the windows "
                     "(as bench.py's timed_run)")
+    ap.add_argument("--sched", default="", help="schedule overrides 'op=cfg:split,...'")
     a = ap.parse_args()
     import torch
     from ddl_amd.config import TrainConfig
@@ -33,6 +34,18 @@ def main():
     cfg = TrainConfig(mode="sync", shard="flat", steps=10 ** 6, batch_size=100, eval_every=0,
                       engine="hip", quiet=True, data_sharding="stride")
     tr = Trainer(cfg, env, dataset=synthetic_mnist())
+    if a.sched:
+        e = tr.engine.eng
+        cf, sp = e.get_cfg(), e.get_splits()
+        for kv in a.sched.split(","):
+            op, val = kv.split("=")
+            c, _, s_ = val.partition(":")
+            cf[int(op)] = int(c)
+            if s_:
+                sp[int(op)] = int(s_)
+        e.set_cfg(cf)
+        e.set_splits(sp)
+        print(f"schedule: cfg {cf} splits {sp}")
     step = 0
     for _ in range(a.prewarm):
         tr.train_step(step)

@@ -399,6 +399,39 @@ def test_mf16_config_matches_reference(setup, mode):
         eng.set_wide(base[2])
 
 
+@pytest.mark.parametrize("op,waves", [(4, 4), (4, 8), (4, 16), (5, 4), (5, 8), (5, 16)])
+def test_kw16_fc_matches_reference(setup, op, waves):
+    """CFG_KW16 = 15 (gemm.h gemm_kw16_kernel: the K-wave launch on 16-row v_mfma_f32_16x16x4
+    tiles, N-contiguous B staged through each wave's swizzled LDS image) on fc1's or fc2's
+    forward (fc2: the head then reads h2 instead of fc2's split-K partials; both are the
+    default), at 4 / 8 / 16 waves: h1 / h2 (ReLU, dropout) within fp32 noise of the CPU reference, the 14 gradients against the fp32 /
+    fp64 autograd reference, bit-deterministic across runs."""
+    eng, flat, params, grads, x, y = setup
+    base_cfg, base_s = eng.get_cfg(), eng.get_splits()
+    cfg, spl = list(base_cfg), list(base_s)
+    cfg[op], spl[op] = 15, waves  # OP_FC1_FWD / OP_FC2_FWD (api.h op order)
+    try:
+        eng.set_cfg(cfg)
+        eng.set_splits(spl)
+        outs = []
+        for _ in range(2):
+            grads.zero_()
+            eng.forward_backward(x.to(DEV), y.to(DEV), 0.5, 88)
+            torch.cuda.synchronize()
+            outs.append(grads.clone())
+        assert torch.equal(outs[0], outs[1])
+        check_grads(outs[0], flat, x, y, 0.5, 88)
+        pv = param_views(flat, CANON_OFFSETS)
+        _, h1, h2 = ref_intermediates(pv, x, 0.5, 88)
+        got = eng.eng.buffer("h1", x.shape[0])
+        assert rel_err(got, h1) < 2e-5
+        assert torch.equal(got.cpu() > 0, h1 > 0)
+        assert rel_err(eng.eng.buffer("h2", x.shape[0]), h2) < 2e-5
+    finally:
+        eng.set_cfg(base_cfg)
+        eng.set_splits(base_s)
+
+
 @pytest.mark.parametrize("conc,dual", [(False, True), (False, False), (True, False)])
 def test_backward_modes_match(setup, conc, dual):
     """Single-stream dual launches, single-stream back-to-back and the two-stream backward

@@ -21,11 +21,18 @@ def data():
     return synthetic_mnist(n_train=2000, n_test=500, seed=5)
 
 
-def _run(data, native, steps=6, ready=None, **kw):
+def _run(data, native, steps=6, ready=None, sched=None, **kw):
     env = DistEnv(0, 1, 0, torch.device("cuda", 0))
     cfg = TrainConfig(mode="sync", steps=steps, batch_size=100, eval_every=0, engine="hip",
                       quiet=True, native_exchange=native, **kw)
     tr = Trainer(cfg, env, dataset=data)
+    if sched is not None:  # {op: (tile config, split)} overrides of the engine defaults
+        e = tr.engine.eng
+        cf, sp = e.get_cfg(), e.get_splits()
+        for op, (c, s_) in sched.items():
+            cf[op], sp[op] = c, s_
+        e.set_cfg(cf)
+        e.set_splits(sp)
     if ready is not None:
         tr.exchange.runner.set_ready_flags(ready)
     assert getattr(tr.exchange, "native", False) == native
@@ -67,13 +74,17 @@ def test_native_matches_python_exchange(data, kw):
 
 
 def test_fc2_reduce_in_head_is_bit_identical(data, monkeypatch):
-    """The native step leaves fc2's split-K reduce to the head kernel (engine.hip
-    Engine::forward defer_fc2, head.hip head_fused_fc2_kernel: same summation order as the
-    wide reduce launch).  Parameters and Adam state match the separate-launch step bitwise."""
+    """With fc2's forward on a split-K tile, the native step leaves its reduce to the head
+    kernel (engine.hip Engine::forward defer_fc2, head.hip head_fused_fc2_kernel: same summation
+    order as the wide reduce launch).  Parameters and Adam state match the separate-launch step
+    bitwise."""
+    # fc2's forward on the split-K 32x32 tile (config 3, split 16): the default runs it on the
+    # 16-row K-wave launch (CFG_KW16), whose epilogue writes h2 itself
+    sched = {5: (3, 16)}
     monkeypatch.setenv("DDL_FC2_REDUCE_IN_HEAD", "0")
-    p_sep, s_sep = _run(data, True, shard="flat")
+    p_sep, s_sep = _run(data, True, sched=sched, shard="flat")
     monkeypatch.setenv("DDL_FC2_REDUCE_IN_HEAD", "1")
-    p_head, s_head = _run(data, True, shard="flat")
+    p_head, s_head = _run(data, True, sched=sched, shard="flat")
     assert torch.equal(p_sep, p_head)
     for p in s_sep:
         assert torch.equal(s_sep[p][1], s_head[p][1])
