@@ -100,7 +100,7 @@ constexpr int CFG_KWAVE = 13;
 // (gemm.h GemmTile::mainloop_dma16); conv2-4 forward / data gradient / weight gradient only
 // (other ops fall back to config 3)
 constexpr int CFG_MF16 = 14;
-// training-only: the K-wave launch on 16-row tiles (gemm.h gemm_kw16_kernel; `splits` picks 4 /
+// training-only: the K-wave launch on 16-row tiles (kwave16.h gemm_kw16_kernel; `splits` picks 4 /
 // 8 / 16 waves); the fc forwards only (other ops fall back to config 3)
 constexpr int CFG_KW16 = 15;
 // (configs 16-20 — one-wave multi-fragment LDS-DMA tiles and the 32x32 ring tiles — were

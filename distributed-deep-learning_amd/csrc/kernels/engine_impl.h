@@ -11,6 +11,7 @@
 #include "layers.h"
 #include "head.h"
 #include "conv1.h"
+#include "kwave16.h"
 #include "engine_decl.h"
 
 namespace ddl {

@@ -971,7 +971,7 @@ struct Mf16OK<ConvDgrad<H, CIN, COUT, HPREV>> : std::true_type {};
 template <int H, int CIN, int COUT>
 struct Mf16OK<ConvWgradBM<H, CIN, COUT>> : std::true_type {};
 
-// ops the 16-row K-wave launch (gemm.h gemm_kw16_kernel, CFG_KW16) is instantiated for: the fc
+// ops the 16-row K-wave launch (kwave16.h gemm_kw16_kernel, CFG_KW16) is instantiated for: the fc
 // forwards (fc2 on it writes h2 itself and the head reads h2 instead of fc2's split-K partials).
 // (The fc data gradients on its body inside the packed launches measured equal or slower,
 // profiles/r6_sched_ab_kw16_dgrad.log, and were not kept.)

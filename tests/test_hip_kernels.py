@@ -401,7 +401,7 @@ def test_mf16_config_matches_reference(setup, mode):
 
 @pytest.mark.parametrize("op,waves", [(4, 4), (4, 8), (4, 16), (5, 4), (5, 8), (5, 16)])
 def test_kw16_fc_matches_reference(setup, op, waves):
-    """CFG_KW16 = 15 (gemm.h gemm_kw16_kernel: the K-wave launch on 16-row v_mfma_f32_16x16x4
+    """CFG_KW16 = 15 (kwave16.h gemm_kw16_kernel: the K-wave launch on 16-row v_mfma_f32_16x16x4
     tiles, N-contiguous B staged through each wave's swizzled LDS image) on fc1's or fc2's
     forward (fc2: the head then reads h2 instead of fc2's split-K partials; both are the
     default), at 4 / 8 / 16 waves: h1 / h2 (ReLU, dropout) within fp32 noise of the CPU reference, the 14 gradients against the fp32 /
