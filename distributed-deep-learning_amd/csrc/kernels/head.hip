@@ -146,14 +146,28 @@ head_fused_kernel(const float* __restrict__ h2, const float* __restrict__ w,
   // fc2's dropout key (layer 2) is also the dh2 mask key below
   const uint32_t key = thr24 ? ddl_mix32((seed ? *seed : seed_v) + 2u * 0x9E3779B9u) : 0u;
   float acc[HC];
-  head_logits(h2 + (size_t)row * HK, w, bias, part, acc);
+  // every operand up front, as head_fused_fc2_kernel: this thread's two h2 columns k = wave*128
+  // + t*64 + lane, their W3 rows (the logits AND the two dh2 columns below), fc3's bias, the
+  // label — one load round instead of a second W3 round after the softmax
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float hv[2], wv[2][HC], bb[HC];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int k = wave * 128 + t * 64 + lane;
+    hv[t] = h2[(size_t)row * HK + k];
+#pragma unroll
+    for (int c = 0; c < HC; ++c) wv[t][c] = w[k * HC + c];
+  }
+#pragma unroll
+  for (int c = 0; c < HC; ++c) bb[c] = bias[c];
+  const int lab = (int)labels[row];
+  head_logits_regs(hv, wv, bb, part, acc);
   float mx = acc[0];
 #pragma unroll
   for (int c = 1; c < HC; ++c) mx = acc[c] > mx ? acc[c] : mx;
   float se = 0.f;
 #pragma unroll
   for (int c = 0; c < HC; ++c) se += __expf(acc[c] - mx);
-  const int lab = (int)labels[row];
   // dlogits of this sample in every thread (same arithmetic as head_fwd_kernel's per-lane form)
   float dl[HC];
 #pragma unroll
@@ -173,12 +187,16 @@ head_fused_kernel(const float* __restrict__ h2, const float* __restrict__ w,
     dlog[(size_t)row * HC + threadIdx.x] = v;
   }
   // dh2 = dlogits W3^T with fc2's dropout backward (mask regenerated from the seed), 2 columns
-  // per thread
-  for (int i = threadIdx.x; i < HK; i += 256) {
+  // per thread, from the W3 rows already in registers (the same fmaf chain per element as the
+  // earlier form that reloaded W3 after the softmax: 0.2596-0.2603 -> 0.2592-0.2597 ms/step, 5
+  // alternating same-box rounds, profiles/r6_ab_head_regs.log)
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int k = wave * 128 + t * 64 + lane;
     float g = 0.f;
 #pragma unroll
-    for (int c = 0; c < HC; ++c) g = fmaf(dl[c], w[i * HC + c], g);
-    const int idx = row * HK + i;
+    for (int c = 0; c < HC; ++c) g = fmaf(dl[c], wv[t][c], g);
+    const int idx = row * HK + k;
     if (thr24) g = ddl_keep(key, (uint32_t)idx, thr24) ? g * inv_keep : 0.f;
     dpre2[idx] = g;
   }
